@@ -1,0 +1,114 @@
+"""Extract the reference's BLS known-answer vectors into tests/golden/kat_reference.json.
+
+Run here (where /root/reference exists); the JSON is committed so tests never read the
+reference at run time.  Only DATA is extracted (keys, messages, signatures the reference's
+own tests hold); signing roots are re-derived with our own SSZ code (oracle/ssz.py) and
+cross-checked against the values the reference files state where they state one.
+
+Sources:
+  * eth2util/signing/signing_test.go:24-74  (teku-produced registration; sk, pk, sig, domain)
+  * eth2util/deposit/deposit_test.go:215-259 + testdata/TestMarshalDepositData.golden
+  * cluster/examples/cluster-lock-00{0..3}.json  (cluster/cluster_test.go:242-260 TestExamples)
+"""
+
+from __future__ import annotations
+
+import base64
+import json
+import os
+import re
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "..", ".."))
+
+from oracle import ssz  # noqa: E402
+
+REF = "/root/reference"
+
+
+def _b(v: str) -> bytes:
+    if v.startswith("0x"):
+        return bytes.fromhex(v[2:])
+    return base64.b64decode(v)
+
+
+def registration_kat():
+    src = open(os.path.join(REF, "eth2util/signing/signing_test.go")).read()
+    sk = re.search(r'hex.DecodeString\("([0-9a-f]{64})"\)', src).group(1)
+    fee = re.search(r'"fee_recipient": "0x([0-9a-fA-F]{40})"', src).group(1)
+    gas = int(re.search(r'"gas_limit": "(\d+)"', src).group(1))
+    ts = int(re.search(r'"timestamp": "(\d+)"', src).group(1))
+    pk = re.search(r'"pubkey": "0x([0-9a-f]{96})"', src).group(1)
+    sig = re.search(r'"signature": "0x([0-9a-f]{192})"', src).group(1)
+    # expected domain literal (TestConstantApplicationBuilder)
+    dom_lit = re.search(r"expect := eth2p0.Domain\{(.*?)\}", src, re.S).group(1)
+    dom = bytes(int(x, 16) for x in re.findall(r"0x([0-9a-f]+)", dom_lit))
+    fork = bytes.fromhex("01017000")  # holesky genesis, eth2util/network.go:78
+    domain = ssz.compute_domain(ssz.DOMAIN_APPLICATION_BUILDER, fork)
+    assert domain == dom, "domain derivation disagrees with signing_test.go literal"
+    root = ssz.validator_registration_root(bytes.fromhex(fee), gas, ts, bytes.fromhex(pk))
+    msg = ssz.signing_root(root, domain)
+    # NOTE: "msg_pubkey" is the validator pubkey INSIDE the registration message; the test
+    # signs with a secret *share* whose public key the reference derives via SecretToPublicKey.
+    return {"source": "eth2util/signing/signing_test.go:24-74", "sk": sk, "msg_pubkey": pk, "msg": msg.hex(),
+            "sig": sig, "domain": domain.hex()}
+
+
+def deposit_kats():
+    src = open(os.path.join(REF, "eth2util/deposit/deposit_test.go")).read()
+    block = re.search(r"privKeys := \[\]string\{(.*?)\}", src, re.S).group(1)
+    sks = re.findall(r'"([0-9a-f]{64})"', block)
+    block = re.search(r"withdrawalAddrs := \[\]string\{(.*?)\}", src, re.S).group(1)
+    addrs = [a.lower() for a in re.findall(r'"0x([0-9a-fA-F]{40})"', block)]
+    golden = json.load(open(os.path.join(REF, "eth2util/deposit/testdata/TestMarshalDepositData.golden")))
+    fork = bytes.fromhex("00001020")  # goerli, eth2util/network.go:49
+    domain = ssz.compute_domain(ssz.DOMAIN_DEPOSIT, fork)
+    out = []
+    for g in golden:
+        creds = bytes.fromhex(g["withdrawal_credentials"])
+        addr = creds[12:].hex()
+        sk = sks[addrs.index(addr)]
+        mroot = ssz.deposit_message_root(bytes.fromhex(g["pubkey"]), creds, g["amount"])
+        assert mroot.hex() == g["deposit_message_root"], "deposit message root mismatch"
+        msg = ssz.signing_root(mroot, domain)
+        out.append({"source": "eth2util/deposit/testdata/TestMarshalDepositData.golden", "sk": sk,
+                    "pk": g["pubkey"], "msg": msg.hex(), "sig": g["signature"]})
+    return out
+
+
+def lock_kats():
+    out = []
+    for i in range(4):
+        path = os.path.join(REF, f"cluster/examples/cluster-lock-00{i}.json")
+        d = json.load(open(path))
+        dfn = d["cluster_definition"]
+        vals = []
+        for v in d["distributed_validators"]:
+            ent = {"dpk": _b(v["distributed_public_key"]).hex(),
+                   "shares": [_b(s).hex() for s in v["public_shares"]]}
+            br = v.get("builder_registration")
+            if br and br.get("signature"):
+                m = br["message"]
+                fork = _b(dfn["fork_version"])
+                domain = ssz.compute_domain(ssz.DOMAIN_APPLICATION_BUILDER, fork)
+                root = ssz.validator_registration_root(_b(m["fee_recipient"]), int(m["gas_limit"]),
+                                                       int(m["timestamp"]), _b(m["pubkey"]))
+                ent["registration"] = {"msg": ssz.signing_root(root, domain).hex(),
+                                       "sig": _b(br["signature"]).hex()}
+            vals.append(ent)
+        out.append({"source": f"cluster/examples/cluster-lock-00{i}.json", "threshold": dfn["threshold"],
+                    "lock_hash": _b(d["lock_hash"]).hex(), "signature_aggregate": _b(d["signature_aggregate"]).hex(),
+                    "validators": vals})
+    return out
+
+
+def main():
+    kats = {"registration": registration_kat(), "deposit": deposit_kats(), "locks": lock_kats()}
+    with open(os.path.join(HERE, "kat_reference.json"), "w") as f:
+        json.dump(kats, f, indent=1)
+    print("wrote", os.path.join(HERE, "kat_reference.json"))
+
+
+if __name__ == "__main__":
+    main()
