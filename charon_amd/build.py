@@ -1,0 +1,67 @@
+"""Build libhipbls.so (gfx950) in-tree, plus the test-only CPU harness.
+
+    python -m charon_amd.build            # product library + test harness
+The product library is compiled by hipcc for --offload-arch=gfx950 only.
+"""
+
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+LIB = os.path.join(HERE, "lib", "libhipbls.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+SOURCES = ["hipbls.hip"]
+HEADERS = ["hd.h", "consts.h", "fp.h", "fr.h", "tower.h", "ec.h", "sha256.h", "h2c.h", "pairing.h", "ops.h"]
+
+
+def _newer(target, deps):
+    if not os.path.exists(target):
+        return False
+    t = os.path.getmtime(target)
+    return all(os.path.getmtime(d) <= t for d in deps)
+
+
+def build_library(force: bool = False, verbose: bool = True) -> str:
+    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(ROOT, "include", "hipbls.h")]
+    if not force and _newer(LIB, deps):
+        return LIB
+    os.makedirs(os.path.dirname(LIB), exist_ok=True)
+    cmd = [HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-shared", "-fPIC", "-o", LIB + ".tmp"]
+    cmd += [os.path.join(CSRC, s) for s in SOURCES]
+    t = time.time()
+    subprocess.run(cmd, check=True, timeout=1800)
+    os.replace(LIB + ".tmp", LIB)
+    if verbose:
+        print(f"built {LIB} in {time.time() - t:.1f}s")
+    return LIB
+
+
+def build_hostcheck(force: bool = False, verbose: bool = True) -> str:
+    src = os.path.join(ROOT, "tests", "native", "hostcheck.cpp")
+    out = os.path.join(ROOT, "tests", "native", "libhbls_hostcheck.so")
+    deps = [src] + [os.path.join(CSRC, f) for f in HEADERS]
+    if not force and _newer(out, deps):
+        return out
+    cmd = ["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-o", out + ".tmp", src]
+    subprocess.run(cmd, check=True, timeout=900)
+    os.replace(out + ".tmp", out)
+    if verbose:
+        print(f"built {out}")
+    return out
+
+
+def main(argv=None):
+    force = "--force" in (argv or sys.argv[1:])
+    build_library(force)
+    build_hostcheck(force)
+
+
+if __name__ == "__main__":
+    main()

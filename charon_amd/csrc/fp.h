@@ -1,0 +1,256 @@
+// Fp: the 381-bit BLS12-381 base field, 12 x 32-bit little-endian limbs, Montgomery form
+// (R = 2^384).  Elements are kept *lazily reduced* in [0, 2p): since 4p < R the
+// no-final-subtraction Montgomery product of two such values is again < 2p, so the
+// hot multiply skips the conditional subtraction; canonical form ([0, p)) is produced only
+// for comparisons and serialisation.
+//
+// The product computes x*y+acc with v_mad_u64_u32 (see fp_mul); the limb count and layout
+// match the structure-of-arrays layout the kernels load from HBM.
+#pragma once
+#include "hd.h"
+#include "consts.h"
+
+namespace hb {
+
+constexpr int NL = 12;
+
+struct Fp {
+  uint32_t v[NL];
+};
+
+HD Fp fp_from_const(const uint32_t* c) {
+  Fp r;
+  HB_UNROLL for (int i = 0; i < NL; i++) r.v[i] = c[i];
+  return r;
+}
+
+HD Fp fp_zero() {
+  Fp r;
+  HB_UNROLL for (int i = 0; i < NL; i++) r.v[i] = 0;
+  return r;
+}
+
+HD Fp fp_one() { return fp_from_const(FP_ONE); }
+
+// a + b over 12 limbs, returns carry
+HD uint32_t raw_add(Fp& r, const Fp& a, const Fp& b) {
+  uint64_t c = 0;
+  HB_UNROLL for (int i = 0; i < NL; i++) {
+    c += (uint64_t)a.v[i] + b.v[i];
+    r.v[i] = (uint32_t)c;
+    c >>= 32;
+  }
+  return (uint32_t)c;
+}
+
+// a - b over 12 limbs, returns borrow (1 if a < b)
+HD uint32_t raw_sub(Fp& r, const Fp& a, const Fp& b) {
+  int64_t c = 0;
+  HB_UNROLL for (int i = 0; i < NL; i++) {
+    c += (int64_t)a.v[i] - (int64_t)b.v[i];
+    r.v[i] = (uint32_t)c;
+    c >>= 32;  // arithmetic shift: 0 or -1
+  }
+  return (uint32_t)(c & 1);
+}
+
+HD uint32_t raw_sub_const(Fp& r, const Fp& a, const uint32_t* b) {
+  int64_t c = 0;
+  HB_UNROLL for (int i = 0; i < NL; i++) {
+    c += (int64_t)a.v[i] - (int64_t)b[i];
+    r.v[i] = (uint32_t)c;
+    c >>= 32;
+  }
+  return (uint32_t)(c & 1);
+}
+
+HD uint32_t raw_add_const(Fp& r, const Fp& a, const uint32_t* b) {
+  uint64_t c = 0;
+  HB_UNROLL for (int i = 0; i < NL; i++) {
+    c += (uint64_t)a.v[i] + b[i];
+    r.v[i] = (uint32_t)c;
+    c >>= 32;
+  }
+  return (uint32_t)c;
+}
+
+HD void fp_select(Fp& r, bool take_b, const Fp& a, const Fp& b) {
+  HB_UNROLL for (int i = 0; i < NL; i++) r.v[i] = take_b ? b.v[i] : a.v[i];
+}
+
+// [0,2p) + [0,2p) -> [0,2p)
+HD Fp fp_add(const Fp& a, const Fp& b) {
+  Fp s, d;
+  raw_add(s, a, b);  // < 4p < 2^383: no carry out
+  uint32_t borrow = raw_sub_const(d, s, P2_RAW);
+  fp_select(s, borrow == 0, s, d);
+  return s;
+}
+
+HD Fp fp_sub(const Fp& a, const Fp& b) {
+  Fp d, e;
+  uint32_t borrow = raw_sub(d, a, b);
+  raw_add_const(e, d, P2_RAW);
+  fp_select(d, borrow != 0, d, e);
+  return d;
+}
+
+HD Fp fp_neg(const Fp& a) { return fp_sub(fp_zero(), a); }
+
+HD Fp fp_dbl(const Fp& a) { return fp_add(a, a); }
+
+// Montgomery product, CIOS with the "no-carry" simplification (top limb of p < 2^31-1).
+// Inputs in [0,2p), output in [0,2p).  (b may be any value < 2^384 if a < p: the
+// intermediate stays below a + p; the result is then < 2p as well.)
+HD Fp fp_mul_generic(const Fp& a, const Fp& b) {
+  uint32_t t[NL];
+  HB_UNROLL for (int j = 0; j < NL; j++) t[j] = 0;
+  HB_UNROLL for (int i = 0; i < NL; i++) {
+    uint64_t A = (uint64_t)a.v[0] * b.v[i] + t[0];
+    t[0] = (uint32_t)A;
+    A >>= 32;
+    uint32_t m = t[0] * HB_P_N0;
+    uint64_t C = (uint64_t)m * P_RAW[0] + t[0];
+    C >>= 32;
+    HB_UNROLL for (int j = 1; j < NL; j++) {
+      A = (uint64_t)a.v[j] * b.v[i] + t[j] + A;
+      t[j] = (uint32_t)A;
+      A >>= 32;
+      C = (uint64_t)m * P_RAW[j] + t[j] + C;
+      t[j - 1] = (uint32_t)C;
+      C >>= 32;
+    }
+    t[NL - 1] = (uint32_t)(C + A);
+  }
+  Fp r;
+  HB_UNROLL for (int j = 0; j < NL; j++) r.v[j] = t[j];
+  return r;
+}
+
+#if defined(__HIP_DEVICE_COMPILE__)
+// Device: one out-of-line copy of the multiplier; operands travel in VGPRs as 12-wide
+// vectors (struct arguments would be passed through scratch memory by the AMDGPU ABI).
+typedef uint32_t u32x12 __attribute__((ext_vector_type(12)));
+__device__ __noinline__ static u32x12 fp_mul_leaf(u32x12 av, u32x12 bv) {
+  Fp a, b;
+  HB_UNROLL for (int i = 0; i < NL; i++) {
+    a.v[i] = av[i];
+    b.v[i] = bv[i];
+  }
+  Fp r = fp_mul_generic(a, b);
+  u32x12 rv;
+  HB_UNROLL for (int i = 0; i < NL; i++) rv[i] = r.v[i];
+  return rv;
+}
+HD Fp fp_mul(const Fp& a, const Fp& b) {
+  u32x12 av, bv;
+  HB_UNROLL for (int i = 0; i < NL; i++) {
+    av[i] = a.v[i];
+    bv[i] = b.v[i];
+  }
+  u32x12 rv = fp_mul_leaf(av, bv);
+  Fp r;
+  HB_UNROLL for (int i = 0; i < NL; i++) r.v[i] = rv[i];
+  return r;
+}
+#else
+HD Fp fp_mul(const Fp& a, const Fp& b) { return fp_mul_generic(a, b); }
+#endif
+
+HD Fp fp_sqr(const Fp& a) { return fp_mul(a, a); }
+
+// reduce [0,2p) -> [0,p)
+HD Fp fp_canon(const Fp& a) {
+  Fp d;
+  uint32_t borrow = raw_sub_const(d, a, P_RAW);
+  Fp r;
+  fp_select(r, borrow == 0, a, d);
+  return r;
+}
+
+HD bool fp_is_zero(const Fp& a) {
+  Fp c = fp_canon(a);
+  uint32_t acc = 0;
+  HB_UNROLL for (int i = 0; i < NL; i++) acc |= c.v[i];
+  return acc == 0;
+}
+
+HD bool fp_eq(const Fp& a, const Fp& b) { return fp_is_zero(fp_sub(a, b)); }
+
+HD Fp fp_to_mont(const Fp& a) { return fp_mul(a, fp_from_const(FP_R2)); }
+
+HD Fp fp_from_mont(const Fp& a) {
+  Fp one = fp_zero();
+  one.v[0] = 1;
+  return fp_canon(fp_mul(a, one));
+}
+
+HD Fp fp_mul_small(const Fp& a, int k) {
+  // k in {2,3,4,8,...}: repeated doubling/adding keeps lazily reduced range
+  Fp r = a;
+  Fp acc = fp_zero();
+  while (k) {
+    if (k & 1) acc = fp_add(acc, r);
+    r = fp_dbl(r);
+    k >>= 1;
+  }
+  return acc;
+}
+
+// a^e for a fixed exponent given as 12 little-endian limbs (left-to-right binary).
+HDNI Fp fp_pow_const(const Fp& a, const uint32_t* e, int top_bit) {
+  Fp r = fp_one();
+  HB_NOUNROLL for (int i = top_bit; i >= 0; i--) {
+    r = fp_sqr(r);
+    if ((e[i >> 5] >> (i & 31)) & 1) r = fp_mul(r, a);
+  }
+  return r;
+}
+
+HD Fp fp_inv(const Fp& a) { return fp_pow_const(a, EXP_P_MINUS_2, 380); }
+
+// Legendre-style squareness check via a^((p-1)/2) (1: square, 0: zero).
+HD bool fp_is_square(const Fp& a) {
+  Fp t = fp_pow_const(a, EXP_LEGENDRE, 379);
+  return fp_is_zero(a) || fp_eq(t, fp_one());
+}
+
+// sqrt for p = 3 mod 4; returns false if a is not a square.
+HDNI bool fp_sqrt(Fp& r, const Fp& a) {
+  r = fp_pow_const(a, EXP_SQRT, 379);
+  return fp_eq(fp_sqr(r), a);
+}
+
+// ---- byte conversions (big-endian, canonical) ----
+HD void fp_from_be_raw(Fp& r, const uint8_t* b) {  // 48 bytes -> raw limbs (not reduced)
+  HB_UNROLL for (int i = 0; i < NL; i++) {
+    const uint8_t* q = b + 44 - 4 * i;
+    r.v[i] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
+  }
+}
+
+HD void fp_to_be_raw(uint8_t* b, const Fp& a) {
+  HB_UNROLL for (int i = 0; i < NL; i++) {
+    uint8_t* q = b + 44 - 4 * i;
+    q[0] = (uint8_t)(a.v[i] >> 24);
+    q[1] = (uint8_t)(a.v[i] >> 16);
+    q[2] = (uint8_t)(a.v[i] >> 8);
+    q[3] = (uint8_t)a.v[i];
+  }
+}
+
+// raw < p ?
+HD bool fp_raw_lt_p(const Fp& a) {
+  Fp d;
+  return raw_sub_const(d, a, P_RAW) != 0;
+}
+
+// canonical (non-Montgomery) value > (p-1)/2 ?  i.e. 2*v > p-1  <=>  2*v >= p
+HD bool fp_raw_is_lex_largest(const Fp& v) {
+  Fp d;
+  raw_add(d, v, v);  // v < p < 2^381 so no carry
+  Fp e;
+  return raw_sub_const(e, d, P_RAW) == 0;
+}
+
+}  // namespace hb

@@ -1,0 +1,202 @@
+// hash_to_curve for G2, RFC 9380 suite BLS12381G2_XMD:SHA-256_SSWU_RO_ with the Ethereum
+// proof-of-possession DST (herumi ETH mode, tbls/herumi.go:173 bls.SetETHmode):
+//   expand_message_xmd(msg, DST, 256) -> 4 Fp elements -> u0, u1 in Fp2
+//   -> simplified SWU on E2' (A' = 240u, B' = 1012(1+u), Z = -(2+u))
+//   -> 3-isogeny E2' -> E2 -> Q0 + Q1 -> clear_cofactor (Budroni-Pintore, = h_eff).
+#pragma once
+#include "ec.h"
+#include "sha256.h"
+
+namespace hb {
+
+// "BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_POP_" || I2OSP(43, 1)
+HB_CONST uint8_t DST_PRIME[44] = {'B', 'L', 'S', '_', 'S', 'I', 'G', '_', 'B', 'L', 'S', '1', '2', '3', '8',
+                                  '1', 'G', '2', '_', 'X', 'M', 'D', ':', 'S', 'H', 'A', '-', '2', '5', '6',
+                                  '_', 'S', 'S', 'W', 'U', '_', 'R', 'O', '_', 'P', 'O', 'P', '_', 43};
+constexpr int DST_PRIME_LEN = 44;
+
+// byte k of the xmd tail after msg: I2OSP(256, 2) || I2OSP(0, 1) || DST_prime
+HD uint8_t xmd_tail_byte(int k) {
+  if (k == 0) return 0x01;
+  if (k < 3) return 0x00;
+  return DST_PRIME[k - 3];
+}
+constexpr int XMD_TAIL_LEN = 3 + DST_PRIME_LEN;
+
+HD uint32_t be_word(uint8_t a, uint8_t b, uint8_t c, uint8_t d) {
+  return ((uint32_t)a << 24) | ((uint32_t)b << 16) | ((uint32_t)c << 8) | d;
+}
+
+// b0 = SHA256(Z_pad || msg || I2OSP(256,2) || 0x00 || DST_prime)
+HDNI Sha256State xmd_b0(const uint8_t* msg, uint32_t len) {
+  Sha256State st = sha256_init();
+  uint32_t zero[16];
+  HB_UNROLL for (int j = 0; j < 16; j++) zero[j] = 0;
+  sha256_compress(st, zero);  // Z_pad block
+  uint32_t body = len + XMD_TAIL_LEN;                       // bytes after Z_pad
+  uint32_t total_bits = (64u + body) * 8u;
+  uint32_t nblk = (body + 8u) / 64u + 1u;                  // blocks after Z_pad incl. padding
+  HB_NOUNROLL for (uint32_t b = 0; b < nblk; b++) {
+    uint32_t w[16];
+    HB_UNROLL for (int j = 0; j < 16; j++) {
+      uint8_t by[4];
+      HB_UNROLL for (int k = 0; k < 4; k++) {
+        uint32_t pos = b * 64u + (uint32_t)(4 * j + k);
+        uint8_t v;
+        if (pos < len) {
+          v = msg[pos];
+        } else if (pos < body) {
+          v = xmd_tail_byte((int)(pos - len));
+        } else if (pos == body) {
+          v = 0x80;
+        } else if (pos >= nblk * 64u - 4u) {
+          v = (uint8_t)(total_bits >> (8 * (int)(nblk * 64u - 1u - pos)));
+        } else {
+          v = 0;
+        }
+        by[k] = v;
+      }
+      w[j] = be_word(by[0], by[1], by[2], by[3]);
+    }
+    sha256_compress(st, w);
+  }
+  return st;
+}
+
+// b_i = SHA256(x || I2OSP(i,1) || DST_prime), x = 32 bytes (8 words); 77 bytes -> 2 blocks
+HDNI Sha256State xmd_bi(const uint32_t* x, uint32_t i) {
+  Sha256State st = sha256_init();
+  uint32_t w[16];
+  HB_UNROLL for (int j = 0; j < 8; j++) w[j] = x[j];
+  w[8] = be_word((uint8_t)i, DST_PRIME[0], DST_PRIME[1], DST_PRIME[2]);
+  HB_UNROLL for (int j = 9; j < 16; j++) {
+    int o = 4 * j - 33;
+    w[j] = be_word(DST_PRIME[o], DST_PRIME[o + 1], DST_PRIME[o + 2], DST_PRIME[o + 3]);
+  }
+  sha256_compress(st, w);
+  // second block: DST_prime[31..43] (13 bytes), 0x80, zeros, bit length 616
+  uint8_t tb[64];
+  HB_UNROLL for (int k = 0; k < 64; k++) tb[k] = 0;
+  HB_UNROLL for (int k = 0; k < 13; k++) tb[k] = DST_PRIME[31 + k];
+  tb[13] = 0x80;
+  tb[62] = (uint8_t)(616 >> 8);
+  tb[63] = (uint8_t)(616 & 0xff);
+  HB_UNROLL for (int j = 0; j < 16; j++) w[j] = be_word(tb[4 * j], tb[4 * j + 1], tb[4 * j + 2], tb[4 * j + 3]);
+  sha256_compress(st, w);
+  return st;
+}
+
+// 64-byte big-endian integer (as 16 BE words) mod p, in Montgomery form
+HD Fp fp_from_be512(const uint32_t* W) {
+  Fp lo, hi = fp_zero();
+  HB_UNROLL for (int i = 0; i < 12; i++) lo.v[i] = W[15 - i];
+  HB_UNROLL for (int i = 0; i < 4; i++) hi.v[i] = W[3 - i];
+  // lo may exceed 2p: it must be the second (unbounded) operand of the Montgomery product,
+  // whose intermediate value stays below a + p for the first operand a.
+  return fp_add(fp_mul(fp_from_const(FP_R2), lo), fp_mul(fp_from_const(FP_R3), hi));
+}
+
+// hash_to_field(msg, count = 2) for Fp2 with L = 64
+HDNI void hash_to_field_fp2(Fp2& u0, Fp2& u1, const uint8_t* msg, uint32_t len) {
+  Sha256State b0 = xmd_b0(msg, len);
+  Fp e[4];
+  uint32_t prev[8];
+  HB_UNROLL for (int j = 0; j < 8; j++) prev[j] = b0.h[j];
+  // b1 = H(b0 || 1 || DST'), b_i = H((b0 ^ b_{i-1}) || i || DST')
+  HB_NOUNROLL for (int k = 0; k < 4; k++) {
+    uint32_t W[16];
+    HB_UNROLL for (int half = 0; half < 2; half++) {
+      uint32_t i = (uint32_t)(2 * k + half + 1);
+      uint32_t x[8];
+      HB_UNROLL for (int j = 0; j < 8; j++) x[j] = (i == 1) ? b0.h[j] : (b0.h[j] ^ prev[j]);
+      Sha256State bi = xmd_bi(x, i);
+      HB_UNROLL for (int j = 0; j < 8; j++) {
+        prev[j] = bi.h[j];
+        W[8 * half + j] = bi.h[j];
+      }
+    }
+    Fp v = fp_from_be512(W);
+    // k is a runtime loop index: place without dynamic register indexing
+    if (k == 0) e[0] = v;
+    if (k == 1) e[1] = v;
+    if (k == 2) e[2] = v;
+    if (k == 3) e[3] = v;
+  }
+  u0 = {e[0], e[1]};
+  u1 = {e[2], e[3]};
+}
+
+// simplified SWU for E2' (RFC 9380 6.6.2); returns affine point on E2'
+HDNI void sswu_map(Fp2& x, Fp2& y, const Fp2& u) {
+  Fp2 A = f2_from_const(SSWU_A), B = f2_from_const(SSWU_B), Z = f2_from_const(SSWU_Z);
+  Fp2 u2 = f2_sqr(u);
+  Fp2 zu2 = f2_mul(Z, u2);
+  Fp2 tv1 = f2_add(f2_sqr(zu2), zu2);
+  Fp2 x1;
+  if (f2_is_zero(tv1)) {
+    x1 = f2_from_const(SSWU_B_OVER_ZA);
+  } else {
+    x1 = f2_mul(f2_from_const(SSWU_MINUS_B_OVER_A), f2_add(f2_one(), f2_inv(tv1)));
+  }
+  Fp2 gx1 = f2_add(f2_mul(f2_add(f2_sqr(x1), A), x1), B);
+  Fp2 y1;
+  if (f2_sqrt(y1, gx1)) {
+    x = x1;
+    y = y1;
+  } else {
+    Fp2 x2 = f2_mul(zu2, x1);
+    Fp2 gx2 = f2_add(f2_mul(f2_add(f2_sqr(x2), A), x2), B);
+    f2_sqrt(y1, gx2);  // gx1 non-square => gx2 square (RFC 9380 appendix F.2)
+    x = x2;
+    y = y1;
+  }
+  if (f2_sgn0(u) != f2_sgn0(y)) y = f2_neg(y);
+}
+
+HDNI Fp2 f2_poly_eval(const uint32_t (*c)[2][12], int n, const Fp2& x) {
+  Fp2 acc = f2_from_const(c[n - 1]);
+  for (int i = n - 2; i >= 0; i--) acc = f2_add(f2_mul(acc, x), f2_from_const(c[i]));
+  return acc;
+}
+
+// 3-isogeny E2' -> E2 (RFC 9380 E.3), output in Jacobian coordinates (no inversion):
+//   x = xn/xd, y = y' yn/yd;  Z = xd yd, X = xn xd yd^2, Y = y' yn xd^3 yd^2
+HDNI G2J iso3_map(const Fp2& x, const Fp2& y) {
+  Fp2 xn = f2_poly_eval(ISO_XNUM, 4, x);
+  Fp2 xd = f2_poly_eval(ISO_XDEN, 3, x);
+  Fp2 yn = f2_poly_eval(ISO_YNUM, 4, x);
+  Fp2 yd = f2_poly_eval(ISO_YDEN, 4, x);
+  G2J r;
+  Fp2 yd2 = f2_sqr(yd);
+  Fp2 xdyd2 = f2_mul(xd, yd2);
+  r.Z = f2_mul(xd, yd);
+  r.X = f2_mul(xn, xdyd2);
+  r.Y = f2_mul(f2_mul(y, yn), f2_mul(xdyd2, f2_sqr(xd)));
+  return r;
+}
+
+// h_eff * P via  [x^2 - x - 1]P + [x - 1]psi(P) + psi^2(2P)  (RFC 9380 G.3), x < 0.
+HDNI G2J g2_clear_cofactor(const G2J& P) {
+  G2J t1 = jac_neg(jac_mul_by_xabs(P));  // [x]P
+  G2J t2 = g2_psi(P);
+  G2J t3 = g2_psi2(jac_dbl(P));
+  t3 = jac_add(t3, jac_neg(t2));
+  t2 = jac_add(t1, t2);
+  t2 = jac_neg(jac_mul_by_xabs(t2));  // [x](xP + psi(P))
+  t3 = jac_add(t3, t2);
+  t3 = jac_add(t3, jac_neg(t1));
+  return jac_add(t3, jac_neg(P));
+}
+
+HDNI G2J hash_to_g2(const uint8_t* msg, uint32_t len) {
+  Fp2 u0, u1;
+  hash_to_field_fp2(u0, u1, msg, len);
+  Fp2 x, y;
+  sswu_map(x, y, u0);
+  G2J q0 = iso3_map(x, y);
+  sswu_map(x, y, u1);
+  G2J q1 = iso3_map(x, y);
+  return g2_clear_cofactor(jac_add(q0, q1));
+}
+
+}  // namespace hb

@@ -1,0 +1,114 @@
+/*
+ * hipbls.h -- C ABI of libhipbls.so, the MI355X (gfx950) BLS12-381 backend for charon's tbls
+ * package.  Plain pointers and sizes only; every hot-path entry point runs as HIP kernels.
+ *
+ * Each entry point replaces one method of charon's tbls.Implementation
+ * (/root/reference/tbls/tbls.go:27-69) as implemented by tbls.Herumi
+ * (/root/reference/tbls/herumi.go), in batched form; see INTEGRATION.md for the cgo binding.
+ *
+ * Byte formats (identical to herumi ETH mode):
+ *   public key  48 B  compressed G1 (ZCash flags 0x80/0x40/0x20, big-endian x)   tbls.go:18
+ *   signature   96 B  compressed G2 (x.c1 || x.c0, flags in byte 0)             tbls.go:24
+ *   secret key  32 B  big-endian scalar < r                                     tbls.go:21
+ *
+ * Per-item status codes (the Go shim maps them to herumi's error strings):
+ */
+#ifndef HIPBLS_H
+#define HIPBLS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum hbls_status {
+  HBLS_OK = 0,
+  HBLS_BAD_PUBKEY = 1,     /* "cannot set compressed public key in Herumi format"   herumi.go:432 */
+  HBLS_BAD_SIGNATURE = 2,  /* "cannot unmarshal signature into Herumi signature"    herumi.go:437 */
+  HBLS_NOT_VERIFIED = 3,   /* "signature not verified" (Verify, herumi.go:441) /
+                              "signature verification failed" (VerifyAggregate, herumi.go:479) */
+  HBLS_COMBINE_FAILED = 4, /* "cannot combine signatures"                           herumi.go:423 */
+  HBLS_BAD_SECRET = 5,     /* "cannot unmarshal secret into Herumi secret key"      herumi.go:451 */
+  HBLS_BAD_INPUT = 6       /* malformed batch description (offsets/lengths)  -- new, batch-only */
+};
+
+/* Return codes of the entry points themselves: 0 on success, <0 on a HIP/runtime error
+ * (text via hbls_last_error()).  Per-item verdicts are in the status arrays. */
+
+/* Select and initialise a device (idempotent, thread-safe; herumi.go:18-36 init()). */
+int hbls_init(int device);
+const char* hbls_last_error(void);
+/* Nonzero if a gfx950 device is present and the kernels are loadable. */
+int hbls_available(void);
+
+/* ---------------------------------------------------------------------------------------
+ * Host-buffer entry points (the drop-in boundary for the Go shim).  Blocking; the library
+ * copies inputs to device memory, runs the kernels and copies results back.
+ * --------------------------------------------------------------------------------------- */
+
+/* Verify: n independent (pk, msg, sig) triples.  tbls.Verify / Herumi.Verify
+ * (tbls.go:121, herumi.go:429-445).  Message i is msgs[msg_off[i] .. msg_off[i]+msg_len[i]).
+ * Identical messages are hashed to G2 once. status[i] in {OK, BAD_PUBKEY, BAD_SIGNATURE,
+ * NOT_VERIFIED}. */
+int hbls_verify_batch(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msgs,
+                      const uint64_t* msg_off, const uint32_t* msg_len, size_t n, uint8_t* status);
+
+/* ThresholdAggregate over groups: group g holds partials grp_off[g] .. grp_off[g+1]-1 with
+ * 96-byte signatures sigs[j] and share indices idx[j].  out[g] = sum_j lambda_j(0) sig_j,
+ * tbls.ThresholdAggregate / Herumi.ThresholdAggregate (tbls.go:115, herumi.go:390-427).
+ * status[g] in {OK, BAD_SIGNATURE, COMBINE_FAILED}. */
+int hbls_threshold_aggregate_batch(const uint8_t* sigs, const int64_t* idx, const uint32_t* grp_off,
+                                   size_t n_groups, uint8_t* out, uint8_t* status);
+
+/* Aggregate: plain sum of each group's signatures (tbls.Aggregate, herumi.go:366-388).
+ * An empty group yields the infinity encoding 0xc0||0^95. status in {OK, BAD_SIGNATURE}. */
+int hbls_aggregate_batch(const uint8_t* sigs, const uint32_t* grp_off, size_t n_groups, uint8_t* out,
+                         uint8_t* status);
+
+/* VerifyAggregate (FastAggregateVerify): group g verifies sigs[g] on message g against the sum of
+ * pks[grp_off[g] .. grp_off[g+1]).  tbls.VerifyAggregate / Herumi.VerifyAggregate
+ * (tbls.go:133, herumi.go:459-483).  status in {OK, BAD_SIGNATURE, BAD_PUBKEY, NOT_VERIFIED}. */
+int hbls_verify_aggregate_batch(const uint8_t* pks, const uint32_t* grp_off, const uint8_t* sigs,
+                                const uint8_t* msgs, const uint64_t* msg_off, const uint32_t* msg_len,
+                                size_t n_groups, uint8_t* status);
+
+/* Sign (herumi.go:447-457) and SecretToPublicKey (herumi.go:207-220), batched.
+ * Sign status in {OK, BAD_SECRET}; SecretToPublicKey additionally rejects the zero key. */
+int hbls_sign_batch(const uint8_t* sks, const uint8_t* msgs, const uint64_t* msg_off,
+                    const uint32_t* msg_len, size_t n, uint8_t* sigs, uint8_t* status);
+int hbls_secret_to_public_key_batch(const uint8_t* sks, size_t n, uint8_t* pks, uint8_t* status);
+
+/* ThresholdSplit core (herumi.go:278-326): shares[i-1] = f(i) for i = 1..total where
+ * f(z) = secret + sum_k coeffs[k-1] z^k (threshold-1 coefficients, 32 B big-endian each; the
+ * caller draws them from a CSPRNG or, for ThresholdSplitInsecure, from its reader).
+ * RecoverSecret (herumi.go:328-364): Lagrange interpolation at 0 over k shares. */
+int hbls_threshold_split(const uint8_t* secret, const uint8_t* coeffs, uint32_t total, uint32_t threshold,
+                         uint8_t* shares, uint8_t* status);
+int hbls_recover_secret(const uint8_t* shares, const int64_t* idx, size_t k, uint8_t* out, uint8_t* status);
+
+/* ---------------------------------------------------------------------------------------
+ * Device-buffer entry points (inputs already resident in HBM; asynchronous on `stream`, a
+ * hipStream_t passed as void*; 0 = the library's stream).  Used by the slot pipeline and the
+ * benchmark.  All pointers are device pointers.
+ *
+ * verify: msg_idx[i] indexes the table of distinct messages hashed by hbls_hash_to_g2_device
+ * into `hm` (192 B affine G2 points, library layout).
+ * --------------------------------------------------------------------------------------- */
+int hbls_hash_to_g2_device(const uint8_t* msgs, const uint64_t* msg_off, const uint32_t* msg_len,
+                           size_t n_msgs, void* hm, void* stream);
+int hbls_verify_device(const uint8_t* pks, const uint8_t* sigs, const uint32_t* msg_idx, const void* hm,
+                       size_t n, uint8_t* status, void* stream);
+int hbls_threshold_aggregate_device(const uint8_t* sigs, const int64_t* idx, const uint32_t* grp_off,
+                                    size_t n_groups, size_t n_partials, uint8_t* out, uint8_t* status,
+                                    void* stream);
+/* Bytes of the `hm` table entry per message. */
+size_t hbls_hm_entry_bytes(void);
+/* Wait for all work the library queued on `stream`. */
+int hbls_sync(void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HIPBLS_H */
