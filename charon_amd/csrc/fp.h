@@ -103,6 +103,7 @@ HD Fp fp_dbl(const Fp& a) { return fp_add(a, a); }
 // Inputs in [0,2p), output in [0,2p).  (b may be any value < 2^384 if a < p: the
 // intermediate stays below a + p; the result is then < 2p as well.)
 HD Fp fp_mul_generic(const Fp& a, const Fp& b) {
+  HB_COUNT_FP_MUL();
   uint32_t t[NL];
   HB_UNROLL for (int j = 0; j < NL; j++) t[j] = 0;
   HB_UNROLL for (int i = 0; i < NL; i++) {

@@ -74,6 +74,7 @@ HD Fr fr_sub(const Fr& a, const Fr& b) {
 
 // Montgomery product (CIOS with explicit top carry; r's top limb is ~0x73ed... > 2^31).
 HDNI Fr fr_mul(const Fr& a, const Fr& b) {
+  HB_COUNT_FR_MUL();
   uint32_t t[NLR + 2];
   HB_UNROLL for (int j = 0; j < NLR + 2; j++) t[j] = 0;
   HB_UNROLL for (int i = 0; i < NLR; i++) {

@@ -23,6 +23,20 @@
 #define HB_DEVICE_CODE 0
 #endif
 
+// Op counting (test harness only: the g++ build of tests/native/hostcheck.cpp defines
+// HB_COUNT_OPS to freeze the algorithmic work per item).  Compiles to nothing
+// in the product library.
+#if defined(HB_COUNT_OPS) && !defined(__HIPCC__)
+namespace hb {
+extern thread_local unsigned long long g_cnt_fp_mul, g_cnt_fr_mul;
+}
+#define HB_COUNT_FP_MUL() (++hb::g_cnt_fp_mul)
+#define HB_COUNT_FR_MUL() (++hb::g_cnt_fr_mul)
+#else
+#define HB_COUNT_FP_MUL() ((void)0)
+#define HB_COUNT_FR_MUL() ((void)0)
+#endif
+
 #if defined(__HIP_DEVICE_COMPILE__)
 #define HB_UNROLL _Pragma("unroll")
 #define HB_NOUNROLL _Pragma("nounroll")

@@ -1,12 +1,67 @@
 // TEST-ONLY harness: compiles the kernels' per-item arithmetic (charon_amd/csrc/*.h) for the
 // host CPU so tests/test_hostcheck.py can compare it with the Python oracle without a GPU.
 // The product library (libhipbls.so) never loads this; it is not a fallback.
+// Built with HB_COUNT_OPS: every Fp / Fr Montgomery product bumps a thread-local counter, which
+// hc_count_* read to freeze the algorithmic work per item (charon_amd/opcounts.py).
+#define HB_COUNT_OPS 1
 #include "../../charon_amd/csrc/ops.h"
 #include <string.h>
+
+namespace hb {
+thread_local unsigned long long g_cnt_fp_mul = 0, g_cnt_fr_mul = 0;
+}
 
 using namespace hb;
 
 extern "C" {
+
+// Fp-mul counts of the kernels' per-item stages, in the kernels' own call structure:
+// out[0] k_verify (G1 decompress+subgroup, G2 decompress+subgroup, verify_core),
+// out[1] k_hash_to_g2 (hash_to_g2 + affine conversion), out[2..4] the three k_verify stages.
+// Returns the verify status.
+int hc_count_verify(const uint8_t* pk48, const uint8_t* msg, uint32_t len, const uint8_t* sig96,
+                    unsigned long long* out) {
+  g_cnt_fp_mul = 0;
+  G2A h = jac_to_aff(hash_to_g2(msg, len));
+  out[1] = g_cnt_fp_mul;
+  g_cnt_fp_mul = 0;
+  G1A pk;
+  G2A sig;
+  int st = ST_OK;
+  if (g1_decompress(pk, pk48)) st = ST_BAD_PUBKEY;
+  out[2] = g_cnt_fp_mul;
+  g_cnt_fp_mul = 0;
+  if (!st && g2_decompress(sig, sig96)) st = ST_BAD_SIGNATURE;
+  out[3] = g_cnt_fp_mul;
+  g_cnt_fp_mul = 0;
+  if (!st && !verify_core(pk, h, sig)) st = ST_NOT_VERIFIED;
+  out[4] = g_cnt_fp_mul;
+  out[0] = out[2] + out[3] + out[4];
+  return st;
+}
+
+// k_group_member work for one partial of a ThresholdAggregate over k partials (index j):
+// out[0] Fp-mul (decompress + subgroup + scalar multiplication), out[1] Fr-mul (lambda_j).
+int hc_count_ta_member(const uint8_t* sigs, const int64_t* idx, int k, int j, unsigned long long* out) {
+  g_cnt_fp_mul = 0;
+  g_cnt_fr_mul = 0;
+  G2A s;
+  if (g2_decompress(s, sigs + 96 * j)) return ST_BAD_SIGNATURE;
+  Fr xi = fr_from_i64(idx[j]);
+  Fr num = fr_one(), den = fr_one();
+  for (int m = 0; m < k; m++) {
+    if (m == j) continue;
+    Fr xm = fr_from_i64(idx[m]);
+    num = fr_mul(num, xm);
+    den = fr_mul(den, fr_sub(xm, xi));
+  }
+  Fr lam = fr_from_mont(fr_mul(num, fr_inv(den)));
+  G2J p = jac_mul_aff(s, lam.v, 255);
+  (void)p;
+  out[0] = g_cnt_fp_mul;
+  out[1] = g_cnt_fr_mul;
+  return 0;
+}
 
 int hc_hash_to_g2(const uint8_t* msg, uint32_t len, uint8_t* out96) {
   G2J h = hash_to_g2(msg, len);
