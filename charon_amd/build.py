@@ -49,7 +49,7 @@ def build_hostcheck(force: bool = False, verbose: bool = True) -> str:
     deps = [src] + [os.path.join(CSRC, f) for f in HEADERS]
     if not force and _newer(out, deps):
         return out
-    cmd = ["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-o", out + ".tmp", src]
+    cmd = ["g++", "-O2", "-std=c++17", "-pthread", "-shared", "-fPIC", "-o", out + ".tmp", src]
     subprocess.run(cmd, check=True, timeout=900)
     os.replace(out + ".tmp", out)
     if verbose:

@@ -1,7 +1,7 @@
 // Fr: the 255-bit scalar field of BLS12-381 (8 x 32-bit limbs, Montgomery form, R = 2^256).
 // Used for Lagrange coefficients lambda_i(0) = prod_{j!=i} x_j / (x_j - x_i)
-// (ThresholdAggregate, herumi.go:390-427 -> mcl LagrangeInterpolation) and for the
-// polynomial evaluation of ThresholdSplit / RecoverSecret (herumi.go:278-364).
+// (ThresholdAggregate, herumi.go:249-286 -> mcl LagrangeInterpolation) and for the
+// polynomial evaluation of ThresholdSplit / RecoverSecret (herumi.go:137-223).
 // Canonical [0, r) representation (r's top limb is too large for lazy tricks).
 #pragma once
 #include "hd.h"

@@ -1,5 +1,5 @@
 // hash_to_curve for G2, RFC 9380 suite BLS12381G2_XMD:SHA-256_SSWU_RO_ with the Ethereum
-// proof-of-possession DST (herumi ETH mode, tbls/herumi.go:173 bls.SetETHmode):
+// proof-of-possession DST (herumi ETH mode, tbls/herumi.go:32 bls.SetETHmode):
 //   expand_message_xmd(msg, DST, 256) -> 4 Fp elements -> u0, u1 in Fp2
 //   -> simplified SWU on E2' (A' = 240u, B' = 1012(1+u), Z = -(2+u))
 //   -> 3-isogeny E2' -> E2 -> Q0 + Q1 -> clear_cofactor (Budroni-Pintore, = h_eff).

@@ -58,7 +58,7 @@ __global__ KERNEL_BOUNDS void k_hash_to_g2(const uint8_t* __restrict__ msgs, con
 }
 
 // One lane per partial signature: decompress + validate pk and sig, pairing check.
-// herumi.go:429-445 (Deserialize pk -> Deserialize sig -> VerifyByte).
+// herumi.go:288-304 (Deserialize pk -> Deserialize sig -> VerifyByte).
 __global__ KERNEL_BOUNDS void k_verify(const uint8_t* __restrict__ pks, const uint8_t* __restrict__ sigs,
                                        const uint32_t* __restrict__ msg_idx, const HmEntry* __restrict__ hm,
                                        uint32_t n, uint8_t* __restrict__ status) {
@@ -132,7 +132,7 @@ __global__ KERNEL_BOUNDS void k_group_member(const uint8_t* __restrict__ sigs, c
 
 // One lane per group: sum the member points, compress (herumi Sign.Recover / Sign.Aggregate +
 // Serialize).  Status precedence follows herumi: any undecodable partial -> BAD_SIGNATURE
-// (deserialisation happens first, herumi.go:396-405), then combine failure.
+// (deserialisation happens first, herumi.go:255-264), then combine failure.
 __global__ KERNEL_BOUNDS void k_group_sum(const uint32_t* __restrict__ grp_off, uint32_t n_groups, int mode,
                                           const G2JEntry* __restrict__ pts, const uint8_t* __restrict__ mstat,
                                           uint8_t* __restrict__ out, uint8_t* __restrict__ status) {
@@ -184,7 +184,7 @@ __global__ KERNEL_BOUNDS void k_g1_member(const uint8_t* __restrict__ pks, uint3
   pts[j] = e;
 }
 
-// VerifyAggregate stage 2: one lane per group (FastAggregateVerify, herumi.go:459-483).
+// VerifyAggregate stage 2: one lane per group (FastAggregateVerify, herumi.go:318-342).
 __global__ KERNEL_BOUNDS void k_verify_aggregate(const uint32_t* __restrict__ grp_off, uint32_t n_groups,
                                                  const G1AEntry* __restrict__ pts, const uint8_t* __restrict__ mstat,
                                                  const uint8_t* __restrict__ sigs, const HmEntry* __restrict__ hm,
@@ -214,7 +214,7 @@ __global__ KERNEL_BOUNDS void k_verify_aggregate(const uint32_t* __restrict__ gr
   status[g] = verify_core(agg, hm_load(hm[g]), sig) ? ST_OK : ST_NOT_VERIFIED;
 }
 
-// Sign: one lane per (sk, message): sigma = sk * H(m)   (herumi.go:447-457)
+// Sign: one lane per (sk, message): sigma = sk * H(m)   (herumi.go:306-316)
 __global__ KERNEL_BOUNDS void k_sign(const uint8_t* __restrict__ sks, const uint32_t* __restrict__ msg_idx,
                                      const HmEntry* __restrict__ hm, uint32_t n, uint8_t* __restrict__ sigs,
                                      uint8_t* __restrict__ status) {
@@ -235,7 +235,7 @@ __global__ KERNEL_BOUNDS void k_sign(const uint8_t* __restrict__ sks, const uint
   status[i] = ST_OK;
 }
 
-// SecretToPublicKey: pk = sk * g1 (herumi.go:207-220; GetSafePublicKey rejects sk = 0)
+// SecretToPublicKey: pk = sk * g1 (herumi.go:66-79; GetSafePublicKey rejects sk = 0)
 __global__ KERNEL_BOUNDS void k_sk_to_pk(const uint8_t* __restrict__ sks, uint32_t n, uint8_t* __restrict__ pks,
                                          uint8_t* __restrict__ status) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;

@@ -1,6 +1,6 @@
 // Per-item building blocks shared by the gfx950 kernels (hipbls.hip):
-// ZCash point (de)serialisation (herumi ETH mode, tbls/herumi.go:429-445 Deserialize/Serialize),
-// and the Verify core e(pk, H(m)) * e(-g1, sig) == 1 (herumi.go:440 VerifyByte).
+// ZCash point (de)serialisation (herumi ETH mode, tbls/herumi.go:288-304 Deserialize/Serialize),
+// and the Verify core e(pk, H(m)) * e(-g1, sig) == 1 (herumi.go:299 VerifyByte).
 #pragma once
 #include "h2c.h"
 #include "pairing.h"

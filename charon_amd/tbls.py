@@ -36,18 +36,18 @@ class TblsError(Exception):
 
 # herumi.go error strings, by status code and call site
 _VERIFY_ERR = {
-    BAD_PUBKEY: "cannot set compressed public key in Herumi format",   # herumi.go:432
-    BAD_SIGNATURE: "cannot unmarshal signature into Herumi signature",  # herumi.go:437
-    NOT_VERIFIED: "signature not verified",                            # herumi.go:441
+    BAD_PUBKEY: "cannot set compressed public key in Herumi format",   # herumi.go:291
+    BAD_SIGNATURE: "cannot unmarshal signature into Herumi signature",  # herumi.go:296
+    NOT_VERIFIED: "signature not verified",                            # herumi.go:300
 }
 _VERIFY_AGG_ERR = {
-    BAD_PUBKEY: "cannot set compressed public key in Herumi format",   # herumi.go:472
-    BAD_SIGNATURE: "cannot unmarshal signature into Herumi signature",  # herumi.go:466
-    NOT_VERIFIED: "signature verification failed",                     # herumi.go:479
+    BAD_PUBKEY: "cannot set compressed public key in Herumi format",   # herumi.go:331
+    BAD_SIGNATURE: "cannot unmarshal signature into Herumi signature",  # herumi.go:325
+    NOT_VERIFIED: "signature verification failed",                     # herumi.go:338
 }
 _TA_ERR = {
-    BAD_SIGNATURE: "cannot unmarshal signature into Herumi signature",  # herumi.go:399-403
-    COMBINE_FAILED: "cannot combine signatures",                       # herumi.go:423
+    BAD_SIGNATURE: "cannot unmarshal signature into Herumi signature",  # herumi.go:258-262
+    COMBINE_FAILED: "cannot combine signatures",                       # herumi.go:282
 }
 
 
@@ -92,14 +92,14 @@ class HIPBLS:
 
     # ------------------------------------------------------------------ key management
     def generate_secret_key(self) -> bytes:
-        """herumi.go:195-205 (SetByCSPRNG): uniform non-zero scalar < r."""
+        """herumi.go:54-64 (SetByCSPRNG): uniform non-zero scalar < r."""
         while True:
             v = int.from_bytes(secrets.token_bytes(32), "big") & ((1 << 255) - 1)
             if 0 < v < R:
                 return v.to_bytes(32, "big")
 
     def generate_insecure_key(self, random) -> bytes:
-        """herumi.go:182-193 + generateInsecureSecret (:485-504): up to 100 reads of 32 bytes."""
+        """herumi.go:43-52 + generateInsecureSecret (:346-363): up to 100 reads of 32 bytes."""
         for _ in range(100):
             b = random.read(32)
             if len(b) == 32 and int.from_bytes(b, "big") < R:
@@ -107,7 +107,7 @@ class HIPBLS:
         raise TblsError("cannot generate insecure key")
 
     def secret_to_public_key(self, secret: bytes) -> bytes:
-        """herumi.go:207-220."""
+        """herumi.go:66-79."""
         sk = _need(secret, PRIVKEY_LEN, "private key")
         out = ctypes.create_string_buffer(48)
         st = ctypes.create_string_buffer(1)
@@ -120,7 +120,7 @@ class HIPBLS:
 
     def _split(self, secret: bytes, total: int, threshold: int, coeffs: List[bytes]) -> Dict[int, bytes]:
         if threshold <= 1:
-            raise TblsError("threshold has to be greater than 1")  # herumi.go:281
+            raise TblsError("threshold has to be greater than 1")  # herumi.go:140
         sk = _need(secret, PRIVKEY_LEN, "private key")
         if int.from_bytes(sk, "big") >= R:
             raise TblsError("cannot unmarshal bytes into Herumi secret key")
@@ -132,19 +132,19 @@ class HIPBLS:
         return {i + 1: shares.raw[32 * i:32 * i + 32] for i in range(total)}
 
     def threshold_split(self, secret: bytes, total: int, threshold: int) -> Dict[int, bytes]:
-        """herumi.go:278-326: random degree-(t-1) polynomial with f(0) = secret, shares f(1..n)."""
+        """herumi.go:137-185: random degree-(t-1) polynomial with f(0) = secret, shares f(1..n)."""
         coeffs = [self.generate_secret_key() for _ in range(max(0, threshold - 1))]
         return self._split(secret, total, threshold, coeffs)
 
     def threshold_split_insecure(self, secret: bytes, total: int, threshold: int, random) -> Dict[int, bytes]:
-        """herumi.go:224-276 (coefficients from the caller's reader)."""
+        """herumi.go:83-135 (coefficients from the caller's reader)."""
         if threshold <= 1:
             raise TblsError("threshold has to be greater than 1")
         coeffs = [self.generate_insecure_key(random) for _ in range(threshold - 1)]
         return self._split(secret, total, threshold, coeffs)
 
     def recover_secret(self, shares: Mapping[int, bytes], total: int = 0, threshold: int = 0) -> bytes:
-        """herumi.go:328-364: Lagrange interpolation at 0 over Fr."""
+        """herumi.go:187-223: Lagrange interpolation at 0 over Fr."""
         ids = list(shares.keys())
         blob = b"".join(_need(shares[i], PRIVKEY_LEN, "private key") for i in ids)
         out = ctypes.create_string_buffer(32)
@@ -158,7 +158,7 @@ class HIPBLS:
 
     # ------------------------------------------------------------------ signatures
     def sign(self, private_key: bytes, data: bytes) -> bytes:
-        """herumi.go:447-457."""
+        """herumi.go:306-316."""
         return self.sign_batch([private_key], [data])[0]
 
     def sign_batch(self, sks: Sequence[bytes], msgs: Sequence[bytes]) -> List[bytes]:
@@ -180,7 +180,7 @@ class HIPBLS:
         return res
 
     def verify(self, compressed_public_key: bytes, data: bytes, signature: bytes) -> None:
-        """herumi.go:429-445; raises TblsError with herumi's message, returns None on success."""
+        """herumi.go:288-304; raises TblsError with herumi's message, returns None on success."""
         st = self.verify_batch([compressed_public_key], [data], [signature])[0]
         if st != OK:
             raise TblsError(_VERIFY_ERR[st])
@@ -200,7 +200,7 @@ class HIPBLS:
         return list(st.raw[:n])
 
     def threshold_aggregate(self, partial_signatures_by_index: Mapping[int, bytes]) -> bytes:
-        """herumi.go:390-427."""
+        """herumi.go:249-286."""
         outs, sts = self.threshold_aggregate_batch([partial_signatures_by_index])
         if sts[0] != OK:
             raise TblsError(_TA_ERR.get(sts[0], "cannot combine signatures"))
@@ -224,7 +224,7 @@ class HIPBLS:
         return [out.raw[96 * i:96 * i + 96] for i in range(g)], list(st.raw[:g])
 
     def aggregate(self, signs: Sequence[bytes]) -> bytes:
-        """herumi.go:366-388 (empty input -> infinity encoding)."""
+        """herumi.go:225-247 (empty input -> infinity encoding)."""
         outs, sts = self.aggregate_batch([signs])
         if sts[0] != OK:
             raise TblsError("cannot unmarshal signature into Herumi signature")
@@ -245,7 +245,7 @@ class HIPBLS:
         return [out.raw[96 * i:96 * i + 96] for i in range(g)], list(st.raw[:g])
 
     def verify_aggregate(self, public_shares: Sequence[bytes], signature: bytes, data: bytes) -> None:
-        """herumi.go:459-483 (FastAggregateVerify)."""
+        """herumi.go:318-342 (FastAggregateVerify)."""
         st = self.verify_aggregate_batch([public_shares], [signature], [data])[0]
         if st != OK:
             raise TblsError(_VERIFY_AGG_ERR[st])

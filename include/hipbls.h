@@ -25,12 +25,12 @@ extern "C" {
 
 enum hbls_status {
   HBLS_OK = 0,
-  HBLS_BAD_PUBKEY = 1,     /* "cannot set compressed public key in Herumi format"   herumi.go:432 */
-  HBLS_BAD_SIGNATURE = 2,  /* "cannot unmarshal signature into Herumi signature"    herumi.go:437 */
-  HBLS_NOT_VERIFIED = 3,   /* "signature not verified" (Verify, herumi.go:441) /
-                              "signature verification failed" (VerifyAggregate, herumi.go:479) */
-  HBLS_COMBINE_FAILED = 4, /* "cannot combine signatures"                           herumi.go:423 */
-  HBLS_BAD_SECRET = 5,     /* "cannot unmarshal secret into Herumi secret key"      herumi.go:451 */
+  HBLS_BAD_PUBKEY = 1,     /* "cannot set compressed public key in Herumi format"   herumi.go:291 */
+  HBLS_BAD_SIGNATURE = 2,  /* "cannot unmarshal signature into Herumi signature"    herumi.go:296 */
+  HBLS_NOT_VERIFIED = 3,   /* "signature not verified" (Verify, herumi.go:300) /
+                              "signature verification failed" (VerifyAggregate, herumi.go:338) */
+  HBLS_COMBINE_FAILED = 4, /* "cannot combine signatures"                           herumi.go:282 */
+  HBLS_BAD_SECRET = 5,     /* "cannot unmarshal secret into Herumi secret key"      herumi.go:310 */
   HBLS_BAD_INPUT = 6       /* malformed batch description (offsets/lengths)  -- new, batch-only */
 };
 
@@ -49,7 +49,7 @@ int hbls_available(void);
  * --------------------------------------------------------------------------------------- */
 
 /* Verify: n independent (pk, msg, sig) triples.  tbls.Verify / Herumi.Verify
- * (tbls.go:121, herumi.go:429-445).  Message i is msgs[msg_off[i] .. msg_off[i]+msg_len[i]).
+ * (tbls.go:121, herumi.go:288-304).  Message i is msgs[msg_off[i] .. msg_off[i]+msg_len[i]).
  * Identical messages are hashed to G2 once. status[i] in {OK, BAD_PUBKEY, BAD_SIGNATURE,
  * NOT_VERIFIED}. */
 int hbls_verify_batch(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msgs,
@@ -57,33 +57,33 @@ int hbls_verify_batch(const uint8_t* pks, const uint8_t* sigs, const uint8_t* ms
 
 /* ThresholdAggregate over groups: group g holds partials grp_off[g] .. grp_off[g+1]-1 with
  * 96-byte signatures sigs[j] and share indices idx[j].  out[g] = sum_j lambda_j(0) sig_j,
- * tbls.ThresholdAggregate / Herumi.ThresholdAggregate (tbls.go:115, herumi.go:390-427).
+ * tbls.ThresholdAggregate / Herumi.ThresholdAggregate (tbls.go:115, herumi.go:249-286).
  * status[g] in {OK, BAD_SIGNATURE, COMBINE_FAILED}. */
 int hbls_threshold_aggregate_batch(const uint8_t* sigs, const int64_t* idx, const uint32_t* grp_off,
                                    size_t n_groups, uint8_t* out, uint8_t* status);
 
-/* Aggregate: plain sum of each group's signatures (tbls.Aggregate, herumi.go:366-388).
+/* Aggregate: plain sum of each group's signatures (tbls.Aggregate, herumi.go:225-247).
  * An empty group yields the infinity encoding 0xc0||0^95. status in {OK, BAD_SIGNATURE}. */
 int hbls_aggregate_batch(const uint8_t* sigs, const uint32_t* grp_off, size_t n_groups, uint8_t* out,
                          uint8_t* status);
 
 /* VerifyAggregate (FastAggregateVerify): group g verifies sigs[g] on message g against the sum of
  * pks[grp_off[g] .. grp_off[g+1]).  tbls.VerifyAggregate / Herumi.VerifyAggregate
- * (tbls.go:133, herumi.go:459-483).  status in {OK, BAD_SIGNATURE, BAD_PUBKEY, NOT_VERIFIED}. */
+ * (tbls.go:133, herumi.go:318-342).  status in {OK, BAD_SIGNATURE, BAD_PUBKEY, NOT_VERIFIED}. */
 int hbls_verify_aggregate_batch(const uint8_t* pks, const uint32_t* grp_off, const uint8_t* sigs,
                                 const uint8_t* msgs, const uint64_t* msg_off, const uint32_t* msg_len,
                                 size_t n_groups, uint8_t* status);
 
-/* Sign (herumi.go:447-457) and SecretToPublicKey (herumi.go:207-220), batched.
+/* Sign (herumi.go:306-316) and SecretToPublicKey (herumi.go:66-79), batched.
  * Sign status in {OK, BAD_SECRET}; SecretToPublicKey additionally rejects the zero key. */
 int hbls_sign_batch(const uint8_t* sks, const uint8_t* msgs, const uint64_t* msg_off,
                     const uint32_t* msg_len, size_t n, uint8_t* sigs, uint8_t* status);
 int hbls_secret_to_public_key_batch(const uint8_t* sks, size_t n, uint8_t* pks, uint8_t* status);
 
-/* ThresholdSplit core (herumi.go:278-326): shares[i-1] = f(i) for i = 1..total where
+/* ThresholdSplit core (herumi.go:137-185): shares[i-1] = f(i) for i = 1..total where
  * f(z) = secret + sum_k coeffs[k-1] z^k (threshold-1 coefficients, 32 B big-endian each; the
  * caller draws them from a CSPRNG or, for ThresholdSplitInsecure, from its reader).
- * RecoverSecret (herumi.go:328-364): Lagrange interpolation at 0 over k shares. */
+ * RecoverSecret (herumi.go:187-223): Lagrange interpolation at 0 over k shares. */
 int hbls_threshold_split(const uint8_t* secret, const uint8_t* coeffs, uint32_t total, uint32_t threshold,
                          uint8_t* shares, uint8_t* status);
 int hbls_recover_secret(const uint8_t* shares, const int64_t* idx, size_t k, uint8_t* out, uint8_t* status);

@@ -10,7 +10,7 @@ charon's BLS backend is `tbls.Herumi` (/root/reference/tbls/herumi.go), a cgo wr
 the third-party `github.com/herumi/bls-eth-go-binary v1.36.1` (go.mod:14, go.sum:233-234),
 which is NOT vendored and not present offline.  We therefore restate the published
 algorithm herumi implements in ETH mode (`bls.SetETHmode(bls.EthModeLatest)`,
-herumi.go:173):
+herumi.go:32):
 
   * BLS signatures, minimal-pubkey-size variant, proof-of-possession ciphersuite
     `BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_POP_` (draft-irtf-cfrg-bls-signature);
@@ -18,7 +18,7 @@ herumi.go:173):
     3-isogenous curve, 3-isogeny, Budroni-Pintore cofactor clearing);
   * ZCash-format compressed point encoding (48 B G1 public keys, 96 B G2 signatures);
   * Lagrange interpolation at 0 over Fr for ThresholdAggregate / RecoverSecret
-    (herumi.go:390-427, 328-364).
+    (herumi.go:249-286, 328-364).
 
 The 3-isogeny map constants are *derived* here (Velu's formulas, see `_derive_iso3`)
 rather than transcribed, and the normalisation among the six candidate maps is pinned by
@@ -735,7 +735,7 @@ def sk_to_bytes(s: int) -> bytes:
 
 
 def secret_to_public_key(sk: bytes) -> bytes:
-    """herumi.go:207-220 (GetSafePublicKey rejects the zero key)."""
+    """herumi.go:66-79 (GetSafePublicKey rejects the zero key)."""
     s = sk_from_bytes(sk)
     if s == 0:
         raise DecodeError("zero secret")
@@ -743,7 +743,7 @@ def secret_to_public_key(sk: bytes) -> bytes:
 
 
 def sign(sk: bytes, msg: bytes) -> bytes:
-    """herumi.go:447-457."""
+    """herumi.go:306-316."""
     s = sk_from_bytes(sk)
     return g2_compress(g2_mul(hash_to_g2(msg), s))
 
@@ -756,7 +756,7 @@ def core_verify(pk_pt, msg: bytes, sig_pt) -> bool:
 
 
 def verify(pk: bytes, msg: bytes, sig: bytes) -> int:
-    """herumi.go:429-445 -> status code."""
+    """herumi.go:288-304 -> status code."""
     try:
         pk_pt = g1_decompress(pk)
     except DecodeError:
@@ -769,7 +769,7 @@ def verify(pk: bytes, msg: bytes, sig: bytes) -> int:
 
 
 def aggregate(sigs) -> tuple[int, bytes]:
-    """herumi.go:366-388.  Empty input -> infinity."""
+    """herumi.go:225-247.  Empty input -> infinity."""
     acc = None
     for s in sigs:
         try:
@@ -780,7 +780,7 @@ def aggregate(sigs) -> tuple[int, bytes]:
 
 
 def verify_aggregate(pks, sig: bytes, msg: bytes) -> int:
-    """herumi.go:459-483 (FastAggregateVerify)."""
+    """herumi.go:318-342 (FastAggregateVerify)."""
     try:
         sig_pt = g2_decompress(sig)
     except DecodeError:
@@ -815,7 +815,7 @@ def lagrange_coeffs_at_zero(ids):
 
 
 def threshold_aggregate(partials: dict) -> tuple[int, bytes]:
-    """herumi.go:390-427: sigma = sum lambda_i(0) sigma_i over all given partials."""
+    """herumi.go:249-286: sigma = sum lambda_i(0) sigma_i over all given partials."""
     ids = list(partials.keys())
     pts = []
     for idx in ids:
@@ -837,7 +837,7 @@ def threshold_aggregate(partials: dict) -> tuple[int, bytes]:
 
 
 def threshold_split(sk: bytes, total: int, threshold: int, coeffs) -> dict:
-    """herumi.go:278-326 with caller-supplied polynomial coefficients a_1..a_{t-1}."""
+    """herumi.go:137-185 with caller-supplied polynomial coefficients a_1..a_{t-1}."""
     s = sk_from_bytes(sk)
     poly = [s] + [c % R for c in coeffs]
     assert len(poly) == threshold
@@ -851,7 +851,7 @@ def threshold_split(sk: bytes, total: int, threshold: int, coeffs) -> dict:
 
 
 def recover_secret(shares: dict) -> bytes:
-    """herumi.go:328-364."""
+    """herumi.go:187-223."""
     ids = list(shares.keys())
     lam = lagrange_coeffs_at_zero(ids)
     if lam is None:

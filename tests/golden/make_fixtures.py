@@ -9,6 +9,13 @@ Cases (status codes as in include/hipbls.h):
            negative index, undecodable partial, empty group
   aggregate / verify_aggregate: tbls_test.go:129-167 shape (10 keys), empty inputs
 Deterministic (seeded); run time ~2-3 minutes.
+
+Parity status: the valid / wrong-message / wrong-key / random-bytes cases follow from the
+ciphersuite the reference KATs pin (tests/golden/kat_reference.json).  The edge cases no reference
+test pins -- off-subgroup points, infinity encodings, non-canonical flags, share index 0 or
+negative, k = 0 / 1, empty Aggregate / VerifyAggregate -- are "parity unpinned": they follow the
+decision rules of SURVEY.md Appendix A (herumi's believed ETH-mode behaviour), since herumi
+(bls-eth-go-binary v1.36.1) is absent offline.
 """
 
 from __future__ import annotations

@@ -231,3 +231,36 @@ int hc_h2c_sum(const uint8_t* msg, uint32_t len, uint8_t* out) {
   return 0;
 }
 }
+
+// CPU baseline for bench.py (reported, not the target): `units` validators of one slot, each =
+// n partial Verifies (each hashing its message to G2, as herumi's VerifyByte does per call) + one
+// ThresholdAggregate over shares 1..t, compared with the root-key signature.  std::thread workers
+// take validators round-robin.  Returns the number of validators whose verdicts or aggregate
+// differ from the expected (all valid, aggregate == root signature).
+#include <atomic>
+#include <thread>
+#include <vector>
+extern "C" int hc_cpu_slot(int threads, int units, int n, int t, const uint8_t* pks, const uint8_t* sigs,
+                           const uint8_t* msgs, const uint32_t* midx, const uint8_t* ta_sigs,
+                           const uint8_t* root_sigs) {
+  std::atomic<int> next{0}, bad{0};
+  std::vector<int64_t> idx(t);
+  for (int i = 0; i < t; i++) idx[i] = i + 1;
+  auto work = [&]() {
+    for (;;) {
+      int v = next.fetch_add(1);
+      if (v >= units) return;
+      bool ok = true;
+      for (int i = v * n; i < v * n + n; i++)
+        ok &= hc_verify(pks + 48ull * i, msgs + 32ull * midx[i], 32, sigs + 96ull * i) == 0;
+      uint8_t out[96];
+      ok &= hc_lagrange_g2(ta_sigs + 96ull * t * v, idx.data(), t, out) == 0;
+      ok &= memcmp(out, root_sigs + 96ull * v, 96) == 0;
+      if (!ok) bad.fetch_add(1);
+    }
+  };
+  std::vector<std::thread> ws;
+  for (int k = 0; k < threads; k++) ws.emplace_back(work);
+  for (auto& w : ws) w.join();
+  return bad.load();
+}
