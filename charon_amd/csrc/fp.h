@@ -129,21 +129,69 @@ HD Fp fp_mul_generic(const Fp& a, const Fp& b) {
 }
 
 #if defined(__HIP_DEVICE_COMPILE__)
-// Device: one out-of-line copy of the multiplier; operands travel in VGPRs as 12-wide
-// vectors (struct arguments would be passed through scratch memory by the AMDGPU ABI).
+// Device: product-scanning ("FIPS") Montgomery product on v_mad_u64_u32 carry chains.
+// Column k of a*b + m*p is accumulated in a 64-bit VGPR pair `acc` plus a third word `c2`
+// that collects the carry-outs of the 64-bit multiply-adds (VCC -> v_addc_co_u32).  Per
+// column the low word of the first 12 columns selects m_k = acc_lo * (-p^-1) mod 2^32 so that
+// it cancels; columns 12..22 emit the result limbs.  288 v_mad_u64_u32 + 288 v_addc_co_u32 +
+// ~70 moves per product (the compiler's own lowering of the CIOS loop spent 764 extra v_movs).
+// Same bounds as fp_mul_generic: inputs < 2p, output < 2p (4p < 2^384).
+// The asm blocks carry 1 or 2 (a_j b_{k-j}, m_j p_{k-j}) pairs each: fewer blocks means fewer
+// of the s_nop's the hazard recognizer places after every inline-asm statement.
+__device__ __forceinline__ void fips_mac(uint64_t& acc, uint32_t& c2, uint32_t a, uint32_t b) {
+  asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc"
+      : "+v"(acc), "+v"(c2) : "v"(a), "v"(b) : "vcc");
+}
+__device__ __forceinline__ void fips_mac_s(uint64_t& acc, uint32_t& c2, uint32_t a, uint32_t b) {
+  asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc"
+      : "+v"(acc), "+v"(c2) : "v"(a), "s"(b) : "vcc");
+}
+__device__ __forceinline__ void fips_mac2(uint64_t& acc, uint32_t& c2, uint32_t a0, uint32_t b0, uint32_t m0,
+                                          uint32_t p0) {
+  asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc\n\t"
+      "v_mad_u64_u32 %0, vcc, %4, %5, %0\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc"
+      : "+v"(acc), "+v"(c2) : "v"(a0), "v"(b0), "v"(m0), "s"(p0) : "vcc");
+}
+__device__ __forceinline__ void fips_mac4(uint64_t& acc, uint32_t& c2, uint32_t a0, uint32_t b0, uint32_t m0,
+                                          uint32_t p0, uint32_t a1, uint32_t b1, uint32_t m1, uint32_t p1) {
+  asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc\n\t"
+      "v_mad_u64_u32 %0, vcc, %4, %5, %0\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc\n\t"
+      "v_mad_u64_u32 %0, vcc, %6, %7, %0\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc\n\t"
+      "v_mad_u64_u32 %0, vcc, %8, %9, %0\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc"
+      : "+v"(acc), "+v"(c2)
+      : "v"(a0), "v"(b0), "v"(m0), "s"(p0), "v"(a1), "v"(b1), "v"(m1), "s"(p1)
+      : "vcc");
+}
+
+// Operands travel in VGPRs as 12-wide vectors (struct arguments would go through scratch).
 typedef uint32_t u32x12 __attribute__((ext_vector_type(12)));
-__device__ __noinline__ static u32x12 fp_mul_leaf(u32x12 av, u32x12 bv) {
-  Fp a, b;
-  HB_UNROLL for (int i = 0; i < NL; i++) {
-    a.v[i] = av[i];
-    b.v[i] = bv[i];
+__device__ __noinline__ static u32x12 fp_mul_leaf(u32x12 a, u32x12 b) {
+  uint32_t m[NL];
+  u32x12 t;
+  uint64_t acc = 0;
+  uint32_t c2 = 0;
+  HB_UNROLL for (int k = 0; k < 2 * NL - 1; k++) {
+    const int lo = k < NL ? 0 : k - (NL - 1);
+    const int hi = k < NL ? k - 1 : NL - 1;  // pairs j in [lo, hi]
+    int j = lo;
+    HB_UNROLL for (; j + 1 <= hi; j += 2)
+      fips_mac4(acc, c2, a[j], b[k - j], m[j], P_RAW[k - j], a[j + 1], b[k - j - 1], m[j + 1], P_RAW[k - j - 1]);
+    if (j <= hi) fips_mac2(acc, c2, a[j], b[k - j], m[j], P_RAW[k - j]);
+    if (k < NL) {
+      fips_mac(acc, c2, a[k], b[0]);
+      m[k] = (uint32_t)acc * HB_P_N0;
+      fips_mac_s(acc, c2, m[k], P_RAW[0]);  // low word becomes 0
+    } else {
+      t[k - NL] = (uint32_t)acc;
+    }
+    acc = (acc >> 32) | ((uint64_t)c2 << 32);
+    c2 = 0;
   }
-  Fp r = fp_mul_generic(a, b);
-  u32x12 rv;
-  HB_UNROLL for (int i = 0; i < NL; i++) rv[i] = r.v[i];
-  return rv;
+  t[NL - 1] = (uint32_t)acc;
+  return t;
 }
 HD Fp fp_mul(const Fp& a, const Fp& b) {
+  HB_COUNT_FP_MUL();
   u32x12 av, bv;
   HB_UNROLL for (int i = 0; i < NL; i++) {
     av[i] = a.v[i];
