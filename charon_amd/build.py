@@ -18,7 +18,7 @@ LIB = os.path.join(HERE, "lib", "libhipbls.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 SOURCES = ["hipbls.hip"]
-HEADERS = ["hd.h", "consts.h", "fp.h", "fr.h", "tower.h", "ec.h", "sha256.h", "h2c.h", "pairing.h", "ops.h"]
+HEADERS = ["hd.h", "consts.h", "fp.h", "fr.h", "tower.h", "ec.h", "sha256.h", "h2c.h", "pairing.h", "ops.h", "pair3.h", "fpmul_asm.inc"]
 
 
 def _newer(target, deps):

@@ -5,6 +5,7 @@
 // (partial signature, group or message); kernels are staged so that work shared between
 // items (hash_to_curve of a message) runs once.
 #include "ops.h"
+#include "pair3.h"
 #include "../../include/hipbls.h"
 
 #include <mutex>
@@ -14,6 +15,12 @@
 #include <vector>
 
 using namespace hb;
+
+#if defined(__HIP_DEVICE_COMPILE__)
+HB_DEFINE_FPMUL_SUBROUTINE
+#else
+__global__ void hb_fpmul_holder() {}
+#endif
 
 // ---------------------------------------------------------------------------------------
 // Device-side storage formats
@@ -34,6 +41,17 @@ struct G1AEntry {  // affine G1 point, 112 B
   uint32_t pad[3];
 };
 
+struct LineEntry {  // one Miller-loop line, 288 B: (a0, c1, c2) unevaluated or (a0, a1, b1)
+  Fp2 a0, a1, b1;
+};
+
+// Per distinct message: H(m) and the 68 unevaluated lines of its Miller chain (pairing.h
+// miller_dbl_c / miller_add_c), shared by every partial signed over that message.
+struct MsgEntry {
+  HmEntry h;
+  LineEntry lines[N_LINES];
+};
+
 __device__ __forceinline__ G2A hm_load(const HmEntry& e) { return {e.x, e.y, e.inf != 0}; }
 
 #define KERNEL_BOUNDS __launch_bounds__(64)
@@ -45,7 +63,7 @@ constexpr int BLOCK = 64;
 
 // One lane per distinct message: hash_to_curve G2 (RFC 9380, DST ..._POP_), affine.
 __global__ KERNEL_BOUNDS void k_hash_to_g2(const uint8_t* __restrict__ msgs, const uint64_t* __restrict__ off,
-                                           const uint32_t* __restrict__ len, uint32_t n, HmEntry* __restrict__ hm) {
+                                           const uint32_t* __restrict__ len, uint32_t n, MsgEntry* __restrict__ hm) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   G2A h = jac_to_aff(hash_to_g2(msgs + off[i], len[i]));
@@ -54,28 +72,117 @@ __global__ KERNEL_BOUNDS void k_hash_to_g2(const uint8_t* __restrict__ msgs, con
   e.y = h.y;
   e.inf = h.inf ? 1u : 0u;
   e.pad[0] = e.pad[1] = e.pad[2] = 0;
-  hm[i] = e;
+  hm[i].h = e;
 }
 
-// One lane per partial signature: decompress + validate pk and sig, pairing check.
-// herumi.go:288-304 (Deserialize pk -> Deserialize sig -> VerifyByte).
-__global__ KERNEL_BOUNDS void k_verify(const uint8_t* __restrict__ pks, const uint8_t* __restrict__ sigs,
-                                       const uint32_t* __restrict__ msg_idx, const HmEntry* __restrict__ hm,
-                                       uint32_t n, uint8_t* __restrict__ status) {
+// The Miller chain of an affine G2 point Q: 68 lines, stored at out[j * stride].  EVAL: evaluate
+// each line at -g1 (pair (-g1, sig) of the verification equation); otherwise store (a0, c1, c2).
+template <bool EVAL>
+__device__ __forceinline__ void line_chain(const G2A& Q, LineEntry* __restrict__ out, size_t stride) {
+  G2Proj T = {Q.x, Q.y, f2_one()};
+  int j = 0;
+  HB_NOUNROLL for (int i = 62; i >= 0; i--) {
+    LineCoeffs l = miller_dbl_c(T);
+    if (EVAL) line_eval(l, fp_from_const(G1_GEN_X), fp_from_const(G1_GEN_NEG_Y));
+    out[(size_t)j * stride] = {l.a0, l.a1, l.b1};
+    j++;
+    if ((HB_X_ABS >> i) & 1) {
+      l = miller_add_c(T, Q.x, Q.y);
+      if (EVAL) line_eval(l, fp_from_const(G1_GEN_X), fp_from_const(G1_GEN_NEG_Y));
+      out[(size_t)j * stride] = {l.a0, l.a1, l.b1};
+      j++;
+    }
+  }
+}
+
+// One lane per distinct message: the unevaluated line chain of H(m).
+__global__ KERNEL_BOUNDS void k_lines_msg(MsgEntry* __restrict__ hm, uint32_t n) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  G1A pk;
-  if (g1_decompress(pk, pks + 48ull * i)) {
-    status[i] = ST_BAD_PUBKEY;
-    return;
+  line_chain<false>(hm_load(hm[i].h), hm[i].lines, 1);
+}
+
+// Verify stage 1a: one lane per partial, decompress + subgroup-check the public key
+// (herumi.go:290 PublicKey.Deserialize).  A rejected key is replaced by g1 so later stages run
+// the same arithmetic on well-formed values; its status byte decides the verdict.
+__global__ KERNEL_BOUNDS void k_dec_pk(const uint8_t* __restrict__ pks, uint32_t n, G1AEntry* __restrict__ out,
+                                       uint8_t* __restrict__ st) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  G1A p;
+  uint8_t bad = g1_decompress(p, pks + 48ull * i);
+  if (bad) p = g1_generator();
+  G1AEntry e;
+  e.x = p.x;
+  e.y = p.y;
+  e.inf = p.inf ? 1u : 0u;
+  e.pad[0] = e.pad[1] = e.pad[2] = 0;
+  out[i] = e;
+  st[i] = bad;
+}
+
+// Verify stage 1b: one lane per partial, decompress + subgroup-check the signature
+// (herumi.go:295 Sign.Deserialize), then its Miller chain evaluated at -g1.
+__global__ KERNEL_BOUNDS void k_dec_sig_lines(const uint8_t* __restrict__ sigs, uint32_t n, uint8_t* __restrict__ inf,
+                                              uint8_t* __restrict__ st, LineEntry* __restrict__ lines) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  G2A q;
+  uint8_t bad = g2_decompress(q, sigs + 96ull * i);
+  st[i] = bad;
+  inf[i] = (!bad && q.inf) ? 1 : 0;
+  // rejected / infinity signatures: the chain runs on whatever was decoded (integer arithmetic
+  // cannot fault) and the status bytes decide the verdict
+  line_chain<true>(q, lines + i, n);
+}
+
+// Verify stage 2: THREE lanes per partial (pair3.h): Miller loop over the streamed lines of
+// (pk, H(m)) and (-g1, sig), final exponentiation, verdict (herumi.go:299 VerifyByte).
+constexpr int GROUPS_PER_WAVE = 21;
+__global__ KERNEL_BOUNDS void k_pair3(const G1AEntry* __restrict__ pk, const uint8_t* __restrict__ pk_st,
+                                      const uint8_t* __restrict__ sig_inf, const uint8_t* __restrict__ sig_st,
+                                      const uint32_t* __restrict__ msg_idx, const MsgEntry* __restrict__ hm,
+                                      const LineEntry* __restrict__ sig_lines, uint32_t n, uint8_t* __restrict__ status) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  Grp g = grp_make();
+  const int grp = (int)(threadIdx.x & 63u) / 3;
+  const uint32_t item = blockIdx.x * GROUPS_PER_WAVE + (uint32_t)grp;
+  const bool valid = grp < GROUPS_PER_WAVE && item < n;
+  const uint32_t it = valid ? item : n - 1;  // idle lanes shadow a real item (no divergence)
+  const G1AEntry P = pk[it];
+  const uint32_t m = msg_idx[it];
+  const LineEntry* ml = hm[m].lines;
+  const LineEntry* sl = sig_lines + it;
+  // Lines in loop order: for each bit i = 62..0 of |x| a doubling line (preceded by f^2 except
+  // at the top) and, if bit i is set, an addition line.  One copy of the line products.
+  Fp4 f = g_one(g);
+  int bit = 62;
+  bool pending_add = false;
+  HB_NOUNROLL for (int j = 0; j < N_LINES; j++) {
+    const bool dbl = !pending_add;
+    if (dbl && j > 0) f = g_sqr(g, f);
+    LineEntry L = ml[j];
+    f = g_mul_line(g, f, L.a0, f2_mul_fp(L.a1, P.x), f2_mul_fp(L.b1, P.y));
+    LineEntry S = sl[(size_t)j * n];
+    f = g_mul_line(g, f, S.a0, S.a1, S.b1);
+    if (dbl) {
+      pending_add = ((HB_X_ABS >> bit) & 1) != 0;
+      bit--;
+    } else {
+      pending_add = false;
+    }
   }
-  G2A sig;
-  if (g2_decompress(sig, sigs + 96ull * i)) {
-    status[i] = ST_BAD_SIGNATURE;
-    return;
+  f = g_final_exp(g, f);
+  const bool one = g_is_one(g, f);
+  if (valid && g.k == 0) {
+    uint8_t s;
+    if (pk_st[item]) s = ST_BAD_PUBKEY;
+    else if (sig_st[item]) s = ST_BAD_SIGNATURE;
+    else if (P.inf || sig_inf[item] || hm[m].h.inf) s = ST_NOT_VERIFIED;  // verify_core (ops.h)
+    else s = one ? ST_OK : ST_NOT_VERIFIED;
+    status[item] = s;
   }
-  G2A h = hm_load(hm[msg_idx[i]]);
-  status[i] = verify_core(pk, h, sig) ? ST_OK : ST_NOT_VERIFIED;
+#endif
 }
 
 __device__ __forceinline__ uint32_t find_group(const uint32_t* grp_off, uint32_t n_groups, uint32_t j) {
@@ -187,7 +294,7 @@ __global__ KERNEL_BOUNDS void k_g1_member(const uint8_t* __restrict__ pks, uint3
 // VerifyAggregate stage 2: one lane per group (FastAggregateVerify, herumi.go:318-342).
 __global__ KERNEL_BOUNDS void k_verify_aggregate(const uint32_t* __restrict__ grp_off, uint32_t n_groups,
                                                  const G1AEntry* __restrict__ pts, const uint8_t* __restrict__ mstat,
-                                                 const uint8_t* __restrict__ sigs, const HmEntry* __restrict__ hm,
+                                                 const uint8_t* __restrict__ sigs, const MsgEntry* __restrict__ hm,
                                                  uint8_t* __restrict__ status) {
   uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= n_groups) return;
@@ -211,12 +318,12 @@ __global__ KERNEL_BOUNDS void k_verify_aggregate(const uint32_t* __restrict__ gr
     return;
   }
   G1A agg = jac_to_aff(acc);
-  status[g] = verify_core(agg, hm_load(hm[g]), sig) ? ST_OK : ST_NOT_VERIFIED;
+  status[g] = verify_core(agg, hm_load(hm[g].h), sig) ? ST_OK : ST_NOT_VERIFIED;
 }
 
 // Sign: one lane per (sk, message): sigma = sk * H(m)   (herumi.go:306-316)
 __global__ KERNEL_BOUNDS void k_sign(const uint8_t* __restrict__ sks, const uint32_t* __restrict__ msg_idx,
-                                     const HmEntry* __restrict__ hm, uint32_t n, uint8_t* __restrict__ sigs,
+                                     const MsgEntry* __restrict__ hm, uint32_t n, uint8_t* __restrict__ sigs,
                                      uint8_t* __restrict__ status) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -229,7 +336,7 @@ __global__ KERNEL_BOUNDS void k_sign(const uint8_t* __restrict__ sks, const uint
     for (int k = 0; k < 96; k++) sigs[96ull * i + k] = 0;
     return;
   }
-  G2J sg = jac_mul_aff(hm_load(hm[msg_idx[i]]), s.v, 255);
+  G2J sg = jac_mul_aff(hm_load(hm[msg_idx[i]].h), s.v, 255);
   g2_compress(buf, jac_to_aff(sg));
   for (int k = 0; k < 96; k++) sigs[96ull * i + k] = buf[k];
   status[i] = ST_OK;
@@ -320,6 +427,8 @@ thread_local std::string g_err;
 std::mutex g_mu;  // serialises host-buffer calls (shared workspace)
 int g_device = -1;
 hipStream_t g_stream = nullptr;
+hipStream_t g_side[2] = {nullptr, nullptr};  // fork/join streams of the staged verify
+hipEvent_t g_ev_fork = nullptr, g_ev_side[2] = {nullptr, nullptr};
 
 struct DevBuf {
   void* p = nullptr;
@@ -328,6 +437,7 @@ struct DevBuf {
 
 enum BufId {
   B_PK, B_SIG, B_MSG, B_OFF, B_LEN, B_MIDX, B_HM, B_STAT, B_IDX, B_GOFF, B_PTS, B_MSTAT, B_OUT, B_SK, B_G1PTS,
+  B_VPK, B_VPKST, B_VSIGINF, B_VSIGST, B_VLINES,  // staged verify: per-partial intermediates
   B_COUNT
 };
 DevBuf g_bufs[B_COUNT];
@@ -376,6 +486,11 @@ int init_locked(int device) {
     return -1;
   }
   HCHK(hipStreamCreateWithFlags(&g_stream, hipStreamNonBlocking));
+  for (int k = 0; k < 2; k++) {
+    HCHK(hipStreamCreateWithFlags(&g_side[k], hipStreamNonBlocking));
+    HCHK(hipEventCreateWithFlags(&g_ev_side[k], hipEventDisableTiming));
+  }
+  HCHK(hipEventCreateWithFlags(&g_ev_fork, hipEventDisableTiming));
   g_device = device;
   return 0;
 }
@@ -427,7 +542,8 @@ void dedup_messages(const uint8_t* msgs, const uint64_t* off, const uint32_t* le
   }
 }
 
-int hash_table_locked(const MsgTable& t, HmEntry** hm_out) {
+// hash every distinct message to G2 (+ its Miller line chain when `lines`) into MsgEntry[].
+int hash_table_locked(const MsgTable& t, MsgEntry** hm_out, bool lines) {
   uint8_t* dmsg;
   uint64_t* doff;
   uint32_t* dlen;
@@ -435,9 +551,42 @@ int hash_table_locked(const MsgTable& t, HmEntry** hm_out) {
   if (upload(B_MSG, t.bytes.data(), t.bytes.size(), &dmsg)) return -1;
   if (upload(B_OFF, t.off.data(), t.off.size(), &doff)) return -1;
   if (upload(B_LEN, t.len.data(), t.len.size(), &dlen)) return -1;
-  if (ensure(B_HM, t.len.size() * sizeof(HmEntry), &hm)) return -1;
-  LAUNCH(k_hash_to_g2, t.len.size(), g_stream, dmsg, doff, dlen, (uint32_t)t.len.size(), (HmEntry*)hm);
-  *hm_out = (HmEntry*)hm;
+  if (ensure(B_HM, t.len.size() * sizeof(MsgEntry), &hm)) return -1;
+  LAUNCH(k_hash_to_g2, t.len.size(), g_stream, dmsg, doff, dlen, (uint32_t)t.len.size(), (MsgEntry*)hm);
+  if (lines) LAUNCH(k_lines_msg, t.len.size(), g_stream, (MsgEntry*)hm, (uint32_t)t.len.size());
+  *hm_out = (MsgEntry*)hm;
+  return 0;
+}
+
+// Staged verify of n partials already in device memory (herumi.go:288-304 per item):
+//   side stream 0: k_dec_pk          (1 lane / partial)
+//   side stream 1: k_dec_sig_lines   (1 lane / partial: decompress sig + its 68 lines at -g1)
+//   stream s:      k_pair3           (3 lanes / partial: Miller loop + final exponentiation)
+// in chunks of at most VERIFY_CHUNK partials (the line buffer is 19.6 KB per partial).
+constexpr size_t VERIFY_CHUNK = 1u << 17;
+int verify_pipeline_locked(const uint8_t* dpk, const uint8_t* dsig, const uint32_t* didx, const MsgEntry* hm,
+                           size_t n, uint8_t* dst, hipStream_t s) {
+  size_t cap = n < VERIFY_CHUNK ? n : VERIFY_CHUNK;
+  void *vpk, *vpkst, *vsinf, *vsst, *vlines;
+  if (ensure(B_VPK, cap * sizeof(G1AEntry), &vpk) || ensure(B_VPKST, cap, &vpkst) || ensure(B_VSIGINF, cap, &vsinf) ||
+      ensure(B_VSIGST, cap, &vsst) || ensure(B_VLINES, cap * N_LINES * sizeof(LineEntry), &vlines))
+    return -1;
+  for (size_t c0 = 0; c0 < n; c0 += cap) {
+    uint32_t cn = (uint32_t)((n - c0) < cap ? (n - c0) : cap);
+    HCHK(hipEventRecord(g_ev_fork, s));
+    for (int k = 0; k < 2; k++) HCHK(hipStreamWaitEvent(g_side[k], g_ev_fork, 0));
+    LAUNCH(k_dec_pk, cn, g_side[0], dpk + 48 * c0, cn, (G1AEntry*)vpk, (uint8_t*)vpkst);
+    LAUNCH(k_dec_sig_lines, cn, g_side[1], dsig + 96 * c0, cn, (uint8_t*)vsinf, (uint8_t*)vsst, (LineEntry*)vlines);
+    for (int k = 0; k < 2; k++) {
+      HCHK(hipEventRecord(g_ev_side[k], g_side[k]));
+      HCHK(hipStreamWaitEvent(s, g_ev_side[k], 0));
+    }
+    unsigned grid = (unsigned)((cn + GROUPS_PER_WAVE - 1) / GROUPS_PER_WAVE);
+    hipLaunchKernelGGL(k_pair3, dim3(grid), dim3(64), 0, s, (const G1AEntry*)vpk, (const uint8_t*)vpkst,
+                       (const uint8_t*)vsinf, (const uint8_t*)vsst, didx + c0, hm, (const LineEntry*)vlines, cn,
+                       dst + c0);
+    HCHK(hipGetLastError());
+  }
   return 0;
 }
 
@@ -460,7 +609,7 @@ int hbls_available(void) {
   return init_locked(-1) == 0 ? 1 : 0;
 }
 
-size_t hbls_hm_entry_bytes(void) { return sizeof(HmEntry); }
+size_t hbls_hm_entry_bytes(void) { return sizeof(MsgEntry); }
 
 int hbls_verify_batch(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msgs, const uint64_t* msg_off,
                       const uint32_t* msg_len, size_t n, uint8_t* status) {
@@ -469,8 +618,8 @@ int hbls_verify_batch(const uint8_t* pks, const uint8_t* sigs, const uint8_t* ms
   if (n == 0) return 0;
   MsgTable t;
   dedup_messages(msgs, msg_off, msg_len, n, t);
-  HmEntry* hm;
-  if (hash_table_locked(t, &hm)) return -1;
+  MsgEntry* hm;
+  if (hash_table_locked(t, &hm, true)) return -1;
   uint8_t *dpk, *dsig, *dst;
   uint32_t* didx;
   if (upload(B_PK, pks, n * 48, &dpk)) return -1;
@@ -479,7 +628,7 @@ int hbls_verify_batch(const uint8_t* pks, const uint8_t* sigs, const uint8_t* ms
   void* p;
   if (ensure(B_STAT, n, &p)) return -1;
   dst = (uint8_t*)p;
-  LAUNCH(k_verify, n, g_stream, dpk, dsig, didx, hm, (uint32_t)n, dst);
+  if (verify_pipeline_locked(dpk, dsig, didx, hm, n, dst, g_stream)) return -1;
   HCHK(hipMemcpyAsync(status, dst, n, hipMemcpyDeviceToHost, g_stream));
   HCHK(hipStreamSynchronize(g_stream));
   return 0;
@@ -548,8 +697,8 @@ int hbls_verify_aggregate_batch(const uint8_t* pks, const uint32_t* grp_off, con
     t.len.push_back(msg_len[g]);
     t.bytes.insert(t.bytes.end(), msgs + msg_off[g], msgs + msg_off[g] + msg_len[g]);
   }
-  HmEntry* hm;
-  if (hash_table_locked(t, &hm)) return -1;
+  MsgEntry* hm;
+  if (hash_table_locked(t, &hm, false)) return -1;
   uint8_t *dpk, *dsig;
   uint32_t* dgoff;
   if (upload(B_PK, pks, np * 48, &dpk)) return -1;
@@ -560,7 +709,7 @@ int hbls_verify_aggregate_batch(const uint8_t* pks, const uint32_t* grp_off, con
     return -1;
   LAUNCH(k_g1_member, np, g_stream, dpk, (uint32_t)np, (G1AEntry*)pts, (uint8_t*)mst);
   LAUNCH(k_verify_aggregate, n_groups, g_stream, dgoff, (uint32_t)n_groups, (const G1AEntry*)pts, (const uint8_t*)mst,
-         dsig, (const HmEntry*)hm, (uint8_t*)dst);
+         dsig, (const MsgEntry*)hm, (uint8_t*)dst);
   HCHK(hipMemcpyAsync(status, dst, n_groups, hipMemcpyDeviceToHost, g_stream));
   HCHK(hipStreamSynchronize(g_stream));
   return 0;
@@ -573,8 +722,8 @@ int hbls_sign_batch(const uint8_t* sks, const uint8_t* msgs, const uint64_t* msg
   if (n == 0) return 0;
   MsgTable t;
   dedup_messages(msgs, msg_off, msg_len, n, t);
-  HmEntry* hm;
-  if (hash_table_locked(t, &hm)) return -1;
+  MsgEntry* hm;
+  if (hash_table_locked(t, &hm, false)) return -1;
   uint8_t* dsk;
   uint32_t* didx;
   if (upload(B_SK, sks, n * 32, &dsk)) return -1;
@@ -647,15 +796,17 @@ int hbls_recover_secret(const uint8_t* shares, const int64_t* idx, size_t k, uin
 int hbls_hash_to_g2_device(const uint8_t* msgs, const uint64_t* msg_off, const uint32_t* msg_len, size_t n_msgs,
                            void* hm, void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  LAUNCH(k_hash_to_g2, n_msgs, s, msgs, msg_off, msg_len, (uint32_t)n_msgs, (HmEntry*)hm);
+  LAUNCH(k_hash_to_g2, n_msgs, s, msgs, msg_off, msg_len, (uint32_t)n_msgs, (MsgEntry*)hm);
+  LAUNCH(k_lines_msg, n_msgs, s, (MsgEntry*)hm, (uint32_t)n_msgs);
   return 0;
 }
 
 int hbls_verify_device(const uint8_t* pks, const uint8_t* sigs, const uint32_t* msg_idx, const void* hm, size_t n,
                        uint8_t* status, void* stream) {
-  hipStream_t s = (hipStream_t)stream;
-  LAUNCH(k_verify, n, s, pks, sigs, msg_idx, (const HmEntry*)hm, (uint32_t)n, status);
-  return 0;
+  std::lock_guard<std::mutex> lk(g_mu);  // the staged pipeline's workspaces are library-owned
+  if (init_locked(-1)) return -1;
+  if (n == 0) return 0;
+  return verify_pipeline_locked(pks, sigs, msg_idx, (const MsgEntry*)hm, n, status, (hipStream_t)stream);
 }
 
 int hbls_threshold_aggregate_device(const uint8_t* sigs, const int64_t* idx, const uint32_t* grp_off, size_t n_groups,

@@ -19,10 +19,56 @@ struct Fp12 {
 HD Fp2 f2_from_const(const uint32_t (*c)[12]) { return {fp_from_const(c[0]), fp_from_const(c[1])}; }
 HD Fp2 f2_zero() { return {fp_zero(), fp_zero()}; }
 HD Fp2 f2_one() { return {fp_one(), fp_zero()}; }
+#if defined(__HIP_DEVICE_COMPILE__)
+// Device: the two components' carry chains are interleaved (c0 and c1 sums, then their 2p
+// corrections one limb behind), so consecutive dependent carry ops are 4 instructions apart
+// and gfx950's carry-forwarding wait states need no s_nop.
+HD Fp2 f2_add(const Fp2& a, const Fp2& b) {
+  Fp s0, s1, d0, d1;
+  unsigned c0 = 0, c1 = 0, e0 = 0, e1 = 0;
+  s0.v[0] = __builtin_addc(a.c0.v[0], b.c0.v[0], c0, &c0);
+  s1.v[0] = __builtin_addc(a.c1.v[0], b.c1.v[0], c1, &c1);
+  HB_UNROLL for (int i = 1; i < NL; i++) {
+    s0.v[i] = __builtin_addc(a.c0.v[i], b.c0.v[i], c0, &c0);
+    s1.v[i] = __builtin_addc(a.c1.v[i], b.c1.v[i], c1, &c1);
+    d0.v[i - 1] = __builtin_subc(s0.v[i - 1], P2_RAW[i - 1], e0, &e0);
+    d1.v[i - 1] = __builtin_subc(s1.v[i - 1], P2_RAW[i - 1], e1, &e1);
+  }
+  d0.v[NL - 1] = __builtin_subc(s0.v[NL - 1], P2_RAW[NL - 1], e0, &e0);
+  d1.v[NL - 1] = __builtin_subc(s1.v[NL - 1], P2_RAW[NL - 1], e1, &e1);
+  Fp2 r;
+  HB_UNROLL for (int i = 0; i < NL; i++) {
+    r.c0.v[i] = e0 ? s0.v[i] : d0.v[i];  // s < 2p: keep s
+    r.c1.v[i] = e1 ? s1.v[i] : d1.v[i];
+  }
+  return r;
+}
+HD Fp2 f2_sub(const Fp2& a, const Fp2& b) {
+  Fp s0, s1, d0, d1;
+  unsigned c0 = 0, c1 = 0, e0 = 0, e1 = 0;
+  s0.v[0] = __builtin_subc(a.c0.v[0], b.c0.v[0], c0, &c0);
+  s1.v[0] = __builtin_subc(a.c1.v[0], b.c1.v[0], c1, &c1);
+  HB_UNROLL for (int i = 1; i < NL; i++) {
+    s0.v[i] = __builtin_subc(a.c0.v[i], b.c0.v[i], c0, &c0);
+    s1.v[i] = __builtin_subc(a.c1.v[i], b.c1.v[i], c1, &c1);
+    d0.v[i - 1] = __builtin_addc(s0.v[i - 1], P2_RAW[i - 1], e0, &e0);
+    d1.v[i - 1] = __builtin_addc(s1.v[i - 1], P2_RAW[i - 1], e1, &e1);
+  }
+  d0.v[NL - 1] = __builtin_addc(s0.v[NL - 1], P2_RAW[NL - 1], e0, &e0);
+  d1.v[NL - 1] = __builtin_addc(s1.v[NL - 1], P2_RAW[NL - 1], e1, &e1);
+  Fp2 r;
+  HB_UNROLL for (int i = 0; i < NL; i++) {
+    r.c0.v[i] = c0 ? d0.v[i] : s0.v[i];  // borrow: add 2p back
+    r.c1.v[i] = c1 ? d1.v[i] : s1.v[i];
+  }
+  return r;
+}
+#else
 HD Fp2 f2_add(const Fp2& a, const Fp2& b) { return {fp_add(a.c0, b.c0), fp_add(a.c1, b.c1)}; }
 HD Fp2 f2_sub(const Fp2& a, const Fp2& b) { return {fp_sub(a.c0, b.c0), fp_sub(a.c1, b.c1)}; }
-HD Fp2 f2_neg(const Fp2& a) { return {fp_neg(a.c0), fp_neg(a.c1)}; }
-HD Fp2 f2_dbl(const Fp2& a) { return {fp_dbl(a.c0), fp_dbl(a.c1)}; }
+#endif
+HD Fp2 f2_neg(const Fp2& a) { return f2_sub(f2_zero(), a); }
+HD Fp2 f2_dbl(const Fp2& a) { return f2_add(a, a); }
 HD Fp2 f2_conj(const Fp2& a) { return {a.c0, fp_neg(a.c1)}; }
 
 HD Fp2 f2_mul(const Fp2& a, const Fp2& b) {

@@ -13,6 +13,12 @@ PEAK_MAD_TOPS: v_mad_u64_u32 lane-ops/s on MI355X, measured by tools/microbench/
 MAC_PER_FPMUL = 2 * 12 * 12 + 12
 PEAK_MAD_TOPS = 29.944
 
+# Executed Fp products of the current kernels' arithmetic (algorithmic savings since r01, e.g.
+# cyclotomic squaring in the final exponentiation); tests/test_opcount.py re-counts these too.
+EXECUTED_FPMUL_PER_ITEM = {
+    "k_verify": 23913,
+}
+
 FPMUL_PER_ITEM = {
     # per partial: G1 decompress+subgroup 1665, G2 decompress+subgroup 2486, 2-pair Miller loop +
     # final exponentiation 25450

@@ -19,7 +19,9 @@ def test_verify_counts(hc, fixtures):
     out = (ctypes.c_ulonglong * 5)()
     m = bytes.fromhex(c["msg"])
     assert hc.hc_count_verify(bytes.fromhex(c["pk"]), m, len(m), bytes.fromhex(c["sig"]), out) == 0
-    assert out[0] == opcounts.FPMUL_PER_ITEM["k_verify"]
+    # the frozen r01 count is the roofline's work unit; the executed count may only go down
+    assert out[0] == opcounts.EXECUTED_FPMUL_PER_ITEM["k_verify"]
+    assert out[0] <= opcounts.FPMUL_PER_ITEM["k_verify"]
     assert out[1] == opcounts.FPMUL_PER_ITEM["k_hash_to_g2"]
 
 
