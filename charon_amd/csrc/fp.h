@@ -189,13 +189,14 @@ __device__ __forceinline__ void fips_mac4(uint64_t& acc, uint32_t& c2, uint32_t 
       : "vcc");
 }
 
-// The product itself is the hand-scheduled subroutine hb_fpmul (fpmul_asm.inc, generated by
-// charon_amd/tools/gen_fpmul_asm.py: the same FIPS schedule as above), entered with a fixed
+#if defined(HB_FAST_FPMUL)
+// pipeline.hip: the product is the hand-scheduled subroutine hb_fpmul (fpmul_asm.inc,
+// generated by charon_amd/tools/gen_fpmul_asm.py: the same FIPS schedule), entered with a fixed
 // register convention: a in v0-v11, b in v12-v23, result in v24-v35, clobbering only v36-v50,
 // vcc and s30-s48.  The standard calling convention would force every value a caller keeps
 // across the call into the 112 callee-saved VGPRs; with this one the caller's state lives in
-// v51-v255 and nothing spills.  The subroutine is emitted once per code object, inside the
-// never-launched kernel hb_fpmul_holder (HB_DEFINE_FPMUL_SUBROUTINE).
+// v51-v255.  The subroutine is emitted once per code object, inside the never-launched kernel
+// hb_fpmul_holder (HB_DEFINE_FPMUL_SUBROUTINE).
 #include "fpmul_asm.inc"
 
 HD Fp fp_mul(const Fp& a, const Fp& b) {
@@ -218,6 +219,48 @@ HD Fp fp_mul(const Fp& a, const Fp& b) {
                  "\t.hidden hb_fpmul\n\t.type hb_fpmul,@function\n" \
                  "hb_fpmul:\n" HB_FPMUL_ASM_BODY);                     \
   }
+#else
+// hipbls.hip: one out-of-line copy of the product (standard calling convention); operands travel
+// in VGPRs as 12-wide vectors (struct arguments would be passed through scratch memory).
+typedef uint32_t u32x12 __attribute__((ext_vector_type(12)));
+__device__ __noinline__ static u32x12 fp_mul_leaf(u32x12 a, u32x12 b) {
+  uint32_t m[NL];
+  u32x12 t;
+  uint64_t acc = 0;
+  uint32_t c2 = 0;
+  HB_UNROLL for (int k = 0; k < 2 * NL - 1; k++) {
+    const int lo = k < NL ? 0 : k - (NL - 1);
+    const int hi = k < NL ? k - 1 : NL - 1;  // pairs j in [lo, hi]
+    int j = lo;
+    HB_UNROLL for (; j + 1 <= hi; j += 2)
+      fips_mac4(acc, c2, a[j], b[k - j], m[j], P_RAW[k - j], a[j + 1], b[k - j - 1], m[j + 1], P_RAW[k - j - 1]);
+    if (j <= hi) fips_mac2(acc, c2, a[j], b[k - j], m[j], P_RAW[k - j]);
+    if (k < NL) {
+      fips_mac(acc, c2, a[k], b[0]);
+      m[k] = (uint32_t)acc * HB_P_N0;
+      fips_mac_s(acc, c2, m[k], P_RAW[0]);  // low word becomes 0
+    } else {
+      t[k - NL] = (uint32_t)acc;
+    }
+    acc = (acc >> 32) | ((uint64_t)c2 << 32);
+    c2 = 0;
+  }
+  t[NL - 1] = (uint32_t)acc;
+  return t;
+}
+HD Fp fp_mul(const Fp& a, const Fp& b) {
+  HB_COUNT_FP_MUL();
+  u32x12 av, bv;
+  HB_UNROLL for (int i = 0; i < NL; i++) {
+    av[i] = a.v[i];
+    bv[i] = b.v[i];
+  }
+  u32x12 rv = fp_mul_leaf(av, bv);
+  Fp r;
+  HB_UNROLL for (int i = 0; i < NL; i++) r.v[i] = rv[i];
+  return r;
+}
+#endif
 #else
 HD Fp fp_mul(const Fp& a, const Fp& b) { return fp_mul_generic(a, b); }
 #endif

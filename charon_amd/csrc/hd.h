@@ -13,7 +13,12 @@
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
 #define HD static __host__ __device__ __forceinline__
+#if defined(HB_FAST_FPMUL)
+// pipeline.hip: everything but the Fp product subroutine is inlined (no ABI calls)
+#define HDNI static __host__ __device__ __forceinline__
+#else
 #define HDNI static __host__ __device__ __noinline__
+#endif
 #define HB_CONST static constexpr __device__
 #define HB_DEVICE_CODE 1
 #else

@@ -4,8 +4,7 @@
 // implemented by tbls.Herumi (/root/reference/tbls/herumi.go).  One lane = one item
 // (partial signature, group or message); kernels are staged so that work shared between
 // items (hash_to_curve of a message) runs once.
-#include "ops.h"
-#include "pair3.h"
+#include "layout.h"
 #include "../../include/hipbls.h"
 
 #include <mutex>
@@ -16,43 +15,6 @@
 
 using namespace hb;
 
-#if defined(__HIP_DEVICE_COMPILE__)
-HB_DEFINE_FPMUL_SUBROUTINE
-#else
-__global__ void hb_fpmul_holder() {}
-#endif
-
-// ---------------------------------------------------------------------------------------
-// Device-side storage formats
-// ---------------------------------------------------------------------------------------
-struct HmEntry {  // affine G2 point (Montgomery limbs) + infinity flag, 208 B
-  Fp2 x, y;
-  uint32_t inf;
-  uint32_t pad[3];
-};
-
-struct G2JEntry {  // Jacobian G2 point, 288 B
-  Fp2 X, Y, Z;
-};
-
-struct G1AEntry {  // affine G1 point, 112 B
-  Fp x, y;
-  uint32_t inf;
-  uint32_t pad[3];
-};
-
-struct LineEntry {  // one Miller-loop line, 288 B: (a0, c1, c2) unevaluated or (a0, a1, b1)
-  Fp2 a0, a1, b1;
-};
-
-// Per distinct message: H(m) and the 68 unevaluated lines of its Miller chain (pairing.h
-// miller_dbl_c / miller_add_c), shared by every partial signed over that message.
-struct MsgEntry {
-  HmEntry h;
-  LineEntry lines[N_LINES];
-};
-
-__device__ __forceinline__ G2A hm_load(const HmEntry& e) { return {e.x, e.y, e.inf != 0}; }
 
 #define KERNEL_BOUNDS __launch_bounds__(64)
 constexpr int BLOCK = 64;
@@ -75,116 +37,6 @@ __global__ KERNEL_BOUNDS void k_hash_to_g2(const uint8_t* __restrict__ msgs, con
   hm[i].h = e;
 }
 
-// The Miller chain of an affine G2 point Q: 68 lines, stored at out[j * stride].  EVAL: evaluate
-// each line at -g1 (pair (-g1, sig) of the verification equation); otherwise store (a0, c1, c2).
-template <bool EVAL>
-__device__ __forceinline__ void line_chain(const G2A& Q, LineEntry* __restrict__ out, size_t stride) {
-  G2Proj T = {Q.x, Q.y, f2_one()};
-  int j = 0;
-  HB_NOUNROLL for (int i = 62; i >= 0; i--) {
-    LineCoeffs l = miller_dbl_c(T);
-    if (EVAL) line_eval(l, fp_from_const(G1_GEN_X), fp_from_const(G1_GEN_NEG_Y));
-    out[(size_t)j * stride] = {l.a0, l.a1, l.b1};
-    j++;
-    if ((HB_X_ABS >> i) & 1) {
-      l = miller_add_c(T, Q.x, Q.y);
-      if (EVAL) line_eval(l, fp_from_const(G1_GEN_X), fp_from_const(G1_GEN_NEG_Y));
-      out[(size_t)j * stride] = {l.a0, l.a1, l.b1};
-      j++;
-    }
-  }
-}
-
-// One lane per distinct message: the unevaluated line chain of H(m).
-__global__ KERNEL_BOUNDS void k_lines_msg(MsgEntry* __restrict__ hm, uint32_t n) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  line_chain<false>(hm_load(hm[i].h), hm[i].lines, 1);
-}
-
-// Verify stage 1a: one lane per partial, decompress + subgroup-check the public key
-// (herumi.go:290 PublicKey.Deserialize).  A rejected key is replaced by g1 so later stages run
-// the same arithmetic on well-formed values; its status byte decides the verdict.
-__global__ KERNEL_BOUNDS void k_dec_pk(const uint8_t* __restrict__ pks, uint32_t n, G1AEntry* __restrict__ out,
-                                       uint8_t* __restrict__ st) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  G1A p;
-  uint8_t bad = g1_decompress(p, pks + 48ull * i);
-  if (bad) p = g1_generator();
-  G1AEntry e;
-  e.x = p.x;
-  e.y = p.y;
-  e.inf = p.inf ? 1u : 0u;
-  e.pad[0] = e.pad[1] = e.pad[2] = 0;
-  out[i] = e;
-  st[i] = bad;
-}
-
-// Verify stage 1b: one lane per partial, decompress + subgroup-check the signature
-// (herumi.go:295 Sign.Deserialize), then its Miller chain evaluated at -g1.
-__global__ KERNEL_BOUNDS void k_dec_sig_lines(const uint8_t* __restrict__ sigs, uint32_t n, uint8_t* __restrict__ inf,
-                                              uint8_t* __restrict__ st, LineEntry* __restrict__ lines) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  G2A q;
-  uint8_t bad = g2_decompress(q, sigs + 96ull * i);
-  st[i] = bad;
-  inf[i] = (!bad && q.inf) ? 1 : 0;
-  // rejected / infinity signatures: the chain runs on whatever was decoded (integer arithmetic
-  // cannot fault) and the status bytes decide the verdict
-  line_chain<true>(q, lines + i, n);
-}
-
-// Verify stage 2: THREE lanes per partial (pair3.h): Miller loop over the streamed lines of
-// (pk, H(m)) and (-g1, sig), final exponentiation, verdict (herumi.go:299 VerifyByte).
-constexpr int GROUPS_PER_WAVE = 21;
-__global__ KERNEL_BOUNDS void k_pair3(const G1AEntry* __restrict__ pk, const uint8_t* __restrict__ pk_st,
-                                      const uint8_t* __restrict__ sig_inf, const uint8_t* __restrict__ sig_st,
-                                      const uint32_t* __restrict__ msg_idx, const MsgEntry* __restrict__ hm,
-                                      const LineEntry* __restrict__ sig_lines, uint32_t n, uint8_t* __restrict__ status) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  Grp g = grp_make();
-  const int grp = (int)(threadIdx.x & 63u) / 3;
-  const uint32_t item = blockIdx.x * GROUPS_PER_WAVE + (uint32_t)grp;
-  const bool valid = grp < GROUPS_PER_WAVE && item < n;
-  const uint32_t it = valid ? item : n - 1;  // idle lanes shadow a real item (no divergence)
-  const G1AEntry P = pk[it];
-  const uint32_t m = msg_idx[it];
-  const LineEntry* ml = hm[m].lines;
-  const LineEntry* sl = sig_lines + it;
-  // Lines in loop order: for each bit i = 62..0 of |x| a doubling line (preceded by f^2 except
-  // at the top) and, if bit i is set, an addition line.  One copy of the line products.
-  Fp4 f = g_one(g);
-  int bit = 62;
-  bool pending_add = false;
-  HB_NOUNROLL for (int j = 0; j < N_LINES; j++) {
-    const bool dbl = !pending_add;
-    if (dbl && j > 0) f = g_sqr(g, f);
-    LineEntry L = ml[j];
-    f = g_mul_line(g, f, L.a0, f2_mul_fp(L.a1, P.x), f2_mul_fp(L.b1, P.y));
-    LineEntry S = sl[(size_t)j * n];
-    f = g_mul_line(g, f, S.a0, S.a1, S.b1);
-    if (dbl) {
-      pending_add = ((HB_X_ABS >> bit) & 1) != 0;
-      bit--;
-    } else {
-      pending_add = false;
-    }
-  }
-  f = g_final_exp(g, f);
-  const bool one = g_is_one(g, f);
-  if (valid && g.k == 0) {
-    uint8_t s;
-    if (pk_st[item]) s = ST_BAD_PUBKEY;
-    else if (sig_st[item]) s = ST_BAD_SIGNATURE;
-    else if (P.inf || sig_inf[item] || hm[m].h.inf) s = ST_NOT_VERIFIED;  // verify_core (ops.h)
-    else s = one ? ST_OK : ST_NOT_VERIFIED;
-    status[item] = s;
-  }
-#endif
-}
-
 __device__ __forceinline__ uint32_t find_group(const uint32_t* grp_off, uint32_t n_groups, uint32_t j) {
   // largest g with grp_off[g] <= j  (groups may be empty)
   uint32_t lo = 0, hi = n_groups;  // invariant: grp_off[lo] <= j < grp_off[hi]
@@ -194,47 +46,6 @@ __device__ __forceinline__ uint32_t find_group(const uint32_t* grp_off, uint32_t
     else hi = mid;
   }
   return lo;
-}
-
-// member status flags
-enum : uint8_t { M_OK = 0, M_BAD_SIG = 1, M_BAD_IDX = 2 };
-
-// One lane per partial: decompress sigma_j, lambda_j(0) over its group's indices,
-// point_j = lambda_j * sigma_j.  mode 0: ThresholdAggregate, mode 1: Aggregate (lambda = 1).
-__global__ KERNEL_BOUNDS void k_group_member(const uint8_t* __restrict__ sigs, const int64_t* __restrict__ idx,
-                                             const uint32_t* __restrict__ grp_off, uint32_t n_groups,
-                                             uint32_t n_partials, int mode, G2JEntry* __restrict__ pts,
-                                             uint8_t* __restrict__ mstat) {
-  uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= n_partials) return;
-  G2A s;
-  if (g2_decompress(s, sigs + 96ull * j)) {
-    mstat[j] = M_BAD_SIG;
-    return;
-  }
-  G2J p;
-  uint32_t g = find_group(grp_off, n_groups, j);
-  uint32_t b = grp_off[g], e = grp_off[g + 1];
-  if (mode == 1 || e - b == 1) {
-    p = jac_from_aff(s);  // Aggregate, or k = 1: the single partial is returned as is
-  } else {
-    Fr xi = fr_from_i64(idx[j]);
-    Fr num = fr_one(), den = fr_one();
-    for (uint32_t m = b; m < e; m++) {
-      if (m == j) continue;
-      Fr xm = fr_from_i64(idx[m]);
-      num = fr_mul(num, xm);
-      den = fr_mul(den, fr_sub(xm, xi));
-    }
-    if (fr_is_zero(num) || fr_is_zero(den)) {  // an index is 0 mod r, or duplicated
-      mstat[j] = M_BAD_IDX;
-      return;
-    }
-    Fr lam = fr_from_mont(fr_mul(num, fr_inv(den)));
-    p = jac_mul_aff(s, lam.v, 255);
-  }
-  mstat[j] = M_OK;
-  pts[j] = {p.X, p.Y, p.Z};
 }
 
 // One lane per group: sum the member points, compress (herumi Sign.Recover / Sign.Aggregate +
@@ -438,6 +249,7 @@ struct DevBuf {
 enum BufId {
   B_PK, B_SIG, B_MSG, B_OFF, B_LEN, B_MIDX, B_HM, B_STAT, B_IDX, B_GOFF, B_PTS, B_MSTAT, B_OUT, B_SK, B_G1PTS,
   B_VPK, B_VPKST, B_VSIGINF, B_VSIGST, B_VLINES,  // staged verify: per-partial intermediates
+  B_TAPTS, B_TADIG,                               // staged ThresholdAggregate
   B_COUNT
 };
 DevBuf g_bufs[B_COUNT];
@@ -553,7 +365,7 @@ int hash_table_locked(const MsgTable& t, MsgEntry** hm_out, bool lines) {
   if (upload(B_LEN, t.len.data(), t.len.size(), &dlen)) return -1;
   if (ensure(B_HM, t.len.size() * sizeof(MsgEntry), &hm)) return -1;
   LAUNCH(k_hash_to_g2, t.len.size(), g_stream, dmsg, doff, dlen, (uint32_t)t.len.size(), (MsgEntry*)hm);
-  if (lines) LAUNCH(k_lines_msg, t.len.size(), g_stream, (MsgEntry*)hm, (uint32_t)t.len.size());
+  if (lines) launch_lines_msg((MsgEntry*)hm, (uint32_t)t.len.size(), g_stream);
   *hm_out = (MsgEntry*)hm;
   return 0;
 }
@@ -575,18 +387,32 @@ int verify_pipeline_locked(const uint8_t* dpk, const uint8_t* dsig, const uint32
     uint32_t cn = (uint32_t)((n - c0) < cap ? (n - c0) : cap);
     HCHK(hipEventRecord(g_ev_fork, s));
     for (int k = 0; k < 2; k++) HCHK(hipStreamWaitEvent(g_side[k], g_ev_fork, 0));
-    LAUNCH(k_dec_pk, cn, g_side[0], dpk + 48 * c0, cn, (G1AEntry*)vpk, (uint8_t*)vpkst);
-    LAUNCH(k_dec_sig_lines, cn, g_side[1], dsig + 96 * c0, cn, (uint8_t*)vsinf, (uint8_t*)vsst, (LineEntry*)vlines);
+    launch_dec_pk(dpk + 48 * c0, cn, (G1AEntry*)vpk, (uint8_t*)vpkst, g_side[0]);
+    HCHK(hipGetLastError());
+    launch_dec_sig_lines(dsig + 96 * c0, cn, (uint8_t*)vsinf, (uint8_t*)vsst, (LineEntry*)vlines, g_side[1]);
+    HCHK(hipGetLastError());
     for (int k = 0; k < 2; k++) {
       HCHK(hipEventRecord(g_ev_side[k], g_side[k]));
       HCHK(hipStreamWaitEvent(s, g_ev_side[k], 0));
     }
-    unsigned grid = (unsigned)((cn + GROUPS_PER_WAVE - 1) / GROUPS_PER_WAVE);
-    hipLaunchKernelGGL(k_pair3, dim3(grid), dim3(64), 0, s, (const G1AEntry*)vpk, (const uint8_t*)vpkst,
-                       (const uint8_t*)vsinf, (const uint8_t*)vsst, didx + c0, hm, (const LineEntry*)vlines, cn,
-                       dst + c0);
+    launch_pair3((const G1AEntry*)vpk, (const uint8_t*)vpkst, (const uint8_t*)vsinf, (const uint8_t*)vsst,
+                 didx + c0, hm, (const LineEntry*)vlines, cn, dst + c0, s);
     HCHK(hipGetLastError());
   }
+  return 0;
+}
+
+// ThresholdAggregate / Aggregate members (herumi.go:249-286, 225-247): decompress + lambda
+// digits (1 lane / partial), then lambda_j sigma_j with 4 lanes / partial (threshold.hip).
+int ta_members_locked(const uint8_t* dsig, const int64_t* didx, const uint32_t* dgoff, size_t n_groups, size_t np,
+                      int mode, G2JEntry* pts, uint8_t* mst, hipStream_t s) {
+  if (np == 0) return 0;
+  void *apts, *dig;
+  if (ensure(B_TAPTS, np * sizeof(HmEntry), &apts) || ensure(B_TADIG, np * sizeof(TaDigits), &dig)) return -1;
+  launch_ta_dec(dsig, didx, dgoff, (uint32_t)n_groups, (uint32_t)np, mode, (HmEntry*)apts, (TaDigits*)dig, mst, s);
+  HCHK(hipGetLastError());
+  launch_ta_mul4((const HmEntry*)apts, (const TaDigits*)dig, (uint32_t)np, pts, s);
+  HCHK(hipGetLastError());
   return 0;
 }
 
@@ -656,8 +482,7 @@ static int group_op_locked(const uint8_t* sigs, const int64_t* idx, const uint32
   if (ensure(B_PTS, np * sizeof(G2JEntry), &pts) || ensure(B_MSTAT, np, &mst) || ensure(B_OUT, n_groups * 96, &dout) ||
       ensure(B_STAT, n_groups, &dst))
     return -1;
-  LAUNCH(k_group_member, np, g_stream, dsig, didx, dgoff, (uint32_t)n_groups, (uint32_t)np, mode, (G2JEntry*)pts,
-         (uint8_t*)mst);
+  if (ta_members_locked(dsig, didx, dgoff, n_groups, np, mode, (G2JEntry*)pts, (uint8_t*)mst, g_stream)) return -1;
   LAUNCH(k_group_sum, n_groups, g_stream, dgoff, (uint32_t)n_groups, mode, (const G2JEntry*)pts, (const uint8_t*)mst,
          (uint8_t*)dout, (uint8_t*)dst);
   HCHK(hipMemcpyAsync(out, dout, n_groups * 96, hipMemcpyDeviceToHost, g_stream));
@@ -797,7 +622,8 @@ int hbls_hash_to_g2_device(const uint8_t* msgs, const uint64_t* msg_off, const u
                            void* hm, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   LAUNCH(k_hash_to_g2, n_msgs, s, msgs, msg_off, msg_len, (uint32_t)n_msgs, (MsgEntry*)hm);
-  LAUNCH(k_lines_msg, n_msgs, s, (MsgEntry*)hm, (uint32_t)n_msgs);
+  launch_lines_msg((MsgEntry*)hm, (uint32_t)n_msgs, s);
+  HCHK(hipGetLastError());
   return 0;
 }
 
@@ -817,8 +643,7 @@ int hbls_threshold_aggregate_device(const uint8_t* sigs, const int64_t* idx, con
   hipStream_t s = (hipStream_t)stream;
   void *pts, *mst;
   if (ensure(B_PTS, n_partials * sizeof(G2JEntry), &pts) || ensure(B_MSTAT, n_partials, &mst)) return -1;
-  LAUNCH(k_group_member, n_partials, s, sigs, idx, grp_off, (uint32_t)n_groups, (uint32_t)n_partials, 0,
-         (G2JEntry*)pts, (uint8_t*)mst);
+  if (ta_members_locked(sigs, idx, grp_off, n_groups, n_partials, 0, (G2JEntry*)pts, (uint8_t*)mst, s)) return -1;
   LAUNCH(k_group_sum, n_groups, s, grp_off, (uint32_t)n_groups, 0, (const G2JEntry*)pts, (const uint8_t*)mst, out,
          status);
   return 0;
