@@ -39,6 +39,8 @@ if ROOT not in sys.path:
 
 from charon_amd.opcounts import FPMUL_PER_ITEM, MAC_PER_FPMUL, PEAK_MAD_TOPS  # noqa: E402
 
+N_LINES = 68  # Miller-loop lines per pairing (pairing.h)
+
 METRIC = "verified partial sigs/sec + ThresholdAggregate/sec per node, 1-8 MI355X"
 
 WORKLOADS = {
@@ -152,6 +154,8 @@ def main(argv=None):
     ap.add_argument("--validators", type=int, default=0, help="override validators per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample (0: skip)")
     ap.add_argument("--host-api", action="store_true", help="also time the host-buffer (PCIe-inclusive) entry points")
+    ap.add_argument("--mode", default="slot", choices=["slot", "staged"],
+                    help="slot: one hbls_slot_device call per step (stages overlap); staged: stage by stage")
     args = ap.parse_args(argv)
 
     rank = int(os.environ.get("RANK", 0))
@@ -195,7 +199,23 @@ def main(argv=None):
     stream = torch.cuda.Stream(device=dev)
     sp = ctypes.c_void_p(stream.cuda_stream)
 
-    def step(ev):
+    def step_slot(ev):
+        # the slot entry point: hashing, verification and threshold aggregation overlap on the
+        # library's side streams; ordered on `stream`
+        ev[0].record(stream)
+        _chk(L, L.hbls_slot_device(_p(d_msg), _p(d_moff), _p(d_mlen), M, _p(d_hm), _p(d_pk), _p(d_sig), _p(d_midx),
+                                   NP, _p(d_vst), _p(d_tsig), _p(d_tidx), _p(d_goff), V, V * t, _p(d_tout),
+                                   _p(d_tst), sp))
+        ev[1].record(stream)
+        if world > 1:  # SURVEY.md §8e: all-gather verdicts + compressed aggregates to every rank
+            with torch.cuda.stream(stream):
+                dist.all_gather_into_tensor(g_vst, d_vst)
+                dist.all_gather_into_tensor(g_tout, d_tout)
+                dist.all_gather_into_tensor(g_tst, d_tst)
+        ev[2].record(stream)
+
+    def step_staged(ev):
+        # the same work stage by stage (no overlap): per-stage event timings
         ev[0].record(stream)
         _chk(L, L.hbls_hash_to_g2_device(_p(d_msg), _p(d_moff), _p(d_mlen), M, _p(d_hm), sp))
         ev[1].record(stream)
@@ -204,15 +224,13 @@ def main(argv=None):
         _chk(L, L.hbls_threshold_aggregate_device(_p(d_tsig), _p(d_tidx), _p(d_goff), V, V * t, _p(d_tout),
                                                   _p(d_tst), sp))
         ev[3].record(stream)
-        if world > 1:  # SURVEY.md §8e: all-gather verdicts + compressed aggregates to every rank
-            with torch.cuda.stream(stream):
-                dist.all_gather_into_tensor(g_vst, d_vst)
-                dist.all_gather_into_tensor(g_tout, d_tout)
-                dist.all_gather_into_tensor(g_tst, d_tst)
-        ev[4].record(stream)
+
+    staged = args.mode == "staged"
+    step = step_staged if staged else step_slot
+    n_ev = 4 if staged else 3
 
     def mk():
-        return [torch.cuda.Event(enable_timing=True) for _ in range(5)]
+        return [torch.cuda.Event(enable_timing=True) for _ in range(n_ev)]
 
     for _ in range(args.warmup):
         step(mk())
@@ -220,6 +238,7 @@ def main(argv=None):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    _chk(L, L.hbls_timing(1))
     evs = [mk() for _ in range(args.steps)]
     t0 = time.perf_counter()
     for k in range(args.steps):
@@ -233,8 +252,14 @@ def main(argv=None):
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 
-    seg = np.array([[e[i].elapsed_time(e[i + 1]) for i in range(4)] for e in evs])  # ms
+    seg = np.array([[e[i].elapsed_time(e[i + 1]) for i in range(n_ev - 1)] for e in evs])  # ms
     k_ms = seg.mean(axis=0)
+    # k_pair3 (the dominant kernel) durations: HIP events the library records on its stream
+    pm = (ctypes.c_float * 4096)()
+    npm = ctypes.c_size_t(0)
+    _chk(L, L.hbls_timing_read(pm, 4096, ctypes.byref(npm)))
+    _chk(L, L.hbls_timing(0))
+    pair3_ms = float(np.sum(np.frombuffer(pm, dtype=np.float32, count=npm.value))) / args.steps
 
     # parity of the timed outputs: every partial verifies, every aggregate is byte-identical to the
     # root-key signature (tbls_test.go:72-97 property), every status OK
@@ -250,23 +275,27 @@ def main(argv=None):
     ms_per_step = elapsed / args.steps * 1e3
     value = items / (elapsed / args.steps)
 
-    fpmul_verify = FPMUL_PER_ITEM["k_verify"]
-    t_verify = k_ms[1] * 1e-3
-    verify_bytes = NP * (48 + 96 + 4 + 1)  # pk + sig + msg index in, status out (+ hm table, negligible)
+    fpmul_pair = FPMUL_PER_ITEM["k_pair3"]
+    t_pair = pair3_ms * 1e-3
+    pair_bytes = NP * (112 + 1 + 1 + 1 + 4 + 2 * N_LINES * 288 + 1)  # P, 3 status bytes, msg index, 2x68 lines, out
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc_path):
         with open(pmc_path) as f:
-            pm = json.load(f).get(args.workload, {}).get("k_verify")
-        if pm and pm.get("partials") == NP:
-            traffic = pm["hbm_bytes_per_launch"]
-    achieved = NP * fpmul_verify * MAC_PER_FPMUL / t_verify / 1e12 if fpmul_verify else None
-    roofline = {"bound": "valu", "kernel": "k_verify", "achieved": achieved and round(achieved, 3),
+            pmc = json.load(f).get(args.workload, {}).get("k_pair3")
+        if pmc and pmc.get("partials") == NP:
+            traffic = pmc["hbm_bytes_per_launch"]
+    achieved = NP * fpmul_pair * MAC_PER_FPMUL / t_pair / 1e12 if t_pair > 0 else None
+    roofline = {"bound": "valu", "kernel": "k_pair3", "achieved": achieved and round(achieved, 3),
                 "peak": PEAK_MAD_TOPS, "unit": "Tops/s (32-bit multiply-add lane-ops, v_mad_u64_u32)",
                 "frac": achieved and round(achieved / PEAK_MAD_TOPS, 4), "traffic": traffic,
-                "algorithmic_work": f"{fpmul_verify} Fp-mul x {MAC_PER_FPMUL} MAC per partial x {NP} partials",
-                "algorithmic_bytes_per_launch": verify_bytes,
-                "hbm_GBps_algorithmic": round(verify_bytes / t_verify / 1e9, 3)}
+                "kernel_ms": round(pair3_ms, 3),
+                "algorithmic_work": f"{fpmul_pair} Fp-mul x {MAC_PER_FPMUL} MAC per partial x {NP} partials "
+                                    f"(2-pair Miller loop + final exponentiation, frozen r01 count)",
+                "algorithmic_bytes_per_launch": pair_bytes,
+                "hbm_GBps_algorithmic": round(pair_bytes / t_pair / 1e9, 3) if t_pair > 0 else None}
+    # whole Verify (decompression + lines + pairing) per partial, frozen r01 count, over the step
+    verify_effective = world * NP * FPMUL_PER_ITEM["k_verify"] * MAC_PER_FPMUL / (elapsed / args.steps) / 1e12
 
     out = {
         "metric": METRIC, "value": round(value, 1),
@@ -280,8 +309,11 @@ def main(argv=None):
                    "distinct_messages": M, "partials_per_gpu": NP, "parallelism": f"validator-sharded x{world}"},
         "verify_per_s": round(world * NP / (elapsed / args.steps), 1),
         "threshold_aggregate_per_s": round(world * V / (elapsed / args.steps), 1),
-        "kernels_ms": {"hash_to_g2": round(k_ms[0], 3), "verify": round(k_ms[1], 3),
-                       "threshold_aggregate": round(k_ms[2], 3), "allgather": round(k_ms[3], 3)},
+        "mode": args.mode,
+        "stage_ms": ({"hash_to_g2": round(k_ms[0], 3), "verify": round(k_ms[1], 3),
+                      "threshold_aggregate": round(k_ms[2], 3)} if staged else
+                     {"slot": round(k_ms[0], 3), "allgather": round(k_ms[1], 3)}),
+        "verify_whole_effective_Tops": round(verify_effective, 3),
         "parity": parity, "roofline": roofline, "cpu_baseline": None,
     }
 

@@ -27,7 +27,8 @@ EXPORTS = (
     "hbls_init", "hbls_last_error", "hbls_available", "hbls_verify_batch", "hbls_threshold_aggregate_batch",
     "hbls_aggregate_batch", "hbls_verify_aggregate_batch", "hbls_sign_batch", "hbls_secret_to_public_key_batch",
     "hbls_threshold_split", "hbls_recover_secret", "hbls_hash_to_g2_device", "hbls_verify_device",
-    "hbls_threshold_aggregate_device", "hbls_hm_entry_bytes", "hbls_sync",
+    "hbls_threshold_aggregate_device", "hbls_slot_device", "hbls_hm_entry_bytes", "hbls_sync",
+    "hbls_timing", "hbls_timing_read",
 )
 
 
@@ -62,8 +63,11 @@ def _declare(lib):
         "hbls_hash_to_g2_device": ([P, P, P, SZ, P, P], ctypes.c_int),
         "hbls_verify_device": ([P, P, P, P, SZ, P, P], ctypes.c_int),
         "hbls_threshold_aggregate_device": ([P, P, P, SZ, SZ, P, P, P], ctypes.c_int),
+        "hbls_slot_device": ([P, P, P, SZ, P, P, P, P, SZ, P, P, P, P, SZ, SZ, P, P, P], ctypes.c_int),
         "hbls_hm_entry_bytes": ([], SZ),
         "hbls_sync": ([P], ctypes.c_int),
+        "hbls_timing": ([ctypes.c_int], ctypes.c_int),
+        "hbls_timing_read": ([P, SZ, P], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)

@@ -213,8 +213,8 @@ HD Fp fp_mul(const Fp& a, const Fp& b) {
   return r;
 }
 
-#define HB_DEFINE_FPMUL_SUBROUTINE                                   \
-  __global__ void hb_fpmul_holder() {                                \
+#define HB_DEFINE_FPMUL_SUBROUTINE(holder)                           \
+  __global__ void holder() {                                \
     asm volatile("\ts_endpgm\n\t.p2align 8\n\t.globl hb_fpmul\n"     \
                  "\t.hidden hb_fpmul\n\t.type hb_fpmul,@function\n" \
                  "hb_fpmul:\n" HB_FPMUL_ASM_BODY);                     \

@@ -23,20 +23,6 @@ constexpr int BLOCK = 64;
 // Kernels
 // ---------------------------------------------------------------------------------------
 
-// One lane per distinct message: hash_to_curve G2 (RFC 9380, DST ..._POP_), affine.
-__global__ KERNEL_BOUNDS void k_hash_to_g2(const uint8_t* __restrict__ msgs, const uint64_t* __restrict__ off,
-                                           const uint32_t* __restrict__ len, uint32_t n, MsgEntry* __restrict__ hm) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  G2A h = jac_to_aff(hash_to_g2(msgs + off[i], len[i]));
-  HmEntry e;
-  e.x = h.x;
-  e.y = h.y;
-  e.inf = h.inf ? 1u : 0u;
-  e.pad[0] = e.pad[1] = e.pad[2] = 0;
-  hm[i].h = e;
-}
-
 __device__ __forceinline__ uint32_t find_group(const uint32_t* grp_off, uint32_t n_groups, uint32_t j) {
   // largest g with grp_off[g] <= j  (groups may be empty)
   uint32_t lo = 0, hi = n_groups;  // invariant: grp_off[lo] <= j < grp_off[hi]
@@ -46,6 +32,22 @@ __device__ __forceinline__ uint32_t find_group(const uint32_t* grp_off, uint32_t
     else hi = mid;
   }
   return lo;
+}
+
+// One lane per partial: decompress + subgroup-check sigma_j (herumi.go:257 Sign.Deserialize).
+__global__ KERNEL_BOUNDS void k_ta_dec(const uint8_t* __restrict__ sigs, uint32_t n_partials,
+                                               HmEntry* __restrict__ pts, uint8_t* __restrict__ mstat) {
+  uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n_partials) return;
+  G2A s;
+  uint8_t bad = g2_decompress(s, sigs + 96ull * j);
+  HmEntry e;
+  e.x = s.x;
+  e.y = s.y;
+  e.inf = (!bad && s.inf) ? 1u : 0u;
+  e.pad[0] = e.pad[1] = e.pad[2] = 0;
+  pts[j] = e;
+  mstat[j] = bad ? M_BAD_SIG : M_OK;
 }
 
 // One lane per group: sum the member points, compress (herumi Sign.Recover / Sign.Aggregate +
@@ -238,8 +240,17 @@ thread_local std::string g_err;
 std::mutex g_mu;  // serialises host-buffer calls (shared workspace)
 int g_device = -1;
 hipStream_t g_stream = nullptr;
-hipStream_t g_side[2] = {nullptr, nullptr};  // fork/join streams of the staged verify
-hipEvent_t g_ev_fork = nullptr, g_ev_side[2] = {nullptr, nullptr};
+// fork/join streams: 0, 1 = the staged verify's decompression kernels, 2 = message hashing,
+// 3 = ThresholdAggregate (hbls_slot_device)
+constexpr int N_SIDE = 4;
+hipStream_t g_side[N_SIDE] = {};
+hipEvent_t g_ev_fork = nullptr, g_ev_slot = nullptr, g_ev_side[N_SIDE] = {};
+
+// optional timing of the pairing kernel (hbls_timing): event pairs recorded on its stream
+bool g_timing = false;
+std::vector<std::pair<hipEvent_t, hipEvent_t>> g_tev;  // pool
+size_t g_tev_used = 0;
+int timing_pair(hipEvent_t* a, hipEvent_t* b);
 
 struct DevBuf {
   void* p = nullptr;
@@ -278,6 +289,19 @@ int ensure(BufId id, size_t bytes, void** out) {
   return 0;
 }
 
+int timing_pair(hipEvent_t* a, hipEvent_t* b) {
+  if (g_tev_used == g_tev.size()) {
+    hipEvent_t x, y;
+    HCHK(hipEventCreate(&x));
+    HCHK(hipEventCreate(&y));
+    g_tev.push_back({x, y});
+  }
+  *a = g_tev[g_tev_used].first;
+  *b = g_tev[g_tev_used].second;
+  g_tev_used++;
+  return 0;
+}
+
 int init_locked(int device) {
   if (g_device >= 0) {
     HCHK(hipSetDevice(g_device));
@@ -298,11 +322,12 @@ int init_locked(int device) {
     return -1;
   }
   HCHK(hipStreamCreateWithFlags(&g_stream, hipStreamNonBlocking));
-  for (int k = 0; k < 2; k++) {
+  for (int k = 0; k < N_SIDE; k++) {
     HCHK(hipStreamCreateWithFlags(&g_side[k], hipStreamNonBlocking));
     HCHK(hipEventCreateWithFlags(&g_ev_side[k], hipEventDisableTiming));
   }
   HCHK(hipEventCreateWithFlags(&g_ev_fork, hipEventDisableTiming));
+  HCHK(hipEventCreateWithFlags(&g_ev_slot, hipEventDisableTiming));
   g_device = device;
   return 0;
 }
@@ -364,7 +389,8 @@ int hash_table_locked(const MsgTable& t, MsgEntry** hm_out, bool lines) {
   if (upload(B_OFF, t.off.data(), t.off.size(), &doff)) return -1;
   if (upload(B_LEN, t.len.data(), t.len.size(), &dlen)) return -1;
   if (ensure(B_HM, t.len.size() * sizeof(MsgEntry), &hm)) return -1;
-  LAUNCH(k_hash_to_g2, t.len.size(), g_stream, dmsg, doff, dlen, (uint32_t)t.len.size(), (MsgEntry*)hm);
+  launch_hash_to_g2(dmsg, doff, dlen, (uint32_t)t.len.size(), (MsgEntry*)hm, g_stream);
+  HCHK(hipGetLastError());
   if (lines) launch_lines_msg((MsgEntry*)hm, (uint32_t)t.len.size(), g_stream);
   *hm_out = (MsgEntry*)hm;
   return 0;
@@ -376,8 +402,10 @@ int hash_table_locked(const MsgTable& t, MsgEntry** hm_out, bool lines) {
 //   stream s:      k_pair3           (3 lanes / partial: Miller loop + final exponentiation)
 // in chunks of at most VERIFY_CHUNK partials (the line buffer is 19.6 KB per partial).
 constexpr size_t VERIFY_CHUNK = 1u << 17;
+// hm_ready (optional): event after which `hm` is complete; only the pairing kernel waits for it,
+// so the decompression kernels overlap the hashing.
 int verify_pipeline_locked(const uint8_t* dpk, const uint8_t* dsig, const uint32_t* didx, const MsgEntry* hm,
-                           size_t n, uint8_t* dst, hipStream_t s) {
+                           size_t n, uint8_t* dst, hipStream_t s, hipEvent_t hm_ready = nullptr) {
   size_t cap = n < VERIFY_CHUNK ? n : VERIFY_CHUNK;
   void *vpk, *vpkst, *vsinf, *vsst, *vlines;
   if (ensure(B_VPK, cap * sizeof(G1AEntry), &vpk) || ensure(B_VPKST, cap, &vpkst) || ensure(B_VSIGINF, cap, &vsinf) ||
@@ -395,8 +423,15 @@ int verify_pipeline_locked(const uint8_t* dpk, const uint8_t* dsig, const uint32
       HCHK(hipEventRecord(g_ev_side[k], g_side[k]));
       HCHK(hipStreamWaitEvent(s, g_ev_side[k], 0));
     }
+    if (hm_ready) HCHK(hipStreamWaitEvent(s, hm_ready, 0));
+    hipEvent_t t0 = nullptr, t1 = nullptr;
+    if (g_timing) {
+      if (timing_pair(&t0, &t1)) return -1;
+      HCHK(hipEventRecord(t0, s));
+    }
     launch_pair3((const G1AEntry*)vpk, (const uint8_t*)vpkst, (const uint8_t*)vsinf, (const uint8_t*)vsst,
                  didx + c0, hm, (const LineEntry*)vlines, cn, dst + c0, s);
+    if (g_timing) HCHK(hipEventRecord(t1, s));
     HCHK(hipGetLastError());
   }
   return 0;
@@ -409,7 +444,8 @@ int ta_members_locked(const uint8_t* dsig, const int64_t* didx, const uint32_t* 
   if (np == 0) return 0;
   void *apts, *dig;
   if (ensure(B_TAPTS, np * sizeof(HmEntry), &apts) || ensure(B_TADIG, np * sizeof(TaDigits), &dig)) return -1;
-  launch_ta_dec(dsig, didx, dgoff, (uint32_t)n_groups, (uint32_t)np, mode, (HmEntry*)apts, (TaDigits*)dig, mst, s);
+  LAUNCH(k_ta_dec, np, s, dsig, (uint32_t)np, (HmEntry*)apts, mst);
+  launch_ta_lambda(didx, dgoff, (uint32_t)n_groups, (uint32_t)np, mode, (TaDigits*)dig, mst, s);
   HCHK(hipGetLastError());
   launch_ta_mul4((const HmEntry*)apts, (const TaDigits*)dig, (uint32_t)np, pts, s);
   HCHK(hipGetLastError());
@@ -621,7 +657,8 @@ int hbls_recover_secret(const uint8_t* shares, const int64_t* idx, size_t k, uin
 int hbls_hash_to_g2_device(const uint8_t* msgs, const uint64_t* msg_off, const uint32_t* msg_len, size_t n_msgs,
                            void* hm, void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  LAUNCH(k_hash_to_g2, n_msgs, s, msgs, msg_off, msg_len, (uint32_t)n_msgs, (MsgEntry*)hm);
+  launch_hash_to_g2(msgs, msg_off, msg_len, (uint32_t)n_msgs, (MsgEntry*)hm, s);
+  HCHK(hipGetLastError());
   launch_lines_msg((MsgEntry*)hm, (uint32_t)n_msgs, s);
   HCHK(hipGetLastError());
   return 0;
@@ -646,6 +683,120 @@ int hbls_threshold_aggregate_device(const uint8_t* sigs, const int64_t* idx, con
   if (ta_members_locked(sigs, idx, grp_off, n_groups, n_partials, 0, (G2JEntry*)pts, (uint8_t*)mst, s)) return -1;
   LAUNCH(k_group_sum, n_groups, s, grp_off, (uint32_t)n_groups, 0, (const G2JEntry*)pts, (const uint8_t*)mst, out,
          status);
+  return 0;
+}
+
+int hbls_slot_device(const uint8_t* msgs, const uint64_t* msg_off, const uint32_t* msg_len, size_t n_msgs, void* hm,
+                     const uint8_t* pks, const uint8_t* sigs, const uint32_t* msg_idx, size_t n, uint8_t* vstatus,
+                     const uint8_t* ta_sigs, const int64_t* ta_idx, const uint32_t* grp_off, size_t n_groups,
+                     size_t n_ta_partials, uint8_t* ta_out, uint8_t* ta_status, void* stream) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (init_locked(-1)) return -1;
+  hipStream_t s = (hipStream_t)stream;
+  HCHK(hipEventRecord(g_ev_slot, s));
+  // messages: hash + Miller lines (side 2)
+  hipStream_t sh = g_side[2];
+  HCHK(hipStreamWaitEvent(sh, g_ev_slot, 0));
+  launch_hash_to_g2(msgs, msg_off, msg_len, (uint32_t)n_msgs, (MsgEntry*)hm, sh);
+  HCHK(hipGetLastError());
+  launch_lines_msg((MsgEntry*)hm, (uint32_t)n_msgs, sh);
+  HCHK(hipGetLastError());
+  HCHK(hipEventRecord(g_ev_side[2], sh));
+  // ThresholdAggregate (side 3)
+  hipStream_t st = g_side[3];
+  HCHK(hipStreamWaitEvent(st, g_ev_slot, 0));
+  if (n_groups) {
+    void *pts, *mst;
+    if (ensure(B_PTS, n_ta_partials * sizeof(G2JEntry), &pts) || ensure(B_MSTAT, n_ta_partials, &mst)) return -1;
+    if (ta_members_locked(ta_sigs, ta_idx, grp_off, n_groups, n_ta_partials, 0, (G2JEntry*)pts, (uint8_t*)mst, st))
+      return -1;
+    LAUNCH(k_group_sum, n_groups, st, grp_off, (uint32_t)n_groups, 0, (const G2JEntry*)pts, (const uint8_t*)mst,
+           ta_out, ta_status);
+  }
+  HCHK(hipEventRecord(g_ev_side[3], st));
+  // partial signatures (sides 0, 1, then s)
+  if (n && verify_pipeline_locked(pks, sigs, msg_idx, (const MsgEntry*)hm, n, vstatus, s, g_ev_side[2])) return -1;
+  HCHK(hipStreamWaitEvent(s, g_ev_side[2], 0));
+  HCHK(hipStreamWaitEvent(s, g_ev_side[3], 0));
+  return 0;
+}
+
+int hbls_timing(int enable) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_timing = enable != 0;
+  g_tev_used = 0;
+  return 0;
+}
+
+int hbls_timing_read(float* ms, size_t max_n, size_t* n_out) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  size_t n = g_tev_used < max_n ? g_tev_used : max_n;
+  for (size_t i = 0; i < n; i++) {
+    HCHK(hipEventSynchronize(g_tev[i].second));
+    HCHK(hipEventElapsedTime(&ms[i], g_tev[i].first, g_tev[i].second));
+  }
+  *n_out = n;
+  return 0;
+}
+
+int hbls_timing(int enable) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_timing = enable != 0;
+  g_tev_used = 0;
+  return 0;
+}
+
+int hbls_timing_read(float* ms, size_t max_n, size_t* n_out) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  size_t n = g_tev_used < max_n ? g_tev_used : max_n;
+  for (size_t i = 0; i < n; i++) {
+    HCHK(hipEventSynchronize(g_tev[i].second));
+    HCHK(hipEventElapsedTime(&ms[i], g_tev[i].first, g_tev[i].second));
+  }
+  *n_out = n;
+  return 0;
+}
+
+// debug: run the ThresholdAggregate member stage on host buffers; returns affine points
+// (HmEntry, 208 B each), digits (32 B each) and member status
+int hbls_debug_ta_members(const uint8_t* sigs, const int64_t* idx, const uint32_t* grp_off, size_t n_groups,
+                          uint8_t* pts_out, uint8_t* dig_out, uint8_t* mst_out) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (init_locked(-1)) return -1;
+  size_t np = grp_off[n_groups];
+  uint8_t* dsig;
+  int64_t* didx;
+  uint32_t* dgoff;
+  if (upload(B_SIG, sigs, np * 96, &dsig) || upload(B_IDX, idx, np, &didx) || upload(B_GOFF, grp_off, n_groups + 1, &dgoff))
+    return -1;
+  void *apts, *dig, *mst;
+  if (ensure(B_TAPTS, np * sizeof(HmEntry), &apts) || ensure(B_TADIG, np * sizeof(TaDigits), &dig) ||
+      ensure(B_MSTAT, np, &mst))
+    return -1;
+  LAUNCH(k_ta_dec, np, g_stream, dsig, (uint32_t)np, (HmEntry*)apts, (uint8_t*)mst);
+  launch_ta_lambda(didx, dgoff, (uint32_t)n_groups, (uint32_t)np, 0, (TaDigits*)dig, (uint8_t*)mst, g_stream);
+  HCHK(hipGetLastError());
+  HCHK(hipMemcpyAsync(pts_out, apts, np * sizeof(HmEntry), hipMemcpyDeviceToHost, g_stream));
+  HCHK(hipMemcpyAsync(dig_out, dig, np * sizeof(TaDigits), hipMemcpyDeviceToHost, g_stream));
+  HCHK(hipMemcpyAsync(mst_out, mst, np, hipMemcpyDeviceToHost, g_stream));
+  HCHK(hipStreamSynchronize(g_stream));
+  return 0;
+}
+
+int hbls_debug_mul(const uint8_t* a, const uint8_t* b, const uint8_t* sigs, size_t n, int which, uint8_t* out,
+                   uint8_t* st) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (init_locked(-1)) return -1;
+  uint8_t *da, *db, *ds;
+  if (upload(B_PK, a, n * 48, &da) || upload(B_SK, b, n * 48, &db) || upload(B_SIG, sigs, n * 96, &ds)) return -1;
+  void *dout, *dst;
+  if (ensure(B_OUT, n * 48, &dout) || ensure(B_STAT, 2 * n, &dst)) return -1;
+  if (which == 0) launch_dbg((const Fp*)da, (const Fp*)db, (Fp*)dout, ds, (uint8_t*)dst, (uint32_t)n, g_stream);
+  else launch_dbg_p((const Fp*)da, (const Fp*)db, (Fp*)dout, ds, (uint8_t*)dst, (uint32_t)n, g_stream);
+  HCHK(hipGetLastError());
+  HCHK(hipMemcpyAsync(out, dout, n * 48, hipMemcpyDeviceToHost, g_stream));
+  HCHK(hipMemcpyAsync(st, dst, 2 * n, hipMemcpyDeviceToHost, g_stream));
+  HCHK(hipStreamSynchronize(g_stream));
   return 0;
 }
 

@@ -43,12 +43,14 @@ struct TaDigits {
 };
 
 // Staged ThresholdAggregate (threshold.hip)
-void launch_ta_dec(const uint8_t* sigs, const int64_t* idx, const uint32_t* grp_off, uint32_t n_groups,
-                   uint32_t n_partials, int mode, HmEntry* pts, TaDigits* dig, uint8_t* mstat, hipStream_t s);
+void launch_ta_lambda(const int64_t* idx, const uint32_t* grp_off, uint32_t n_groups, uint32_t n_partials, int mode,
+                      TaDigits* dig, uint8_t* mstat, hipStream_t s);
 void launch_ta_mul4(const HmEntry* pts, const TaDigits* dig, uint32_t n_partials, G2JEntry* out, hipStream_t s);
 
 // Staged verify pipeline (pipeline.hip): kernel launches on caller-provided streams.
 constexpr int GROUPS_PER_WAVE = 21;  // k_pair3: 3 lanes per partial, 21 partials per wave
+void launch_hash_to_g2(const uint8_t* msgs, const uint64_t* off, const uint32_t* len, uint32_t n, MsgEntry* hm,
+                       hipStream_t s);
 void launch_lines_msg(MsgEntry* hm, uint32_t n, hipStream_t s);
 void launch_dec_pk(const uint8_t* pks, uint32_t n, G1AEntry* out, uint8_t* st, hipStream_t s);
 void launch_dec_sig_lines(const uint8_t* sigs, uint32_t n, uint8_t* inf, uint8_t* st, LineEntry* lines,

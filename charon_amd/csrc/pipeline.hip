@@ -11,13 +11,27 @@
 namespace hb {
 
 #if defined(__HIP_DEVICE_COMPILE__)
-HB_DEFINE_FPMUL_SUBROUTINE
+HB_DEFINE_FPMUL_SUBROUTINE(hb_fpmul_holder_pipeline)
 #else
-__global__ void hb_fpmul_holder() {}
+__global__ void hb_fpmul_holder_pipeline() {}
 #endif
 
 #define KERNEL_BOUNDS __launch_bounds__(64)
 constexpr int BLOCK = 64;
+
+// One lane per distinct message: hash_to_curve G2 (RFC 9380, DST ..._POP_), affine.
+__global__ KERNEL_BOUNDS void k_hash_to_g2(const uint8_t* __restrict__ msgs, const uint64_t* __restrict__ off,
+                                           const uint32_t* __restrict__ len, uint32_t n, MsgEntry* __restrict__ hm) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  G2A h = jac_to_aff(hash_to_g2(msgs + off[i], len[i]));
+  HmEntry e;
+  e.x = h.x;
+  e.y = h.y;
+  e.inf = h.inf ? 1u : 0u;
+  e.pad[0] = e.pad[1] = e.pad[2] = 0;
+  hm[i].h = e;
+}
 
 // The Miller chain of an affine G2 point Q: 68 lines, stored at out[j * stride].  EVAL: evaluate
 // each line at -g1 (pair (-g1, sig) of the verification equation); otherwise store (a0, c1, c2).
@@ -131,6 +145,10 @@ __global__ __launch_bounds__(64, 2) void k_pair3(const G1AEntry* __restrict__ pk
 
 static inline unsigned blocks_for(size_t n) { return (unsigned)((n + BLOCK - 1) / BLOCK); }
 
+void launch_hash_to_g2(const uint8_t* msgs, const uint64_t* off, const uint32_t* len, uint32_t n, MsgEntry* hm,
+                       hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_hash_to_g2, dim3(blocks_for(n)), dim3(BLOCK), 0, s, msgs, off, len, n, hm);
+}
 void launch_lines_msg(MsgEntry* hm, uint32_t n, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_lines_msg, dim3(blocks_for(n)), dim3(BLOCK), 0, s, hm, n);
 }

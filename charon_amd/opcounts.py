@@ -23,6 +23,8 @@ FPMUL_PER_ITEM = {
     # per partial: G1 decompress+subgroup 1665, G2 decompress+subgroup 2486, 2-pair Miller loop +
     # final exponentiation 25450
     "k_verify": 29601,
+    # the pairing part alone (k_pair3: 2-pair Miller loop + final exponentiation)
+    "k_pair3": 25450,
     # per distinct 32-byte message: expand_message_xmd -> 2 SSWU -> 3-isogeny -> cofactor -> affine
     "k_hash_to_g2": 7813,
     # per validator of the bench's ThresholdAggregate (share indices {1,2,3}: lambda = 3, -3, 1;

@@ -103,8 +103,24 @@ int hbls_verify_device(const uint8_t* pks, const uint8_t* sigs, const uint32_t* 
 int hbls_threshold_aggregate_device(const uint8_t* sigs, const int64_t* idx, const uint32_t* grp_off,
                                     size_t n_groups, size_t n_partials, uint8_t* out, uint8_t* status,
                                     void* stream);
+/* One attestation slot in one call (the batch entry point of SURVEY.md §8b for sigagg/parsigex):
+ * hash the n_msgs distinct messages (+ their Miller lines) into `hm`, verify the n partials
+ * (msg_idx[i] indexes the messages) into vstatus, and threshold-aggregate n_groups groups
+ * (grp_off over n_ta_partials partials) into ta_out / ta_status -- hashing, signature
+ * decompression and aggregation run concurrently on the library's side streams; everything is
+ * ordered after prior work on `stream` and complete when later work on `stream` starts.
+ * Semantics per item as hbls_verify_batch / hbls_threshold_aggregate_batch. */
+int hbls_slot_device(const uint8_t* msgs, const uint64_t* msg_off, const uint32_t* msg_len, size_t n_msgs, void* hm,
+                     const uint8_t* pks, const uint8_t* sigs, const uint32_t* msg_idx, size_t n, uint8_t* vstatus,
+                     const uint8_t* ta_sigs, const int64_t* ta_idx, const uint32_t* grp_off, size_t n_groups,
+                     size_t n_ta_partials, uint8_t* ta_out, uint8_t* ta_status, void* stream);
 /* Bytes of the `hm` table entry per message. */
 size_t hbls_hm_entry_bytes(void);
+/* Measurement: with timing enabled (which also resets the record), every launch of the pairing
+ * kernel (k_pair3, the dominant kernel) is bracketed by HIP events on the stream it runs on;
+ * hbls_timing_read returns their durations in milliseconds, in launch order. */
+int hbls_timing(int enable);
+int hbls_timing_read(float* ms, size_t max_n, size_t* n_out);
 /* Wait for all work the library queued on `stream`. */
 int hbls_sync(void* stream);
 
