@@ -739,67 +739,6 @@ int hbls_timing_read(float* ms, size_t max_n, size_t* n_out) {
   return 0;
 }
 
-int hbls_timing(int enable) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  g_timing = enable != 0;
-  g_tev_used = 0;
-  return 0;
-}
-
-int hbls_timing_read(float* ms, size_t max_n, size_t* n_out) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  size_t n = g_tev_used < max_n ? g_tev_used : max_n;
-  for (size_t i = 0; i < n; i++) {
-    HCHK(hipEventSynchronize(g_tev[i].second));
-    HCHK(hipEventElapsedTime(&ms[i], g_tev[i].first, g_tev[i].second));
-  }
-  *n_out = n;
-  return 0;
-}
-
-// debug: run the ThresholdAggregate member stage on host buffers; returns affine points
-// (HmEntry, 208 B each), digits (32 B each) and member status
-int hbls_debug_ta_members(const uint8_t* sigs, const int64_t* idx, const uint32_t* grp_off, size_t n_groups,
-                          uint8_t* pts_out, uint8_t* dig_out, uint8_t* mst_out) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  if (init_locked(-1)) return -1;
-  size_t np = grp_off[n_groups];
-  uint8_t* dsig;
-  int64_t* didx;
-  uint32_t* dgoff;
-  if (upload(B_SIG, sigs, np * 96, &dsig) || upload(B_IDX, idx, np, &didx) || upload(B_GOFF, grp_off, n_groups + 1, &dgoff))
-    return -1;
-  void *apts, *dig, *mst;
-  if (ensure(B_TAPTS, np * sizeof(HmEntry), &apts) || ensure(B_TADIG, np * sizeof(TaDigits), &dig) ||
-      ensure(B_MSTAT, np, &mst))
-    return -1;
-  LAUNCH(k_ta_dec, np, g_stream, dsig, (uint32_t)np, (HmEntry*)apts, (uint8_t*)mst);
-  launch_ta_lambda(didx, dgoff, (uint32_t)n_groups, (uint32_t)np, 0, (TaDigits*)dig, (uint8_t*)mst, g_stream);
-  HCHK(hipGetLastError());
-  HCHK(hipMemcpyAsync(pts_out, apts, np * sizeof(HmEntry), hipMemcpyDeviceToHost, g_stream));
-  HCHK(hipMemcpyAsync(dig_out, dig, np * sizeof(TaDigits), hipMemcpyDeviceToHost, g_stream));
-  HCHK(hipMemcpyAsync(mst_out, mst, np, hipMemcpyDeviceToHost, g_stream));
-  HCHK(hipStreamSynchronize(g_stream));
-  return 0;
-}
-
-int hbls_debug_mul(const uint8_t* a, const uint8_t* b, const uint8_t* sigs, size_t n, int which, uint8_t* out,
-                   uint8_t* st) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  if (init_locked(-1)) return -1;
-  uint8_t *da, *db, *ds;
-  if (upload(B_PK, a, n * 48, &da) || upload(B_SK, b, n * 48, &db) || upload(B_SIG, sigs, n * 96, &ds)) return -1;
-  void *dout, *dst;
-  if (ensure(B_OUT, n * 48, &dout) || ensure(B_STAT, 2 * n, &dst)) return -1;
-  if (which == 0) launch_dbg((const Fp*)da, (const Fp*)db, (Fp*)dout, ds, (uint8_t*)dst, (uint32_t)n, g_stream);
-  else launch_dbg_p((const Fp*)da, (const Fp*)db, (Fp*)dout, ds, (uint8_t*)dst, (uint32_t)n, g_stream);
-  HCHK(hipGetLastError());
-  HCHK(hipMemcpyAsync(out, dout, n * 48, hipMemcpyDeviceToHost, g_stream));
-  HCHK(hipMemcpyAsync(st, dst, 2 * n, hipMemcpyDeviceToHost, g_stream));
-  HCHK(hipStreamSynchronize(g_stream));
-  return 0;
-}
-
 int hbls_sync(void* stream) {
   HCHK(hipStreamSynchronize((hipStream_t)stream));
   return 0;
