@@ -126,29 +126,41 @@ HDNI void hash_to_field_fp2(Fp2& u0, Fp2& u1, const uint8_t* msg, uint32_t len) 
   u1 = {e[2], e[3]};
 }
 
-// simplified SWU for E2' (RFC 9380 6.6.2); returns affine point on E2'
+// simplified SWU for E2' (RFC 9380 6.6.2); returns affine point on E2'.  Straight-line with three
+// Fp exponentiations (1/tv1, one norm square root, one (p-3)/4 power), so the lanes of a wave do
+// not diverge on the square / non-square case:
+//   s1 = N(gx1)^((p+1)/4) is sqrt(N(gx1)) if gx1 is a square, else sqrt(-N(gx1)); in that case
+//   gx2 = (Z u^2)^3 gx1 is the square and sqrt(N(gx2)) = s1 N(u)^3 sqrt(-N(Z)^3).
+// The Fp2 root of the chosen g(x) then follows the norm method of f2_sqrt.
 HDNI void sswu_map(Fp2& x, Fp2& y, const Fp2& u) {
   Fp2 A = f2_from_const(SSWU_A), B = f2_from_const(SSWU_B), Z = f2_from_const(SSWU_Z);
   Fp2 u2 = f2_sqr(u);
   Fp2 zu2 = f2_mul(Z, u2);
   Fp2 tv1 = f2_add(f2_sqr(zu2), zu2);
-  Fp2 x1;
-  if (f2_is_zero(tv1)) {
-    x1 = f2_from_const(SSWU_B_OVER_ZA);
-  } else {
-    x1 = f2_mul(f2_from_const(SSWU_MINUS_B_OVER_A), f2_add(f2_one(), f2_inv(tv1)));
-  }
+  const bool tv1_zero = f2_is_zero(tv1);
+  Fp2 x1 = f2_mul(f2_from_const(SSWU_MINUS_B_OVER_A), f2_add(f2_one(), f2_inv(tv1)));
+  if (tv1_zero) x1 = f2_from_const(SSWU_B_OVER_ZA);
   Fp2 gx1 = f2_add(f2_mul(f2_add(f2_sqr(x1), A), x1), B);
-  Fp2 y1;
-  if (f2_sqrt(y1, gx1)) {
-    x = x1;
-    y = y1;
+  Fp2 x2 = f2_mul(zu2, x1);
+  Fp2 gx2 = f2_add(f2_mul(f2_add(f2_sqr(x2), A), x2), B);
+  Fp n1 = fp_add(fp_sqr(gx1.c0), fp_sqr(gx1.c1));
+  Fp s1 = fp_pow_const(n1, EXP_SQRT, 379);
+  const bool sq1 = fp_eq(fp_sqr(s1), n1);
+  Fp nu = fp_add(fp_sqr(u.c0), fp_sqr(u.c1));
+  Fp s2 = fp_mul(fp_mul(s1, fp_mul(fp_sqr(nu), nu)), fp_from_const(SSWU_SQRT_MNZ3));
+  Fp2 a = sq1 ? gx1 : gx2;
+  Fp s = sq1 ? s1 : s2;
+  x = sq1 ? x1 : x2;
+  Fp inv2 = fp_from_const(FP_INV2);
+  Fp c = fp_mul(fp_add(a.c0, s), inv2);
+  if (fp_is_zero(c)) c = fp_mul(fp_sub(a.c0, s), inv2);
+  Fp t = fp_pow_const(c, EXP_P_M3_4, 378);
+  Fp y0 = fp_mul(c, t);
+  Fp h = fp_mul(fp_mul(a.c1, t), inv2);
+  if (fp_eq(fp_sqr(y0), c)) {
+    y = {y0, h};
   } else {
-    Fp2 x2 = f2_mul(zu2, x1);
-    Fp2 gx2 = f2_add(f2_mul(f2_add(f2_sqr(x2), A), x2), B);
-    f2_sqrt(y1, gx2);  // gx1 non-square => gx2 square (RFC 9380 appendix F.2)
-    x = x2;
-    y = y1;
+    y = {fp_neg(h), y0};
   }
   if (f2_sgn0(u) != f2_sgn0(y)) y = f2_neg(y);
 }

@@ -260,7 +260,7 @@ struct DevBuf {
 enum BufId {
   B_PK, B_SIG, B_MSG, B_OFF, B_LEN, B_MIDX, B_HM, B_STAT, B_IDX, B_GOFF, B_PTS, B_MSTAT, B_OUT, B_SK, B_G1PTS,
   B_VPK, B_VPKST, B_VSIGINF, B_VSIGST, B_VLINES,  // staged verify: per-partial intermediates
-  B_TAPTS, B_TADIG,                               // staged ThresholdAggregate
+  B_TAPTS, B_TADIG, B_TATAB,                      // staged ThresholdAggregate
   B_COUNT
 };
 DevBuf g_bufs[B_COUNT];
@@ -438,16 +438,19 @@ int verify_pipeline_locked(const uint8_t* dpk, const uint8_t* dsig, const uint32
 }
 
 // ThresholdAggregate / Aggregate members (herumi.go:249-286, 225-247): decompress + lambda
-// digits (1 lane / partial), then lambda_j sigma_j with 4 lanes / partial (threshold.hip).
+// digits (1 lane / partial), then lambda_j sigma_j as a 4-scalar Straus ladder (threshold.hip).
 int ta_members_locked(const uint8_t* dsig, const int64_t* didx, const uint32_t* dgoff, size_t n_groups, size_t np,
                       int mode, G2JEntry* pts, uint8_t* mst, hipStream_t s) {
   if (np == 0) return 0;
   void *apts, *dig;
-  if (ensure(B_TAPTS, np * sizeof(HmEntry), &apts) || ensure(B_TADIG, np * sizeof(TaDigits), &dig)) return -1;
+  void* tab;
+  if (ensure(B_TAPTS, np * sizeof(HmEntry), &apts) || ensure(B_TADIG, np * sizeof(TaDigits), &dig) ||
+      ensure(B_TATAB, ta_table_bytes((uint32_t)np), &tab))
+    return -1;
   LAUNCH(k_ta_dec, np, s, dsig, (uint32_t)np, (HmEntry*)apts, mst);
   launch_ta_lambda(didx, dgoff, (uint32_t)n_groups, (uint32_t)np, mode, (TaDigits*)dig, mst, s);
   HCHK(hipGetLastError());
-  launch_ta_mul4((const HmEntry*)apts, (const TaDigits*)dig, (uint32_t)np, pts, s);
+  launch_ta_straus((const HmEntry*)apts, (const TaDigits*)dig, (uint32_t)np, tab, pts, s);
   HCHK(hipGetLastError());
   return 0;
 }

@@ -45,7 +45,9 @@ struct TaDigits {
 // Staged ThresholdAggregate (threshold.hip)
 void launch_ta_lambda(const int64_t* idx, const uint32_t* grp_off, uint32_t n_groups, uint32_t n_partials, int mode,
                       TaDigits* dig, uint8_t* mstat, hipStream_t s);
-void launch_ta_mul4(const HmEntry* pts, const TaDigits* dig, uint32_t n_partials, G2JEntry* out, hipStream_t s);
+size_t ta_table_bytes(uint32_t n_partials);
+void launch_ta_straus(const HmEntry* pts, const TaDigits* dig, uint32_t n_partials, void* tab, G2JEntry* out,
+                      hipStream_t s);
 
 // Staged verify pipeline (pipeline.hip): kernel launches on caller-provided streams.
 constexpr int GROUPS_PER_WAVE = 21;  // k_pair3: 3 lanes per partial, 21 partials per wave

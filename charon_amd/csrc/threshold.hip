@@ -4,17 +4,17 @@
 // product, everything else inlined).
 //
 //   k_ta_dec   (hipbls.hip) 1 lane / partial: decompress + subgroup-check sigma_j
-//   k_ta_lambda 1 lane / partial: lambda_j(0) over its group's share indices (Fr), and the
-//              base-|x| digits of lambda_j
-//   k_ta_mul4  4 lanes / partial: lambda_j sigma_j = sum_i [a_i] psi^i(sigma_j) (-1)^i, one
-//              64-bit digit per lane, then a 2-round lane reduction
+//   k_ta_lambda 1 lane / partial: lambda_j(0) over its group's share indices (Fr, 1/d table for
+//              the denominators), and the base-|x| digits of lambda_j
+//   k_ta_straus 1 lane / partial: lambda_j sigma_j = sum_i [a_i] (-1)^i psi^i(sigma_j), one
+//              joint 64-step ladder over the four digits (15-entry subset table)
 //   k_group_sum (hipbls.hip) 1 lane / group: sum, affine, compress
 //
 // The split of lambda uses the G2 endomorphism psi, which acts on G2 as multiplication by the
 // curve parameter x (this is the subgroup test of ec.h, psi(Q) == [x]Q).  With z = |x| = -x and
 // lambda = a0 + a1 z + a2 z^2 + a3 z^3 (0 <= a_i < z; lambda < r < z^4):
 //   [lambda] Q = [a0] Q - [a1] psi(Q) + [a2] psi^2(Q) - [a3] psi^3(Q),
-// four independent 64-bit scalar multiplications instead of one 255-bit one.  The result is the
+// a 4-scalar multiplication with 64-bit scalars instead of one 255-bit one.  The result is the
 // same group element, so the 96-byte output is byte-identical to herumi's Sign.Recover.
 #define HB_FAST_FPMUL 1
 #include "layout.h"
@@ -69,18 +69,33 @@ __global__ __launch_bounds__(64) void k_ta_lambda(const int64_t* __restrict__ id
   uint32_t g = find_group_ta(grp_off, n_groups, j);
   uint32_t b = grp_off[g], en = grp_off[g + 1];
   if (mode == 0 && en - b > 1) {  // k = 1: the single partial is returned as is
-    Fr xi = fr_from_i64(idx[j]);
-    Fr num = fr_one(), den = fr_one();
+    // lambda_j = prod_m x_m / prod_m (x_m - x_j).  Share indices are small integers, so each
+    // denominator factor normally comes from the 1/d table (no Fr inversion); anything else
+    // (large or duplicated indices) goes through one Fermat inversion of their product.
+    const int64_t ij = idx[j];
+    const bool ij_small = ij > -(int64_t(1) << 62) && ij < (int64_t(1) << 62);
+    Fr num = fr_one(), den_inv = fr_one(), den = fr_one();
+    bool slow = false;
     for (uint32_t m = b; m < en; m++) {
       if (m == j) continue;
-      Fr xm = fr_from_i64(idx[m]);
-      num = fr_mul(num, xm);
-      den = fr_mul(den, fr_sub(xm, xi));
+      const int64_t im = idx[m];
+      num = fr_mul(num, fr_from_i64(im));
+      const int64_t dd = im - ij;  // only used when both indices are below 2^62 in magnitude
+      const bool small = ij_small && im > -(int64_t(1) << 62) && im < (int64_t(1) << 62) && dd != 0 &&
+                         dd >= -FR_SMALL_INV_N && dd <= FR_SMALL_INV_N;
+      if (small) {
+        Fr t = fr_from_const(FR_SMALL_INV[(dd < 0 ? -dd : dd) - 1]);
+        den_inv = fr_mul(den_inv, dd < 0 ? fr_sub(fr_zero(), t) : t);
+      } else {
+        den = fr_mul(den, fr_sub(fr_from_i64(im), fr_from_i64(ij)));
+        slow = true;
+      }
     }
     if (fr_is_zero(num) || fr_is_zero(den)) {
       if (mstat[j] == M_OK) mstat[j] = M_BAD_IDX;
     } else {
-      Fr lam = fr_from_mont(fr_mul(num, fr_inv(den)));
+      if (slow) den_inv = fr_mul(den_inv, fr_inv(den));
+      Fr lam = fr_from_mont(fr_mul(num, den_inv));
       uint32_t u[NLR];
       HB_UNROLL for (int i = 0; i < NLR; i++) u[i] = lam.v[i];
       d.a[0] = divmod_xabs(u);
@@ -93,19 +108,27 @@ __global__ __launch_bounds__(64) void k_ta_lambda(const int64_t* __restrict__ id
 }
 
 #if defined(__HIP_DEVICE_COMPILE__)
-__device__ __forceinline__ uint32_t xch4(uint32_t v, int lane) {
-  return (uint32_t)__builtin_amdgcn_ds_bpermute(lane << 2, (int)v);
+// Per-lane subset table, lane-interleaved so that one 16-byte load per (entry, quad) coalesces
+// over the lanes that picked the same entry: uint4 index ((wave * 15 + e) * 18 + q) * 64 + lane.
+constexpr int TA_TAB_QUADS = (int)(sizeof(G2JEntry) / 16);  // 18
+__device__ __forceinline__ void tab_store(uint4* wt, int e, const G2J& p) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(&p);
+  static_assert(sizeof(G2J) == sizeof(G2JEntry), "G2J layout");
+  HB_UNROLL for (int q = 0; q < TA_TAB_QUADS; q++)
+    wt[(e * TA_TAB_QUADS + q) * 64] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
 }
-__device__ __forceinline__ Fp2 xch4(const Fp2& a, int lane) {
-  Fp2 r;
-  HB_UNROLL for (int i = 0; i < NL; i++) {
-    r.c0.v[i] = xch4(a.c0.v[i], lane);
-    r.c1.v[i] = xch4(a.c1.v[i], lane);
+__device__ __forceinline__ G2J tab_load(const uint4* wt, int e) {
+  G2J p;
+  uint32_t* w = reinterpret_cast<uint32_t*>(&p);
+  HB_UNROLL for (int q = 0; q < TA_TAB_QUADS; q++) {
+    uint4 v = wt[(e * TA_TAB_QUADS + q) * 64];
+    w[4 * q] = v.x;
+    w[4 * q + 1] = v.y;
+    w[4 * q + 2] = v.z;
+    w[4 * q + 3] = v.w;
   }
-  return r;
+  return p;
 }
-__device__ __forceinline__ G2J xch4(const G2J& p, int lane) { return {xch4(p.X, lane), xch4(p.Y, lane), xch4(p.Z, lane)}; }
-
 __device__ __forceinline__ void f2_select(Fp2& r, bool take_b, const Fp2& a, const Fp2& b) {
   HB_UNROLL for (int i = 0; i < NL; i++) {
     r.c0.v[i] = take_b ? b.c0.v[i] : a.c0.v[i];
@@ -114,44 +137,52 @@ __device__ __forceinline__ void f2_select(Fp2& r, bool take_b, const Fp2& a, con
 }
 #endif
 
-// Four lanes per partial (16 partials per wave): lane i computes (-1)^i [a_i] psi^i(sigma), the
-// quad then sums its four points.  Uniform control flow: the add of every step is computed and
-// kept or dropped per lane by select.
-__global__ __launch_bounds__(64, 2) void k_ta_mul4(const HmEntry* __restrict__ pts, const TaDigits* __restrict__ dig,
-                                                   uint32_t n_partials, G2JEntry* __restrict__ out) {
+// One lane per partial: lambda sigma = sum_i [a_i] P_i with P_i = (-1)^i psi^i(sigma), as a
+// 4-scalar Straus ladder over the 15-entry subset table T[s] = sum_{i in s} P_i (built with 11
+// mixed additions, kept in global memory): 64 doublings + 64 table additions per partial, against
+// 4 x 64 of each for four independent ladders.  Uniform control flow: the table addition of
+// every step is computed and kept or dropped per lane by select.
+__global__ __launch_bounds__(64, 2) void k_ta_straus(const HmEntry* __restrict__ pts, const TaDigits* __restrict__ dig,
+                                                     uint32_t n_partials, uint4* __restrict__ tab,
+                                                     G2JEntry* __restrict__ out) {
 #if defined(__HIP_DEVICE_COMPILE__)
   const int lane = (int)(threadIdx.x & 63u);
-  const int i = lane & 3;
-  const uint32_t item = blockIdx.x * 16 + (uint32_t)(lane >> 2);
+  const uint32_t item = blockIdx.x * 64 + (uint32_t)lane;
   const bool valid = item < n_partials;
   const uint32_t it = valid ? item : n_partials - 1;
-  const HmEntry e = pts[it];
-  const uint64_t a = dig[it].a[i];
-  // psi^i(sigma): psi^2 (x, y) = (x c2x, y c2y); psi (x, y) = (conj(x) c1x, conj(y) c1y)
-  Fp2 x = e.x, y = e.y;
+  uint4* wt = tab + (size_t)blockIdx.x * 15 * TA_TAB_QUADS * 64 + lane;
+  const TaDigits d = dig[it];
   {
-    Fp2 x2 = f2_mul(x, f2_from_const(PSI2_CX)), y2 = f2_mul(y, f2_from_const(PSI2_CY));
-    f2_select(x, (i & 2) != 0, x, x2);
-    f2_select(y, (i & 2) != 0, y, y2);
-    Fp2 x1 = f2_mul(f2_conj(x), f2_from_const(PSI_CX)), y1 = f2_mul(f2_conj(y), f2_from_const(PSI_CY));
-    f2_select(x, (i & 1) != 0, x, x1);
-    f2_select(y, (i & 1) != 0, y, y1);
-    Fp2 ny = f2_neg(y);  // (-1)^i
-    f2_select(y, (i & 1) != 0, y, ny);
+    const HmEntry e = pts[it];
+    // psi (x, y) = (conj(x) c1x, conj(y) c1y); psi^2 (x, y) = (x c2x, y c2y)
+    G2A P0 = {e.x, e.y, e.inf != 0};
+    G2A P1 = {f2_mul(f2_conj(e.x), f2_from_const(PSI_CX)), f2_neg(f2_mul(f2_conj(e.y), f2_from_const(PSI_CY))), P0.inf};
+    G2A P2 = {f2_mul(e.x, f2_from_const(PSI2_CX)), f2_mul(e.y, f2_from_const(PSI2_CY)), P0.inf};
+    G2A P3 = {f2_mul(f2_conj(P2.x), f2_from_const(PSI_CX)), f2_neg(f2_mul(f2_conj(P2.y), f2_from_const(PSI_CY))), P0.inf};
+    tab_store(wt, 0, jac_from_aff(P0));
+    tab_store(wt, 1, jac_from_aff(P1));
+    tab_store(wt, 3, jac_from_aff(P2));
+    tab_store(wt, 7, jac_from_aff(P3));
   }
-  const G2A P = {x, y, e.inf != 0};
+  // T[s] (entry s - 1) = T[s - hi] + T[hi], hi the top bit of s; T[hi] is affine (Z = 1 or infinity)
+  HB_NOUNROLL for (int s = 3; s < 16; s++) {
+    const int hi = s >= 8 ? 8 : (s >= 4 ? 4 : 2);
+    if (s == hi) continue;
+    const G2J h = tab_load(wt, hi - 1);
+    const G2A ha = {h.X, h.Y, f2_is_zero(h.Z)};
+    tab_store(wt, s - 1, jac_add_aff(tab_load(wt, s - hi - 1), ha));
+  }
   G2J R = jac_infinity<Fp2>();
   HB_NOUNROLL for (int b = 63; b >= 0; b--) {
     R = jac_dbl(R);
-    G2J S = jac_add_aff(R, P);
-    const bool take = ((a >> b) & 1) != 0;
-    f2_select(R.X, take, R.X, S.X);
-    f2_select(R.Y, take, R.Y, S.Y);
-    f2_select(R.Z, take, R.Z, S.Z);
+    const uint32_t sel = (uint32_t)((d.a[0] >> b) & 1) | ((uint32_t)((d.a[1] >> b) & 1) << 1) |
+                         ((uint32_t)((d.a[2] >> b) & 1) << 2) | ((uint32_t)((d.a[3] >> b) & 1) << 3);
+    const G2J S = jac_add(R, tab_load(wt, sel == 0 ? 0 : (int)sel - 1));
+    f2_select(R.X, sel != 0, R.X, S.X);
+    f2_select(R.Y, sel != 0, R.Y, S.Y);
+    f2_select(R.Z, sel != 0, R.Z, S.Z);
   }
-  R = jac_add(R, xch4(R, lane ^ 1));
-  R = jac_add(R, xch4(R, lane ^ 2));
-  if (valid && i == 0) out[item] = {R.X, R.Y, R.Z};
+  if (valid) out[item] = {R.X, R.Y, R.Z};
 #endif
 }
 
@@ -164,9 +195,13 @@ void launch_ta_lambda(const int64_t* idx, const uint32_t* grp_off, uint32_t n_gr
                      n_partials, mode, dig, mstat);
 }
 
-void launch_ta_mul4(const HmEntry* pts, const TaDigits* dig, uint32_t n_partials, G2JEntry* out, hipStream_t s) {
+size_t ta_table_bytes(uint32_t n_partials) { return (size_t)blocks_of(n_partials, 64) * 15 * sizeof(G2JEntry) * 64; }
+
+void launch_ta_straus(const HmEntry* pts, const TaDigits* dig, uint32_t n_partials, void* tab, G2JEntry* out,
+                      hipStream_t s) {
   if (n_partials)
-    hipLaunchKernelGGL(k_ta_mul4, dim3(blocks_of(n_partials, 16)), dim3(64), 0, s, pts, dig, n_partials, out);
+    hipLaunchKernelGGL(k_ta_straus, dim3(blocks_of(n_partials, 64)), dim3(64), 0, s, pts, dig, n_partials,
+                       (uint4*)tab, out);
 }
 
 }  // namespace hb

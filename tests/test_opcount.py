@@ -22,7 +22,8 @@ def test_verify_counts(hc, fixtures):
     # the frozen r01 count is the roofline's work unit; the executed count may only go down
     assert out[0] == opcounts.EXECUTED_FPMUL_PER_ITEM["k_verify"]
     assert out[0] <= opcounts.FPMUL_PER_ITEM["k_verify"]
-    assert out[1] == opcounts.FPMUL_PER_ITEM["k_hash_to_g2"]
+    assert out[1] == opcounts.EXECUTED_FPMUL_PER_ITEM["k_hash_to_g2"]
+    assert out[1] <= opcounts.FPMUL_PER_ITEM["k_hash_to_g2"]
 
 
 def test_threshold_aggregate_counts(hc, fixtures):
