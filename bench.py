@@ -38,6 +38,7 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 from charon_amd.opcounts import FPMUL_PER_ITEM, MAC_PER_FPMUL, PEAK_MAD_TOPS  # noqa: E402
+from charon_amd.shard import SlotExchange, max_over_ranks, owned_validators  # noqa: E402
 
 N_LINES = 68  # Miller-loop lines per pairing (pairing.h)
 
@@ -69,7 +70,7 @@ def setup_inputs(L, wl, V, rank):
     """Synthetic cluster -> host arrays; keys and signatures are derived on the GPU."""
     from charon_amd import synth
     n, t = wl["n"], wl["t"]
-    cl = synth.make_cluster(V, n, t, first_validator=rank * V, n_msgs=wl["n_msgs"] or 64,
+    cl = synth.make_cluster(V, n, t, first_validator=owned_validators(rank, V).start, n_msgs=wl["n_msgs"] or 64,
                             distinct_messages=wl["distinct"])
     NP = V * n
     M = len(cl.msgs)
@@ -191,10 +192,7 @@ def main(argv=None):
     d_vst = torch.full((NP,), 255, dtype=torch.uint8, device=dev)
     d_tout = torch.zeros(V * 96, dtype=torch.uint8, device=dev)
     d_tst = torch.full((V,), 255, dtype=torch.uint8, device=dev)
-    if world > 1:
-        g_vst = torch.empty(world * NP, dtype=torch.uint8, device=dev)
-        g_tout = torch.empty(world * V * 96, dtype=torch.uint8, device=dev)
-        g_tst = torch.empty(world * V, dtype=torch.uint8, device=dev)
+    xchg = SlotExchange(world, V, d["n"], dev) if world > 1 else None
 
     stream = torch.cuda.Stream(device=dev)
     sp = ctypes.c_void_p(stream.cuda_stream)
@@ -209,9 +207,7 @@ def main(argv=None):
         ev[1].record(stream)
         if world > 1:  # all-gather verdicts + compressed aggregates to every rank
             with torch.cuda.stream(stream):
-                dist.all_gather_into_tensor(g_vst, d_vst)
-                dist.all_gather_into_tensor(g_tout, d_tout)
-                dist.all_gather_into_tensor(g_tst, d_tst)
+                xchg.exchange(d_vst, d_tout, d_tst)
         ev[2].record(stream)
 
     def step_staged(ev):
@@ -248,9 +244,7 @@ def main(argv=None):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+        elapsed = max_over_ranks(elapsed, dev)
 
     seg = np.array([[e[i].elapsed_time(e[i + 1]) for i in range(n_ev - 1)] for e in evs])  # ms
     k_ms = seg.mean(axis=0)
@@ -269,7 +263,7 @@ def main(argv=None):
     parity = {"verify_all_ok": bool((vst == 0).all()), "ta_all_ok": bool((tst == 0).all()),
               "ta_equals_root_signature": bool(np.array_equal(tout, d["root_sigs"]))}
     if world > 1:
-        parity["allgather_ok"] = bool((g_vst.cpu().numpy() == 0).all() and (g_tst.cpu().numpy() == 0).all())
+        parity["allgather_ok"] = xchg.all_ok()
 
     items = world * (NP + V)
     ms_per_step = elapsed / args.steps * 1e3

@@ -1,0 +1,93 @@
+"""N > 1 path on CPU: validator sharding and the slot's all-gather (charon_amd/shard.py, bench.py
+--gpus N) with world_size 2 over gloo.
+
+The sharded cluster must be the unsharded one split in rank order (weak scaling: rank r owns
+validators [r*V, (r+1)*V)), and after the exchange every rank must hold every rank's verdicts,
+aggregates and statuses in global validator order.  The per-rank slot results are stand-ins
+(deterministic bytes derived from each validator's shares); the GPU computes the real ones.
+"""
+
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from charon_amd import synth
+from charon_amd.shard import SlotExchange, max_over_ranks, owned_validators
+
+V, N, T, WORLD = 3, 4, 3, 2
+
+
+def _slot_results(cl):
+    """Stand-in slot outputs of one shard: verdict byte per partial, 96 B and a status per validator."""
+    vst = torch.tensor([sk[0] % 5 for sk in cl.share_sks], dtype=torch.uint8)
+    tout = torch.tensor(list(b"".join(r * 3 for r in cl.root_sks)), dtype=torch.uint8)
+    tst = torch.tensor([r[-1] % 3 for r in cl.root_sks], dtype=torch.uint8)
+    return vst, tout, tst
+
+
+def _worker(rank, port, errq):
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+        first = owned_validators(rank, V).start
+        cl = synth.make_cluster(V, N, T, first_validator=first)
+        full = synth.make_cluster(WORLD * V, N, T)
+        # sharding == the unsharded cluster split in rank order
+        assert cl.root_sks == full.root_sks[first:first + V]
+        assert cl.share_sks == full.share_sks[first * N:(first + V) * N]
+        assert [cl.msgs[m] for m in cl.msg_of_validator] == [full.msgs[m] for m in full.msg_of_validator][first:first + V]
+        xchg = SlotExchange(WORLD, V, N, "cpu")
+        xchg.exchange(*_slot_results(cl))
+        want = [torch.cat(x) for x in zip(*[_slot_results(synth.make_cluster(V, N, T, first_validator=owned_validators(r, V).start))
+                                             for r in range(WORLD)])]
+        assert torch.equal(xchg.vst_all, want[0])
+        assert torch.equal(xchg.tout_all, want[1])
+        assert torch.equal(xchg.tst_all, want[2])
+        assert torch.equal(xchg.tout_all, _slot_results(full)[1])  # global validator order
+        assert xchg.all_ok() == bool((want[0] == 0).all() and (want[2] == 0).all())
+        with pytest.raises(ValueError):
+            xchg.exchange(torch.zeros(1, dtype=torch.uint8), torch.zeros(1, dtype=torch.uint8),
+                          torch.zeros(1, dtype=torch.uint8))
+        # bench.py reports throughput against the slowest rank
+        assert max_over_ranks(1.5 + rank, "cpu") == 1.5 + (WORLD - 1)
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001 -- reported to the parent
+        errq.put(f"rank {rank}: {type(e).__name__}: {e}")
+        raise
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_owned_validators_partition():
+    got = [v for r in range(4) for v in owned_validators(r, 5)]
+    assert got == list(range(20))
+
+
+def test_sharded_slot_exchange_gloo_world2():
+    ctx = mp.get_context("spawn")
+    errq = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, port, errq)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=180)
+    errs = []
+    while not errq.empty():
+        errs.append(errq.get())
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+            errs.append("rank timed out")
+    assert not errs, errs
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
