@@ -241,7 +241,7 @@ std::mutex g_mu;  // serialises host-buffer calls (shared workspace)
 int g_device = -1;
 hipStream_t g_stream = nullptr;
 // fork/join streams: 0, 1 = the staged verify's decompression kernels, 2 = message hashing,
-// 3 = ThresholdAggregate (hbls_slot_device)
+// 3 = unused (hbls_slot_device runs its ThresholdAggregate on g_stream)
 constexpr int N_SIDE = 4;
 hipStream_t g_side[N_SIDE] = {};
 hipEvent_t g_ev_fork = nullptr, g_ev_slot = nullptr, g_ev_side[N_SIDE] = {};
@@ -705,8 +705,13 @@ int hbls_slot_device(const uint8_t* msgs, const uint64_t* msg_off, const uint32_
   launch_lines_msg((MsgEntry*)hm, (uint32_t)n_msgs, sh);
   HCHK(hipGetLastError());
   HCHK(hipEventRecord(g_ev_side[2], sh));
-  // ThresholdAggregate (side 3)
-  hipStream_t st = g_side[3];
+  // partial signatures (sides 0, 1, then s)
+  if (n && verify_pipeline_locked(pks, sigs, msg_idx, (const MsgEntry*)hm, n, vstatus, s, g_ev_side[2])) return -1;
+  // ThresholdAggregate on the library's own stream, which no other slot kernel uses: the runtime
+  // has 4 hardware queues, and with five busy streams two would share one, serialising the
+  // aggregation chain behind the hashing (profiles/r01h_slot_timeline.txt).  In-order with the
+  // host-buffer entry points that share its workspaces.
+  hipStream_t st = g_stream;
   HCHK(hipStreamWaitEvent(st, g_ev_slot, 0));
   if (n_groups) {
     void *pts, *mst;
@@ -717,8 +722,6 @@ int hbls_slot_device(const uint8_t* msgs, const uint64_t* msg_off, const uint32_
            ta_out, ta_status);
   }
   HCHK(hipEventRecord(g_ev_side[3], st));
-  // partial signatures (sides 0, 1, then s)
-  if (n && verify_pipeline_locked(pks, sigs, msg_idx, (const MsgEntry*)hm, n, vstatus, s, g_ev_side[2])) return -1;
   HCHK(hipStreamWaitEvent(s, g_ev_side[2], 0));
   HCHK(hipStreamWaitEvent(s, g_ev_side[3], 0));
   return 0;
