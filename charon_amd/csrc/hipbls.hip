@@ -322,8 +322,12 @@ int init_locked(int device) {
     return -1;
   }
   HCHK(hipStreamCreateWithFlags(&g_stream, hipStreamNonBlocking));
+  // the verify pipeline's streams (decompression, hashing) get the highest priority: they gate the
+  // pairing kernel, while the aggregation chain on g_stream has slack in the slot
+  int prio_lo = 0, prio_hi = 0;
+  HCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
   for (int k = 0; k < N_SIDE; k++) {
-    HCHK(hipStreamCreateWithFlags(&g_side[k], hipStreamNonBlocking));
+    HCHK(hipStreamCreateWithPriority(&g_side[k], hipStreamNonBlocking, prio_hi));
     HCHK(hipEventCreateWithFlags(&g_ev_side[k], hipEventDisableTiming));
   }
   HCHK(hipEventCreateWithFlags(&g_ev_fork, hipEventDisableTiming));
