@@ -106,9 +106,10 @@ int hbls_threshold_aggregate_device(const uint8_t* sigs, const int64_t* idx, con
 /* One attestation slot in one call (the batch entry point of SURVEY.md §8b for sigagg/parsigex):
  * hash the n_msgs distinct messages (+ their Miller lines) into `hm`, verify the n partials
  * (msg_idx[i] indexes the messages) into vstatus, and threshold-aggregate n_groups groups
- * (grp_off over n_ta_partials partials) into ta_out / ta_status -- hashing, signature
- * decompression and aggregation run concurrently on the library's side streams; everything is
- * ordered after prior work on `stream` and complete when later work on `stream` starts.
+ * (grp_off over n_ta_partials partials) into ta_out / ta_status -- hashing and signature
+ * decompression run concurrently on the library's high-priority side streams, the aggregation
+ * on the library's own stream, the pairing kernel on `stream`; everything is ordered after prior
+ * work on `stream` and complete when later work on `stream` starts.
  * Semantics per item as hbls_verify_batch / hbls_threshold_aggregate_batch. */
 int hbls_slot_device(const uint8_t* msgs, const uint64_t* msg_off, const uint32_t* msg_len, size_t n_msgs, void* hm,
                      const uint8_t* pks, const uint8_t* sigs, const uint32_t* msg_idx, size_t n, uint8_t* vstatus,
