@@ -321,11 +321,11 @@ int init_locked(int device) {
     g_err = std::string("libhipbls is built for gfx950, device is ") + prop.gcnArchName;
     return -1;
   }
-  HCHK(hipStreamCreateWithFlags(&g_stream, hipStreamNonBlocking));
   // the verify pipeline's streams (decompression, hashing) get the highest priority: they gate the
-  // pairing kernel, while the aggregation chain on g_stream has slack in the slot
+  // pairing kernel, while the aggregation chain on g_stream (lowest priority) has slack in the slot
   int prio_lo = 0, prio_hi = 0;
   HCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+  HCHK(hipStreamCreateWithPriority(&g_stream, hipStreamNonBlocking, prio_lo));
   for (int k = 0; k < N_SIDE; k++) {
     HCHK(hipStreamCreateWithPriority(&g_side[k], hipStreamNonBlocking, prio_hi));
     HCHK(hipEventCreateWithFlags(&g_ev_side[k], hipEventDisableTiming));
