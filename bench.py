@@ -1,22 +1,27 @@
 #!/usr/bin/env python3
 """bench.py -- charon's BLS hot path on MI355X (BASELINE.json metric).
 
-One step = one attestation slot of BASELINE.json configs[1] ("C2"): for V = 10 000 validators of a
-4-operator threshold-3 cluster,
-  1. hash the slot's 64 distinct signing roots to G2          (k_hash_to_g2)
-  2. verify all V*n = 40 000 partial signatures                (k_verify: tbls.Verify,
-     /root/reference/tbls/herumi.go:288-304, callers core/parsigex/parsigex.go:93-98)
-  3. threshold-aggregate every validator's first t partials   (k_group_member + k_group_sum:
-     tbls.ThresholdAggregate, herumi.go:249-286, caller core/sigagg/sigagg.go:105).
-Inputs (compressed pubshares, partial signatures, messages, share indices) are resident in HBM
-before the timed region; outputs are per-item status bytes and 96-byte aggregates in HBM.
+One step = one attestation slot of BASELINE.json configs[2] ("C3", the largest single-GPU
+config): for V = 100 000 validators of a 10-operator threshold-7 cluster, each signing its own
+32-byte signing root,
+  1. hash the slot's 100 000 distinct signing roots to G2 (+ their Miller lines)
+  2. verify all V*n = 1 000 000 partial signatures            (tbls.Verify,
+     /root/reference/tbls/herumi.go:288-304; callers core/parsigex/parsigex.go:93-98)
+  3. threshold-aggregate every validator's first t = 7 partials  (tbls.ThresholdAggregate,
+     herumi.go:249-286; caller core/sigagg/sigagg.go:105)
+  4. verify every aggregate under the validator's DV public key (core/sigagg/sigagg.go:117).
+All of it is one hbls_slot_device call (include/hipbls.h).  Inputs (compressed pubshares, partial
+signatures, DV public keys, messages, share indices) are resident in HBM before the timed region;
+outputs are per-item status bytes and 96-byte aggregates in HBM.
 
-value = (verified partials + threshold aggregates) per second summed over all ranks.  Weak
-scaling: every rank owns its own V validators (validator sharding); with N > 1
-ranks each step ends with the RCCL all-gather of verdicts and aggregates over xGMI.
+value = (verified partials + threshold aggregates) per second summed over all ranks; the
+post-aggregate verifications are extra work not counted in it.  Weak scaling: every rank owns
+its own V validators (validator sharding); with N > 1 ranks each step ends with the
+library's RCCL all-gather of verdicts and aggregates over xGMI (hbls_allgather_device).
 
-roofline: integer VALU: k_verify's algorithmic 32-bit multiply-adds per launch
-divided by its HIP-event duration, against the measured v_mad_u64_u32 peak.
+roofline: integer VALU: the dominant kernel's algorithmic Fp products (textbook
+count, charon_amd/opcounts.py) x 300 multiply-adds, over its HIP-event time in the timed region,
+against the measured v_mad_u64_u32 peak.
 cpu_baseline: the same per-item arithmetic compiled for the host by g++ (tests/native/hostcheck.cpp,
 a port -- herumi and the Go toolchain are absent), timed on a bounded sample of validators.
 """
@@ -27,9 +32,10 @@ import argparse
 import ctypes
 import json
 import os
+import statistics
 import sys
+import threading
 import time
-from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 
@@ -37,25 +43,30 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
-from charon_amd.opcounts import FPMUL_PER_ITEM, MAC_PER_FPMUL, PEAK_MAD_TOPS  # noqa: E402
-from charon_amd.shard import SlotExchange, max_over_ranks, owned_validators  # noqa: E402
-
-N_LINES = 68  # Miller-loop lines per pairing (pairing.h)
+from charon_amd import opcounts  # noqa: E402
+from charon_amd.shard import max_over_ranks, owned_validators  # noqa: E402
 
 METRIC = "verified partial sigs/sec + ThresholdAggregate/sec per node, 1-8 MI355X"
 
 WORKLOADS = {
-    "c2": dict(validators=10_000, n=4, t=3, distinct=False, n_msgs=64,
-               desc="C2 (BASELINE configs[1]): 10k validators, 4-operator threshold-3 cluster, one attestation "
-                    "slot with 64 committee signing roots: 40k partial Verify + 10k ThresholdAggregate"),
     "c3": dict(validators=100_000, n=10, t=7, distinct=True, n_msgs=0,
                desc="C3 (BASELINE configs[2]): 100k validators, 10-operator threshold-7 cluster, distinct "
-                    "per-validator messages: 1M partial Verify + 100k ThresholdAggregate"),
+                    "per-validator messages: 1M partial Verify + 100k ThresholdAggregate (+100k aggregate Verify)"),
+    "c2": dict(validators=10_000, n=4, t=3, distinct=False, n_msgs=64,
+               desc="C2 (BASELINE configs[1]): 10k validators, 4-operator threshold-3 cluster, one attestation "
+                    "slot with 64 committee signing roots: 40k partial Verify + 10k ThresholdAggregate "
+                    "(+10k aggregate Verify)"),
+    "c4": dict(validators=125_000, n=7, t=5, distinct=False, n_msgs=64,
+               desc="C4 (BASELINE configs[3]) per-GPU shard: 1M validators over 8 GPUs = 125k validators, "
+                    "7-operator threshold-5 cluster, 64 committee signing roots: 875k partial Verify + 125k "
+                    "ThresholdAggregate (+125k aggregate Verify) per GPU"),
 }
 
 
 def _p(x) -> ctypes.c_void_p:
     """Device pointer of a torch tensor or host pointer of a numpy array."""
+    if x is None:
+        return None
     if isinstance(x, np.ndarray):
         return ctypes.c_void_p(x.ctypes.data)
     return ctypes.c_void_p(x.data_ptr())
@@ -79,7 +90,6 @@ def setup_inputs(L, wl, V, rank):
     msgs = np.frombuffer(b"".join(cl.msgs), dtype=np.uint8).copy()
     moff = (np.arange(M, dtype=np.uint64) * 32)
     mlen = np.full(M, 32, dtype=np.uint32)
-    # per-item message tables for the host-buffer sign calls
     item_msgs = msgs.reshape(M, 32)[midx].reshape(-1).copy()
     item_off = np.arange(NP, dtype=np.uint64) * 32
     item_len = np.full(NP, 32, dtype=np.uint32)
@@ -94,21 +104,25 @@ def setup_inputs(L, wl, V, rank):
     root_sks = np.frombuffer(b"".join(cl.root_sks), dtype=np.uint8).copy()
     root_msgs = msgs.reshape(M, 32)[msg_of_v].reshape(-1).copy()
     root_sigs = np.zeros(V * 96, dtype=np.uint8)
+    dv_pks = np.zeros(V * 48, dtype=np.uint8)
     stv = np.zeros(V, dtype=np.uint8)
     root_off = np.arange(V, dtype=np.uint64) * 32  # named: a temporary would be freed before the call
     root_len = np.full(V, 32, dtype=np.uint32)
     _chk(L, L.hbls_sign_batch(_p(root_sks), _p(root_msgs), _p(root_off), _p(root_len), V, _p(root_sigs),
                               _p(stv)))
     assert not stv.any(), "root signing failed"
+    _chk(L, L.hbls_secret_to_public_key_batch(_p(root_sks), V, _p(dv_pks), _p(stv)))
+    assert not stv.any(), "DV key derivation failed"
     # ThresholdAggregate input: shares 1..t of every validator (parsigdb fires with exactly t,
-    # core/parsigdb/memory.go:218-221)
-    sel = (np.arange(V)[:, None] * n + np.arange(t)[None, :]).reshape(-1)
-    ta_sigs = sigs.reshape(NP, 96)[sel].reshape(-1).copy()
+    # core/parsigdb/memory.go:218-221), given as indices of the verified partials
+    ta_src = (np.arange(V)[:, None] * n + np.arange(t)[None, :]).reshape(-1).astype(np.uint32)
+    ta_sigs = sigs.reshape(NP, 96)[ta_src].reshape(-1).copy()
     ta_idx = np.tile(np.arange(1, t + 1, dtype=np.int64), V)
     grp_off = (np.arange(V + 1, dtype=np.uint32) * t)
+    vgrp_off = (np.arange(V + 1, dtype=np.uint32) * n)  # one verification group per validator
     return dict(n=n, t=t, V=V, NP=NP, M=M, msgs=msgs, moff=moff, mlen=mlen, midx=midx, pks=pks, sigs=sigs,
-                item_msgs=item_msgs, item_off=item_off, item_len=item_len, ta_sigs=ta_sigs, ta_idx=ta_idx,
-                grp_off=grp_off, root_sigs=root_sigs)
+                item_msgs=item_msgs, item_off=item_off, item_len=item_len, ta_sigs=ta_sigs, ta_src=ta_src,
+                ta_idx=ta_idx, grp_off=grp_off, vgrp_off=vgrp_off, root_sigs=root_sigs, dv_pks=dv_pks)
 
 
 def cpu_baseline(d, seconds: float):
@@ -140,10 +154,81 @@ def cpu_baseline(d, seconds: float):
             "unit": "items/s (verified partial signatures + ThresholdAggregates)",
             "cores": threads, "kind": "port",
             "sample": f"{units} validators x ({n} partial Verify + 1 ThresholdAggregate of {t}) of the same "
-                      f"synthetic cluster; g++ -O2 build of the kernels' per-item arithmetic "
-                      f"(tests/native/hostcheck.cpp hc_cpu_slot, {threads} std::threads), one hash_to_G2 per "
-                      f"Verify as herumi does; not herumi (absent offline)",
+                      f"synthetic cluster; g++ -O3 -march=x86-64-v3 build of the kernels' per-item arithmetic "
+                      f"(tests/native/hostcheck.cpp hc_cpu_slot, {threads} std::threads), one hash_to_G2 and one "
+                      f"pairing check per Verify as herumi does; not herumi (absent offline), a lower bound on "
+                      f"a CPU backend's rate",
             "agrees_with_expected": bad == 0 and bad2 == 0, "wall_s": round(wall, 2)}
+
+
+def concurrent_callers(L, d, threads: int, seconds: float):
+    """Unchanged callers: `threads` host threads each calling hbls_verify_batch with ONE item in
+    a loop (tbls.Verify from one goroutine per libp2p stream, p2p/receive.go:52); the library
+    coalesces them.  Returns single-call latency (idle library) and N-thread throughput."""
+    NP = d["NP"]
+    pks, sigs, msgs = d["pks"], d["sigs"], d["item_msgs"]
+    off0 = np.zeros(1, dtype=np.uint64)
+    len32 = np.full(1, 32, dtype=np.uint32)
+    lat = []
+    for k in range(5):
+        st = np.zeros(1, dtype=np.uint8)
+        i = (k * 7919) % NP
+        t0 = time.perf_counter()
+        _chk(L, L.hbls_verify_batch(_p(pks[48 * i:]), _p(sigs[96 * i:]), _p(msgs[32 * i:]), _p(off0), _p(len32), 1,
+                                    _p(st)))
+        lat.append(time.perf_counter() - t0)
+        assert st[0] == 0
+    stop = time.perf_counter() + seconds
+    counts = [0] * threads
+    lats = [[] for _ in range(threads)]
+    bad = [0]
+
+    def worker(w):
+        st = np.zeros(1, dtype=np.uint8)
+        k = w
+        while time.perf_counter() < stop:
+            i = (k * 104729) % NP
+            t0 = time.perf_counter()
+            rc = L.hbls_verify_batch(_p(pks[48 * i:]), _p(sigs[96 * i:]), _p(msgs[32 * i:]), _p(off0), _p(len32),
+                                     1, _p(st))
+            lats[w].append(time.perf_counter() - t0)
+            if rc != 0 or st[0] != 0:
+                bad[0] += 1
+            counts[w] += 1
+            k += threads
+
+    t0 = time.perf_counter()
+    ths = [threading.Thread(target=worker, args=(w,)) for w in range(threads)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    wall = time.perf_counter() - t0
+    all_l = [x for l in lats for x in l]
+    return {"threads": threads, "calls_per_s": round(sum(counts) / wall, 1),
+            "mean_latency_ms": round(1e3 * statistics.mean(all_l), 2) if all_l else None,
+            "single_call_latency_ms": round(1e3 * statistics.median(lat), 2), "all_ok": bad[0] == 0,
+            "coalesce_us": int(os.environ.get("HBLS_COALESCE_US", "200"))}
+
+
+def roofline_from_timing(recs, steps, units):
+    """Per-kernel totals over the timed steps; the dominant kernel's roofline entry."""
+    tot, cnt = {}, {}
+    for name, ms in recs:
+        tot[name] = tot.get(name, 0.0) + ms
+        cnt[name] = cnt.get(name, 0) + 1
+    per = {}
+    for name in tot:
+        if name not in units:
+            continue
+        u, (alg, exe) = units[name]
+        t = tot[name] / steps * 1e-3  # s per step
+        per[name] = {"ms_per_step": round(tot[name] / steps, 3), "launches_per_step": cnt[name] / steps,
+                     "units_per_step": u, "fpmul_per_unit_alg": alg, "fpmul_per_unit_exec": exe,
+                     "achieved_Tops_alg": round(u * alg * opcounts.MAC_PER_FPMUL / t / 1e12, 3) if t > 0 else None,
+                     "achieved_Tops_exec": round(u * exe * opcounts.MAC_PER_FPMUL / t / 1e12, 3) if t > 0 else None}
+    dom = max(per, key=lambda k: per[k]["ms_per_step"]) if per else None
+    return dom, per
 
 
 def main(argv=None):
@@ -151,9 +236,11 @@ def main(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
     ap.add_argument("--validators", type=int, default=0, help="override validators per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample (0: skip)")
+    ap.add_argument("--callers", type=int, default=64, help="threads of the concurrent-caller measurement (0: skip)")
+    ap.add_argument("--callers-seconds", type=float, default=4.0)
     ap.add_argument("--host-api", action="store_true", help="also time the host-buffer (PCIe-inclusive) entry points")
     ap.add_argument("--mode", default="slot", choices=["slot", "staged"],
                     help="slot: one hbls_slot_device call per step (stages overlap); staged: stage by stage")
@@ -170,11 +257,11 @@ def main(argv=None):
 
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group("gloo")  # control plane only: the slot exchange is the library's RCCL
 
     from charon_amd import _lib
     L = _lib.load_library()
-    _chk(L, L.hbls_init(local))
+    _chk(L, L.hbls_init(1 << local))
 
     wl = WORKLOADS[args.workload]
     V = args.validators or wl["validators"]
@@ -187,35 +274,56 @@ def main(argv=None):
 
     d_msg, d_moff, d_mlen = up(d["msgs"]), up(d["moff"].view(np.int64)), up(d["mlen"].view(np.int32))
     d_midx, d_pk, d_sig = up(d["midx"].view(np.int32)), up(d["pks"]), up(d["sigs"])
-    d_tsig, d_tidx, d_goff = up(d["ta_sigs"]), up(d["ta_idx"]), up(d["grp_off"].view(np.int32))
+    d_tsrc, d_tidx, d_goff = up(d["ta_src"].view(np.int32)), up(d["ta_idx"]), up(d["grp_off"].view(np.int32))
+    d_vgoff, d_dvpk, d_tsig = up(d["vgrp_off"].view(np.int32)), up(d["dv_pks"]), up(d["ta_sigs"])
     d_hm = torch.zeros(M * L.hbls_hm_entry_bytes(), dtype=torch.uint8, device=dev)
     d_vst = torch.full((NP,), 255, dtype=torch.uint8, device=dev)
     d_tout = torch.zeros(V * 96, dtype=torch.uint8, device=dev)
     d_tst = torch.full((V,), 255, dtype=torch.uint8, device=dev)
-    xchg = SlotExchange(world, V, d["n"], dev) if world > 1 else None
+    d_ast = torch.full((V,), 255, dtype=torch.uint8, device=dev)
+
+    xchg = None
+    if world > 1:
+        # RCCL communicator of the library: rank 0's id travels over the gloo control plane
+        idb = np.zeros(L.hbls_comm_id_bytes(), dtype=np.uint8)
+        if rank == 0:
+            _chk(L, L.hbls_comm_unique_id(_p(idb)))
+        obj = [idb.tobytes()]
+        dist.broadcast_object_list(obj, src=0)
+        idb = np.frombuffer(obj[0], dtype=np.uint8).copy()
+        _chk(L, L.hbls_comm_init(world, rank, _p(idb)))
+        xchg = {"vst": torch.empty(world * NP, dtype=torch.uint8, device=dev),
+                "tout": torch.empty(world * V * 96, dtype=torch.uint8, device=dev),
+                "tst": torch.empty(world * V, dtype=torch.uint8, device=dev),
+                "ast": torch.empty(world * V, dtype=torch.uint8, device=dev)}
 
     stream = torch.cuda.Stream(device=dev)
     sp = ctypes.c_void_p(stream.cuda_stream)
+    slot = _lib.HblsSlot(msgs=_p(d_msg).value, msg_off=_p(d_moff).value, msg_len=_p(d_mlen).value, n_msgs=M,
+                         hm=_p(d_hm).value, pks=_p(d_pk).value, sigs=_p(d_sig).value, msg_idx=_p(d_midx).value, n=NP,
+                         vgrp_off=_p(d_vgoff).value, n_vgroups=V, vstatus=_p(d_vst).value, ta_sigs=None,
+                         ta_src=_p(d_tsrc).value, ta_idx=_p(d_tidx).value, grp_off=_p(d_goff).value, n_groups=V,
+                         n_ta_partials=V * t, ta_out=_p(d_tout).value, ta_status=_p(d_tst).value,
+                         dv_pks=_p(d_dvpk).value, agg_vstatus=_p(d_ast).value)
+
+    def exchange():  # all-gather verdicts + compressed aggregates to every rank (RCCL)
+        for src, dst in ((d_vst, "vst"), (d_tout, "tout"), (d_tst, "tst"), (d_ast, "ast")):
+            _chk(L, L.hbls_allgather_device(_p(src), _p(xchg[dst]), src.numel(), sp))
 
     def step_slot(ev):
-        # the slot entry point: hashing, verification and threshold aggregation overlap on the
-        # library's side streams; ordered on `stream`
         ev[0].record(stream)
-        _chk(L, L.hbls_slot_device(_p(d_msg), _p(d_moff), _p(d_mlen), M, _p(d_hm), _p(d_pk), _p(d_sig), _p(d_midx),
-                                   NP, _p(d_vst), _p(d_tsig), _p(d_tidx), _p(d_goff), V, V * t, _p(d_tout),
-                                   _p(d_tst), sp))
+        _chk(L, L.hbls_slot_device(ctypes.byref(slot), sp))
         ev[1].record(stream)
-        if world > 1:  # all-gather verdicts + compressed aggregates to every rank
-            with torch.cuda.stream(stream):
-                xchg.exchange(d_vst, d_tout, d_tst)
+        if world > 1:
+            exchange()
         ev[2].record(stream)
 
     def step_staged(ev):
-        # the same work stage by stage (no overlap): per-stage event timings
+        # the same work stage by stage (no overlap; the aggregation decompresses its own bytes)
         ev[0].record(stream)
         _chk(L, L.hbls_hash_to_g2_device(_p(d_msg), _p(d_moff), _p(d_mlen), M, _p(d_hm), sp))
         ev[1].record(stream)
-        _chk(L, L.hbls_verify_device(_p(d_pk), _p(d_sig), _p(d_midx), _p(d_hm), NP, _p(d_vst), sp))
+        _chk(L, L.hbls_verify_device(_p(d_pk), _p(d_sig), _p(d_midx), _p(d_hm), NP, _p(d_vgoff), V, _p(d_vst), sp))
         ev[2].record(stream)
         _chk(L, L.hbls_threshold_aggregate_device(_p(d_tsig), _p(d_tidx), _p(d_goff), V, V * t, _p(d_tout),
                                                   _p(d_tst), sp))
@@ -244,52 +352,61 @@ def main(argv=None):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        elapsed = max_over_ranks(elapsed, dev)
+        elapsed = max_over_ranks(elapsed, torch.device("cpu"))
 
     seg = np.array([[e[i].elapsed_time(e[i + 1]) for i in range(n_ev - 1)] for e in evs])  # ms
     k_ms = seg.mean(axis=0)
-    # k_pair3 (the dominant kernel) durations: HIP events the library records on its stream
-    pm = (ctypes.c_float * 4096)()
-    npm = ctypes.c_size_t(0)
-    _chk(L, L.hbls_timing_read(pm, 4096, ctypes.byref(npm)))
+    recs = _lib.timing_read(L)
     _chk(L, L.hbls_timing(0))
-    pair3_ms = float(np.sum(np.frombuffer(pm, dtype=np.float32, count=npm.value))) / args.steps
 
     # parity of the timed outputs: every partial verifies, every aggregate is byte-identical to the
-    # root-key signature (tbls_test.go:72-97 property), every status OK
+    # root-key signature (tbls_test.go:72-97 property) and verifies under the DV key
     vst = d_vst.cpu().numpy()
     tst = d_tst.cpu().numpy()
     tout = d_tout.cpu().numpy()
     parity = {"verify_all_ok": bool((vst == 0).all()), "ta_all_ok": bool((tst == 0).all()),
               "ta_equals_root_signature": bool(np.array_equal(tout, d["root_sigs"]))}
+    if not staged:
+        parity["aggregate_verify_all_ok"] = bool((d_ast.cpu().numpy() == 0).all())
     if world > 1:
-        parity["allgather_ok"] = xchg.all_ok()
+        parity["allgather_ok"] = bool((xchg["vst"] == 0).all().item() and (xchg["tst"] == 0).all().item() and
+                                      (xchg["ast"] == 0).all().item())
+        # rank r's block of the gathered aggregates is rank r's root signatures: check our own block
+        parity["allgather_own_block"] = bool(np.array_equal(
+            xchg["tout"][rank * V * 96:(rank + 1) * V * 96].cpu().numpy(), d["root_sigs"]))
 
     items = world * (NP + V)
     ms_per_step = elapsed / args.steps * 1e3
     value = items / (elapsed / args.steps)
 
-    fpmul_pair = FPMUL_PER_ITEM["k_pair3"]
-    t_pair = pair3_ms * 1e-3
-    pair_bytes = NP * (112 + 1 + 1 + 1 + 4 + 2 * N_LINES * 288 + 1)  # P, 3 status bytes, msg index, 2x68 lines, out
-    traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc_path):
-        with open(pmc_path) as f:
-            pmc = json.load(f).get(args.workload, {}).get("k_pair3")
-        if pmc and pmc.get("partials") == NP:
-            traffic = pmc["hbm_bytes_per_launch"]
-    achieved = NP * fpmul_pair * MAC_PER_FPMUL / t_pair / 1e12 if t_pair > 0 else None
-    roofline = {"bound": "valu", "kernel": "k_pair3", "achieved": achieved and round(achieved, 3),
-                "peak": PEAK_MAD_TOPS, "unit": "Tops/s (32-bit multiply-add lane-ops, v_mad_u64_u32)",
-                "frac": achieved and round(achieved / PEAK_MAD_TOPS, 4), "traffic": traffic,
-                "kernel_ms": round(pair3_ms, 3),
-                "algorithmic_work": f"{fpmul_pair} Fp-mul x {MAC_PER_FPMUL} MAC per partial x {NP} partials "
-                                    f"(2-pair Miller loop + final exponentiation, frozen r01 count)",
-                "algorithmic_bytes_per_launch": pair_bytes,
-                "hbm_GBps_algorithmic": round(pair_bytes / t_pair / 1e9, 3) if t_pair > 0 else None}
-    # whole Verify (decompression + lines + pairing) per partial, frozen r01 count, over the step
-    verify_effective = world * NP * FPMUL_PER_ITEM["k_verify"] * MAC_PER_FPMUL / (elapsed / args.steps) / 1e12
+    per_unit = opcounts.per_unit(group_size=n, t=t)
+    ta_units = V * t
+    units = {"k_pair3": (V, per_unit["k_pair3"]), "k_rlc": (NP + (0 if staged else V), per_unit["k_rlc"]),
+             "k_dec_pk": (NP + (0 if staged else V), per_unit["k_dec_pk"]),
+             "k_dec_sig_pt": (NP + (ta_units if staged else 0), per_unit["k_dec_sig_pt"]),
+             "k_group_prep": (V, opcounts.per_unit(group_size=n + (0 if staged else 1), t=t)["k_group_prep"]),
+             "k_ta_straus": (ta_units, per_unit["k_ta_straus"]), "k_group_sum": (V, per_unit["k_group_sum"]),
+             "k_hash_to_g2": (M, per_unit["k_hash_to_g2"]), "k_lines_msg": (M, per_unit["k_lines_msg"])}
+    dom, per = roofline_from_timing(recs, args.steps, units)
+    pair = per.get("k_pair3")
+    roofline = None
+    if dom:
+        x = per[dom]
+        roofline = {"bound": "valu", "kernel": dom, "unit_of_work": opcounts.UNITS.get(dom),
+                    "achieved": x["achieved_Tops_alg"], "peak": opcounts.PEAK_MAD_TOPS,
+                    "unit": "Tops/s (32-bit multiply-add lane-ops, v_mad_u64_u32)",
+                    "frac": round(x["achieved_Tops_alg"] / opcounts.PEAK_MAD_TOPS, 4),
+                    "frac_executed": round(x["achieved_Tops_exec"] / opcounts.PEAK_MAD_TOPS, 4),
+                    "frac_vs_nominal_clock": round(x["achieved_Tops_alg"] / opcounts.PEAK_MAD_TOPS_NOMINAL, 4),
+                    "traffic": None,
+                    "algorithmic_work": f"{x['units_per_step']} units x {x['fpmul_per_unit_alg']} Fp-mul x "
+                                        f"{opcounts.MAC_PER_FPMUL} MAC per step (executed {x['fpmul_per_unit_exec']} "
+                                        f"Fp-mul per unit)",
+                    "kernel_ms_per_step": x["ms_per_step"],
+                    "k_pair3": pair}
+    # whole-slot effective rate against the r01 (herumi-equivalent, one pairing per partial) work
+    verify_effective = world * NP * opcounts.FPMUL_PER_ITEM_R01["verify"] * opcounts.MAC_PER_FPMUL / \
+        (elapsed / args.steps) / 1e12
 
     out = {
         "metric": METRIC, "value": round(value, 1),
@@ -303,11 +420,13 @@ def main(argv=None):
                    "distinct_messages": M, "partials_per_gpu": NP, "parallelism": f"validator-sharded x{world}"},
         "verify_per_s": round(world * NP / (elapsed / args.steps), 1),
         "threshold_aggregate_per_s": round(world * V / (elapsed / args.steps), 1),
+        "aggregate_verify_per_s": None if staged else round(world * V / (elapsed / args.steps), 1),
         "mode": args.mode,
         "stage_ms": ({"hash_to_g2": round(k_ms[0], 3), "verify": round(k_ms[1], 3),
                       "threshold_aggregate": round(k_ms[2], 3)} if staged else
                      {"slot": round(k_ms[0], 3), "allgather": round(k_ms[1], 3)}),
-        "verify_whole_effective_Tops": round(verify_effective, 3),
+        "verify_whole_effective_Tops_vs_r01_work": round(verify_effective, 3),
+        "kernels": per,
         "parity": parity, "roofline": roofline, "cpu_baseline": None,
     }
 
@@ -321,11 +440,17 @@ def main(argv=None):
         _chk(L, L.hbls_threshold_aggregate_batch(_p(d["ta_sigs"]), _p(d["ta_idx"]), _p(d["grp_off"]), V,
                                                  _p(tout_h), _p(tst_h)))
         out["host_buffer_items_per_s"] = round((NP + V) / (time.perf_counter() - t0), 1)
+        out["host_buffer_parity"] = bool((st == 0).all() and (tst_h == 0).all() and
+                                         np.array_equal(tout_h, d["root_sigs"]))
+
+    if rank == 0 and world == 1 and args.callers > 0:
+        out["concurrent_callers"] = concurrent_callers(L, d, args.callers, args.callers_seconds)
 
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         out["cpu_baseline"] = cpu_baseline(d, args.cpu_seconds)
 
     if world > 1:
+        _chk(L, L.hbls_comm_destroy())
         dist.destroy_process_group()
     if rank == 0:
         print(json.dumps(out), flush=True)

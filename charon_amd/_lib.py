@@ -24,12 +24,24 @@ BAD_SECRET = 5
 BAD_INPUT = 6
 
 EXPORTS = (
-    "hbls_init", "hbls_last_error", "hbls_available", "hbls_verify_batch", "hbls_threshold_aggregate_batch",
-    "hbls_aggregate_batch", "hbls_verify_aggregate_batch", "hbls_sign_batch", "hbls_secret_to_public_key_batch",
-    "hbls_threshold_split", "hbls_recover_secret", "hbls_hash_to_g2_device", "hbls_verify_device",
-    "hbls_threshold_aggregate_device", "hbls_slot_device", "hbls_hm_entry_bytes", "hbls_sync",
-    "hbls_timing", "hbls_timing_read",
+    "hbls_init", "hbls_last_error", "hbls_available", "hbls_device_count", "hbls_verify_batch",
+    "hbls_threshold_aggregate_batch", "hbls_aggregate_batch", "hbls_verify_aggregate_batch", "hbls_sign_batch",
+    "hbls_secret_to_public_key_batch", "hbls_threshold_split", "hbls_recover_secret", "hbls_hash_to_g2_device",
+    "hbls_verify_device", "hbls_threshold_aggregate_device", "hbls_slot_device", "hbls_hm_entry_bytes", "hbls_sync",
+    "hbls_timing", "hbls_timing_read", "hbls_comm_id_bytes", "hbls_comm_unique_id", "hbls_comm_init",
+    "hbls_allgather_device", "hbls_comm_destroy", "hbls_stats",
 )
+
+ALL_DEVICES = 0xFFFFFFFF
+
+
+class HblsSlot(ctypes.Structure):
+    """struct hbls_slot (include/hipbls.h)."""
+    _fields_ = [(name, ctypes.c_void_p if kind == "p" else ctypes.c_size_t) for name, kind in (
+        ("msgs", "p"), ("msg_off", "p"), ("msg_len", "p"), ("n_msgs", "s"), ("hm", "p"),
+        ("pks", "p"), ("sigs", "p"), ("msg_idx", "p"), ("n", "s"), ("vgrp_off", "p"), ("n_vgroups", "s"),
+        ("vstatus", "p"), ("ta_sigs", "p"), ("ta_src", "p"), ("ta_idx", "p"), ("grp_off", "p"), ("n_groups", "s"),
+        ("n_ta_partials", "s"), ("ta_out", "p"), ("ta_status", "p"), ("dv_pks", "p"), ("agg_vstatus", "p"))]
 
 
 class HipBlsUnavailable(RuntimeError):
@@ -49,9 +61,10 @@ def _declare(lib):
     SZ = ctypes.c_size_t
     U32 = ctypes.c_uint32
     sig = {
-        "hbls_init": ([ctypes.c_int], ctypes.c_int),
+        "hbls_init": ([ctypes.c_uint32], ctypes.c_int),
         "hbls_last_error": ([], ctypes.c_char_p),
         "hbls_available": ([], ctypes.c_int),
+        "hbls_device_count": ([], ctypes.c_int),
         "hbls_verify_batch": ([P, P, P, P, P, SZ, P], ctypes.c_int),
         "hbls_threshold_aggregate_batch": ([P, P, P, SZ, P, P], ctypes.c_int),
         "hbls_aggregate_batch": ([P, P, SZ, P, P], ctypes.c_int),
@@ -61,13 +74,19 @@ def _declare(lib):
         "hbls_threshold_split": ([P, P, U32, U32, P, P], ctypes.c_int),
         "hbls_recover_secret": ([P, P, SZ, P, P], ctypes.c_int),
         "hbls_hash_to_g2_device": ([P, P, P, SZ, P, P], ctypes.c_int),
-        "hbls_verify_device": ([P, P, P, P, SZ, P, P], ctypes.c_int),
+        "hbls_verify_device": ([P, P, P, P, SZ, P, SZ, P, P], ctypes.c_int),
         "hbls_threshold_aggregate_device": ([P, P, P, SZ, SZ, P, P, P], ctypes.c_int),
-        "hbls_slot_device": ([P, P, P, SZ, P, P, P, P, SZ, P, P, P, P, SZ, SZ, P, P, P], ctypes.c_int),
+        "hbls_slot_device": ([ctypes.POINTER(HblsSlot), P], ctypes.c_int),
         "hbls_hm_entry_bytes": ([], SZ),
         "hbls_sync": ([P], ctypes.c_int),
         "hbls_timing": ([ctypes.c_int], ctypes.c_int),
-        "hbls_timing_read": ([P, SZ, P], ctypes.c_int),
+        "hbls_timing_read": ([P, P, SZ, P], ctypes.c_int),
+        "hbls_comm_id_bytes": ([], SZ),
+        "hbls_comm_unique_id": ([P], ctypes.c_int),
+        "hbls_comm_init": ([ctypes.c_int, ctypes.c_int, P], ctypes.c_int),
+        "hbls_allgather_device": ([P, P, SZ, P], ctypes.c_int),
+        "hbls_comm_destroy": ([], ctypes.c_int),
+        "hbls_stats": ([P, SZ], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)
@@ -88,12 +107,22 @@ def load_library(path: str = LIB_PATH):
         return _lib
 
 
-def lib():
-    """The library, initialised on a gfx950 device; raises if that is impossible."""
+def lib(device_mask: int = 0):
+    """The library, initialised on its gfx950 devices (mask 0: HBLS_DEVICE_MASK or device 0);
+    raises if that is impossible."""
     L = load_library()
-    if L.hbls_init(-1) != 0:
+    if L.hbls_init(device_mask) != 0:
         raise HipBlsUnavailable("hipbls: " + L.hbls_last_error().decode(errors="replace"))
     return L
+
+
+def timing_read(L, max_n: int = 1 << 16):
+    """[(kernel name, ms)] of the launches recorded since hbls_timing(1)."""
+    names = (ctypes.c_char_p * max_n)()
+    ms = (ctypes.c_float * max_n)()
+    n = ctypes.c_size_t(0)
+    check(L.hbls_timing_read(names, ms, max_n, ctypes.byref(n)))
+    return [(names[i].decode(), float(ms[i])) for i in range(n.value)]
 
 
 def check(rc: int):

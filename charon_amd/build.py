@@ -17,8 +17,8 @@ CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "lib", "libhipbls.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
-SOURCES = ["hipbls.hip", "pipeline.hip", "threshold.hip"]
-HEADERS = ["hd.h", "consts.h", "fp.h", "fr.h", "tower.h", "ec.h", "sha256.h", "h2c.h", "pairing.h", "ops.h", "pair3.h", "fpmul_asm.inc", "layout.h"]
+SOURCES = ["hipbls.hip", "pipeline.hip", "threshold.hip", "vbatch.hip", "vgroup.hip"]
+HEADERS = ["hd.h", "consts.h", "fp.h", "fr.h", "tower.h", "ec.h", "sha256.h", "h2c.h", "pairing.h", "ops.h", "pair3.h", "fpmul_asm.inc", "layout.h", "lines.h", "rlc.h"]
 
 
 def _newer(target, deps):
@@ -44,8 +44,8 @@ def build_library(force: bool = False, verbose: bool = True) -> str:
     for p in procs:
         if p.wait(timeout=3000) != 0:
             raise RuntimeError("hipcc failed")
-    subprocess.run([HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", LIB + ".tmp"] + objs, check=True,
-                   timeout=600)
+    subprocess.run([HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", LIB + ".tmp"] + objs +
+                   ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"], check=True, timeout=600)
     os.replace(LIB + ".tmp", LIB)
     if verbose:
         print(f"built {LIB} in {time.time() - t:.1f}s")
@@ -58,7 +58,7 @@ def build_hostcheck(force: bool = False, verbose: bool = True) -> str:
     deps = [src] + [os.path.join(CSRC, f) for f in HEADERS]
     if not force and _newer(out, deps):
         return out
-    cmd = ["g++", "-O2", "-std=c++17", "-pthread", "-shared", "-fPIC", "-o", out + ".tmp", src]
+    cmd = ["g++", "-O3", "-march=x86-64-v3", "-std=c++17", "-pthread", "-shared", "-fPIC", "-o", out + ".tmp", src]
     subprocess.run(cmd, check=True, timeout=900)
     os.replace(out + ".tmp", out)
     if verbose:

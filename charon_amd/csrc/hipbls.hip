@@ -1,61 +1,49 @@
 // libhipbls.so: gfx950 kernels + C ABI (include/hipbls.h) for charon's BLS hot path.
 //
 // Reference interface replaced: tbls.Implementation (/root/reference/tbls/tbls.go:27-69) as
-// implemented by tbls.Herumi (/root/reference/tbls/herumi.go).  One lane = one item
-// (partial signature, group or message); kernels are staged so that work shared between
-// items (hash_to_curve of a message) runs once.
+// implemented by tbls.Herumi (/root/reference/tbls/herumi.go).  This file holds the one-lane
+// kernels of the cold entry points (Sign, SecretToPublicKey, split/recover, group sums) and the
+// host runtime: per-device contexts (one process may drive every GPU in its device mask),
+// workspace sets ordered by events, the batched verification pipeline, a coalescing queue for
+// concurrent callers (charon calls tbls.Verify from one goroutine per libp2p stream,
+// p2p/receive.go:52) and the RCCL exchange of slot results between processes.
 #include "layout.h"
 #include "../../include/hipbls.h"
 
+#include <rccl/rccl.h>
+#include <sys/random.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <functional>
 #include <mutex>
+#include <numeric>
 #include <string>
 #include <string.h>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
 using namespace hb;
 
-
 #define KERNEL_BOUNDS __launch_bounds__(64)
 constexpr int BLOCK = 64;
 
 // ---------------------------------------------------------------------------------------
-// Kernels
+// One-lane kernels (standard calling convention product: code size over speed)
 // ---------------------------------------------------------------------------------------
-
-__device__ __forceinline__ uint32_t find_group(const uint32_t* grp_off, uint32_t n_groups, uint32_t j) {
-  // largest g with grp_off[g] <= j  (groups may be empty)
-  uint32_t lo = 0, hi = n_groups;  // invariant: grp_off[lo] <= j < grp_off[hi]
-  while (hi - lo > 1) {
-    uint32_t mid = (lo + hi) >> 1;
-    if (grp_off[mid] <= j) lo = mid;
-    else hi = mid;
-  }
-  return lo;
-}
-
-// One lane per partial: decompress + subgroup-check sigma_j (herumi.go:257 Sign.Deserialize).
-__global__ KERNEL_BOUNDS void k_ta_dec(const uint8_t* __restrict__ sigs, uint32_t n_partials,
-                                               HmEntry* __restrict__ pts, uint8_t* __restrict__ mstat) {
-  uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= n_partials) return;
-  G2A s;
-  uint8_t bad = g2_decompress(s, sigs + 96ull * j);
-  HmEntry e;
-  e.x = s.x;
-  e.y = s.y;
-  e.inf = (!bad && s.inf) ? 1u : 0u;
-  e.pad[0] = e.pad[1] = e.pad[2] = 0;
-  pts[j] = e;
-  mstat[j] = bad ? M_BAD_SIG : M_OK;
-}
 
 // One lane per group: sum the member points, compress (herumi Sign.Recover / Sign.Aggregate +
 // Serialize).  Status precedence follows herumi: any undecodable partial -> BAD_SIGNATURE
-// (deserialisation happens first, herumi.go:255-264), then combine failure.
+// (deserialisation happens first, herumi.go:255-264), then combine failure.  agg_pt (nullable):
+// the affine result, for the folded post-aggregate verification of the slot entry point.
 __global__ KERNEL_BOUNDS void k_group_sum(const uint32_t* __restrict__ grp_off, uint32_t n_groups, int mode,
                                           const G2JEntry* __restrict__ pts, const uint8_t* __restrict__ mstat,
-                                          uint8_t* __restrict__ out, uint8_t* __restrict__ status) {
+                                          uint8_t* __restrict__ out, uint8_t* __restrict__ status,
+                                          HmEntry* __restrict__ agg_pt) {
   uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= n_groups) return;
   uint32_t b = grp_off[g], e = grp_off[g + 1];
@@ -72,6 +60,7 @@ __global__ KERNEL_BOUNDS void k_group_sum(const uint32_t* __restrict__ grp_off, 
   if (st != ST_OK) {
     for (int k = 0; k < 96; k++) o[k] = 0;
     status[g] = st;
+    if (agg_pt) agg_pt[g].inf = 1;
     return;
   }
   G2J acc = jac_infinity<Fp2>();
@@ -79,10 +68,19 @@ __global__ KERNEL_BOUNDS void k_group_sum(const uint32_t* __restrict__ grp_off, 
     G2JEntry q = pts[m];
     acc = jac_add(acc, G2J{q.X, q.Y, q.Z});
   }
+  const G2A a = jac_to_aff(acc);
   uint8_t buf[96];
-  g2_compress(buf, jac_to_aff(acc));
+  g2_compress(buf, a);
   for (int k = 0; k < 96; k++) o[k] = buf[k];
   status[g] = ST_OK;
+  if (agg_pt) {
+    HmEntry h;
+    h.x = a.x;
+    h.y = a.y;
+    h.inf = a.inf ? 1u : 0u;
+    h.pad[0] = h.pad[1] = h.pad[2] = 0;
+    agg_pt[g] = h;
+  }
 }
 
 // VerifyAggregate stage 1: one lane per public key.
@@ -232,109 +230,23 @@ __global__ void k_recover(const uint8_t* __restrict__ shares, const int64_t* __r
 }
 
 // ---------------------------------------------------------------------------------------
-// Host runtime: device selection, grow-only workspaces, error reporting
+// Host runtime
 // ---------------------------------------------------------------------------------------
 namespace {
 
 thread_local std::string g_err;
-std::mutex g_mu;  // serialises host-buffer calls (shared workspace)
-int g_device = -1;
-hipStream_t g_stream = nullptr;
-// fork/join streams: 0, 1 = the staged verify's decompression kernels, 2 = message hashing,
-// 3 = unused (hbls_slot_device runs its ThresholdAggregate on g_stream)
-constexpr int N_SIDE = 4;
-hipStream_t g_side[N_SIDE] = {};
-hipEvent_t g_ev_fork = nullptr, g_ev_slot = nullptr, g_ev_side[N_SIDE] = {};
 
-// optional timing of the pairing kernel (hbls_timing): event pairs recorded on its stream
-bool g_timing = false;
-std::vector<std::pair<hipEvent_t, hipEvent_t>> g_tev;  // pool
-size_t g_tev_used = 0;
-int timing_pair(hipEvent_t* a, hipEvent_t* b);
-
-struct DevBuf {
-  void* p = nullptr;
-  size_t cap = 0;
-};
-
-enum BufId {
-  B_PK, B_SIG, B_MSG, B_OFF, B_LEN, B_MIDX, B_HM, B_STAT, B_IDX, B_GOFF, B_PTS, B_MSTAT, B_OUT, B_SK, B_G1PTS,
-  B_VPK, B_VPKST, B_VSIGINF, B_VSIGST, B_VLINES,  // staged verify: per-partial intermediates
-  B_TAPTS, B_TADIG, B_TATAB,                      // staged ThresholdAggregate
-  B_COUNT
-};
-DevBuf g_bufs[B_COUNT];
-
-int set_err(const char* what, hipError_t e) {
-  g_err = std::string(what) + ": " + hipGetErrorString(e);
+int set_err(const std::string& what) {
+  g_err = what;
   return -1;
 }
+int set_err(const char* what, hipError_t e) { return set_err(std::string(what) + ": " + hipGetErrorString(e)); }
 
 #define HCHK(expr)                                         \
   do {                                                     \
     hipError_t _e = (expr);                                \
     if (_e != hipSuccess) return set_err(#expr, _e);       \
   } while (0)
-
-int ensure(BufId id, size_t bytes, void** out) {
-  DevBuf& b = g_bufs[id];
-  if (bytes == 0) bytes = 16;
-  if (b.cap < bytes) {
-    if (b.p) HCHK(hipFree(b.p));
-    size_t cap = bytes + bytes / 4;
-    HCHK(hipMalloc(&b.p, cap));
-    b.cap = cap;
-  }
-  *out = b.p;
-  return 0;
-}
-
-int timing_pair(hipEvent_t* a, hipEvent_t* b) {
-  if (g_tev_used == g_tev.size()) {
-    hipEvent_t x, y;
-    HCHK(hipEventCreate(&x));
-    HCHK(hipEventCreate(&y));
-    g_tev.push_back({x, y});
-  }
-  *a = g_tev[g_tev_used].first;
-  *b = g_tev[g_tev_used].second;
-  g_tev_used++;
-  return 0;
-}
-
-int init_locked(int device) {
-  if (g_device >= 0) {
-    HCHK(hipSetDevice(g_device));
-    return 0;
-  }
-  int n = 0;
-  HCHK(hipGetDeviceCount(&n));
-  if (n <= 0) {
-    g_err = "no HIP device";
-    return -1;
-  }
-  if (device < 0) device = 0;
-  HCHK(hipSetDevice(device));
-  hipDeviceProp_t prop;
-  HCHK(hipGetDeviceProperties(&prop, device));
-  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
-    g_err = std::string("libhipbls is built for gfx950, device is ") + prop.gcnArchName;
-    return -1;
-  }
-  // the verify pipeline's streams (decompression, hashing) get the highest priority: they gate the
-  // pairing kernel, while the aggregation chain on g_stream (lowest priority) has slack in the slot
-  int prio_lo = 0, prio_hi = 0;
-  HCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
-  HCHK(hipStreamCreateWithPriority(&g_stream, hipStreamNonBlocking, prio_lo));
-  for (int k = 0; k < N_SIDE; k++) {
-    HCHK(hipStreamCreateWithPriority(&g_side[k], hipStreamNonBlocking, prio_hi));
-    HCHK(hipEventCreateWithFlags(&g_ev_side[k], hipEventDisableTiming));
-  }
-  HCHK(hipEventCreateWithFlags(&g_ev_fork, hipEventDisableTiming));
-  HCHK(hipEventCreateWithFlags(&g_ev_slot, hipEventDisableTiming));
-  g_device = device;
-  return 0;
-}
 
 inline unsigned blocks_for(size_t n) { return (unsigned)((n + BLOCK - 1) / BLOCK); }
 
@@ -346,28 +258,492 @@ inline unsigned blocks_for(size_t n) { return (unsigned)((n + BLOCK - 1) / BLOCK
     }                                                                                             \
   } while (0)
 
+size_t env_size(const char* name, size_t dflt) {
+  const char* v = getenv(name);
+  if (!v || !*v) return dflt;
+  char* end = nullptr;
+  unsigned long long x = strtoull(v, &end, 0);
+  return (end && *end == 0) ? (size_t)x : dflt;
+}
+
+// Verification groups are chunked for the line buffers: GCAP groups per pairing launch, FB_CAP
+// fallback items per pass (HBLS_GROUP_CHUNK / HBLS_FALLBACK_CHUNK).  Host-buffer calls build
+// groups of at most GMAX items over one message (HBLS_GROUP_MAX).
+size_t g_gcap = 131072, g_fbcap = 65536, g_gmax = 16;
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+};
+
+// workspace buffers of one set
+enum WsId {
+  W_VPK, W_VPKST, W_VSIG, W_VSIGST, W_IGRP, W_PR, W_SR, W_GP, W_GST, W_GMSG, W_GVER, W_GLINES, W_LIST, W_COUNT,
+  W_FBLINES,
+  W_APK, W_APKST, W_ASIG, W_APR, W_ASR,          // folded aggregates (post-aggregate verification)
+  W_TAPTS, W_TADST, W_TAMST, W_TADIG, W_TATAB, W_TAJ,  // ThresholdAggregate / Aggregate
+  W_COUNT_
+};
+
+// A workspace set: grow-only device buffers plus the event recorded after the last kernel that
+// used them.  Every user waits on `free_ev` in each stream it launches on before touching the
+// set, so two calls never share a set concurrently, whatever streams they run on.
+struct Ws {
+  DevBuf b[W_COUNT_];
+  hipEvent_t free_ev = nullptr;
+  bool used = false;
+};
+
+// host-call staging buffers (inputs and outputs of the host-buffer entry points)
+enum IoId { I_PK, I_SIG, I_MSG, I_OFF, I_LEN, I_MIDX, I_HM, I_STAT, I_IDX, I_GOFF, I_OUT, I_SK, I_VGOFF, I_COUNT };
+
+constexpr int N_SIDE = 4;
+constexpr int N_WS = 2;
+
+struct Timed {
+  const char* name;
+  hipEvent_t a, b;
+};
+
+struct Dev {
+  int ord = -1;
+  hipStream_t stream = nullptr;  // the library stream of host-buffer calls
+  hipStream_t side[N_SIDE] = {};
+  hipEvent_t ev_fork = nullptr, ev_side[N_SIDE] = {}, ev_join = nullptr, ev_ta = nullptr;
+  Ws ws[N_WS];
+  unsigned next_ws = 0;
+  DevBuf io[I_COUNT];
+  std::mutex mu;  // one call at a time enqueues on this device
+  // timing (hbls_timing)
+  bool timing = false;
+  std::vector<Timed> tev;
+  size_t tev_used = 0;
+};
+
+std::mutex g_init_mu;
+std::vector<Dev*> g_devs;  // in device-mask order
+uint32_t g_mask = 0;
+std::atomic<bool> g_ready{false};
+
+int ensure_buf(DevBuf& b, size_t bytes, void** out) {
+  if (bytes == 0) bytes = 16;
+  if (b.cap < bytes) {
+    if (b.p) HCHK(hipFree(b.p));
+    b.p = nullptr;
+    size_t cap = bytes + bytes / 4;
+    HCHK(hipMalloc(&b.p, cap));
+    b.cap = cap;
+  }
+  *out = b.p;
+  return 0;
+}
+
 template <class T>
-int upload(BufId id, const T* src, size_t count, T** dst) {
+int wsbuf(Ws& w, WsId id, size_t count, T** out) {
+  // growing a buffer frees the old one: its last user (on any stream) must be done with it
+  if (w.used && w.b[id].cap < std::max<size_t>(count * sizeof(T), 16)) HCHK(hipEventSynchronize(w.free_ev));
   void* p;
-  if (ensure(id, count * sizeof(T), &p)) return -1;
-  if (count) HCHK(hipMemcpyAsync(p, src, count * sizeof(T), hipMemcpyHostToDevice, g_stream));
+  if (ensure_buf(w.b[id], count * sizeof(T), &p)) return -1;
+  *out = (T*)p;
+  return 0;
+}
+
+// Acquire a workspace set for a call whose kernels run on `streams`.
+Ws& ws_acquire(Dev& d, std::initializer_list<hipStream_t> streams) {
+  Ws& w = d.ws[d.next_ws++ % N_WS];
+  if (w.used)
+    for (hipStream_t s : streams) (void)hipStreamWaitEvent(s, w.free_ev, 0);
+  return w;
+}
+int ws_release(Ws& w, hipStream_t last) {
+  HCHK(hipEventRecord(w.free_ev, last));
+  w.used = true;
+  return 0;
+}
+
+// --- timing of kernel launches (hbls_timing): event pairs on the launch's stream -------------
+int timed_begin(Dev& d, const char* name, hipStream_t s, Timed** t) {
+  *t = nullptr;
+  if (!d.timing) return 0;
+  if (d.tev_used == d.tev.size()) {
+    Timed x{name, nullptr, nullptr};
+    HCHK(hipEventCreate(&x.a));
+    HCHK(hipEventCreate(&x.b));
+    d.tev.push_back(x);
+  }
+  Timed& x = d.tev[d.tev_used++];
+  x.name = name;
+  HCHK(hipEventRecord(x.a, s));
+  *t = &x;
+  return 0;
+}
+int timed_end(Timed* t, hipStream_t s) {
+  if (t) HCHK(hipEventRecord(t->b, s));
+  return 0;
+}
+#define TIMED(dev, name, s, call)                  \
+  do {                                             \
+    Timed* _t;                                     \
+    if (timed_begin((dev), (name), (s), &_t)) return -1; \
+    call;                                          \
+    HCHK(hipGetLastError());                       \
+    if (timed_end(_t, (s))) return -1;             \
+  } while (0)
+
+int dev_create(int ord, Dev** out) {
+  HCHK(hipSetDevice(ord));
+  hipDeviceProp_t prop;
+  HCHK(hipGetDeviceProperties(&prop, ord));
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return set_err(std::string("libhipbls is built for gfx950, device ") + std::to_string(ord) + " is " +
+                   prop.gcnArchName);
+  Dev* d = new Dev();
+  d->ord = ord;
+  // the verification's side streams (decompression, hashing) get the highest priority: they
+  // gate the pairing kernel; the library stream is the lowest
+  int prio_lo = 0, prio_hi = 0;
+  HCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+  HCHK(hipStreamCreateWithPriority(&d->stream, hipStreamNonBlocking, prio_lo));
+  for (int k = 0; k < N_SIDE; k++) {
+    HCHK(hipStreamCreateWithPriority(&d->side[k], hipStreamNonBlocking, k == 3 ? prio_lo : prio_hi));
+    HCHK(hipEventCreateWithFlags(&d->ev_side[k], hipEventDisableTiming));
+  }
+  HCHK(hipEventCreateWithFlags(&d->ev_fork, hipEventDisableTiming));
+  HCHK(hipEventCreateWithFlags(&d->ev_join, hipEventDisableTiming));
+  HCHK(hipEventCreateWithFlags(&d->ev_ta, hipEventDisableTiming));
+  for (auto& w : d->ws) HCHK(hipEventCreateWithFlags(&w.free_ev, hipEventDisableTiming));
+  *out = d;
+  return 0;
+}
+
+// hbls_init: mask 0 = HBLS_DEVICE_MASK from the environment, else device 0; 0xffffffff = every
+// visible device.  Idempotent for the same mask; a different mask afterwards is an error.
+int init_mask(uint32_t mask) {
+  if (g_ready.load()) {
+    if (mask != 0 && mask != g_mask && !(mask == 0xffffffffu && g_mask == ((1u << g_devs.size()) - 1)))
+      return set_err("hipbls already initialised with device mask " + std::to_string(g_mask));
+    return 0;
+  }
+  std::lock_guard<std::mutex> lk(g_init_mu);
+  if (g_ready.load()) return init_mask(mask);
+  int n = 0;
+  HCHK(hipGetDeviceCount(&n));
+  if (n <= 0) return set_err("no HIP device");
+  if (mask == 0) mask = (uint32_t)env_size("HBLS_DEVICE_MASK", 1);
+  const uint32_t visible = n >= 32 ? 0xffffffffu : ((1u << n) - 1);
+  if (mask == 0xffffffffu) mask = visible;
+  if ((mask & visible) != mask || mask == 0)
+    return set_err("device mask " + std::to_string(mask) + " names devices that are not visible (" +
+                   std::to_string(n) + " devices)");
+  g_gcap = env_size("HBLS_GROUP_CHUNK", g_gcap);
+  g_fbcap = env_size("HBLS_FALLBACK_CHUNK", g_fbcap);
+  g_gmax = std::max<size_t>(1, env_size("HBLS_GROUP_MAX", g_gmax));
+  std::vector<Dev*> devs;
+  for (int k = 0; k < 32; k++)
+    if (mask & (1u << k)) {
+      Dev* d;
+      if (dev_create(k, &d)) return -1;
+      devs.push_back(d);
+    }
+  g_devs = devs;
+  g_mask = mask;
+  g_ready.store(true);
+  return 0;
+}
+
+int ensure_init() { return g_ready.load() ? 0 : init_mask(0); }
+
+// the device of a caller's stream (device entry points); stream 0: the first device
+int dev_of_stream(hipStream_t s, Dev** out) {
+  if (ensure_init()) return -1;
+  int ord = g_devs[0]->ord;
+  if (s) {
+    hipDevice_t dv;
+    HCHK(hipStreamGetDevice(s, &dv));
+    ord = (int)dv;
+  }
+  for (Dev* d : g_devs)
+    if (d->ord == ord) {
+      HCHK(hipSetDevice(ord));
+      *out = d;
+      return 0;
+    }
+  return set_err("stream belongs to device " + std::to_string(ord) + ", outside the library's device mask");
+}
+
+template <class T>
+int upload(Dev& d, IoId id, const T* src, size_t count, T** dst) {
+  void* p;
+  if (ensure_buf(d.io[id], count * sizeof(T), &p)) return -1;
+  if (count) HCHK(hipMemcpyAsync(p, src, count * sizeof(T), hipMemcpyHostToDevice, d.stream));
   *dst = (T*)p;
   return 0;
 }
 
-// Deduplicate messages: returns packed table + per-item index (host-side bookkeeping only).
+// per-call random linear combination key (OS CSPRNG)
+int rlc_key(RlcKey& k) {
+  uint8_t* p = reinterpret_cast<uint8_t*>(k.w);
+  size_t got = 0;
+  while (got < sizeof(k.w)) {
+    ssize_t r = getrandom(p + got, sizeof(k.w) - got, 0);
+    if (r <= 0) return set_err("getrandom failed");
+    got += (size_t)r;
+  }
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------
+// Batched verification of n partials already in device memory (vbatch.hip):
+//   side 0: k_dec_pk            side 1: k_dec_sig_pt
+//   s:      k_item_group, k_rlc, then per chunk of groups k_group_prep -> k_pair3,
+//           k_scatter, then the fallback passes (k_fb_lines -> k_pair3 over the listed items)
+// Optional fold of the slot's ThresholdAggregate (reusing the decompressed partials) and of the
+// post-aggregate verification under the DV keys (sigagg.go:117) into the same groups.
+// ---------------------------------------------------------------------------------------
+// verification statistics (HBLS_STATS=1): items, groups, items re-checked alone
+std::atomic<uint64_t> g_stats[3];
+bool stats_on() {
+  const char* v = getenv("HBLS_STATS");
+  return v && v[0] == '1';
+}
+
+struct TaFold {
+  // aggregation members: verified partial src[j] (src == nullptr: decompress sigs instead)
+  const uint8_t* ta_sigs;
+  const uint32_t* ta_src;
+  const int64_t* ta_idx;
+  const uint32_t* grp_off;
+  size_t n_groups, n_partials;
+  uint8_t* ta_out;
+  uint8_t* ta_status;
+  // post-aggregate verification (nullable): DV public key per group, verdict per group
+  const uint8_t* dv_pks;
+  uint8_t* agg_status;
+};
+
+// ThresholdAggregate (mode 0) / Aggregate (mode 1) of groups whose members are already
+// decompressed (pts, mst) into ta_out / ta_status; agg_pt (nullable) gets the affine results.
+int ta_tail(Dev& d, Ws& w, const HmEntry* pts, const uint32_t* src, const uint8_t* mst_in, const int64_t* didx,
+            const uint32_t* dgoff, size_t n_groups, size_t np, int mode, uint8_t* out, uint8_t* status,
+            HmEntry* agg_pt, hipStream_t s) {
+  uint8_t* mst;
+  TaDigits* dig;
+  void* tab;
+  G2JEntry* pj;
+  if (wsbuf(w, W_TAMST, np, &mst) || wsbuf(w, W_TADIG, np, &dig) || wsbuf(w, W_TAJ, np, &pj)) return -1;
+  if (wsbuf(w, W_TATAB, ta_table_bytes((uint32_t)np), (uint8_t**)&tab)) return -1;
+  if (np) {
+    if (src) launch_ta_member_status(mst_in, src, (uint32_t)np, mst, s);
+    else HCHK(hipMemcpyAsync(mst, mst_in, np, hipMemcpyDeviceToDevice, s));
+    HCHK(hipGetLastError());
+    TIMED(d, "k_ta_lambda", s, launch_ta_lambda(didx, dgoff, (uint32_t)n_groups, (uint32_t)np, mode, dig, mst, s));
+    TIMED(d, "k_ta_straus", s, launch_ta_straus(pts, src, dig, (uint32_t)np, tab, pj, s));
+  }
+  TIMED(d, "k_group_sum", s,
+        LAUNCH(k_group_sum, n_groups, s, dgoff, (uint32_t)n_groups, mode, (const G2JEntry*)pj, (const uint8_t*)mst,
+               out, status, agg_pt));
+  return 0;
+}
+
+int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, const uint32_t* didx,
+                    const MsgEntry* hm, size_t n, const uint32_t* dgoff, size_t n_groups, uint8_t* dst,
+                    hipStream_t s, hipEvent_t hm_ready, const TaFold* fold) {
+  if (!dgoff) n_groups = n;
+  G1AEntry* vpk;
+  HmEntry* vsig;
+  uint8_t *vpkst, *vsigst, *gst, *gver;
+  uint32_t *igrp, *gmsg, *list, *count;
+  G1JEntry* pr;
+  G2JEntry* sr;
+  G1AEntry* gP;
+  LineEntry *glines, *fbl;
+  const size_t gcap = std::min(g_gcap, std::max<size_t>(n_groups, 1));
+  const size_t n_agg = (fold && fold->dv_pks) ? fold->n_groups : 0;
+  const size_t fbcap = std::min(g_fbcap, std::max<size_t>(n + n_agg, 1));
+  if (wsbuf(w, W_VPK, n, &vpk) || wsbuf(w, W_VPKST, n, &vpkst) || wsbuf(w, W_VSIG, n, &vsig) ||
+      wsbuf(w, W_VSIGST, n, &vsigst) || wsbuf(w, W_IGRP, n, &igrp) || wsbuf(w, W_PR, n, &pr) ||
+      wsbuf(w, W_SR, n, &sr) || wsbuf(w, W_GP, gcap, &gP) || wsbuf(w, W_GST, gcap, &gst) ||
+      wsbuf(w, W_GMSG, n_groups, &gmsg) || wsbuf(w, W_GVER, n_groups, &gver) ||
+      wsbuf(w, W_GLINES, gcap * N_LINES, &glines) || wsbuf(w, W_LIST, n + n_agg, &list) ||
+      wsbuf(w, W_COUNT, 1, &count) || wsbuf(w, W_FBLINES, fbcap * N_LINES, &fbl))
+    return -1;
+  G1AEntry* apk = nullptr;
+  uint8_t* apkst = nullptr;
+  HmEntry* asig = nullptr;
+  G1JEntry* apr = nullptr;
+  G2JEntry* asr = nullptr;
+  if (n_agg && (wsbuf(w, W_APK, n_agg, &apk) || wsbuf(w, W_APKST, n_agg, &apkst) ||
+                wsbuf(w, W_ASIG, n_agg, &asig) || wsbuf(w, W_APR, n_agg, &apr) || wsbuf(w, W_ASR, n_agg, &asr)))
+    return -1;
+  RlcKey key;
+  if (rlc_key(key)) return -1;
+
+  // fork: decompression on the side streams
+  HCHK(hipEventRecord(d.ev_fork, s));
+  for (int k = 0; k < 2; k++) HCHK(hipStreamWaitEvent(d.side[k], d.ev_fork, 0));
+  TIMED(d, "k_dec_pk", d.side[0], launch_dec_pk(dpk, (uint32_t)n, vpk, vpkst, d.side[0]));
+  if (n_agg) TIMED(d, "k_dec_pk", d.side[0], launch_dec_pk(fold->dv_pks, (uint32_t)n_agg, apk, apkst, d.side[0]));
+  TIMED(d, "k_dec_sig_pt", d.side[1], launch_dec_sig_pt(dsig, (uint32_t)n, vsig, vsigst, d.side[1]));
+  HCHK(hipEventRecord(d.ev_side[0], d.side[0]));
+  HCHK(hipEventRecord(d.ev_side[1], d.side[1]));
+
+  // the slot's ThresholdAggregate on side 3 (needs the decompressed partials when it reuses them)
+  const bool ta = fold && fold->n_groups;
+  if (ta) {
+    hipStream_t st = d.side[3];
+    HCHK(hipStreamWaitEvent(st, d.ev_fork, 0));
+    const HmEntry* pts = vsig;
+    const uint8_t* mst_in = vsigst;
+    if (fold->ta_src) {
+      HCHK(hipStreamWaitEvent(st, d.ev_side[1], 0));
+    } else {  // the aggregation members come as their own bytes: decompress them here
+      HmEntry* tpts;
+      uint8_t* tdst;
+      if (wsbuf(w, W_TAPTS, fold->n_partials, &tpts) || wsbuf(w, W_TADST, fold->n_partials, &tdst)) return -1;
+      TIMED(d, "k_dec_sig_pt", st, launch_dec_sig_pt(fold->ta_sigs, (uint32_t)fold->n_partials, tpts, tdst, st));
+      pts = tpts;
+      mst_in = tdst;
+    }
+    if (ta_tail(d, w, pts, fold->ta_src, mst_in, fold->ta_idx, fold->grp_off, fold->n_groups, fold->n_partials, 0,
+                fold->ta_out, fold->ta_status, asig, st))
+      return -1;
+    HCHK(hipEventRecord(d.ev_ta, st));
+  }
+
+  // random linear combinations per item, then per group
+  HCHK(hipStreamWaitEvent(s, d.ev_side[0], 0));
+  HCHK(hipStreamWaitEvent(s, d.ev_side[1], 0));
+  TIMED(d, "k_item_group", s, launch_item_group(dgoff, (uint32_t)n_groups, (uint32_t)n, igrp, s));
+  TIMED(d, "k_rlc", s, launch_rlc(vpk, vpkst, vsig, vsigst, igrp, dgoff, 0, (uint32_t)n, 0, key, pr, sr, s));
+  if (n_agg) {
+    HCHK(hipStreamWaitEvent(s, d.ev_ta, 0));
+    TIMED(d, "k_rlc", s,
+          launch_rlc(apk, apkst, asig, fold->ta_status, nullptr, nullptr, 1, (uint32_t)n_agg, (uint32_t)n, key, apr,
+                     asr, s));
+  }
+  if (hm_ready) HCHK(hipStreamWaitEvent(s, hm_ready, 0));
+  for (size_t g0 = 0; g0 < n_groups; g0 += gcap) {
+    const uint32_t ng = (uint32_t)std::min(gcap, n_groups - g0);
+    GroupPrepArgs ga{};
+    ga.grp_off = dgoff;
+    ga.g0 = (uint32_t)g0;
+    ga.ng = ng;
+    ga.msg_idx = didx;
+    ga.hm = hm;
+    ga.pk = vpk;
+    ga.pk_st = vpkst;
+    ga.sig = vsig;
+    ga.sig_st = vsigst;
+    ga.pr = pr;
+    ga.sr = sr;
+    if (n_agg) {
+      ga.agg_pk = apk;
+      ga.agg_pk_st = apkst;
+      ga.agg_sig = asig;
+      ga.agg_st = fold->ta_status;
+      ga.agg_pr = apr;
+      ga.agg_sr = asr;
+    }
+    ga.gP = gP;
+    ga.gmsg = gmsg;
+    ga.gst = gst;
+    ga.glines = glines;
+    TIMED(d, "k_group_prep", s, launch_group_prep(ga, s));
+    Pair3Args pa{};
+    pa.pk = gP;
+    pa.pk_st = gst;
+    pa.msg_idx = gmsg + g0;
+    pa.hm = hm;
+    pa.sig_lines = glines;
+    pa.stride = ng;
+    pa.n = ng;
+    pa.n_items = 0xffffffffu;
+    pa.status = gver + g0;
+    TIMED(d, "k_pair3", s, launch_pair3(pa, s));
+  }
+  HCHK(hipMemsetAsync(count, 0, sizeof(uint32_t), s));
+  ScatterArgs sa{};
+  sa.n = (uint32_t)n;
+  sa.item_grp = igrp;
+  sa.msg_idx = didx;
+  sa.hm = hm;
+  sa.pk = vpk;
+  sa.pk_st = vpkst;
+  sa.sig = vsig;
+  sa.sig_st = vsigst;
+  sa.gverdict = gver;
+  sa.n_agg = (uint32_t)n_agg;
+  if (n_agg) {
+    sa.ta_status = fold->ta_status;
+    sa.agg_pk = apk;
+    sa.agg_pk_st = apkst;
+    sa.agg_sig = asig;
+    sa.agg_status = fold->agg_status;
+  }
+  sa.status = dst;
+  sa.list = list;
+  sa.count = count;
+  TIMED(d, "k_scatter", s, launch_scatter(sa, s));
+  // fallback: every item of a failing group on its own; passes beyond the list end exit at once
+  for (size_t base = 0; base < n + n_agg; base += fbcap) {
+    TIMED(d, "k_fb_lines", s,
+          launch_fb_lines(list, count, (uint32_t)base, (uint32_t)fbcap, vsig, asig, (uint32_t)n, fbl, s));
+    Pair3Args pa{};
+    pa.pk = vpk;
+    pa.msg_idx = didx;
+    pa.hm = hm;
+    pa.sig_lines = fbl;
+    pa.stride = (uint32_t)fbcap;
+    pa.n = (uint32_t)fbcap;
+    pa.list = list;
+    pa.count = count;
+    pa.base = (uint32_t)base;
+    pa.n_items = (uint32_t)n;
+    pa.agg_pk = apk;
+    pa.agg_msg = gmsg;
+    pa.status = dst;
+    pa.agg_status = n_agg ? fold->agg_status : nullptr;
+    TIMED(d, "k_pair3_fallback", s, launch_pair3(pa, s));
+  }
+  if (ta && !n_agg) {  // the aggregation ran beside the verification: join it
+    HCHK(hipStreamWaitEvent(s, d.ev_ta, 0));
+  }
+  if (stats_on()) {  // HBLS_STATS=1: count the fallback items (synchronises; tests and diagnosis)
+    uint32_t c = 0;
+    HCHK(hipMemcpyAsync(&c, count, sizeof(c), hipMemcpyDeviceToHost, s));
+    HCHK(hipStreamSynchronize(s));
+    g_stats[0] += n + n_agg;
+    g_stats[1] += n_groups;
+    g_stats[2] += c;
+  }
+  return 0;
+}
+
+// hash every distinct message to G2 (+ its Miller line chain) into hm, on stream s
+int hash_messages(Dev& d, const uint8_t* dmsg, const uint64_t* doff, const uint32_t* dlen, size_t n_msgs,
+                  MsgEntry* hm, hipStream_t s) {
+  TIMED(d, "k_hash_to_g2", s, launch_hash_to_g2(dmsg, doff, dlen, (uint32_t)n_msgs, hm, s));
+  TIMED(d, "k_lines_msg", s, launch_lines_msg(hm, (uint32_t)n_msgs, s));
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------
+// Host-buffer calls: staging, message dedup, multi-device sharding
+// ---------------------------------------------------------------------------------------
 struct MsgTable {
   std::vector<uint8_t> bytes;
   std::vector<uint64_t> off;
   std::vector<uint32_t> len;
-  std::vector<uint32_t> idx;
+  std::vector<uint32_t> idx;  // per item
 };
 
-void dedup_messages(const uint8_t* msgs, const uint64_t* off, const uint32_t* len, size_t n, MsgTable& t) {
+void dedup_messages(const uint8_t* msgs, const uint64_t* off, const uint32_t* len, size_t n, const size_t* items,
+                    MsgTable& t) {
   std::unordered_map<std::string, uint32_t> seen;
   seen.reserve(n * 2 + 1);
   t.idx.resize(n);
-  for (size_t i = 0; i < n; i++) {
+  for (size_t k = 0; k < n; k++) {
+    const size_t i = items ? items[k] : k;
     std::string key((const char*)msgs + off[i], len[i]);
     auto it = seen.find(key);
     if (it == seen.end()) {
@@ -376,88 +752,261 @@ void dedup_messages(const uint8_t* msgs, const uint64_t* off, const uint32_t* le
       t.off.push_back(t.bytes.size());
       t.len.push_back(len[i]);
       t.bytes.insert(t.bytes.end(), msgs + off[i], msgs + off[i] + len[i]);
-      t.idx[i] = id;
+      t.idx[k] = id;
     } else {
-      t.idx[i] = it->second;
+      t.idx[k] = it->second;
     }
   }
 }
 
-// hash every distinct message to G2 (+ its Miller line chain when `lines`) into MsgEntry[].
-int hash_table_locked(const MsgTable& t, MsgEntry** hm_out, bool lines) {
+int hash_table(Dev& d, const MsgTable& t, MsgEntry** hm_out, bool lines) {
   uint8_t* dmsg;
   uint64_t* doff;
   uint32_t* dlen;
   void* hm;
-  if (upload(B_MSG, t.bytes.data(), t.bytes.size(), &dmsg)) return -1;
-  if (upload(B_OFF, t.off.data(), t.off.size(), &doff)) return -1;
-  if (upload(B_LEN, t.len.data(), t.len.size(), &dlen)) return -1;
-  if (ensure(B_HM, t.len.size() * sizeof(MsgEntry), &hm)) return -1;
-  launch_hash_to_g2(dmsg, doff, dlen, (uint32_t)t.len.size(), (MsgEntry*)hm, g_stream);
-  HCHK(hipGetLastError());
-  if (lines) launch_lines_msg((MsgEntry*)hm, (uint32_t)t.len.size(), g_stream);
+  if (upload(d, I_MSG, t.bytes.data(), t.bytes.size(), &dmsg)) return -1;
+  if (upload(d, I_OFF, t.off.data(), t.off.size(), &doff)) return -1;
+  if (upload(d, I_LEN, t.len.data(), t.len.size(), &dlen)) return -1;
+  if (ensure_buf(d.io[I_HM], t.len.size() * sizeof(MsgEntry), &hm)) return -1;
+  TIMED(d, "k_hash_to_g2", d.stream,
+        launch_hash_to_g2(dmsg, doff, dlen, (uint32_t)t.len.size(), (MsgEntry*)hm, d.stream));
+  if (lines) TIMED(d, "k_lines_msg", d.stream, launch_lines_msg((MsgEntry*)hm, (uint32_t)t.len.size(), d.stream));
   *hm_out = (MsgEntry*)hm;
   return 0;
 }
 
-// Staged verify of n partials already in device memory (herumi.go:288-304 per item):
-//   side stream 0: k_dec_pk          (1 lane / partial)
-//   side stream 1: k_dec_sig_lines   (1 lane / partial: decompress sig + its 68 lines at -g1)
-//   stream s:      k_pair3           (3 lanes / partial: Miller loop + final exponentiation)
-// in chunks of at most VERIFY_CHUNK partials (the line buffer is 19.6 KB per partial).
-constexpr size_t VERIFY_CHUNK = 1u << 17;
-// hm_ready (optional): event after which `hm` is complete; only the pairing kernel waits for it,
-// so the decompression kernels overlap the hashing.
-int verify_pipeline_locked(const uint8_t* dpk, const uint8_t* dsig, const uint32_t* didx, const MsgEntry* hm,
-                           size_t n, uint8_t* dst, hipStream_t s, hipEvent_t hm_ready = nullptr) {
-  size_t cap = n < VERIFY_CHUNK ? n : VERIFY_CHUNK;
-  void *vpk, *vpkst, *vsinf, *vsst, *vlines;
-  if (ensure(B_VPK, cap * sizeof(G1AEntry), &vpk) || ensure(B_VPKST, cap, &vpkst) || ensure(B_VSIGINF, cap, &vsinf) ||
-      ensure(B_VSIGST, cap, &vsst) || ensure(B_VLINES, cap * N_LINES * sizeof(LineEntry), &vlines))
-    return -1;
-  for (size_t c0 = 0; c0 < n; c0 += cap) {
-    uint32_t cn = (uint32_t)((n - c0) < cap ? (n - c0) : cap);
-    HCHK(hipEventRecord(g_ev_fork, s));
-    for (int k = 0; k < 2; k++) HCHK(hipStreamWaitEvent(g_side[k], g_ev_fork, 0));
-    launch_dec_pk(dpk + 48 * c0, cn, (G1AEntry*)vpk, (uint8_t*)vpkst, g_side[0]);
-    HCHK(hipGetLastError());
-    launch_dec_sig_lines(dsig + 96 * c0, cn, (uint8_t*)vsinf, (uint8_t*)vsst, (LineEntry*)vlines, g_side[1]);
-    HCHK(hipGetLastError());
-    for (int k = 0; k < 2; k++) {
-      HCHK(hipEventRecord(g_ev_side[k], g_side[k]));
-      HCHK(hipStreamWaitEvent(s, g_ev_side[k], 0));
-    }
-    if (hm_ready) HCHK(hipStreamWaitEvent(s, hm_ready, 0));
-    hipEvent_t t0 = nullptr, t1 = nullptr;
-    if (g_timing) {
-      if (timing_pair(&t0, &t1)) return -1;
-      HCHK(hipEventRecord(t0, s));
-    }
-    launch_pair3((const G1AEntry*)vpk, (const uint8_t*)vpkst, (const uint8_t*)vsinf, (const uint8_t*)vsst,
-                 didx + c0, hm, (const LineEntry*)vlines, cn, dst + c0, s);
-    if (g_timing) HCHK(hipEventRecord(t1, s));
-    HCHK(hipGetLastError());
+// Run fn(dev, shard) for each device's shard concurrently (one host thread per extra device).
+int for_each_device(size_t n_units, const std::function<int(Dev&, size_t, size_t)>& fn) {
+  const size_t nd = std::min(g_devs.size(), std::max<size_t>(n_units, 1));
+  if (nd <= 1) {
+    Dev& d = *g_devs[0];
+    std::lock_guard<std::mutex> lk(d.mu);
+    if (hipSetDevice(d.ord) != hipSuccess) return set_err("hipSetDevice failed");
+    return fn(d, 0, n_units);
   }
+  std::vector<int> rc(nd, 0);
+  std::vector<std::string> errs(nd);
+  std::vector<std::thread> th;
+  for (size_t k = 0; k < nd; k++) {
+    const size_t b = n_units * k / nd, e = n_units * (k + 1) / nd;
+    th.emplace_back([&, k, b, e]() {
+      Dev& d = *g_devs[k];
+      std::lock_guard<std::mutex> lk(d.mu);
+      if (hipSetDevice(d.ord) != hipSuccess) {
+        rc[k] = -1;
+        errs[k] = "hipSetDevice failed";
+        return;
+      }
+      rc[k] = fn(d, b, e);
+      if (rc[k]) errs[k] = g_err;
+    });
+  }
+  for (auto& t : th) t.join();
+  for (size_t k = 0; k < nd; k++)
+    if (rc[k]) return set_err("device " + std::to_string(g_devs[k]->ord) + ": " + errs[k]);
   return 0;
 }
 
-// ThresholdAggregate / Aggregate members (herumi.go:249-286, 225-247): decompress + lambda
-// digits (1 lane / partial), then lambda_j sigma_j as a 4-scalar Straus ladder (threshold.hip).
-int ta_members_locked(const uint8_t* dsig, const int64_t* didx, const uint32_t* dgoff, size_t n_groups, size_t np,
-                      int mode, G2JEntry* pts, uint8_t* mst, hipStream_t s) {
-  if (np == 0) return 0;
-  void *apts, *dig;
-  void* tab;
-  if (ensure(B_TAPTS, np * sizeof(HmEntry), &apts) || ensure(B_TADIG, np * sizeof(TaDigits), &dig) ||
-      ensure(B_TATAB, ta_table_bytes((uint32_t)np), &tab))
-    return -1;
-  LAUNCH(k_ta_dec, np, s, dsig, (uint32_t)np, (HmEntry*)apts, mst);
-  launch_ta_lambda(didx, dgoff, (uint32_t)n_groups, (uint32_t)np, mode, (TaDigits*)dig, mst, s);
-  HCHK(hipGetLastError());
-  launch_ta_straus((const HmEntry*)apts, (const TaDigits*)dig, (uint32_t)np, tab, pts, s);
-  HCHK(hipGetLastError());
+// Verify n host-buffer items (tbls.Verify per item): items are ordered by message and grouped
+// (at most g_gmax per group), the groups sharded over the devices, statuses scattered back.
+int verify_host(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msgs, const uint64_t* msg_off,
+                const uint32_t* msg_len, size_t n, uint8_t* status) {
+  if (n == 0) return 0;
+  // global message ids, order items by (message, position), groups of <= g_gmax
+  MsgTable all;
+  dedup_messages(msgs, msg_off, msg_len, n, nullptr, all);
+  std::vector<size_t> order(n);
+  std::iota(order.begin(), order.end(), 0);
+  std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) { return all.idx[a] < all.idx[b]; });
+  std::vector<size_t> gstart;  // group starts in `order`
+  for (size_t k = 0; k < n; k++)
+    if (k == 0 || all.idx[order[k]] != all.idx[order[k - 1]] || k - gstart.back() >= g_gmax) gstart.push_back(k);
+  const size_t n_groups = gstart.size();
+  gstart.push_back(n);
+  return for_each_device(n_groups, [&](Dev& d, size_t gb, size_t ge) -> int {
+    const size_t ib = gstart[gb], ie = gstart[ge], m = ie - ib;
+    if (m == 0) return 0;
+    MsgTable t;
+    dedup_messages(msgs, msg_off, msg_len, m, order.data() + ib, t);
+    std::vector<uint8_t> hpk(48 * m), hsig(96 * m);
+    for (size_t k = 0; k < m; k++) {
+      memcpy(&hpk[48 * k], pks + 48 * order[ib + k], 48);
+      memcpy(&hsig[96 * k], sigs + 96 * order[ib + k], 96);
+    }
+    std::vector<uint32_t> goff(ge - gb + 1);
+    for (size_t g = gb; g <= ge; g++) goff[g - gb] = (uint32_t)(gstart[g] - ib);
+    MsgEntry* hm;
+    if (hash_table(d, t, &hm, true)) return -1;
+    uint8_t *dpk, *dsig, *dst;
+    uint32_t *didx, *dgoff;
+    if (upload(d, I_PK, hpk.data(), hpk.size(), &dpk) || upload(d, I_SIG, hsig.data(), hsig.size(), &dsig) ||
+        upload(d, I_MIDX, t.idx.data(), m, &didx) || upload(d, I_VGOFF, goff.data(), goff.size(), &dgoff))
+      return -1;
+    void* p;
+    if (ensure_buf(d.io[I_STAT], m, &p)) return -1;
+    dst = (uint8_t*)p;
+    Ws& w = ws_acquire(d, {d.stream, d.side[0], d.side[1], d.side[3]});
+    if (verify_pipeline(d, w, dpk, dsig, didx, hm, m, dgoff, ge - gb, dst, d.stream, nullptr, nullptr)) return -1;
+    if (ws_release(w, d.stream)) return -1;
+    std::vector<uint8_t> hst(m);
+    HCHK(hipMemcpyAsync(hst.data(), dst, m, hipMemcpyDeviceToHost, d.stream));
+    HCHK(hipStreamSynchronize(d.stream));
+    for (size_t k = 0; k < m; k++) status[order[ib + k]] = hst[k];
+    return 0;
+  });
+}
+
+int check_offsets(const uint32_t* grp_off, size_t n_groups) {
+  if (grp_off[0] != 0) return set_err("grp_off[0] must be 0");
+  for (size_t g = 0; g < n_groups; g++)
+    if (grp_off[g + 1] < grp_off[g]) return set_err("grp_off must be non-decreasing");
   return 0;
 }
+
+// ThresholdAggregate (mode 0) / Aggregate (mode 1) of host-buffer groups, sharded over devices
+int group_op_host(const uint8_t* sigs, const int64_t* idx, const uint32_t* grp_off, size_t n_groups, int mode,
+                  uint8_t* out, uint8_t* status) {
+  if (check_offsets(grp_off, n_groups)) return -1;
+  return for_each_device(n_groups, [&](Dev& d, size_t gb, size_t ge) -> int {
+    const size_t ng = ge - gb, pb = grp_off[gb], np = grp_off[ge] - pb;
+    if (ng == 0) return 0;
+    std::vector<uint32_t> goff(ng + 1);
+    for (size_t g = 0; g <= ng; g++) goff[g] = grp_off[gb + g] - (uint32_t)pb;
+    uint8_t* dsig;
+    int64_t* didx = nullptr;
+    uint32_t* dgoff;
+    if (upload(d, I_SIG, sigs + 96 * pb, np * 96, &dsig)) return -1;
+    if (mode == 0 && upload(d, I_IDX, idx + pb, np, &didx)) return -1;
+    if (upload(d, I_GOFF, goff.data(), ng + 1, &dgoff)) return -1;
+    void *dout, *dst;
+    if (ensure_buf(d.io[I_OUT], ng * 96, &dout) || ensure_buf(d.io[I_STAT], ng, &dst)) return -1;
+    Ws& w = ws_acquire(d, {d.stream});
+    HmEntry* pts;
+    uint8_t* mst0;
+    if (wsbuf(w, W_TAPTS, np, &pts) || wsbuf(w, W_TADST, np, &mst0)) return -1;
+    if (np) TIMED(d, "k_dec_sig_pt", d.stream, launch_dec_sig_pt(dsig, (uint32_t)np, pts, mst0, d.stream));
+    if (ta_tail(d, w, pts, nullptr, mst0, didx, dgoff, ng, np, mode, (uint8_t*)dout, (uint8_t*)dst, nullptr,
+                d.stream))
+      return -1;
+    if (ws_release(w, d.stream)) return -1;
+    HCHK(hipMemcpyAsync(out + 96 * gb, dout, ng * 96, hipMemcpyDeviceToHost, d.stream));
+    HCHK(hipMemcpyAsync(status + gb, dst, ng, hipMemcpyDeviceToHost, d.stream));
+    HCHK(hipStreamSynchronize(d.stream));
+    return 0;
+  });
+}
+
+// ---------------------------------------------------------------------------------------
+// Coalescing of concurrent host calls: the first caller of an idle queue becomes the leader,
+// waits at most HBLS_COALESCE_US for more requests (or until HBLS_COALESCE_MAX items queue up),
+// runs them as one batch and wakes every requester with its own statuses.  Requests that arrive
+// while a batch runs form the next batch.
+// ---------------------------------------------------------------------------------------
+struct VReq {
+  const uint8_t *pk, *sig, *msg;
+  const uint64_t* off;
+  const uint32_t* len;
+  size_t n;
+  uint8_t* st;
+  int rc = 0;
+  std::string err;
+  bool done = false;
+};
+
+struct Coalescer {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<VReq*> q;
+  size_t queued = 0;
+  bool running = false;
+};
+Coalescer g_vq;
+size_t g_coalesce_us = (size_t)-1, g_coalesce_max = 0;
+
+void coalesce_params() {
+  if (g_coalesce_us == (size_t)-1) {
+    g_coalesce_us = env_size("HBLS_COALESCE_US", 200);
+    g_coalesce_max = env_size("HBLS_COALESCE_MAX", 1u << 16);
+  }
+}
+
+void run_verify_batch(std::vector<VReq*>& batch) {
+  size_t tot = 0;
+  for (VReq* r : batch) tot += r->n;
+  std::vector<uint8_t> pk(48 * tot), sig(96 * tot), msg, st(tot);
+  std::vector<uint64_t> off(tot);
+  std::vector<uint32_t> len(tot);
+  size_t k = 0;
+  for (VReq* r : batch)
+    for (size_t i = 0; i < r->n; i++, k++) {
+      memcpy(&pk[48 * k], r->pk + 48 * i, 48);
+      memcpy(&sig[96 * k], r->sig + 96 * i, 96);
+      off[k] = msg.size();
+      len[k] = r->len[i];
+      msg.insert(msg.end(), r->msg + r->off[i], r->msg + r->off[i] + r->len[i]);
+    }
+  if (msg.empty()) msg.push_back(0);
+  int rc = verify_host(pk.data(), sig.data(), msg.data(), off.data(), len.data(), tot, st.data());
+  std::string err = rc ? g_err : std::string();
+  k = 0;
+  for (VReq* r : batch) {
+    r->rc = rc;
+    r->err = err;
+    if (!rc) memcpy(r->st, &st[k], r->n);
+    k += r->n;
+  }
+}
+
+int verify_coalesced(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msgs, const uint64_t* msg_off,
+                     const uint32_t* msg_len, size_t n, uint8_t* status) {
+  coalesce_params();
+  if (g_coalesce_us == 0 || n >= g_coalesce_max) return verify_host(pks, sigs, msgs, msg_off, msg_len, n, status);
+  VReq me;
+  me.pk = pks;
+  me.sig = sigs;
+  me.msg = msgs;
+  me.off = msg_off;
+  me.len = msg_len;
+  me.n = n;
+  me.st = status;
+  Coalescer& c = g_vq;
+  std::unique_lock<std::mutex> lk(c.mu);
+  c.q.push_back(&me);
+  c.queued += n;
+  c.cv.notify_all();
+  while (!me.done) {
+    if (!c.running) {
+      c.running = true;
+      auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(g_coalesce_us);
+      while (c.queued < g_coalesce_max && std::chrono::steady_clock::now() < deadline) c.cv.wait_until(lk, deadline);
+      std::vector<VReq*> batch(c.q.begin(), c.q.end());
+      c.q.clear();
+      c.queued = 0;
+      lk.unlock();
+      run_verify_batch(batch);
+      lk.lock();
+      for (VReq* r : batch) r->done = true;
+      c.running = false;
+      c.cv.notify_all();
+    } else {
+      c.cv.wait(lk);
+    }
+  }
+  if (me.rc) g_err = me.err;
+  return me.rc;
+}
+
+// ---------------------------------------------------------------------------------------
+// RCCL: one communicator per process (one GPU each) for the exchange of slot results
+// ---------------------------------------------------------------------------------------
+ncclComm_t g_comm = nullptr;
+int g_comm_ranks = 0;
+
+#define NCHK(expr)                                                                        \
+  do {                                                                                    \
+    ncclResult_t _r = (expr);                                                             \
+    if (_r != ncclSuccess) return set_err(std::string(#expr) + ": " + ncclGetErrorString(_r)); \
+  } while (0)
 
 }  // namespace
 
@@ -466,291 +1015,307 @@ int ta_members_locked(const uint8_t* dsig, const int64_t* didx, const uint32_t* 
 // ---------------------------------------------------------------------------------------
 extern "C" {
 
-int hbls_init(int device) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  return init_locked(device);
-}
+int hbls_init(uint32_t device_mask) { return init_mask(device_mask); }
 
 const char* hbls_last_error(void) { return g_err.c_str(); }
 
-int hbls_available(void) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  return init_locked(-1) == 0 ? 1 : 0;
-}
+int hbls_available(void) { return ensure_init() == 0 ? 1 : 0; }
+
+int hbls_device_count(void) { return ensure_init() ? -1 : (int)g_devs.size(); }
 
 size_t hbls_hm_entry_bytes(void) { return sizeof(MsgEntry); }
 
 int hbls_verify_batch(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msgs, const uint64_t* msg_off,
                       const uint32_t* msg_len, size_t n, uint8_t* status) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  if (init_locked(-1)) return -1;
+  if (ensure_init()) return -1;
   if (n == 0) return 0;
-  MsgTable t;
-  dedup_messages(msgs, msg_off, msg_len, n, t);
-  MsgEntry* hm;
-  if (hash_table_locked(t, &hm, true)) return -1;
-  uint8_t *dpk, *dsig, *dst;
-  uint32_t* didx;
-  if (upload(B_PK, pks, n * 48, &dpk)) return -1;
-  if (upload(B_SIG, sigs, n * 96, &dsig)) return -1;
-  if (upload(B_MIDX, t.idx.data(), n, &didx)) return -1;
-  void* p;
-  if (ensure(B_STAT, n, &p)) return -1;
-  dst = (uint8_t*)p;
-  if (verify_pipeline_locked(dpk, dsig, didx, hm, n, dst, g_stream)) return -1;
-  HCHK(hipMemcpyAsync(status, dst, n, hipMemcpyDeviceToHost, g_stream));
-  HCHK(hipStreamSynchronize(g_stream));
-  return 0;
-}
-
-static int group_op_locked(const uint8_t* sigs, const int64_t* idx, const uint32_t* grp_off, size_t n_groups,
-                           int mode, uint8_t* out, uint8_t* status) {
-  size_t np = grp_off[n_groups] - grp_off[0];
-  if (grp_off[0] != 0) {
-    g_err = "grp_off[0] must be 0";
-    return -1;
-  }
-  for (size_t g = 0; g < n_groups; g++)
-    if (grp_off[g + 1] < grp_off[g]) {
-      g_err = "grp_off must be non-decreasing";
-      return -1;
-    }
-  uint8_t* dsig;
-  int64_t* didx = nullptr;
-  uint32_t* dgoff;
-  if (upload(B_SIG, sigs, np * 96, &dsig)) return -1;
-  if (mode == 0 && upload(B_IDX, idx, np, &didx)) return -1;
-  if (upload(B_GOFF, grp_off, n_groups + 1, &dgoff)) return -1;
-  void *pts, *mst, *dout, *dst;
-  if (ensure(B_PTS, np * sizeof(G2JEntry), &pts) || ensure(B_MSTAT, np, &mst) || ensure(B_OUT, n_groups * 96, &dout) ||
-      ensure(B_STAT, n_groups, &dst))
-    return -1;
-  if (ta_members_locked(dsig, didx, dgoff, n_groups, np, mode, (G2JEntry*)pts, (uint8_t*)mst, g_stream)) return -1;
-  LAUNCH(k_group_sum, n_groups, g_stream, dgoff, (uint32_t)n_groups, mode, (const G2JEntry*)pts, (const uint8_t*)mst,
-         (uint8_t*)dout, (uint8_t*)dst);
-  HCHK(hipMemcpyAsync(out, dout, n_groups * 96, hipMemcpyDeviceToHost, g_stream));
-  HCHK(hipMemcpyAsync(status, dst, n_groups, hipMemcpyDeviceToHost, g_stream));
-  HCHK(hipStreamSynchronize(g_stream));
-  return 0;
+  return verify_coalesced(pks, sigs, msgs, msg_off, msg_len, n, status);
 }
 
 int hbls_threshold_aggregate_batch(const uint8_t* sigs, const int64_t* idx, const uint32_t* grp_off, size_t n_groups,
                                    uint8_t* out, uint8_t* status) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  if (init_locked(-1)) return -1;
+  if (ensure_init()) return -1;
   if (n_groups == 0) return 0;
-  return group_op_locked(sigs, idx, grp_off, n_groups, 0, out, status);
+  return group_op_host(sigs, idx, grp_off, n_groups, 0, out, status);
 }
 
 int hbls_aggregate_batch(const uint8_t* sigs, const uint32_t* grp_off, size_t n_groups, uint8_t* out,
                          uint8_t* status) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  if (init_locked(-1)) return -1;
+  if (ensure_init()) return -1;
   if (n_groups == 0) return 0;
-  return group_op_locked(sigs, nullptr, grp_off, n_groups, 1, out, status);
+  return group_op_host(sigs, nullptr, grp_off, n_groups, 1, out, status);
 }
 
 int hbls_verify_aggregate_batch(const uint8_t* pks, const uint32_t* grp_off, const uint8_t* sigs,
                                 const uint8_t* msgs, const uint64_t* msg_off, const uint32_t* msg_len,
                                 size_t n_groups, uint8_t* status) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  if (init_locked(-1)) return -1;
+  if (ensure_init()) return -1;
   if (n_groups == 0) return 0;
-  size_t np = grp_off[n_groups];
-  // one hash per group (messages need not be distinct)
-  MsgTable t;
-  t.idx.resize(n_groups);
-  for (size_t g = 0; g < n_groups; g++) {
-    t.off.push_back(t.bytes.size());
-    t.len.push_back(msg_len[g]);
-    t.bytes.insert(t.bytes.end(), msgs + msg_off[g], msgs + msg_off[g] + msg_len[g]);
-  }
-  MsgEntry* hm;
-  if (hash_table_locked(t, &hm, false)) return -1;
-  uint8_t *dpk, *dsig;
-  uint32_t* dgoff;
-  if (upload(B_PK, pks, np * 48, &dpk)) return -1;
-  if (upload(B_SIG, sigs, n_groups * 96, &dsig)) return -1;
-  if (upload(B_GOFF, grp_off, n_groups + 1, &dgoff)) return -1;
-  void *pts, *mst, *dst;
-  if (ensure(B_G1PTS, np * sizeof(G1AEntry), &pts) || ensure(B_MSTAT, np, &mst) || ensure(B_STAT, n_groups, &dst))
-    return -1;
-  LAUNCH(k_g1_member, np, g_stream, dpk, (uint32_t)np, (G1AEntry*)pts, (uint8_t*)mst);
-  LAUNCH(k_verify_aggregate, n_groups, g_stream, dgoff, (uint32_t)n_groups, (const G1AEntry*)pts, (const uint8_t*)mst,
-         dsig, (const MsgEntry*)hm, (uint8_t*)dst);
-  HCHK(hipMemcpyAsync(status, dst, n_groups, hipMemcpyDeviceToHost, g_stream));
-  HCHK(hipStreamSynchronize(g_stream));
-  return 0;
+  if (check_offsets(grp_off, n_groups)) return -1;
+  return for_each_device(n_groups, [&](Dev& d, size_t gb, size_t ge) -> int {
+    const size_t ng = ge - gb, pb = grp_off[gb], np = grp_off[ge] - pb;
+    if (ng == 0) return 0;
+    MsgTable t;  // one hash per group (messages need not be distinct)
+    t.idx.resize(ng);
+    for (size_t g = gb; g < ge; g++) {
+      t.off.push_back(t.bytes.size());
+      t.len.push_back(msg_len[g]);
+      t.bytes.insert(t.bytes.end(), msgs + msg_off[g], msgs + msg_off[g] + msg_len[g]);
+    }
+    std::vector<uint32_t> goff(ng + 1);
+    for (size_t g = 0; g <= ng; g++) goff[g] = grp_off[gb + g] - (uint32_t)pb;
+    MsgEntry* hm;
+    if (hash_table(d, t, &hm, false)) return -1;
+    uint8_t *dpk, *dsig;
+    uint32_t* dgoff;
+    if (upload(d, I_PK, pks + 48 * pb, np * 48, &dpk) || upload(d, I_SIG, sigs + 96 * gb, ng * 96, &dsig) ||
+        upload(d, I_GOFF, goff.data(), ng + 1, &dgoff))
+      return -1;
+    Ws& w = ws_acquire(d, {d.stream});
+    G1AEntry* pts;
+    uint8_t *mst, *dst;
+    if (wsbuf(w, W_VPK, np, &pts) || wsbuf(w, W_VPKST, np, &mst)) return -1;
+    void* p;
+    if (ensure_buf(d.io[I_STAT], ng, &p)) return -1;
+    dst = (uint8_t*)p;
+    LAUNCH(k_g1_member, np, d.stream, dpk, (uint32_t)np, pts, mst);
+    LAUNCH(k_verify_aggregate, ng, d.stream, dgoff, (uint32_t)ng, (const G1AEntry*)pts, (const uint8_t*)mst, dsig,
+           (const MsgEntry*)hm, dst);
+    if (ws_release(w, d.stream)) return -1;
+    HCHK(hipMemcpyAsync(status + gb, dst, ng, hipMemcpyDeviceToHost, d.stream));
+    HCHK(hipStreamSynchronize(d.stream));
+    return 0;
+  });
 }
 
 int hbls_sign_batch(const uint8_t* sks, const uint8_t* msgs, const uint64_t* msg_off, const uint32_t* msg_len,
                     size_t n, uint8_t* sigs, uint8_t* status) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  if (init_locked(-1)) return -1;
+  if (ensure_init()) return -1;
   if (n == 0) return 0;
-  MsgTable t;
-  dedup_messages(msgs, msg_off, msg_len, n, t);
-  MsgEntry* hm;
-  if (hash_table_locked(t, &hm, false)) return -1;
-  uint8_t* dsk;
-  uint32_t* didx;
-  if (upload(B_SK, sks, n * 32, &dsk)) return -1;
-  if (upload(B_MIDX, t.idx.data(), n, &didx)) return -1;
-  void *dout, *dst;
-  if (ensure(B_OUT, n * 96, &dout) || ensure(B_STAT, n, &dst)) return -1;
-  LAUNCH(k_sign, n, g_stream, dsk, didx, hm, (uint32_t)n, (uint8_t*)dout, (uint8_t*)dst);
-  HCHK(hipMemcpyAsync(sigs, dout, n * 96, hipMemcpyDeviceToHost, g_stream));
-  HCHK(hipMemcpyAsync(status, dst, n, hipMemcpyDeviceToHost, g_stream));
-  HCHK(hipStreamSynchronize(g_stream));
-  return 0;
+  return for_each_device(n, [&](Dev& d, size_t b, size_t e) -> int {
+    const size_t m = e - b;
+    std::vector<size_t> items(m);
+    std::iota(items.begin(), items.end(), b);
+    MsgTable t;
+    dedup_messages(msgs, msg_off, msg_len, m, items.data(), t);
+    MsgEntry* hm;
+    if (hash_table(d, t, &hm, false)) return -1;
+    uint8_t* dsk;
+    uint32_t* didx;
+    if (upload(d, I_SK, sks + 32 * b, m * 32, &dsk) || upload(d, I_MIDX, t.idx.data(), m, &didx)) return -1;
+    void *dout, *dst;
+    if (ensure_buf(d.io[I_OUT], m * 96, &dout) || ensure_buf(d.io[I_STAT], m, &dst)) return -1;
+    LAUNCH(k_sign, m, d.stream, dsk, didx, hm, (uint32_t)m, (uint8_t*)dout, (uint8_t*)dst);
+    HCHK(hipMemcpyAsync(sigs + 96 * b, dout, m * 96, hipMemcpyDeviceToHost, d.stream));
+    HCHK(hipMemcpyAsync(status + b, dst, m, hipMemcpyDeviceToHost, d.stream));
+    HCHK(hipStreamSynchronize(d.stream));
+    return 0;
+  });
 }
 
 int hbls_secret_to_public_key_batch(const uint8_t* sks, size_t n, uint8_t* pks, uint8_t* status) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  if (init_locked(-1)) return -1;
+  if (ensure_init()) return -1;
   if (n == 0) return 0;
-  uint8_t* dsk;
-  if (upload(B_SK, sks, n * 32, &dsk)) return -1;
-  void *dout, *dst;
-  if (ensure(B_OUT, n * 48, &dout) || ensure(B_STAT, n, &dst)) return -1;
-  LAUNCH(k_sk_to_pk, n, g_stream, dsk, (uint32_t)n, (uint8_t*)dout, (uint8_t*)dst);
-  HCHK(hipMemcpyAsync(pks, dout, n * 48, hipMemcpyDeviceToHost, g_stream));
-  HCHK(hipMemcpyAsync(status, dst, n, hipMemcpyDeviceToHost, g_stream));
-  HCHK(hipStreamSynchronize(g_stream));
-  return 0;
+  return for_each_device(n, [&](Dev& d, size_t b, size_t e) -> int {
+    const size_t m = e - b;
+    uint8_t* dsk;
+    if (upload(d, I_SK, sks + 32 * b, m * 32, &dsk)) return -1;
+    void *dout, *dst;
+    if (ensure_buf(d.io[I_OUT], m * 48, &dout) || ensure_buf(d.io[I_STAT], m, &dst)) return -1;
+    LAUNCH(k_sk_to_pk, m, d.stream, dsk, (uint32_t)m, (uint8_t*)dout, (uint8_t*)dst);
+    HCHK(hipMemcpyAsync(pks + 48 * b, dout, m * 48, hipMemcpyDeviceToHost, d.stream));
+    HCHK(hipMemcpyAsync(status + b, dst, m, hipMemcpyDeviceToHost, d.stream));
+    HCHK(hipStreamSynchronize(d.stream));
+    return 0;
+  });
 }
 
 int hbls_threshold_split(const uint8_t* secret, const uint8_t* coeffs, uint32_t total, uint32_t threshold,
                          uint8_t* shares, uint8_t* status) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  if (init_locked(-1)) return -1;
+  if (ensure_init()) return -1;
   if (total == 0 || threshold == 0) return 0;
   std::vector<uint8_t> poly(32ull * threshold);
   memcpy(poly.data(), secret, 32);
   if (threshold > 1) memcpy(poly.data() + 32, coeffs, 32ull * (threshold - 1));
-  uint8_t* dpoly;
-  if (upload(B_SK, poly.data(), poly.size(), &dpoly)) return -1;
-  void *dout, *dst;
-  if (ensure(B_OUT, 32ull * total, &dout) || ensure(B_STAT, total, &dst)) return -1;
-  LAUNCH(k_split, total, g_stream, dpoly, threshold, total, (uint8_t*)dout, (uint8_t*)dst);
-  HCHK(hipMemcpyAsync(shares, dout, 32ull * total, hipMemcpyDeviceToHost, g_stream));
-  HCHK(hipMemcpyAsync(status, dst, total, hipMemcpyDeviceToHost, g_stream));
-  HCHK(hipStreamSynchronize(g_stream));
-  return 0;
+  return for_each_device(1, [&](Dev& d, size_t, size_t) -> int {
+    uint8_t* dpoly;
+    if (upload(d, I_SK, poly.data(), poly.size(), &dpoly)) return -1;
+    void *dout, *dst;
+    if (ensure_buf(d.io[I_OUT], 32ull * total, &dout) || ensure_buf(d.io[I_STAT], total, &dst)) return -1;
+    LAUNCH(k_split, total, d.stream, dpoly, threshold, total, (uint8_t*)dout, (uint8_t*)dst);
+    HCHK(hipMemcpyAsync(shares, dout, 32ull * total, hipMemcpyDeviceToHost, d.stream));
+    HCHK(hipMemcpyAsync(status, dst, total, hipMemcpyDeviceToHost, d.stream));
+    HCHK(hipStreamSynchronize(d.stream));
+    return 0;
+  });
 }
 
 int hbls_recover_secret(const uint8_t* shares, const int64_t* idx, size_t k, uint8_t* out, uint8_t* status) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  if (init_locked(-1)) return -1;
-  uint8_t* dsh;
-  int64_t* didx;
-  std::vector<uint8_t> dummy(32);
-  if (upload(B_SK, k ? shares : dummy.data(), k ? 32 * k : 32, &dsh)) return -1;
-  std::vector<int64_t> di(k ? k : 1, 0);
-  if (k) memcpy(di.data(), idx, 8 * k);
-  if (upload(B_IDX, di.data(), di.size(), &didx)) return -1;
-  void *dout, *dst;
-  if (ensure(B_OUT, 32, &dout) || ensure(B_STAT, 1, &dst)) return -1;
-  hipLaunchKernelGGL(k_recover, dim3(1), dim3(64), 0, g_stream, dsh, didx, (uint32_t)k, (uint8_t*)dout,
-                     (uint8_t*)dst);
-  HCHK(hipGetLastError());
-  HCHK(hipMemcpyAsync(out, dout, 32, hipMemcpyDeviceToHost, g_stream));
-  HCHK(hipMemcpyAsync(status, dst, 1, hipMemcpyDeviceToHost, g_stream));
-  HCHK(hipStreamSynchronize(g_stream));
-  return 0;
+  if (ensure_init()) return -1;
+  return for_each_device(1, [&](Dev& d, size_t, size_t) -> int {
+    uint8_t* dsh;
+    int64_t* didx;
+    std::vector<uint8_t> dummy(32);
+    if (upload(d, I_SK, k ? shares : dummy.data(), k ? 32 * k : 32, &dsh)) return -1;
+    std::vector<int64_t> di(k ? k : 1, 0);
+    if (k) memcpy(di.data(), idx, 8 * k);
+    if (upload(d, I_IDX, di.data(), di.size(), &didx)) return -1;
+    void *dout, *dst;
+    if (ensure_buf(d.io[I_OUT], 32, &dout) || ensure_buf(d.io[I_STAT], 1, &dst)) return -1;
+    hipLaunchKernelGGL(k_recover, dim3(1), dim3(64), 0, d.stream, dsh, didx, (uint32_t)k, (uint8_t*)dout,
+                       (uint8_t*)dst);
+    HCHK(hipGetLastError());
+    HCHK(hipMemcpyAsync(out, dout, 32, hipMemcpyDeviceToHost, d.stream));
+    HCHK(hipMemcpyAsync(status, dst, 1, hipMemcpyDeviceToHost, d.stream));
+    HCHK(hipStreamSynchronize(d.stream));
+    return 0;
+  });
 }
 
-// ---- device-buffer entry points (bench / slot pipeline) ----
+// ---- device-buffer entry points (slot pipeline) ----
 int hbls_hash_to_g2_device(const uint8_t* msgs, const uint64_t* msg_off, const uint32_t* msg_len, size_t n_msgs,
                            void* hm, void* stream) {
+  Dev* d;
   hipStream_t s = (hipStream_t)stream;
-  launch_hash_to_g2(msgs, msg_off, msg_len, (uint32_t)n_msgs, (MsgEntry*)hm, s);
-  HCHK(hipGetLastError());
-  launch_lines_msg((MsgEntry*)hm, (uint32_t)n_msgs, s);
-  HCHK(hipGetLastError());
-  return 0;
+  if (dev_of_stream(s, &d)) return -1;
+  std::lock_guard<std::mutex> lk(d->mu);
+  return hash_messages(*d, msgs, msg_off, msg_len, n_msgs, (MsgEntry*)hm, s);
 }
 
 int hbls_verify_device(const uint8_t* pks, const uint8_t* sigs, const uint32_t* msg_idx, const void* hm, size_t n,
-                       uint8_t* status, void* stream) {
-  std::lock_guard<std::mutex> lk(g_mu);  // the staged pipeline's workspaces are library-owned
-  if (init_locked(-1)) return -1;
+                       const uint32_t* vgrp_off, size_t n_vgroups, uint8_t* status, void* stream) {
+  Dev* d;
+  hipStream_t s = (hipStream_t)stream;
+  if (dev_of_stream(s, &d)) return -1;
   if (n == 0) return 0;
-  return verify_pipeline_locked(pks, sigs, msg_idx, (const MsgEntry*)hm, n, status, (hipStream_t)stream);
+  std::lock_guard<std::mutex> lk(d->mu);
+  Ws& w = ws_acquire(*d, {s, d->side[0], d->side[1], d->side[3]});
+  if (verify_pipeline(*d, w, pks, sigs, msg_idx, (const MsgEntry*)hm, n, vgrp_off, n_vgroups, status, s, nullptr,
+                      nullptr))
+    return -1;
+  return ws_release(w, s);
 }
 
 int hbls_threshold_aggregate_device(const uint8_t* sigs, const int64_t* idx, const uint32_t* grp_off, size_t n_groups,
                                     size_t n_partials, uint8_t* out, uint8_t* status, void* stream) {
-  // workspace for member points is owned by the library (grow-only)
-  std::lock_guard<std::mutex> lk(g_mu);
-  if (init_locked(-1)) return -1;
+  Dev* d;
   hipStream_t s = (hipStream_t)stream;
-  void *pts, *mst;
-  if (ensure(B_PTS, n_partials * sizeof(G2JEntry), &pts) || ensure(B_MSTAT, n_partials, &mst)) return -1;
-  if (ta_members_locked(sigs, idx, grp_off, n_groups, n_partials, 0, (G2JEntry*)pts, (uint8_t*)mst, s)) return -1;
-  LAUNCH(k_group_sum, n_groups, s, grp_off, (uint32_t)n_groups, 0, (const G2JEntry*)pts, (const uint8_t*)mst, out,
-         status);
-  return 0;
+  if (dev_of_stream(s, &d)) return -1;
+  std::lock_guard<std::mutex> lk(d->mu);
+  Ws& w = ws_acquire(*d, {s});
+  HmEntry* pts;
+  uint8_t* mst0;
+  if (wsbuf(w, W_TAPTS, n_partials, &pts) || wsbuf(w, W_TADST, n_partials, &mst0)) return -1;
+  if (n_partials) TIMED(*d, "k_dec_sig_pt", s, launch_dec_sig_pt(sigs, (uint32_t)n_partials, pts, mst0, s));
+  if (ta_tail(*d, w, pts, nullptr, mst0, idx, grp_off, n_groups, n_partials, 0, out, status, nullptr, s)) return -1;
+  return ws_release(w, s);
 }
 
-int hbls_slot_device(const uint8_t* msgs, const uint64_t* msg_off, const uint32_t* msg_len, size_t n_msgs, void* hm,
-                     const uint8_t* pks, const uint8_t* sigs, const uint32_t* msg_idx, size_t n, uint8_t* vstatus,
-                     const uint8_t* ta_sigs, const int64_t* ta_idx, const uint32_t* grp_off, size_t n_groups,
-                     size_t n_ta_partials, uint8_t* ta_out, uint8_t* ta_status, void* stream) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  if (init_locked(-1)) return -1;
+int hbls_slot_device(const hbls_slot* a, void* stream) {
+  Dev* d;
   hipStream_t s = (hipStream_t)stream;
-  HCHK(hipEventRecord(g_ev_slot, s));
+  if (dev_of_stream(s, &d)) return -1;
+  if (!a) return set_err("hbls_slot_device: null arguments");
+  if (a->n_groups && !a->ta_src && !a->ta_sigs) return set_err("hbls_slot_device: ta_src or ta_sigs is required");
+  if (a->dv_pks && a->n_vgroups != a->n_groups)
+    return set_err("hbls_slot_device: the folded post-aggregate verification needs one verification group per "
+                   "aggregation group");
+  std::lock_guard<std::mutex> lk(d->mu);
+  Ws& w = ws_acquire(*d, {s, d->side[0], d->side[1], d->side[2], d->side[3]});
+  HCHK(hipEventRecord(d->ev_fork, s));
   // messages: hash + Miller lines (side 2)
-  hipStream_t sh = g_side[2];
-  HCHK(hipStreamWaitEvent(sh, g_ev_slot, 0));
-  launch_hash_to_g2(msgs, msg_off, msg_len, (uint32_t)n_msgs, (MsgEntry*)hm, sh);
-  HCHK(hipGetLastError());
-  launch_lines_msg((MsgEntry*)hm, (uint32_t)n_msgs, sh);
-  HCHK(hipGetLastError());
-  HCHK(hipEventRecord(g_ev_side[2], sh));
-  // partial signatures (sides 0, 1, then s)
-  if (n && verify_pipeline_locked(pks, sigs, msg_idx, (const MsgEntry*)hm, n, vstatus, s, g_ev_side[2])) return -1;
-  // ThresholdAggregate on the library's own stream, which no other slot kernel uses: the runtime
-  // has 4 hardware queues, and with five busy streams two would share one, serialising the
-  // aggregation chain behind the hashing (profiles/r01h_slot_timeline.txt).  In-order with the
-  // host-buffer entry points that share its workspaces.
-  hipStream_t st = g_stream;
-  HCHK(hipStreamWaitEvent(st, g_ev_slot, 0));
-  if (n_groups) {
-    void *pts, *mst;
-    if (ensure(B_PTS, n_ta_partials * sizeof(G2JEntry), &pts) || ensure(B_MSTAT, n_ta_partials, &mst)) return -1;
-    if (ta_members_locked(ta_sigs, ta_idx, grp_off, n_groups, n_ta_partials, 0, (G2JEntry*)pts, (uint8_t*)mst, st))
-      return -1;
-    LAUNCH(k_group_sum, n_groups, st, grp_off, (uint32_t)n_groups, 0, (const G2JEntry*)pts, (const uint8_t*)mst,
-           ta_out, ta_status);
-  }
-  HCHK(hipEventRecord(g_ev_side[3], st));
-  HCHK(hipStreamWaitEvent(s, g_ev_side[2], 0));
-  HCHK(hipStreamWaitEvent(s, g_ev_side[3], 0));
-  return 0;
+  hipStream_t sh = d->side[2];
+  HCHK(hipStreamWaitEvent(sh, d->ev_fork, 0));
+  if (hash_messages(*d, a->msgs, a->msg_off, a->msg_len, a->n_msgs, (MsgEntry*)a->hm, sh)) return -1;
+  HCHK(hipEventRecord(d->ev_side[2], sh));
+  TaFold fold{};
+  fold.ta_sigs = a->ta_sigs;
+  fold.ta_src = a->ta_src;
+  fold.ta_idx = a->ta_idx;
+  fold.grp_off = a->grp_off;
+  fold.n_groups = a->n_groups;
+  fold.n_partials = a->n_ta_partials;
+  fold.ta_out = a->ta_out;
+  fold.ta_status = a->ta_status;
+  fold.dv_pks = a->dv_pks;
+  fold.agg_status = a->agg_vstatus;
+  if (verify_pipeline(*d, w, a->pks, a->sigs, a->msg_idx, (const MsgEntry*)a->hm, a->n, a->vgrp_off, a->n_vgroups,
+                      a->vstatus, s, d->ev_side[2], &fold))
+    return -1;
+  HCHK(hipStreamWaitEvent(s, d->ev_side[2], 0));
+  return ws_release(w, s);
 }
 
 int hbls_timing(int enable) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  g_timing = enable != 0;
-  g_tev_used = 0;
+  if (ensure_init()) return -1;
+  for (Dev* d : g_devs) {
+    std::lock_guard<std::mutex> lk(d->mu);
+    d->timing = enable != 0;
+    d->tev_used = 0;
+  }
   return 0;
 }
 
-int hbls_timing_read(float* ms, size_t max_n, size_t* n_out) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  size_t n = g_tev_used < max_n ? g_tev_used : max_n;
-  for (size_t i = 0; i < n; i++) {
-    HCHK(hipEventSynchronize(g_tev[i].second));
-    HCHK(hipEventElapsedTime(&ms[i], g_tev[i].first, g_tev[i].second));
+// Launch durations recorded since hbls_timing(1), in launch order over the devices of the mask:
+// names[i] (kernel name, static storage) and ms[i].
+int hbls_timing_read(const char** names, float* ms, size_t max_n, size_t* n_out) {
+  if (ensure_init()) return -1;
+  size_t k = 0;
+  for (Dev* d : g_devs) {
+    std::lock_guard<std::mutex> lk(d->mu);
+    HCHK(hipSetDevice(d->ord));
+    for (size_t i = 0; i < d->tev_used && k < max_n; i++, k++) {
+      HCHK(hipEventSynchronize(d->tev[i].b));
+      HCHK(hipEventElapsedTime(&ms[k], d->tev[i].a, d->tev[i].b));
+      if (names) names[k] = d->tev[i].name;
+    }
   }
-  *n_out = n;
+  *n_out = k;
   return 0;
+}
+
+int hbls_stats(uint64_t* out, size_t n) {
+  for (size_t k = 0; k < n && k < 3; k++) out[k] = g_stats[k].load();
+  return stats_on() ? 0 : set_err("statistics are collected only with HBLS_STATS=1");
 }
 
 int hbls_sync(void* stream) {
   HCHK(hipStreamSynchronize((hipStream_t)stream));
+  return 0;
+}
+
+// ---- RCCL exchange between processes (one GPU each) ----
+size_t hbls_comm_id_bytes(void) { return sizeof(ncclUniqueId); }
+
+int hbls_comm_unique_id(uint8_t* id) {
+  ncclUniqueId u;
+  NCHK(ncclGetUniqueId(&u));
+  memcpy(id, &u, sizeof(u));
+  return 0;
+}
+
+int hbls_comm_init(int nranks, int rank, const uint8_t* id) {
+  if (ensure_init()) return -1;
+  if (g_devs.size() != 1) return set_err("hbls_comm_init: one device per process");
+  if (g_comm) return g_comm_ranks == nranks ? 0 : set_err("communicator already initialised");
+  HCHK(hipSetDevice(g_devs[0]->ord));
+  ncclUniqueId u;
+  memcpy(&u, id, sizeof(u));
+  NCHK(ncclCommInitRank(&g_comm, nranks, u, rank));
+  g_comm_ranks = nranks;
+  return 0;
+}
+
+int hbls_allgather_device(const void* send, void* recv, size_t bytes, void* stream) {
+  if (!g_comm) return set_err("hbls_allgather_device: no communicator (hbls_comm_init)");
+  NCHK(ncclAllGather(send, recv, bytes, ncclUint8, g_comm, (hipStream_t)stream));
+  return 0;
+}
+
+int hbls_comm_destroy(void) {
+  if (g_comm) NCHK(ncclCommDestroy(g_comm));
+  g_comm = nullptr;
+  g_comm_ranks = 0;
   return 0;
 }
 

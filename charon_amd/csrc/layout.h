@@ -1,27 +1,32 @@
-// Device-side storage formats shared by the two translation units of libhipbls.so
-// (hipbls.hip: host runtime + one-lane kernels; pipeline.hip: the staged verify pipeline).
+// Device-side storage formats and kernel launchers shared by the translation units of
+// libhipbls.so (hipbls.hip: host runtime + one-lane kernels; pipeline.hip: hashing and the
+// pairing kernel; vbatch.hip: batched verification; threshold.hip: ThresholdAggregate).
 #pragma once
 #include "ops.h"
 
 namespace hb {
 
-struct HmEntry {  // affine G2 point (Montgomery limbs) + infinity flag, 208 B
+struct HmEntry {  // affine G2 point (Montgomery limbs) + infinity flag
   Fp2 x, y;
   uint32_t inf;
   uint32_t pad[3];
 };
 
-struct G2JEntry {  // Jacobian G2 point, 288 B
+struct G2JEntry {  // Jacobian G2 point
   Fp2 X, Y, Z;
 };
 
-struct G1AEntry {  // affine G1 point, 112 B
+struct G1AEntry {  // affine G1 point
   Fp x, y;
   uint32_t inf;
   uint32_t pad[3];
 };
 
-struct LineEntry {  // one Miller-loop line, 288 B: (a0, c1, c2) unevaluated or (a0, a1, b1)
+struct G1JEntry {  // Jacobian G1 point
+  Fp X, Y, Z;
+};
+
+struct LineEntry {  // one Miller-loop line: (a0, c1, c2) unevaluated or (a0, a1, b1)
   Fp2 a0, a1, b1;
 };
 
@@ -33,6 +38,7 @@ struct MsgEntry {
 };
 
 __device__ __forceinline__ G2A hm_load(const HmEntry& e) { return {e.x, e.y, e.inf != 0}; }
+__device__ __forceinline__ G1A g1a_load(const G1AEntry& e) { return {e.x, e.y, e.inf != 0}; }
 
 // ThresholdAggregate member status flags (threshold.hip -> k_group_sum)
 enum : uint8_t { M_OK = 0, M_BAD_SIG = 1, M_BAD_IDX = 2 };
@@ -42,23 +48,113 @@ struct TaDigits {
   uint64_t a[4];
 };
 
-// Staged ThresholdAggregate (threshold.hip)
+// Verification group state (vbatch.hip): READY groups go through the pairing kernel; EMPTY
+// groups have no item left to check; FALLBACK groups send every usable item to the per-item
+// path (inconsistent messages inside the group, or a degenerate combination).
+enum : uint8_t { G_READY = 0, G_FALLBACK = 1, G_EMPTY = 2 };
+
+// Key of the random linear combination (32 bytes drawn from the OS CSPRNG per call).
+struct RlcKey {
+  uint32_t w[8];
+};
+
+// Staged ThresholdAggregate (threshold.hip).  src (nullable): member j's point is pts[src[j]].
 void launch_ta_lambda(const int64_t* idx, const uint32_t* grp_off, uint32_t n_groups, uint32_t n_partials, int mode,
                       TaDigits* dig, uint8_t* mstat, hipStream_t s);
 size_t ta_table_bytes(uint32_t n_partials);
-void launch_ta_straus(const HmEntry* pts, const TaDigits* dig, uint32_t n_partials, void* tab, G2JEntry* out,
-                      hipStream_t s);
+void launch_ta_straus(const HmEntry* pts, const uint32_t* src, const TaDigits* dig, uint32_t n_partials, void* tab,
+                      G2JEntry* out, hipStream_t s);
+void launch_ta_member_status(const uint8_t* sig_st, const uint32_t* src, uint32_t n_partials, uint8_t* mstat,
+                             hipStream_t s);
 
-// Staged verify pipeline (pipeline.hip): kernel launches on caller-provided streams.
-constexpr int GROUPS_PER_WAVE = 21;  // k_pair3: 3 lanes per partial, 21 partials per wave
+// Hashing and the pairing kernel (pipeline.hip).
+constexpr int GROUPS_PER_WAVE = 21;  // k_pair3: 3 lanes per pairing, 21 pairings per wave
 void launch_hash_to_g2(const uint8_t* msgs, const uint64_t* off, const uint32_t* len, uint32_t n, MsgEntry* hm,
                        hipStream_t s);
 void launch_lines_msg(MsgEntry* hm, uint32_t n, hipStream_t s);
+
+// k_pair3 arguments.  Unit u of a launch pairs (P, H(m)) and (-g1, S) where S's lines evaluated at
+// -g1 are sig_lines[j * stride + u].  Direct mode (list == nullptr): unit u is entry u of pk /
+// msg_idx / status.  List mode: unit u is entry e = list[base + u] when base + u < *count, where
+// entries e >= n_items denote the folded aggregate of validator e - n_items (agg_pk, agg_msg,
+// agg_status).  Statuses: a nonzero pk_st / sig_st byte (nullable arrays) decides the verdict
+// without the pairing; otherwise OK iff the product of the two pairings is one.
+struct Pair3Args {
+  const G1AEntry* pk;
+  const uint8_t* pk_st;
+  const uint8_t* sig_st;
+  const uint8_t* sig_inf;
+  const uint32_t* msg_idx;
+  const MsgEntry* hm;
+  const LineEntry* sig_lines;
+  uint32_t stride;
+  uint32_t n;
+  const uint32_t* list;
+  const uint32_t* count;
+  uint32_t base;
+  uint32_t n_items;
+  const G1AEntry* agg_pk;
+  const uint32_t* agg_msg;
+  uint8_t* status;
+  uint8_t* agg_status;
+};
+void launch_pair3(const Pair3Args& a, hipStream_t s);
+
+// Batched verification (vbatch.hip).
+void launch_item_group(const uint32_t* grp_off, uint32_t n_groups, uint32_t n, uint32_t* item_grp, hipStream_t s);
 void launch_dec_pk(const uint8_t* pks, uint32_t n, G1AEntry* out, uint8_t* st, hipStream_t s);
-void launch_dec_sig_lines(const uint8_t* sigs, uint32_t n, uint8_t* inf, uint8_t* st, LineEntry* lines,
-                          hipStream_t s);
-void launch_pair3(const G1AEntry* pk, const uint8_t* pk_st, const uint8_t* sig_inf, const uint8_t* sig_st,
-                  const uint32_t* msg_idx, const MsgEntry* hm, const LineEntry* sig_lines, uint32_t n,
-                  uint8_t* status, hipStream_t s);
+void launch_dec_sig_pt(const uint8_t* sigs, uint32_t n, HmEntry* out, uint8_t* st, hipStream_t s);
+void launch_rlc(const G1AEntry* pk, const uint8_t* pk_st, const HmEntry* sig, const uint8_t* sig_st,
+                const uint32_t* item_grp, const uint32_t* grp_off, int always, uint32_t n, uint32_t key_base,
+                const RlcKey& key, G1JEntry* pout, G2JEntry* sout, hipStream_t s);
+struct GroupPrepArgs {
+  const uint32_t* grp_off;  // nullable: group g = item g
+  uint32_t g0, ng;          // groups [g0, g0 + ng) of this launch
+  const uint32_t* msg_idx;
+  const MsgEntry* hm;
+  const G1AEntry* pk;
+  const uint8_t* pk_st;
+  const HmEntry* sig;
+  const uint8_t* sig_st;
+  const G1JEntry* pr;
+  const G2JEntry* sr;
+  // folded aggregate of validator g (nullable): its pk / signature / decode statuses / combinations
+  const G1AEntry* agg_pk;
+  const uint8_t* agg_pk_st;
+  const HmEntry* agg_sig;
+  const uint8_t* agg_st;
+  const G1JEntry* agg_pr;
+  const G2JEntry* agg_sr;
+  G1AEntry* gP;      // [ng]
+  uint32_t* gmsg;    // [n_groups] (indexed by g)
+  uint8_t* gst;      // [ng]
+  LineEntry* glines; // [N_LINES][ng]
+};
+void launch_group_prep(const GroupPrepArgs& a, hipStream_t s);
+struct ScatterArgs {
+  uint32_t n;
+  const uint32_t* item_grp;
+  const uint32_t* msg_idx;
+  const MsgEntry* hm;
+  const G1AEntry* pk;
+  const uint8_t* pk_st;
+  const HmEntry* sig;
+  const uint8_t* sig_st;
+  const uint8_t* gverdict;  // [n_groups], 0 = the group's combined check passed
+  // folded aggregates (nullable)
+  uint32_t n_agg;
+  const uint8_t* ta_status;
+  const G1AEntry* agg_pk;
+  const uint8_t* agg_pk_st;
+  const HmEntry* agg_sig;
+  uint8_t* agg_status;
+  uint8_t* status;
+  uint32_t* list;
+  uint32_t* count;
+};
+void launch_scatter(const ScatterArgs& a, hipStream_t s);
+// fallback: lines at -g1 of the listed signatures (entries >= n_items: folded aggregates)
+void launch_fb_lines(const uint32_t* list, const uint32_t* count, uint32_t base, uint32_t cap, const HmEntry* sig,
+                     const HmEntry* agg_sig, uint32_t n_items, LineEntry* lines, hipStream_t s);
 
 }  // namespace hb

@@ -3,7 +3,8 @@
 // herumi.go:225-247).  Compiled like pipeline.hip (HB_FAST_FPMUL: register-convention Fp
 // product, everything else inlined).
 //
-//   k_ta_dec   (hipbls.hip) 1 lane / partial: decompress + subgroup-check sigma_j
+//   k_dec_sig_pt (vbatch.hip) 1 lane / partial: decompress + subgroup-check sigma_j (or, in the
+//              slot entry point, the verification's decompressed points through src[])
 //   k_ta_lambda 1 lane / partial: lambda_j(0) over its group's share indices (Fr, 1/d table for
 //              the denominators), and the base-|x| digits of lambda_j
 //   k_ta_straus 1 lane / partial: lambda_j sigma_j = sum_i [a_i] (-1)^i psi^i(sigma_j), one
@@ -142,7 +143,8 @@ __device__ __forceinline__ void f2_select(Fp2& r, bool take_b, const Fp2& a, con
 // mixed additions, kept in global memory): 64 doublings + 64 table additions per partial, against
 // 4 x 64 of each for four independent ladders.  Uniform control flow: the table addition of
 // every step is computed and kept or dropped per lane by select.
-__global__ __launch_bounds__(64, 2) void k_ta_straus(const HmEntry* __restrict__ pts, const TaDigits* __restrict__ dig,
+__global__ __launch_bounds__(64, 2) void k_ta_straus(const HmEntry* __restrict__ pts, const uint32_t* __restrict__ src,
+                                                     const TaDigits* __restrict__ dig,
                                                      uint32_t n_partials, uint4* __restrict__ tab,
                                                      G2JEntry* __restrict__ out) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -153,7 +155,7 @@ __global__ __launch_bounds__(64, 2) void k_ta_straus(const HmEntry* __restrict__
   uint4* wt = tab + (size_t)blockIdx.x * 15 * TA_TAB_QUADS * 64 + lane;
   const TaDigits d = dig[it];
   {
-    const HmEntry e = pts[it];
+    const HmEntry e = pts[src ? src[it] : it];
     // psi (x, y) = (conj(x) c1x, conj(y) c1y); psi^2 (x, y) = (x c2x, y c2y)
     G2A P0 = {e.x, e.y, e.inf != 0};
     G2A P1 = {f2_mul(f2_conj(e.x), f2_from_const(PSI_CX)), f2_neg(f2_mul(f2_conj(e.y), f2_from_const(PSI_CY))), P0.inf};
@@ -197,11 +199,28 @@ void launch_ta_lambda(const int64_t* idx, const uint32_t* grp_off, uint32_t n_gr
 
 size_t ta_table_bytes(uint32_t n_partials) { return (size_t)blocks_of(n_partials, 64) * 15 * sizeof(G2JEntry) * 64; }
 
-void launch_ta_straus(const HmEntry* pts, const TaDigits* dig, uint32_t n_partials, void* tab, G2JEntry* out,
-                      hipStream_t s) {
+void launch_ta_straus(const HmEntry* pts, const uint32_t* src, const TaDigits* dig, uint32_t n_partials, void* tab,
+                      G2JEntry* out, hipStream_t s) {
   if (n_partials)
-    hipLaunchKernelGGL(k_ta_straus, dim3(blocks_of(n_partials, 64)), dim3(64), 0, s, pts, dig, n_partials,
+    hipLaunchKernelGGL(k_ta_straus, dim3(blocks_of(n_partials, 64)), dim3(64), 0, s, pts, src, dig, n_partials,
                        (uint4*)tab, out);
+}
+
+// Member statuses of a ThresholdAggregate whose partials were decompressed by the verification
+// of the same slot (member j = verified partial src[j]): undecodable there = undecodable here.
+__global__ __launch_bounds__(64) void k_ta_member_status(const uint8_t* __restrict__ sig_st,
+                                                         const uint32_t* __restrict__ src, uint32_t n_partials,
+                                                         uint8_t* __restrict__ mstat) {
+  uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n_partials) return;
+  mstat[j] = sig_st[src[j]] ? M_BAD_SIG : M_OK;
+}
+
+void launch_ta_member_status(const uint8_t* sig_st, const uint32_t* src, uint32_t n_partials, uint8_t* mstat,
+                             hipStream_t s) {
+  if (n_partials)
+    hipLaunchKernelGGL(k_ta_member_status, dim3(blocks_of(n_partials, 64)), dim3(64), 0, s, sig_st, src,
+                       n_partials, mstat);
 }
 
 }  // namespace hb

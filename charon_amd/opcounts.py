@@ -1,36 +1,84 @@
-"""Frozen algorithmic work per unit for the roofline.
+"""Algorithmic work per kernel unit for the roofline.
 
-FPMUL_PER_ITEM: Fp Montgomery products (squarings counted as products) per item, counted by the
-op-counting host build of the kernels' own arithmetic (tests/native/hostcheck.cpp, hc_count_*) on
-the r01 algorithms and frozen here, so that later algorithmic savings show up as a higher
-effective fraction; tests/test_opcount.py re-derives the r01 numbers.
+All work is counted in Fp Montgomery products (squarings counted as products): the building
+blocks below are counted by the op-counting host build of the kernels' own arithmetic
+(tests/native/hostcheck.cpp hc_count_blocks) and re-derived by tests/test_opcount.py.  One Fp
+product is MAC_PER_FPMUL = 2*12*12 + 12 = 300 32x32->64-bit multiply-adds (textbook 12-limb
+CIOS), the unit of the peak.
 
-MAC_PER_FPMUL: one 12-limb CIOS Montgomery product = 2*12*12 + 12 = 300 32x32->64 multiply-adds.
 PEAK_MAD_TOPS: v_mad_u64_u32 lane-ops/s on MI355X, measured by tools/microbench/int_rates.hip
-(profiles/r01_int_rates_microbench.txt, 16 waves/CU: 29.944 Tops/s).
+(profiles/r01_int_rates_microbench.txt, 16 waves/CU: 29.944 Tops/s, i.e. the chip's clock under
+that load; 39.3 T at the nominal 2.4 GHz with half-rate issue).
+
+Per kernel two counts: `alg` is the textbook tower-arithmetic work of the unit (what a one-lane
+implementation of the same algorithm executes); `exec` is what the kernel executes (e.g. the
+three-lane pairing evaluates every H(m) line in all three lanes and inverts in all three).
 """
 
 MAC_PER_FPMUL = 2 * 12 * 12 + 12
 PEAK_MAD_TOPS = 29.944
+PEAK_MAD_TOPS_NOMINAL = 39.3
 
-# Executed Fp products of the current kernels' arithmetic (algorithmic savings since r01, e.g.
-# cyclotomic squaring in the final exponentiation); tests/test_opcount.py re-counts these too.
-EXECUTED_FPMUL_PER_ITEM = {
-    "k_verify": 23913,
-    # straight-line SSWU (three exponentiations per map; the r01 map took a divergent fourth or
-    # fifth on the non-square branch)
-    "k_hash_to_g2": 7217,
-}
+# hc_count_blocks, in its order
+BLOCK_NAMES = ("f12_sqr", "f12_mul_line", "final_exp", "fp_inv", "g1_dec", "g2_dec", "rlc_g1", "rlc_g2",
+               "jac_add_g1", "jac_add_g2", "to_aff_g1", "to_aff_g2", "lines_eval", "lines_uneval", "jac_dbl_g2",
+               "jac_add_aff_g2", "cyclo_sqr", "f12_mul", "g2_compress")
+BLOCKS = dict(zip(BLOCK_NAMES, (36, 39, 8288, 610, 1665, 2486, 732, 1880, 16, 43, 614, 625, 1843, 1571, 16, 29, 18,
+                                54, 4)))
 
-FPMUL_PER_ITEM = {
-    # per partial: G1 decompress+subgroup 1665, G2 decompress+subgroup 2486, 2-pair Miller loop +
-    # final exponentiation 25450
-    "k_verify": 29601,
-    # the pairing part alone (k_pair3: 2-pair Miller loop + final exponentiation)
-    "k_pair3": 25450,
-    # per distinct 32-byte message: expand_message_xmd -> 2 SSWU -> 3-isogeny -> cofactor -> affine
-    "k_hash_to_g2": 7813,
-    # per validator of the bench's ThresholdAggregate (share indices {1,2,3}: lambda = 3, -3, 1;
-    # decompress+subgroup + 255-bit double-and-add per partial; 428 Fr products each on top)
-    "k_group_member_t3_123": 6595 + 11264 + 6566,
-}
+N_LINES = 68      # Miller-loop lines (63 doublings + 5 additions)
+N_SQR = 62        # Fp12 squarings of the Miller loop
+LINE_PRODUCTS = 2 * N_LINES  # two pairs per check
+
+# expand_message_xmd -> 2 SSWU (straight-line, 3 exponentiations each) -> 3-isogeny -> cofactor -> affine
+HASH_TO_G2 = 7217
+
+
+def _pair3_exec_per_lane(b=BLOCKS):
+    """Executed Fp products per lane of pair3.h's final exponentiation (3 lanes per pairing)."""
+    f4_mul, f4_sqr, g_mul, frob = 9, 6, 18, 6
+    g_inv = f4_sqr + f4_mul + f4_mul + 4 + (b["fp_inv"] + 4) + 6 + f4_mul
+    pow_x = 63 * 6 + 5 * g_mul
+    return (g_mul + g_inv) + (frob + g_mul) + 5 * pow_x + 2 * g_mul + (frob + g_mul) + (frob + 2 * g_mul) + \
+        (6 + 2 * g_mul)
+
+
+def pair3(b=BLOCKS):
+    """k_pair3, per pairing check (Miller loop over precomputed lines + final exponentiation)."""
+    alg = N_SQR * b["f12_sqr"] + LINE_PRODUCTS * b["f12_mul_line"] + N_LINES * 4 + b["final_exp"]
+    exe = N_SQR * 36 + LINE_PRODUCTS * 45 + N_LINES * 12 + 3 * _pair3_exec_per_lane(b)
+    return alg, exe
+
+
+def per_unit(b=BLOCKS, group_size=1, t=1):
+    """{kernel: (alg, exec)} Fp products per unit (unit named in UNITS)."""
+    p = pair3(b)
+    k = group_size
+    prep = (b["lines_eval"] if k == 1 else
+            (k - 1) * (b["jac_add_g1"] + b["jac_add_g2"]) + b["to_aff_g1"] + b["to_aff_g2"] + b["lines_eval"])
+    straus = 18 + 11 * b["jac_add_aff_g2"] + 64 * (b["jac_dbl_g2"] + b["jac_add_g2"])
+    gsum = t * b["jac_add_g2"] + b["to_aff_g2"] + b["g2_compress"]
+    out = {
+        "k_pair3": p, "k_pair3_fallback": p,
+        "k_dec_pk": (b["g1_dec"],) * 2,
+        "k_dec_sig_pt": (b["g2_dec"],) * 2,
+        "k_rlc": (b["rlc_g1"] + b["rlc_g2"],) * 2,
+        "k_group_prep": (prep,) * 2,
+        "k_fb_lines": (b["lines_eval"],) * 2,
+        "k_ta_straus": (straus,) * 2,
+        "k_group_sum": (gsum,) * 2,
+        "k_hash_to_g2": (HASH_TO_G2,) * 2,
+        "k_lines_msg": (b["lines_uneval"],) * 2,
+    }
+    return out
+
+
+UNITS = {"k_pair3": "pairing check", "k_pair3_fallback": "pairing check", "k_dec_pk": "public key",
+         "k_dec_sig_pt": "signature", "k_rlc": "partial", "k_group_prep": "verification group",
+         "k_fb_lines": "partial", "k_ta_straus": "aggregation member", "k_group_sum": "aggregation group",
+         "k_hash_to_g2": "message", "k_lines_msg": "message"}
+
+# The herumi-equivalent per-item work of r01 (frozen): one Verify = G1 + G2 decompression with
+# subgroup checks + a 2-pair Miller loop with line construction + final exponentiation, counted
+# on the r01 algorithms.  The slot's effective rate is quoted against it.
+FPMUL_PER_ITEM_R01 = {"verify": 29601, "hash_to_g2": 7813}

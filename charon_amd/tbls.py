@@ -85,10 +85,11 @@ def _pack_msgs(msgs: Sequence[bytes]):
 
 
 class HIPBLS:
-    """tbls.Implementation on the MI355X.  Thread-safe: the library serialises host calls."""
+    """tbls.Implementation on the MI355X.  Thread-safe: the library coalesces concurrent
+    verification calls into one launch and shards batches over its devices."""
 
-    def __init__(self):
-        self._L = _lib.lib()
+    def __init__(self, device_mask: int = 0):
+        self._L = _lib.lib(device_mask)
 
     # ------------------------------------------------------------------ key management
     def generate_secret_key(self) -> bytes:
@@ -183,7 +184,7 @@ class HIPBLS:
         """herumi.go:288-304; raises TblsError with herumi's message, returns None on success."""
         st = self.verify_batch([compressed_public_key], [data], [signature])[0]
         if st != OK:
-            raise TblsError(_VERIFY_ERR[st])
+            raise TblsError(_VERIFY_ERR.get(st, "signature not verified"))
 
     def verify_batch(self, pks: Sequence[bytes], msgs: Sequence[bytes], sigs: Sequence[bytes]) -> List[int]:
         """Batch tbls.Verify: one status code per item (0 = verified)."""
@@ -248,7 +249,7 @@ class HIPBLS:
         """herumi.go:318-342 (FastAggregateVerify)."""
         st = self.verify_aggregate_batch([public_shares], [signature], [data])[0]
         if st != OK:
-            raise TblsError(_VERIFY_AGG_ERR[st])
+            raise TblsError(_VERIFY_AGG_ERR.get(st, "signature verification failed"))
 
     def verify_aggregate_batch(self, pk_groups: Sequence[Sequence[bytes]], sigs: Sequence[bytes],
                                msgs: Sequence[bytes]) -> List[int]:

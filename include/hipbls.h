@@ -34,14 +34,21 @@ enum hbls_status {
   HBLS_BAD_INPUT = 6       /* malformed batch description (offsets/lengths)  -- new, batch-only */
 };
 
-/* Return codes of the entry points themselves: 0 on success, <0 on a HIP/runtime error
- * (text via hbls_last_error()).  Per-item verdicts are in the status arrays. */
+/* Return codes of the entry points themselves: 0 on success, <0 on a HIP/runtime error or a
+ * malformed batch description (text via hbls_last_error()).  Per-item verdicts are in the status
+ * arrays. */
 
-/* Select and initialise a device (idempotent, thread-safe; herumi.go:18-36 init()). */
-int hbls_init(int device);
+/* Select and initialise the devices the library drives (herumi.go:18-36 init(), idempotent and
+ * thread-safe).  device_mask: bit k = HIP device k; 0 = HBLS_DEVICE_MASK from the environment
+ * (default: device 0); 0xffffffff = every visible device.  Host-buffer calls shard their items
+ * over the devices of the mask (one process, several GPUs: charon runs as one Go process,
+ * app/app.go:131).  Calling again with a different mask fails. */
+int hbls_init(uint32_t device_mask);
 const char* hbls_last_error(void);
 /* Nonzero if a gfx950 device is present and the kernels are loadable. */
 int hbls_available(void);
+/* Devices driven by the library (after hbls_init). */
+int hbls_device_count(void);
 
 /* ---------------------------------------------------------------------------------------
  * Host-buffer entry points (the drop-in boundary for the Go shim).  Blocking; the library
@@ -50,8 +57,12 @@ int hbls_available(void);
 
 /* Verify: n independent (pk, msg, sig) triples.  tbls.Verify / Herumi.Verify
  * (tbls.go:121, herumi.go:288-304).  Message i is msgs[msg_off[i] .. msg_off[i]+msg_len[i]).
- * Identical messages are hashed to G2 once. status[i] in {OK, BAD_PUBKEY, BAD_SIGNATURE,
- * NOT_VERIFIED}. */
+ * Identical messages are hashed to G2 once; items over one message are checked together by a
+ * random linear combination (one pairing per group, each item re-checked alone if its group
+ * fails), so every status equals the per-item verdict.  status[i] in {OK, BAD_PUBKEY,
+ * BAD_SIGNATURE, NOT_VERIFIED}.  Thread-safe: concurrent calls (one goroutine per libp2p stream,
+ * p2p/receive.go:52) are coalesced into one launch after at most HBLS_COALESCE_US microseconds
+ * (default 200; 0 disables). */
 int hbls_verify_batch(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msgs,
                       const uint64_t* msg_off, const uint32_t* msg_len, size_t n, uint8_t* status);
 
@@ -90,40 +101,88 @@ int hbls_recover_secret(const uint8_t* shares, const int64_t* idx, size_t k, uin
 
 /* ---------------------------------------------------------------------------------------
  * Device-buffer entry points (inputs already resident in HBM; asynchronous on `stream`, a
- * hipStream_t passed as void*; 0 = the library's stream).  Used by the slot pipeline and the
- * benchmark.  All pointers are device pointers.
+ * hipStream_t passed as void*; 0 = the first device's null stream).  The device is the one the
+ * stream belongs to.  All pointers are device pointers.  Work is ordered after prior work on
+ * `stream` and complete when later work on `stream` starts; library workspaces are ordered by
+ * events, so calls on different streams never race on them.
  *
  * verify: msg_idx[i] indexes the table of distinct messages hashed by hbls_hash_to_g2_device
- * into `hm` (192 B affine G2 points, library layout).
+ * into `hm` (hbls_hm_entry_bytes() per message, library layout).  vgrp_off (nullable): groups
+ * of consecutive partials over one message (group g = [vgrp_off[g], vgrp_off[g+1])), checked
+ * together; NULL = every partial on its own.
  * --------------------------------------------------------------------------------------- */
 int hbls_hash_to_g2_device(const uint8_t* msgs, const uint64_t* msg_off, const uint32_t* msg_len,
                            size_t n_msgs, void* hm, void* stream);
 int hbls_verify_device(const uint8_t* pks, const uint8_t* sigs, const uint32_t* msg_idx, const void* hm,
-                       size_t n, uint8_t* status, void* stream);
+                       size_t n, const uint32_t* vgrp_off, size_t n_vgroups, uint8_t* status, void* stream);
 int hbls_threshold_aggregate_device(const uint8_t* sigs, const int64_t* idx, const uint32_t* grp_off,
                                     size_t n_groups, size_t n_partials, uint8_t* out, uint8_t* status,
                                     void* stream);
-/* One attestation slot in one call (the batch entry point of SURVEY.md §8b for sigagg/parsigex):
- * hash the n_msgs distinct messages (+ their Miller lines) into `hm`, verify the n partials
- * (msg_idx[i] indexes the messages) into vstatus, and threshold-aggregate n_groups groups
- * (grp_off over n_ta_partials partials) into ta_out / ta_status -- hashing and signature
- * decompression run concurrently on the library's high-priority side streams, the aggregation
- * on the library's own stream, the pairing kernel on `stream`; everything is ordered after prior
- * work on `stream` and complete when later work on `stream` starts.
+
+/* One attestation slot in one call: the batch entry point of SURVEY.md section 8b for
+ * sigagg/parsigex (core/parsigex/parsigex.go:93-98, core/sigagg/sigagg.go:56-63,105,117).
+ *   - hash the n_msgs distinct messages (+ their Miller lines) into hm;
+ *   - verify the n partials (msg_idx[i] indexes the messages, vgrp_off groups as in
+ *     hbls_verify_device) into vstatus;
+ *   - threshold-aggregate n_groups groups (grp_off over n_ta_partials members with share indices
+ *     ta_idx) into ta_out / ta_status.  Members are either verified partials (ta_src[j] = index
+ *     of member j among the n partials: their decompression is shared) or their own 96-byte
+ *     signatures ta_sigs (ta_src == NULL);
+ *   - optionally (dv_pks != NULL, requires n_vgroups == n_groups with group g = validator g):
+ *     verify each aggregate under the validator's DV public key (sigagg.go:117) into
+ *     agg_vstatus, folded into group g's combined check.  agg_vstatus[g] is the aggregation
+ *     status when no aggregate was produced.
  * Semantics per item as hbls_verify_batch / hbls_threshold_aggregate_batch. */
-int hbls_slot_device(const uint8_t* msgs, const uint64_t* msg_off, const uint32_t* msg_len, size_t n_msgs, void* hm,
-                     const uint8_t* pks, const uint8_t* sigs, const uint32_t* msg_idx, size_t n, uint8_t* vstatus,
-                     const uint8_t* ta_sigs, const int64_t* ta_idx, const uint32_t* grp_off, size_t n_groups,
-                     size_t n_ta_partials, uint8_t* ta_out, uint8_t* ta_status, void* stream);
+typedef struct hbls_slot {
+  const uint8_t* msgs;
+  const uint64_t* msg_off;
+  const uint32_t* msg_len;
+  size_t n_msgs;
+  void* hm;
+  const uint8_t* pks;
+  const uint8_t* sigs;
+  const uint32_t* msg_idx;
+  size_t n;
+  const uint32_t* vgrp_off;
+  size_t n_vgroups;
+  uint8_t* vstatus;
+  const uint8_t* ta_sigs;
+  const uint32_t* ta_src;
+  const int64_t* ta_idx;
+  const uint32_t* grp_off;
+  size_t n_groups;
+  size_t n_ta_partials;
+  uint8_t* ta_out;
+  uint8_t* ta_status;
+  const uint8_t* dv_pks;
+  uint8_t* agg_vstatus;
+} hbls_slot;
+int hbls_slot_device(const hbls_slot* args, void* stream);
 /* Bytes of the `hm` table entry per message. */
 size_t hbls_hm_entry_bytes(void);
-/* Measurement: with timing enabled (which also resets the record), every launch of the pairing
- * kernel (k_pair3, the dominant kernel) is bracketed by HIP events on the stream it runs on;
- * hbls_timing_read returns their durations in milliseconds, in launch order. */
+/* Measurement: with timing enabled (which also resets the record), every kernel launch of the
+ * verification, aggregation and hashing paths is bracketed by HIP events on the stream it runs
+ * on; hbls_timing_read returns kernel names (static strings) and durations in milliseconds, in
+ * launch order. */
 int hbls_timing(int enable);
-int hbls_timing_read(float* ms, size_t max_n, size_t* n_out);
+int hbls_timing_read(const char** names, float* ms, size_t max_n, size_t* n_out);
+/* Verification statistics, collected only with HBLS_STATS=1 in the environment (each call then
+ * synchronises): out[0] items verified, out[1] verification groups, out[2] items re-checked
+ * alone because their group's combined check failed. */
+int hbls_stats(uint64_t* out, size_t n);
 /* Wait for all work the library queued on `stream`. */
 int hbls_sync(void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Exchange of slot results between processes that drive one GPU each:
+ * RCCL over xGMI.  Rank 0 creates the id, every rank passes it to hbls_comm_init, then
+ * hbls_allgather_device gathers `bytes` from every rank into recv (rank order) on `stream`.
+ * --------------------------------------------------------------------------------------- */
+size_t hbls_comm_id_bytes(void);
+int hbls_comm_unique_id(uint8_t* id);
+int hbls_comm_init(int nranks, int rank, const uint8_t* id);
+int hbls_allgather_device(const void* send, void* recv, size_t bytes, void* stream);
+int hbls_comm_destroy(void);
 
 #ifdef __cplusplus
 }

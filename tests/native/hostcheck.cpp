@@ -5,10 +5,31 @@
 // hc_count_* read to freeze the algorithmic work per item (charon_amd/opcounts.py).
 #define HB_COUNT_OPS 1
 #include "../../charon_amd/csrc/ops.h"
+#include "../../charon_amd/csrc/rlc.h"
 #include <string.h>
 
 namespace hb {
 thread_local unsigned long long g_cnt_fp_mul = 0, g_cnt_fr_mul = 0;
+}
+
+// host restatement of lines.h line_chain (68 lines of the Miller chain of Q)
+struct LineEntryHost {
+  hb::Fp2 a0, a1, b1;
+};
+static void hc_line_chain(const hb::G2A& Q, LineEntryHost* out, bool eval) {
+  using namespace hb;
+  G2Proj T = {Q.x, Q.y, f2_one()};
+  int j = 0;
+  for (int i = 62; i >= 0; i--) {
+    LineCoeffs l = miller_dbl_c(T);
+    if (eval) line_eval(l, fp_from_const(G1_GEN_X), fp_from_const(G1_GEN_NEG_Y));
+    out[j++] = {l.a0, l.a1, l.b1};
+    if ((HB_X_ABS >> i) & 1) {
+      l = miller_add_c(T, Q.x, Q.y);
+      if (eval) line_eval(l, fp_from_const(G1_GEN_X), fp_from_const(G1_GEN_NEG_Y));
+      out[j++] = {l.a0, l.a1, l.b1};
+    }
+  }
 }
 
 using namespace hb;
@@ -263,4 +284,165 @@ extern "C" int hc_cpu_slot(int threads, int units, int n, int t, const uint8_t* 
   for (int k = 0; k < threads; k++) ws.emplace_back(work);
   for (auto& w : ws) w.join();
   return bad.load();
+}
+
+// ---------------------------------------------------------------------------------------
+// Batched verification (vbatch.hip) on the host.
+// hc_rlc: [a + b lambda] P and S through the endomorphism ladders of rlc.h, compressed
+// (out48, out96); tests/test_hostcheck.py compares them with the oracle's [r] P, [r] S.
+extern "C" int hc_rlc(const uint8_t* pk48, const uint8_t* sig96, uint32_t a, uint32_t b, uint8_t* out48,
+                      uint8_t* out96) {
+  G1A p;
+  G2A q;
+  if (g1_decompress(p, pk48)) return 1;
+  if (g2_decompress(q, sig96)) return 2;
+  g1_compress(out48, jac_to_aff(rlc_g1(p, a, b)));
+  g2_compress(out96, jac_to_aff(rlc_g2(q, a, b)));
+  return 0;
+}
+
+// Fp-mul counts of the building blocks the per-kernel roofline counts are assembled from
+// (charon_amd/opcounts.py), on a valid (pk, sig):
+//  0 f12_sqr            1 f12_mul_line        2 final_exponentiation   3 fp_inv
+//  4 g1_decompress      5 g2_decompress       6 rlc_g1 (a, b top bits set)  7 rlc_g2
+//  8 jac_add G1         9 jac_add G2          10 jac_to_aff G1 (Z != 1)     11 jac_to_aff G2
+//  12 line chain at -g1 (68 lines, evaluated) 13 line chain unevaluated     14 jac_dbl G2
+//  15 jac_add_aff G2    16 f12_cyclo_sqr      17 f12_mul                    18 g2_compress
+extern "C" int hc_count_blocks(const uint8_t* pk48, const uint8_t* sig96, unsigned long long* out) {
+  G1A p;
+  G2A q;
+  if (g1_decompress(p, pk48)) return 1;
+  if (g2_decompress(q, sig96)) return 2;
+  Fp12 f = miller_loop2(p, q, g1_generator_neg(), q);
+  auto cnt = [&](int k, auto&& fn) {
+    g_cnt_fp_mul = 0;
+    fn();
+    out[k] = g_cnt_fp_mul;
+  };
+  Fp12 r;
+  cnt(0, [&] { r = f12_sqr(f); });
+  cnt(1, [&] { r = f12_mul_line(f, q.x, q.y, q.x); });
+  cnt(2, [&] { r = final_exponentiation(f); });
+  Fp t;
+  cnt(3, [&] { t = fp_inv(p.x); });
+  G1A p2;
+  G2A q2;
+  cnt(4, [&] { g1_decompress(p2, pk48); });
+  cnt(5, [&] { g2_decompress(q2, sig96); });
+  G1J pj;
+  G2J qj;
+  cnt(6, [&] { pj = rlc_g1(p, 0x80000001u, 0x80000001u); });
+  cnt(7, [&] { qj = rlc_g2(q, 0x80000001u, 0x80000001u); });
+  G1J pj2 = jac_dbl(pj);
+  G2J qj2 = jac_dbl(qj);
+  cnt(8, [&] { pj2 = jac_add(pj2, pj); });
+  cnt(9, [&] { qj2 = jac_add(qj2, qj); });
+  cnt(10, [&] { p2 = jac_to_aff(pj2); });
+  cnt(11, [&] { q2 = jac_to_aff(qj2); });
+  static LineEntryHost lines[N_LINES];
+  cnt(12, [&] { hc_line_chain(q, lines, true); });
+  cnt(13, [&] { hc_line_chain(q, lines, false); });
+  cnt(14, [&] { qj2 = jac_dbl(qj2); });
+  cnt(15, [&] { qj2 = jac_add_aff(qj2, q); });
+  Fp12 fe = final_exponentiation(f);
+  cnt(16, [&] { r = f12_cyclo_sqr(fe); });
+  cnt(17, [&] { r = f12_mul(f, fe); });
+  uint8_t buf[96];
+  cnt(18, [&] { g2_compress(buf, q); });
+  (void)r;
+  (void)t;
+  return 0;
+}
+
+// The batched verification's group check on the host (vbatch.hip k_rlc + k_group_prep + the
+// pairing product): k items over one message with coefficients (a_i, b_i).  Returns 1 if the
+// combined equation holds, 0 if not, <0 on a decoding error.
+extern "C" int hc_group_check(int k, const uint8_t* pks, const uint8_t* sigs, const uint8_t* msg, uint32_t len,
+                              const uint32_t* a, const uint32_t* b) {
+  G1J pacc = jac_infinity<Fp>();
+  G2J sacc = jac_infinity<Fp2>();
+  for (int i = 0; i < k; i++) {
+    G1A p;
+    G2A q;
+    if (g1_decompress(p, pks + 48 * i)) return -1;
+    if (g2_decompress(q, sigs + 96 * i)) return -2;
+    pacc = jac_add(pacc, rlc_g1(p, a[i], b[i]));
+    sacc = jac_add(sacc, rlc_g2(q, a[i], b[i]));
+  }
+  G1A P = jac_to_aff(pacc);
+  G2A S = jac_to_aff(sacc);
+  G2A H = jac_to_aff(hash_to_g2(msg, len));
+  Fp12 f = miller_loop2(P, H, g1_generator_neg(), S);
+  return f12_is_one(final_exponentiation(f)) ? 1 : 0;
+}
+
+// Raw device Jacobian points (G1JEntry / G2JEntry limbs) -> compressed affine encodings.
+extern "C" int hc_jac_compress(const uint8_t* g1raw, uint8_t* out48, const uint8_t* g2raw, uint8_t* out96) {
+  G1J p;
+  G2J q;
+  memcpy(&p, g1raw, sizeof(p));
+  memcpy(&q, g2raw, sizeof(q));
+  g1_compress(out48, jac_to_aff(p));
+  g2_compress(out96, jac_to_aff(q));
+  return 0;
+}
+
+// The batched verification's coefficients on the host (vbatch.hip rlc_coeffs).
+extern "C" void hc_rlc_coeffs(const uint32_t* key8, uint32_t item, uint32_t* ab) {
+  uint32_t w[16];
+  for (int j = 0; j < 8; j++) w[j] = key8[j];
+  w[8] = item;
+  w[9] = 0x80000000u;
+  for (int j = 10; j < 15; j++) w[j] = 0;
+  w[15] = 36 * 8;
+  Sha256State st = sha256_init();
+  sha256_compress(st, w);
+  ab[0] = st.h[0];
+  ab[1] = st.h[1];
+  if ((ab[0] | ab[1]) == 0) ab[0] = 1;
+}
+
+// G1AEntry-layout affine point (x, y Montgomery limbs, inf) -> compressed
+extern "C" int hc_g1a_compress(const uint8_t* raw, uint8_t* out48) {
+  G1A p;
+  memcpy(&p.x, raw, sizeof(Fp));
+  memcpy(&p.y, raw + sizeof(Fp), sizeof(Fp));
+  uint32_t inf;
+  memcpy(&inf, raw + 2 * sizeof(Fp), 4);
+  p.inf = inf != 0;
+  g1_compress(out48, p);
+  return 0;
+}
+
+// sum over k items of [a_i + b_i lambda] pk_i (G1), compressed
+extern "C" int hc_rlc_sum_g1(int k, const uint8_t* pks, const uint32_t* ab, uint8_t* out48) {
+  G1J acc = jac_infinity<Fp>();
+  for (int i = 0; i < k; i++) {
+    G1A p;
+    if (g1_decompress(p, pks + 48 * i)) return 1;
+    acc = jac_add(acc, rlc_g1(p, ab[2 * i], ab[2 * i + 1]));
+  }
+  g1_compress(out48, jac_to_aff(acc));
+  return 0;
+}
+
+extern "C" int hc_jac_add(const uint8_t* pk48, const uint8_t* sig96, uint32_t k1, uint32_t k2, uint8_t* out48,
+                          uint8_t* out96) {
+  G1A p;
+  G2A q;
+  if (g1_decompress(p, pk48) || g2_decompress(q, sig96)) return 1;
+  g1_compress(out48, jac_to_aff(jac_add(jac_mul_aff(p, &k1, 32), jac_mul_aff(p, &k2, 32))));
+  g2_compress(out96, jac_to_aff(jac_add(jac_mul_aff(q, &k1, 32), jac_mul_aff(q, &k2, 32))));
+  return 0;
+}
+
+extern "C" int hc_sum_raw(const uint8_t* pr_raw, uint32_t n, uint8_t* out48) {
+  G1J acc = jac_infinity<Fp>();
+  for (uint32_t i = 0; i < n; i++) {
+    G1J p;
+    memcpy(&p, pr_raw + sizeof(G1J) * i, sizeof(G1J));
+    acc = jac_add(acc, p);
+  }
+  g1_compress(out48, jac_to_aff(acc));
+  return 0;
 }

@@ -1,0 +1,328 @@
+"""GPU parity at BASELINE sizes through the C ABI (-m gpu).
+
+* The slot entry point (hbls_slot_device: hashing, batched verification, ThresholdAggregate over
+  the verified partials, post-aggregate verification under the DV keys) on a C2-size cluster with
+  the C5 adversarial mix: 1 % of the partials corrupted in equal fifths (random bytes, on-curve
+  off-subgroup points, wrong message, wrong share index, infinity) plus a few undecodable public
+  keys.  Expected statuses follow from the construction (reference semantics:
+  core/parsigex/parsigex_test.go:285-289 random signature -> error, core/sigagg/sigagg_test.go
+  wrong partials, validatorapi_test.go wrong message -> "signature not verified"), cross-checked
+  on a sample by the oracle.
+* VerifyAggregate with 512 public keys per message (sync committee, BASELINE configs[4]).
+* Concurrent single-item callers (the library's coalescing queue) and a device entry point
+  racing a host-buffer call on another stream (the workspaces are ordered by events).
+"""
+import ctypes
+import hashlib
+import random
+import threading
+
+import numpy as np
+import pytest
+
+from charon_amd import _lib
+from charon_amd._lib import BAD_PUBKEY, BAD_SIGNATURE, NOT_VERIFIED, OK
+
+pytestmark = pytest.mark.gpu
+
+
+def _p(x):
+    if x is None:
+        return None
+    if isinstance(x, np.ndarray):
+        return ctypes.c_void_p(x.ctypes.data)
+    return ctypes.c_void_p(x.data_ptr())
+
+
+def _chk(L, rc):
+    assert rc == 0, L.hbls_last_error().decode()
+
+
+def _off_subgroup_g2(rng, count):
+    """On-curve G2 points outside the r-torsion, compressed (oracle: test infrastructure)."""
+    from oracle import bls12381 as B
+    out = []
+    while len(out) < count:
+        x = (rng.randrange(B.P), rng.randrange(B.P))
+        rhs = B.f2_add(B.f2_mul(B.f2_sqr(x), x), B.B_G2)
+        y = B.f2_sqrt(rhs)
+        if y is None:
+            continue
+        pt = (x, y)
+        if B.g2_in_subgroup(pt):
+            continue
+        out.append(B.g2_compress(pt))
+    return out
+
+
+@pytest.fixture(scope="module")
+def L():
+    from charon_amd import tbls
+    tbls.HIPBLS()  # initialises the library on its devices
+    return _lib.load_library()
+
+
+def _sign(L, sks, msgs):
+    n = len(msgs) // 32
+    out = np.zeros(96 * n, dtype=np.uint8)
+    st = np.zeros(n, dtype=np.uint8)
+    off = np.arange(n, dtype=np.uint64) * 32
+    ln = np.full(n, 32, dtype=np.uint32)
+    _chk(L, L.hbls_sign_batch(_p(sks), _p(msgs), _p(off), _p(ln), n, _p(out), _p(st)))
+    assert not st.any()
+    return out
+
+
+def _pks(L, sks):
+    n = len(sks) // 32
+    out = np.zeros(48 * n, dtype=np.uint8)
+    st = np.zeros(n, dtype=np.uint8)
+    _chk(L, L.hbls_secret_to_public_key_batch(_p(sks), n, _p(out), _p(st)))
+    assert not st.any()
+    return out
+
+
+def test_slot_adversarial_c2(L):
+    import torch
+    from charon_amd import synth
+    V, n, t = 10_000, 4, 3
+    rng = random.Random(2024)
+    cl = synth.make_cluster(V, n, t, n_msgs=64)
+    NP = V * n
+    M = len(cl.msgs)
+    msgs = np.frombuffer(b"".join(cl.msgs), dtype=np.uint8).copy()
+    msg_of_v = np.asarray(cl.msg_of_validator, dtype=np.uint32)
+    midx = np.repeat(msg_of_v, n)
+    item_msgs = msgs.reshape(M, 32)[midx].reshape(-1).copy()
+    sks = np.frombuffer(b"".join(cl.share_sks), dtype=np.uint8).copy()
+    pks = _pks(L, sks)
+    sigs = _sign(L, sks, item_msgs)
+    root_sks = np.frombuffer(b"".join(cl.root_sks), dtype=np.uint8).copy()
+    root_sigs = _sign(L, root_sks, msgs.reshape(M, 32)[msg_of_v].reshape(-1).copy())
+    dv_pks = _pks(L, root_sks)
+
+    # 1 % corrupted partials in equal fifths + 20 undecodable public keys
+    bad = rng.sample(range(NP), NP // 100)
+    cls = {i: k % 5 for k, i in enumerate(bad)}
+    offsub = _off_subgroup_g2(rng, 8)
+    expect = np.zeros(NP, dtype=np.uint8)
+    wrong_msg = hashlib.sha256(b"some other signing root").digest()
+    wm_items = [i for i, c in cls.items() if c == 2]
+    wm_sigs = _sign(L, np.concatenate([sks[32 * i:32 * i + 32] for i in wm_items]),
+                    np.frombuffer(wrong_msg * len(wm_items), dtype=np.uint8).copy())
+    for k, i in enumerate(wm_items):
+        sigs[96 * i:96 * i + 96] = wm_sigs[96 * k:96 * k + 96]
+    for i, c in cls.items():
+        v, s = divmod(i, n)
+        if c == 0:
+            b = bytearray(rng.randrange(256) for _ in range(96))
+            b[0] &= 0x7F  # no compression flag: never decodable
+            sigs[96 * i:96 * i + 96] = np.frombuffer(bytes(b), dtype=np.uint8)
+            expect[i] = BAD_SIGNATURE
+        elif c == 1:
+            sigs[96 * i:96 * i + 96] = np.frombuffer(offsub[i % len(offsub)], dtype=np.uint8)
+            expect[i] = BAD_SIGNATURE
+        elif c == 2:
+            expect[i] = NOT_VERIFIED
+        elif c == 3:  # a correct partial of another share of the same validator
+            j = v * n + (s + 1) % n
+            sigs[96 * i:96 * i + 96] = _sign(L, sks[32 * j:32 * j + 32].copy(), msgs.reshape(M, 32)[midx[i]].copy())
+            expect[i] = NOT_VERIFIED
+        else:
+            sigs[96 * i:96 * i + 96] = 0
+            sigs[96 * i] = 0xC0
+            expect[i] = NOT_VERIFIED
+    bad_pk = [i for i in rng.sample(range(NP), 20) if i not in cls]
+    for i in bad_pk:
+        pks[48 * i] = 0x9A  # compressed, x >= p
+        pks[48 * i + 1:48 * i + 48] = 0xFF
+        expect[i] = BAD_PUBKEY
+
+    ta_src = (np.arange(V)[:, None] * n + np.arange(t)[None, :]).reshape(-1).astype(np.uint32)
+    ta_idx = np.tile(np.arange(1, t + 1, dtype=np.int64), V)
+    grp_off = np.arange(V + 1, dtype=np.uint32) * t
+    vgrp_off = np.arange(V + 1, dtype=np.uint32) * n
+    exp_ta = np.zeros(V, dtype=np.uint8)
+    exp_agg = np.zeros(V, dtype=np.uint8)
+    for v in range(V):
+        mem = [cls.get(v * n + s) for s in range(t)]  # the aggregation sees signatures only
+        if any(c in (0, 1) for c in mem):
+            exp_ta[v] = BAD_SIGNATURE
+            exp_agg[v] = BAD_SIGNATURE
+        elif any(c is not None for c in mem):
+            exp_agg[v] = NOT_VERIFIED  # decodable but wrong members: a wrong aggregate
+
+    dev = torch.device("cuda", 0)
+
+    def up(a):
+        return torch.from_numpy(a).to(dev)
+
+    d = {k: up(a) for k, a in dict(msgs=msgs, moff=(np.arange(M, dtype=np.uint64) * 32).view(np.int64),
+                                   mlen=np.full(M, 32, dtype=np.uint32).view(np.int32), pks=pks, sigs=sigs,
+                                   midx=midx.view(np.int32), vgoff=vgrp_off.view(np.int32), tsrc=ta_src.view(np.int32),
+                                   tidx=ta_idx, goff=grp_off.view(np.int32), dvpk=dv_pks).items()}
+    hm = torch.zeros(M * L.hbls_hm_entry_bytes(), dtype=torch.uint8, device=dev)
+    vst = torch.full((NP,), 255, dtype=torch.uint8, device=dev)
+    tout = torch.zeros(V * 96, dtype=torch.uint8, device=dev)
+    tst = torch.full((V,), 255, dtype=torch.uint8, device=dev)
+    ast = torch.full((V,), 255, dtype=torch.uint8, device=dev)
+    slot = _lib.HblsSlot(msgs=_p(d["msgs"]).value, msg_off=_p(d["moff"]).value, msg_len=_p(d["mlen"]).value,
+                         n_msgs=M, hm=_p(hm).value, pks=_p(d["pks"]).value, sigs=_p(d["sigs"]).value,
+                         msg_idx=_p(d["midx"]).value, n=NP, vgrp_off=_p(d["vgoff"]).value, n_vgroups=V,
+                         vstatus=_p(vst).value, ta_sigs=None, ta_src=_p(d["tsrc"]).value,
+                         ta_idx=_p(d["tidx"]).value, grp_off=_p(d["goff"]).value, n_groups=V, n_ta_partials=V * t,
+                         ta_out=_p(tout).value, ta_status=_p(tst).value, dv_pks=_p(d["dvpk"]).value,
+                         agg_vstatus=_p(ast).value)
+    s = torch.cuda.Stream(device=dev)
+    _chk(L, L.hbls_slot_device(ctypes.byref(slot), ctypes.c_void_p(s.cuda_stream)))
+    s.synchronize()
+    got = vst.cpu().numpy()
+    mism = np.nonzero(got != expect)[0]
+    assert len(mism) == 0, [(int(i), int(got[i]), int(expect[i]), cls.get(int(i))) for i in mism[:10]]
+    assert np.array_equal(tst.cpu().numpy(), exp_ta)
+    ga = ast.cpu().numpy()
+    bad_a = np.nonzero(ga != exp_agg)[0]
+    assert len(bad_a) == 0, [(int(v), int(ga[v]), int(exp_agg[v]), [cls.get(int(v) * n + s) for s in range(n)])
+                             for v in bad_a[:10]]
+    ok_v = np.nonzero(exp_agg == 0)[0]
+    to = tout.cpu().numpy().reshape(V, 96)
+    assert np.array_equal(to[ok_v], root_sigs.reshape(V, 96)[ok_v])
+
+    # oracle spot check on a sample of corrupted and clean partials
+    from oracle import bls12381 as B
+    sample = [bad[k] for k in range(5)] + bad_pk[:1] + [int(rng.randrange(NP))]
+    for i in sample:
+        st = B.verify(bytes(pks[48 * i:48 * i + 48]), bytes(item_msgs[32 * i:32 * i + 32]),
+                      bytes(sigs[96 * i:96 * i + 96]))
+        assert st == got[i], (i, st, got[i])
+
+
+def test_verify_aggregate_512(L):
+    """FastAggregateVerify over 512 public keys per message (sync committee)."""
+    rng = random.Random(5)
+    G, K = 4, 512
+    sks = np.frombuffer(b"".join(rng.randrange(1, 2 ** 250).to_bytes(32, "big") for _ in range(G * K)),
+                        dtype=np.uint8).copy()
+    pks = _pks(L, sks)
+    msgs = [hashlib.sha256(b"sync committee root %d" % g).digest() for g in range(G)]
+    item_msgs = np.frombuffer(b"".join(msgs[g] for g in range(G) for _ in range(K)), dtype=np.uint8).copy()
+    sigs = _sign(L, sks, item_msgs)
+    aggs = np.zeros(96 * G, dtype=np.uint8)
+    ast = np.zeros(G, dtype=np.uint8)
+    goff = np.arange(G + 1, dtype=np.uint32) * K
+    _chk(L, L.hbls_aggregate_batch(_p(sigs), _p(goff), G, _p(aggs), _p(ast)))
+    assert not ast.any()
+    # group 1: a wrong aggregate (group 2's); group 3: one undecodable key
+    aggs2 = aggs.copy()
+    aggs2[96:192] = aggs[192:288]
+    pks2 = pks.copy()
+    pks2[48 * (3 * K + 7)] = 0x9A
+    pks2[48 * (3 * K + 7) + 1:48 * (3 * K + 8)] = 0xFF
+    mb = np.frombuffer(b"".join(msgs), dtype=np.uint8).copy()
+    moff = np.arange(G, dtype=np.uint64) * 32
+    mlen = np.full(G, 32, dtype=np.uint32)
+    st = np.full(G, 255, dtype=np.uint8)
+    _chk(L, L.hbls_verify_aggregate_batch(_p(pks2), _p(goff), _p(aggs2), _p(mb), _p(moff), _p(mlen), G, _p(st)))
+    assert list(st) == [OK, NOT_VERIFIED, OK, BAD_PUBKEY]
+
+
+def test_verify_aggregate_bad_offsets(L):
+    pks = np.zeros(48 * 4, dtype=np.uint8)
+    sigs = np.zeros(96 * 2, dtype=np.uint8)
+    mb = np.zeros(64, dtype=np.uint8)
+    moff = np.array([0, 32], dtype=np.uint64)
+    mlen = np.array([32, 32], dtype=np.uint32)
+    st = np.zeros(2, dtype=np.uint8)
+    goff = np.array([0, 3, 2], dtype=np.uint32)  # decreasing
+    assert L.hbls_verify_aggregate_batch(_p(pks), _p(goff), _p(sigs), _p(mb), _p(moff), _p(mlen), 2, _p(st)) != 0
+    assert b"non-decreasing" in L.hbls_last_error()
+
+
+def test_concurrent_single_item_callers(hipbls):
+    """32 threads, each calling verify with one item (valid or wrong message), as charon's stream
+    handlers do; every caller gets its own verdict from the coalesced launches."""
+    rng = random.Random(9)
+    keys = [hipbls.generate_secret_key() for _ in range(64)]
+    msgs = [hashlib.sha256(b"duty %d" % (k % 7)).digest() for k in range(64)]
+    sigs = hipbls.sign_batch(keys, msgs)
+    pks = [hipbls.secret_to_public_key(k) for k in keys]
+    cases = []
+    for k in range(256):
+        j = rng.randrange(64)
+        if rng.random() < 0.2:
+            cases.append((pks[j], hashlib.sha256(b"wrong").digest(), sigs[j], NOT_VERIFIED))
+        else:
+            cases.append((pks[j], msgs[j], sigs[j], OK))
+    results = [None] * len(cases)
+
+    def worker(w):
+        for c in range(w, len(cases), 32):
+            pk, m, s, _ = cases[c]
+            results[c] = hipbls.verify_batch([pk], [m], [s])[0]
+
+    th = [threading.Thread(target=worker, args=(w,)) for w in range(32)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert results == [c[3] for c in cases]
+
+
+def test_device_call_and_host_call_do_not_race(L, hipbls):
+    """hbls_verify_device on a side stream, then at once a host-buffer verify with other inputs:
+    both verdict arrays are right (the library orders its workspaces by events)."""
+    import torch
+    dev = torch.device("cuda", 0)
+    keys = [hipbls.generate_secret_key() for _ in range(96)]
+    m = hashlib.sha256(b"race").digest()
+    sigs = hipbls.sign_batch(keys, [m] * 96)
+    pks = [hipbls.secret_to_public_key(k) for k in keys]
+    # device call: 96 partials over one message, every third signature of another key
+    dsig = [sigs[(i + 1) % 96] if i % 3 == 0 else sigs[i] for i in range(96)]
+    mt = torch.from_numpy(np.frombuffer(m, dtype=np.uint8).copy()).to(dev)
+    moff = torch.zeros(1, dtype=torch.int64, device=dev)
+    mlen = torch.full((1,), 32, dtype=torch.int32, device=dev)
+    hm = torch.zeros(L.hbls_hm_entry_bytes(), dtype=torch.uint8, device=dev)
+    dpk = torch.from_numpy(np.frombuffer(b"".join(pks), dtype=np.uint8).copy()).to(dev)
+    ds = torch.from_numpy(np.frombuffer(b"".join(dsig), dtype=np.uint8).copy()).to(dev)
+    midx = torch.zeros(96, dtype=torch.int32, device=dev)
+    goff = torch.tensor([0, 16, 48, 96], dtype=torch.int32, device=dev)
+    vst = torch.full((96,), 255, dtype=torch.uint8, device=dev)
+    s = torch.cuda.Stream(device=dev)
+    sp = ctypes.c_void_p(s.cuda_stream)
+    _chk(L, L.hbls_hash_to_g2_device(_p(mt), _p(moff), _p(mlen), 1, _p(hm), sp))
+    _chk(L, L.hbls_verify_device(_p(dpk), _p(ds), _p(midx), _p(hm), 96, _p(goff), 3, _p(vst), sp))
+    # immediately: host call with different inputs (all valid, other message)
+    m2 = hashlib.sha256(b"race 2").digest()
+    sigs2 = hipbls.sign_batch(keys[:40], [m2] * 40)
+    assert hipbls.verify_batch(pks[:40], [m2] * 40, sigs2) == [OK] * 40
+    s.synchronize()
+    assert list(vst.cpu().numpy()) == [NOT_VERIFIED if i % 3 == 0 else OK for i in range(96)]
+
+
+def _stats(L):
+    out = (ctypes.c_uint64 * 3)()
+    assert L.hbls_stats(out, 3) == 0
+    return list(out)
+
+
+def test_batched_groups_pass_without_fallback(L, hipbls, monkeypatch):
+    """Clean partials over a few messages: every verification group passes its combined check,
+    no item is re-checked alone (the random linear combination is effective, not just correct)."""
+    monkeypatch.setenv("HBLS_STATS", "1")
+    keys = [hipbls.generate_secret_key() for _ in range(48)]
+    msgs = [hashlib.sha256(b"committee %d" % (k % 3)).digest() for k in range(48)]
+    sigs = hipbls.sign_batch(keys, msgs)
+    pks = [hipbls.secret_to_public_key(k) for k in keys]
+    s0 = _stats(L)
+    assert hipbls.verify_batch(pks, msgs, sigs) == [OK] * 48
+    d = [b - a for a, b in zip(s0, _stats(L))]
+    assert d[0] == 48 and d[1] == 3 and d[2] == 0, d  # 3 groups of 16 (HBLS_GROUP_MAX), no fallback
+    # one wrong partial: only its group (16 items) is re-checked alone
+    bad = list(sigs)
+    bad[5] = sigs[6]
+    s0 = _stats(L)
+    st = hipbls.verify_batch(pks, msgs, bad)
+    assert st == [NOT_VERIFIED if i == 5 else OK for i in range(48)]
+    d = [b - a for a, b in zip(s0, _stats(L))]
+    assert d[2] == 16, d

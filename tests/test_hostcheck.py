@@ -120,3 +120,19 @@ def test_pairing_matches_oracle(hc):
         bb = e3[k + 6]
         vals += [(e3[k] + bb) % B.P, bb]
     assert vals == ours
+
+
+def test_rlc_endomorphism_ladders(hc, kats):
+    """rlc.h: [a] P + [b] phi(P) == [a + b lambda] P on G1 and [a] S + [b] (-psi^2 S) ==
+    [a + b lambda] S on G2 with lambda = -x^2 mod r (the batched verification's coefficients)."""
+    lam = (-B.X_PARAM ** 2) % B.R
+    rng = random.Random(11)
+    for v in kats["deposit"]:
+        pk, sig = bytes.fromhex(v["pk"]), bytes.fromhex(v["sig"])
+        P, S = B.g1_decompress(pk), B.g2_decompress(sig)
+        for a, b in ((rng.getrandbits(32), rng.getrandbits(32)), (0xFFFFFFFF, 0xFFFFFFFF), (1, 0), (0, 1)):
+            o48, o96 = _b(48), _b(96)
+            assert hc.hc_rlc(pk, sig, a, b, o48, o96) == 0
+            r = (a + b * lam) % B.R
+            assert o48.raw == B.g1_compress(B.g1_mul(P, r))
+            assert o96.raw == B.g2_compress(B.g2_mul(S, r))
