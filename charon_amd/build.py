@@ -18,7 +18,7 @@ LIB = os.path.join(HERE, "lib", "libhipbls.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 SOURCES = ["hipbls.hip", "pipeline.hip", "threshold.hip", "vbatch.hip", "vgroup.hip"]
-HEADERS = ["hd.h", "consts.h", "fp.h", "fr.h", "tower.h", "ec.h", "sha256.h", "h2c.h", "pairing.h", "ops.h", "pair3.h", "fpmul_asm.inc", "layout.h", "lines.h", "rlc.h"]
+HEADERS = ["hd.h", "consts.h", "fp.h", "fr.h", "tower.h", "ec.h", "sha256.h", "h2c.h", "pairing.h", "ops.h", "pair3.h", "layout.h", "lines.h", "rlc.h"]
 
 
 def _newer(target, deps):

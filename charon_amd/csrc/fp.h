@@ -1,11 +1,11 @@
 // Fp: the 381-bit BLS12-381 base field, 12 x 32-bit little-endian limbs, Montgomery form
-// (R = 2^384).  Elements are kept *lazily reduced* in [0, 2p): since 4p < R the
+// (R = 2^392, see fp_mul).  Elements are kept *lazily reduced* in [0, 2p): since 4p < 2^384 the
 // no-final-subtraction Montgomery product of two such values is again < 2p, so the
 // hot multiply skips the conditional subtraction; canonical form ([0, p)) is produced only
 // for comparisons and serialisation.
 //
-// The product computes x*y+acc with v_mad_u64_u32 (see fp_mul); the limb count and layout
-// match the structure-of-arrays layout the kernels load from HBM.
+// The product (fp_mul) re-splits its operands into 14 limbs of 28 bits and reduces with
+// R = 2^392; all other operations work on the 12 stored words.
 #pragma once
 #include "hd.h"
 #include "consts.h"
@@ -125,128 +125,104 @@ HD Fp fp_neg(const Fp& a) { return fp_sub(fp_zero(), a); }
 
 HD Fp fp_dbl(const Fp& a) { return fp_add(a, a); }
 
-// Montgomery product, CIOS with the "no-carry" simplification (top limb of p < 2^31-1).
-// Inputs in [0,2p), output in [0,2p).  (b may be any value < 2^384 if a < p: the
-// intermediate stays below a + p; the result is then < 2p as well.)
-HD Fp fp_mul_generic(const Fp& a, const Fp& b) {
-  HB_COUNT_FP_MUL();
-  uint32_t t[NL];
-  HB_UNROLL for (int j = 0; j < NL; j++) t[j] = 0;
-  HB_UNROLL for (int i = 0; i < NL; i++) {
-    uint64_t A = (uint64_t)a.v[0] * b.v[i] + t[0];
-    t[0] = (uint32_t)A;
-    A >>= 32;
-    uint32_t m = t[0] * HB_P_N0;
-    uint64_t C = (uint64_t)m * P_RAW[0] + t[0];
-    C >>= 32;
-    HB_UNROLL for (int j = 1; j < NL; j++) {
-      A = (uint64_t)a.v[j] * b.v[i] + t[j] + A;
-      t[j] = (uint32_t)A;
-      A >>= 32;
-      C = (uint64_t)m * P_RAW[j] + t[j] + C;
-      t[j - 1] = (uint32_t)C;
-      C >>= 32;
-    }
-    t[NL - 1] = (uint32_t)(C + A);
+// ---------------------------------------------------------------------------------------
+// Montgomery product over 14 limbs of 28 bits (R = 2^392), carry-free.
+//
+// The operands are stored as 12 x 32-bit words (cheap exact additions with carry chains); the
+// product re-splits them into 14 limbs of 28 bits, so that every partial product a_j b_i (and
+// m_j p_i) is < 2^56 and a whole column of product scanning -- at most 14 + 14 such terms plus
+// the incoming carry, < 2^61 -- accumulates in ONE 64-bit register with plain 64-bit
+// multiply-adds (v_mad_u64_u32) and no carry words: 406 multiply-adds against the 288
+// multiply-adds + 288 carry additions of 32-bit limbs.  Column k < 14 fixes m_k = low28 * (-p^-1)
+// mod 2^28 so that its low 28 bits cancel; columns 14..26 emit the result limbs.
+// Bounds: inputs a, b < 2^384 with a*b < 2^392 p (in particular both < 2p, or one < 2^384 and the
+// other < p) give a result < 2p, so the [0, 2p) lazy reduction of the rest of the code holds.
+// All of it is plain C++: the compiler schedules it and handles every gfx950 hazard (the r01
+// hand-written register-convention subroutine is gone).
+HD void fp_split28(uint32_t* l, const uint32_t* w) {  // 12 x 32 -> 14 x 28
+  HB_UNROLL for (int j = 0; j < 14; j++) {
+    const int bit = 28 * j, i = bit >> 5, s = bit & 31;
+    uint32_t v = w[i] >> s;
+    if (s > 4 && i + 1 < 12) v |= w[i + 1] << (32 - s);
+    l[j] = v & 0x0FFFFFFFu;
   }
-  Fp r;
-  HB_UNROLL for (int j = 0; j < NL; j++) r.v[j] = t[j];
-  return r;
+}
+HD void fp_join28(uint32_t* w, const uint32_t* l) {  // 14 x 28 (normalised, < 2^384) -> 12 x 32
+  HB_UNROLL for (int i = 0; i < 12; i++) {
+    const int bit = 32 * i, j = bit / 28, s = bit % 28;  // s <= 24: two limbs cover a word
+    w[i] = (l[j] >> s) | (l[j + 1] << (28 - s));
+  }
+}
+
+// one column of the reduction: m_k p_{k-j} terms for the columns k >= 14 (and j < k below)
+#define HB_MONT28_TAIL(acc, m, k, r)                                                     \
+  if ((k) < 14) {                                                                       \
+    m[(k)] = ((uint32_t)(acc) * HB_P_N0_28) & 0x0FFFFFFFu;                               \
+    acc += (uint64_t)m[(k)] * P28[0];                                                    \
+  } else {                                                                              \
+    r[(k) - 14] = (uint32_t)(acc) & 0x0FFFFFFFu;                                          \
+  }                                                                                     \
+  acc >>= 28;
+
+HD void fp_mul_core(uint32_t* out, const uint32_t* aw, const uint32_t* bw) {
+  uint32_t a[14], b[14], m[14], r[14];
+  fp_split28(a, aw);
+  fp_split28(b, bw);
+  uint64_t acc = 0;
+  HB_UNROLL for (int k = 0; k < 27; k++) {
+    const int lo = k < 14 ? 0 : k - 13, hi = k < 14 ? k : 13;
+    HB_UNROLL for (int j = lo; j <= hi; j++) acc += (uint64_t)a[j] * b[k - j];
+    HB_UNROLL for (int j = lo; j <= hi; j++)
+      if (j < k || k >= 14) acc += (uint64_t)m[j] * P28[k - j];
+    HB_MONT28_TAIL(acc, m, k, r)
+  }
+  r[13] = (uint32_t)acc;
+  fp_join28(out, r);
+}
+
+// squaring: the cross products a_j a_{k-j}, j < k - j, once against the doubled limb
+HD void fp_sqr_core(uint32_t* out, const uint32_t* aw) {
+  uint32_t a[14], a2[14], m[14], r[14];
+  fp_split28(a, aw);
+  HB_UNROLL for (int j = 0; j < 14; j++) a2[j] = a[j] << 1;
+  uint64_t acc = 0;
+  HB_UNROLL for (int k = 0; k < 27; k++) {
+    const int lo = k < 14 ? 0 : k - 13, hi = k < 14 ? k : 13;
+    HB_UNROLL for (int j = lo; j <= hi; j++) {
+      if (2 * j < k) acc += (uint64_t)a2[j] * a[k - j];
+      else if (2 * j == k) acc += (uint64_t)a[j] * a[j];
+    }
+    HB_UNROLL for (int j = lo; j <= hi; j++)
+      if (j < k || k >= 14) acc += (uint64_t)m[j] * P28[k - j];
+    HB_MONT28_TAIL(acc, m, k, r)
+  }
+  r[13] = (uint32_t)acc;
+  fp_join28(out, r);
 }
 
 #if defined(__HIP_DEVICE_COMPILE__)
-// Device: product-scanning ("FIPS") Montgomery product on v_mad_u64_u32 carry chains.
-// Column k of a*b + m*p is accumulated in a 64-bit VGPR pair `acc` plus a third word `c2`
-// that collects the carry-outs of the 64-bit multiply-adds (VCC -> v_addc_co_u32).  Per
-// column the low word of the first 12 columns selects m_k = acc_lo * (-p^-1) mod 2^32 so that
-// it cancels; columns 12..22 emit the result limbs.  288 v_mad_u64_u32 + 288 v_addc_co_u32 +
-// ~70 moves per product (the compiler's own lowering of the CIOS loop spent 764 extra v_movs).
-// Same bounds as fp_mul_generic: inputs < 2p, output < 2p (4p < 2^384).
-// The asm blocks carry 1 or 2 (a_j b_{k-j}, m_j p_{k-j}) pairs each: fewer blocks means fewer
-// of the s_nop's the hazard recognizer places after every inline-asm statement.
-__device__ __forceinline__ void fips_mac(uint64_t& acc, uint32_t& c2, uint32_t a, uint32_t b) {
-  asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc"
-      : "+v"(acc), "+v"(c2) : "v"(a), "v"(b) : "vcc");
-}
-__device__ __forceinline__ void fips_mac_s(uint64_t& acc, uint32_t& c2, uint32_t a, uint32_t b) {
-  asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc"
-      : "+v"(acc), "+v"(c2) : "v"(a), "s"(b) : "vcc");
-}
-__device__ __forceinline__ void fips_mac2(uint64_t& acc, uint32_t& c2, uint32_t a0, uint32_t b0, uint32_t m0,
-                                          uint32_t p0) {
-  asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc\n\t"
-      "v_mad_u64_u32 %0, vcc, %4, %5, %0\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc"
-      : "+v"(acc), "+v"(c2) : "v"(a0), "v"(b0), "v"(m0), "s"(p0) : "vcc");
-}
-__device__ __forceinline__ void fips_mac4(uint64_t& acc, uint32_t& c2, uint32_t a0, uint32_t b0, uint32_t m0,
-                                          uint32_t p0, uint32_t a1, uint32_t b1, uint32_t m1, uint32_t p1) {
-  asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc\n\t"
-      "v_mad_u64_u32 %0, vcc, %4, %5, %0\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc\n\t"
-      "v_mad_u64_u32 %0, vcc, %6, %7, %0\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc\n\t"
-      "v_mad_u64_u32 %0, vcc, %8, %9, %0\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc"
-      : "+v"(acc), "+v"(c2)
-      : "v"(a0), "v"(b0), "v"(m0), "s"(p0), "v"(a1), "v"(b1), "v"(m1), "s"(p1)
-      : "vcc");
-}
-
-#if defined(HB_FAST_FPMUL)
-// pipeline.hip: the product is the hand-scheduled subroutine hb_fpmul (fpmul_asm.inc,
-// generated by charon_amd/tools/gen_fpmul_asm.py: the same FIPS schedule), entered with a fixed
-// register convention: a in v0-v11, b in v12-v23, result in v24-v35, clobbering only v36-v50,
-// vcc and s30-s48.  The standard calling convention would force every value a caller keeps
-// across the call into the 112 callee-saved VGPRs; with this one the caller's state lives in
-// v51-v255.  The subroutine is emitted once per code object, inside the never-launched kernel
-// hb_fpmul_holder (HB_DEFINE_FPMUL_SUBROUTINE).
-#include "fpmul_asm.inc"
-
-HD Fp fp_mul(const Fp& a, const Fp& b) {
-  HB_COUNT_FP_MUL();
-  Fp r;
-  asm volatile(
-      "s_getpc_b64 s[34:35]\n\t"
-      "s_add_u32 s34, s34, hb_fpmul@rel32@lo+4\n\t"
-      "s_addc_u32 s35, s35, hb_fpmul@rel32@hi+12\n\t"
-      "s_swappc_b64 s[30:31], s[34:35]"
-      : HB_FPMUL_OUTPUTS(r)
-      : HB_FPMUL_INPUTS(a, b)
-      : HB_FPMUL_CLOBBERS);
-  return r;
-}
-
-#define HB_DEFINE_FPMUL_SUBROUTINE(holder)                           \
-  __global__ void holder() {                                \
-    asm volatile("\ts_endpgm\n\t.p2align 8\n\t.globl hb_fpmul\n"     \
-                 "\t.hidden hb_fpmul\n\t.type hb_fpmul,@function\n" \
-                 "hb_fpmul:\n" HB_FPMUL_ASM_BODY);                     \
-  }
-#else
-// hipbls.hip: one out-of-line copy of the product (standard calling convention); operands travel
-// in VGPRs as 12-wide vectors (struct arguments would be passed through scratch memory).
+// Device: one out-of-line copy per code object (standard calling convention: the operands travel
+// in VGPRs as 12-wide vectors; struct arguments would go through scratch).  Everything around it
+// is inlined in the kernels (HB_FAST_FPMUL), so the product is the only call.
 typedef uint32_t u32x12 __attribute__((ext_vector_type(12)));
 __device__ __noinline__ static u32x12 fp_mul_leaf(u32x12 a, u32x12 b) {
-  uint32_t m[NL];
-  u32x12 t;
-  uint64_t acc = 0;
-  uint32_t c2 = 0;
-  HB_UNROLL for (int k = 0; k < 2 * NL - 1; k++) {
-    const int lo = k < NL ? 0 : k - (NL - 1);
-    const int hi = k < NL ? k - 1 : NL - 1;  // pairs j in [lo, hi]
-    int j = lo;
-    HB_UNROLL for (; j + 1 <= hi; j += 2)
-      fips_mac4(acc, c2, a[j], b[k - j], m[j], P_RAW[k - j], a[j + 1], b[k - j - 1], m[j + 1], P_RAW[k - j - 1]);
-    if (j <= hi) fips_mac2(acc, c2, a[j], b[k - j], m[j], P_RAW[k - j]);
-    if (k < NL) {
-      fips_mac(acc, c2, a[k], b[0]);
-      m[k] = (uint32_t)acc * HB_P_N0;
-      fips_mac_s(acc, c2, m[k], P_RAW[0]);  // low word becomes 0
-    } else {
-      t[k - NL] = (uint32_t)acc;
-    }
-    acc = (acc >> 32) | ((uint64_t)c2 << 32);
-    c2 = 0;
+  uint32_t x[12], y[12], r[12];
+  HB_UNROLL for (int i = 0; i < 12; i++) {
+    x[i] = a[i];
+    y[i] = b[i];
   }
-  t[NL - 1] = (uint32_t)acc;
-  return t;
+  fp_mul_core(r, x, y);
+  u32x12 o;
+  HB_UNROLL for (int i = 0; i < 12; i++) o[i] = r[i];
+  return o;
+}
+__device__ __noinline__ static u32x12 fp_sqr_leaf(u32x12 a) {
+  uint32_t x[12], r[12];
+  HB_UNROLL for (int i = 0; i < 12; i++) x[i] = a[i];
+  fp_sqr_core(r, x);
+  u32x12 o;
+  HB_UNROLL for (int i = 0; i < 12; i++) o[i] = r[i];
+  return o;
 }
 HD Fp fp_mul(const Fp& a, const Fp& b) {
   HB_COUNT_FP_MUL();
@@ -260,12 +236,31 @@ HD Fp fp_mul(const Fp& a, const Fp& b) {
   HB_UNROLL for (int i = 0; i < NL; i++) r.v[i] = rv[i];
   return r;
 }
-#endif
+HD Fp fp_sqr(const Fp& a) {
+  HB_COUNT_FP_MUL();
+  u32x12 av;
+  HB_UNROLL for (int i = 0; i < NL; i++) av[i] = a.v[i];
+  u32x12 rv = fp_sqr_leaf(av);
+  Fp r;
+  HB_UNROLL for (int i = 0; i < NL; i++) r.v[i] = rv[i];
+  return r;
+}
 #else
-HD Fp fp_mul(const Fp& a, const Fp& b) { return fp_mul_generic(a, b); }
+HD Fp fp_mul(const Fp& a, const Fp& b) {
+  HB_COUNT_FP_MUL();
+  Fp r;
+  fp_mul_core(r.v, a.v, b.v);
+  return r;
+}
+HD Fp fp_sqr(const Fp& a) {
+  HB_COUNT_FP_MUL();
+  Fp r;
+  fp_sqr_core(r.v, a.v);
+  return r;
+}
 #endif
 
-HD Fp fp_sqr(const Fp& a) { return fp_mul(a, a); }
+
 
 // reduce [0,2p) -> [0,p)
 HD Fp fp_canon(const Fp& a) {

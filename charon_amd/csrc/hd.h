@@ -14,7 +14,7 @@
 #include <hip/hip_runtime.h>
 #define HD static __host__ __device__ __forceinline__
 #if defined(HB_FAST_FPMUL)
-// pipeline.hip: everything but the Fp product subroutine is inlined (no ABI calls)
+// fast units: everything but the Fp product / square (fp.h leaves) is inlined
 #define HDNI static __host__ __device__ __forceinline__
 #else
 #define HDNI static __host__ __device__ __noinline__

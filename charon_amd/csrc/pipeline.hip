@@ -1,20 +1,13 @@
 // pipeline.hip: message hashing and the pairing kernel of libhipbls.so (tbls.Verify,
 // herumi.go:288-304).
 //
-// Compiled with HB_FAST_FPMUL: every Fp product is the register-convention subroutine hb_fpmul
-// (fp.h, fpmul_asm.inc) and every other field / curve / tower function is inlined, so these
-// kernels make no ABI calls and keep their state in registers.
+// Compiled with HB_FAST_FPMUL: every field / curve / tower function is inlined; the Fp product and
+// square are the only calls (fp.h fp_mul_leaf / fp_sqr_leaf, compiler-visible C++).
 #define HB_FAST_FPMUL 1
 #include "lines.h"
 #include "pair3.h"
 
 namespace hb {
-
-#if defined(__HIP_DEVICE_COMPILE__)
-HB_DEFINE_FPMUL_SUBROUTINE(hb_fpmul_holder_pipeline)
-#else
-__global__ void hb_fpmul_holder_pipeline() {}
-#endif
 
 #define KERNEL_BOUNDS __launch_bounds__(64)
 constexpr int BLOCK = 64;

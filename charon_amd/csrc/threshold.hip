@@ -1,7 +1,7 @@
 // threshold.hip: staged ThresholdAggregate / Aggregate kernels of libhipbls.so
 // (tbls.ThresholdAggregate -> Herumi.ThresholdAggregate, herumi.go:249-286; tbls.Aggregate,
-// herumi.go:225-247).  Compiled like pipeline.hip (HB_FAST_FPMUL: register-convention Fp
-// product, everything else inlined).
+// herumi.go:225-247).  Compiled like pipeline.hip (HB_FAST_FPMUL: everything but the Fp
+// product inlined).
 //
 //   k_dec_sig_pt (vbatch.hip) 1 lane / partial: decompress + subgroup-check sigma_j (or, in the
 //              slot entry point, the verification's decompressed points through src[])
@@ -21,13 +21,6 @@
 #include "layout.h"
 
 namespace hb {
-
-#if defined(__HIP_DEVICE_COMPILE__)
-// hb_fpmul has hidden visibility per code object: each translation unit carries its own copy
-HB_DEFINE_FPMUL_SUBROUTINE(hb_fpmul_holder_threshold)
-#else
-__global__ void hb_fpmul_holder_threshold() {}
-#endif
 
 // u (8 little-endian limbs, < 2^256) <- u / z, returns u mod z   (z = |x|, bit-serial: the three
 // divisions per partial cost a few Fp products)

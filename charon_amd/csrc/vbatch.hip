@@ -21,12 +21,6 @@
 
 namespace hb {
 
-#if defined(__HIP_DEVICE_COMPILE__)
-HB_DEFINE_FPMUL_SUBROUTINE(hb_fpmul_holder_vbatch)
-#else
-__global__ void hb_fpmul_holder_vbatch() {}
-#endif
-
 #define KB __launch_bounds__(64)
 constexpr int BLOCK = 64;
 

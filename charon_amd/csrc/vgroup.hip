@@ -1,11 +1,11 @@
-// vgroup.hip: the per-group stage of the batched verification (vbatch.hip), compiled with the
-// compiler-visible standard-convention Fp product (no HB_FAST_FPMUL).
+// vgroup.hip: the per-group stage of the batched verification (vbatch.hip).
 //
-// Why a translation unit of its own: built with the register-convention product subroutine of the
-// fast units (fp.h hb_fpmul, entered through inline asm the compiler cannot see into), this
-// kernel returned a wrong group sum -- a point off the curve -- on the GPU, deterministically,
-// while the same source compiled here is exact (tests/native/devcheck_vb.hip).  It
-// runs once per group of ~10 partials, so the slower product costs little.
+// History: built with r01's register-convention product subroutine (a hand-written routine
+// entered through inline asm the compiler could not see into), this kernel returned a wrong group
+// sum -- a point off the curve -- on the GPU, deterministically, while the same source built with
+// a compiler-visible product was exact (tests/native/devcheck_vb.hip).  That
+// subroutine is gone; the kernel is compiled like the other fast units.
+#define HB_FAST_FPMUL 1
 #include "lines.h"
 
 namespace hb {

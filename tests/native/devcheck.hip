@@ -8,12 +8,6 @@
 
 using namespace hb;
 
-#if defined(__HIP_DEVICE_COMPILE__)
-HB_DEFINE_FPMUL_SUBROUTINE(hb_fpmul_holder_devcheck)
-#else
-__global__ void hb_fpmul_holder_devcheck() {}
-#endif
-
 // case i: (pk, sig, a, b) -> compressed [a + b lambda] pk, [a + b lambda] sig, and the sum of the
 // two cases i, i+1 (Jacobian adds, affine) in sum48 / sum96 (last case: itself)
 __global__ __launch_bounds__(64) void k_dc_rlc(const uint8_t* pks, const uint8_t* sigs, const uint32_t* ab, int n,

@@ -9,9 +9,7 @@
 using namespace hb;
 
 #if defined(__HIP_DEVICE_COMPILE__)
-// no subroutine
 #else
-__global__ void hb_fpmul_holder_devcheck() {}
 #endif
 
 // case i: (pk, sig, a, b) -> compressed [a + b lambda] pk, [a + b lambda] sig, and the sum of the
