@@ -120,7 +120,7 @@ def setup_inputs(L, wl, V, rank):
     ta_idx = np.tile(np.arange(1, t + 1, dtype=np.int64), V)
     grp_off = (np.arange(V + 1, dtype=np.uint32) * t)
     vgrp_off = (np.arange(V + 1, dtype=np.uint32) * n)  # one verification group per validator
-    return dict(n=n, t=t, V=V, NP=NP, M=M, msgs=msgs, moff=moff, mlen=mlen, midx=midx, pks=pks, sigs=sigs,
+    return dict(n=n, t=t, V=V, NP=NP, M=M, sks=sks, msgs=msgs, moff=moff, mlen=mlen, midx=midx, pks=pks, sigs=sigs,
                 item_msgs=item_msgs, item_off=item_off, item_len=item_len, ta_sigs=ta_sigs, ta_src=ta_src,
                 ta_idx=ta_idx, grp_off=grp_off, vgrp_off=vgrp_off, root_sigs=root_sigs, dv_pks=dv_pks)
 
@@ -211,6 +211,85 @@ def concurrent_callers(L, d, threads: int, seconds: float):
             "coalesce_us": int(os.environ.get("HBLS_COALESCE_US", "200"))}
 
 
+R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+
+
+def aggregate_verify(L, d, d_pk, dev, sp, reps: int = 3, sync_size: int = 512):
+    """VerifyAggregate at scale on the resident pubshares (hbls_verify_aggregate_device):
+      lock: ONE group of all V*n public shares against a lock hash (cluster/lock.go:185, run at
+            every charon start over every validator's every pubshare);
+      sync: groups of 512 public keys, each over its own message (sync-committee aggregate,
+            BASELINE configs[4]), message hashing included.
+    The signatures are sum(sk) * H(m), produced once by hbls_sign_batch outside the timed region."""
+    import hashlib
+    import torch
+    NP, sks = d["NP"], d["sks"]
+    ints = [int.from_bytes(sks[32 * i:32 * i + 32].tobytes(), "big") for i in range(NP)]
+    G = NP // sync_size
+    sums = [sum(ints) % R_ORDER] + [sum(ints[g * sync_size:(g + 1) * sync_size]) % R_ORDER for g in range(G)]
+    msgs = [hashlib.sha256(b"cluster lock hash").digest()] + \
+        [hashlib.sha256(b"sync committee root %d" % g).digest() for g in range(G)]
+    m = np.frombuffer(b"".join(msgs), dtype=np.uint8).copy()
+    moff = np.arange(G + 1, dtype=np.uint64) * 32
+    mlen = np.full(G + 1, 32, dtype=np.uint32)
+    sk_b = np.frombuffer(b"".join(x.to_bytes(32, "big") for x in sums), dtype=np.uint8).copy()
+    sigs = np.zeros(96 * (G + 1), dtype=np.uint8)
+    st = np.zeros(G + 1, dtype=np.uint8)
+    _chk(L, L.hbls_sign_batch(_p(sk_b), _p(m), _p(moff), _p(mlen), G + 1, _p(sigs), _p(st)))
+    assert not st.any()
+    up = lambda a: torch.from_numpy(a).to(dev)  # noqa: E731
+    d_m, d_mo, d_ml, d_sig = up(m), up(moff.view(np.int64)), up(mlen.view(np.int32)), up(sigs)
+    d_hm = torch.zeros((G + 1) * L.hbls_hm_entry_bytes(), dtype=torch.uint8, device=dev)
+    d_st = torch.full((G + 1,), 255, dtype=torch.uint8, device=dev)
+    lock_off = np.array([0, NP], dtype=np.uint32)
+    sync_off = np.arange(G + 1, dtype=np.uint32) * sync_size
+    spp = sp
+    hm_sz = L.hbls_hm_entry_bytes()
+
+    def lock():
+        _chk(L, L.hbls_hash_to_g2_device(_p(d_m), _p(d_mo), _p(d_ml), 1, _p(d_hm), spp))
+        _chk(L, L.hbls_verify_aggregate_device(_p(d_pk), _p(lock_off), 1, _p(d_sig), _p(d_hm), _p(d_st), spp))
+
+    def sync():
+        hm1 = ctypes.c_void_p(d_hm.data_ptr() + hm_sz)
+        _chk(L, L.hbls_hash_to_g2_device(ctypes.c_void_p(d_m.data_ptr() + 32), _p(d_mo[:G]), _p(d_ml[:G]), G, hm1,
+                                         spp))
+        _chk(L, L.hbls_verify_aggregate_device(_p(d_pk), _p(sync_off), G, ctypes.c_void_p(d_sig.data_ptr() + 96),
+                                               hm1, ctypes.c_void_p(d_st.data_ptr() + 1), spp))
+
+    out = {}
+    for name, fn, units in (("lock", lock, 1), ("sync_committee", sync, G)):
+        fn()  # warm-up (workspace growth)
+        torch.cuda.synchronize(dev)
+        _chk(L, L.hbls_timing(1))
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize(dev)
+        wall = (time.perf_counter() - t0) / reps
+        recs = _lib_timing(L)
+        _chk(L, L.hbls_timing(0))
+        stv = d_st.cpu().numpy()
+        ok = bool(stv[0] == 0) if name == "lock" else bool((stv[1:] == 0).all())
+        kern = {}
+        for k, ms in recs:
+            kern[k] = round(kern.get(k, 0.0) + ms / reps, 3)
+        per_group = NP if name == "lock" else sync_size
+        dec_ms = kern.get("k_dec_pk")
+        dec_tops = (units * per_group * opcounts.BLOCKS["g1_dec"] * opcounts.MAC_PER_FPMUL / (dec_ms * 1e-3) / 1e12
+                    if dec_ms else None)
+        out[name] = {"groups": units, "keys_per_group": per_group, "ms": round(wall * 1e3, 3),
+                     "keys_per_s": round(units * per_group / wall, 1), "all_ok": ok, "kernel_ms": kern,
+                     "k_dec_pk_Tops_alg": round(dec_tops, 3) if dec_tops else None,
+                     "k_dec_pk_frac": round(dec_tops / opcounts.PEAK_MAD_TOPS, 4) if dec_tops else None}
+    return out
+
+
+def _lib_timing(L):
+    from charon_amd import _lib
+    return _lib.timing_read(L)
+
+
 def roofline_from_timing(recs, steps, units):
     """Per-kernel totals over the timed steps; the dominant kernel's roofline entry."""
     tot, cnt = {}, {}
@@ -241,6 +320,8 @@ def main(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample (0: skip)")
     ap.add_argument("--callers", type=int, default=64, help="threads of the concurrent-caller measurement (0: skip)")
     ap.add_argument("--callers-seconds", type=float, default=4.0)
+    ap.add_argument("--aggregate-verify", type=int, default=1,
+                    help="also time VerifyAggregate at scale (lock over all pubshares, sync-committee groups)")
     ap.add_argument("--host-api", action="store_true", help="also time the host-buffer (PCIe-inclusive) entry points")
     ap.add_argument("--mode", default="slot", choices=["slot", "staged"],
                     help="slot: one hbls_slot_device call per step (stages overlap); staged: stage by stage")
@@ -442,6 +523,10 @@ def main(argv=None):
         out["host_buffer_items_per_s"] = round((NP + V) / (time.perf_counter() - t0), 1)
         out["host_buffer_parity"] = bool((st == 0).all() and (tst_h == 0).all() and
                                          np.array_equal(tout_h, d["root_sigs"]))
+
+    if rank == 0 and world == 1 and args.aggregate_verify:
+        out["verify_aggregate"] = aggregate_verify(L, d, d_pk, dev, sp)
+        parity["verify_aggregate_ok"] = all(x["all_ok"] for x in out["verify_aggregate"].values())
 
     if rank == 0 and world == 1 and args.callers > 0:
         out["concurrent_callers"] = concurrent_callers(L, d, args.callers, args.callers_seconds)

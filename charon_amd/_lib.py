@@ -27,7 +27,8 @@ EXPORTS = (
     "hbls_init", "hbls_last_error", "hbls_available", "hbls_device_count", "hbls_verify_batch",
     "hbls_threshold_aggregate_batch", "hbls_aggregate_batch", "hbls_verify_aggregate_batch", "hbls_sign_batch",
     "hbls_secret_to_public_key_batch", "hbls_threshold_split", "hbls_recover_secret", "hbls_hash_to_g2_device",
-    "hbls_verify_device", "hbls_threshold_aggregate_device", "hbls_slot_device", "hbls_hm_entry_bytes", "hbls_sync",
+    "hbls_verify_device", "hbls_threshold_aggregate_device", "hbls_verify_aggregate_device", "hbls_slot_device",
+    "hbls_hm_entry_bytes", "hbls_sync",
     "hbls_timing", "hbls_timing_read", "hbls_comm_id_bytes", "hbls_comm_unique_id", "hbls_comm_init",
     "hbls_allgather_device", "hbls_comm_destroy", "hbls_stats",
 )
@@ -76,6 +77,7 @@ def _declare(lib):
         "hbls_hash_to_g2_device": ([P, P, P, SZ, P, P], ctypes.c_int),
         "hbls_verify_device": ([P, P, P, P, SZ, P, SZ, P, P], ctypes.c_int),
         "hbls_threshold_aggregate_device": ([P, P, P, SZ, SZ, P, P, P], ctypes.c_int),
+        "hbls_verify_aggregate_device": ([P, P, SZ, P, P, P, P], ctypes.c_int),
         "hbls_slot_device": ([ctypes.POINTER(HblsSlot), P], ctypes.c_int),
         "hbls_hm_entry_bytes": ([], SZ),
         "hbls_sync": ([P], ctypes.c_int),

@@ -83,55 +83,6 @@ __global__ KERNEL_BOUNDS void k_group_sum(const uint32_t* __restrict__ grp_off, 
   }
 }
 
-// VerifyAggregate stage 1: one lane per public key.
-__global__ KERNEL_BOUNDS void k_g1_member(const uint8_t* __restrict__ pks, uint32_t n, G1AEntry* __restrict__ pts,
-                                          uint8_t* __restrict__ mstat) {
-  uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= n) return;
-  G1A p;
-  if (g1_decompress(p, pks + 48ull * j)) {
-    mstat[j] = 1;
-    return;
-  }
-  mstat[j] = 0;
-  G1AEntry e;
-  e.x = p.x;
-  e.y = p.y;
-  e.inf = p.inf;
-  e.pad[0] = e.pad[1] = e.pad[2] = 0;
-  pts[j] = e;
-}
-
-// VerifyAggregate stage 2: one lane per group (FastAggregateVerify, herumi.go:318-342).
-__global__ KERNEL_BOUNDS void k_verify_aggregate(const uint32_t* __restrict__ grp_off, uint32_t n_groups,
-                                                 const G1AEntry* __restrict__ pts, const uint8_t* __restrict__ mstat,
-                                                 const uint8_t* __restrict__ sigs, const MsgEntry* __restrict__ hm,
-                                                 uint8_t* __restrict__ status) {
-  uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= n_groups) return;
-  G2A sig;
-  if (g2_decompress(sig, sigs + 96ull * g)) {
-    status[g] = ST_BAD_SIGNATURE;
-    return;
-  }
-  uint32_t b = grp_off[g], e = grp_off[g + 1];
-  G1J acc = jac_infinity<Fp>();
-  for (uint32_t m = b; m < e; m++) {
-    if (mstat[m]) {
-      status[g] = ST_BAD_PUBKEY;
-      return;
-    }
-    G1AEntry q = pts[m];
-    acc = jac_add_aff(acc, G1A{q.x, q.y, q.inf != 0});
-  }
-  if (e == b) {
-    status[g] = ST_NOT_VERIFIED;
-    return;
-  }
-  G1A agg = jac_to_aff(acc);
-  status[g] = verify_core(agg, hm_load(hm[g].h), sig) ? ST_OK : ST_NOT_VERIFIED;
-}
-
 // Sign: one lane per (sk, message): sigma = sk * H(m)   (herumi.go:306-316)
 __global__ KERNEL_BOUNDS void k_sign(const uint8_t* __restrict__ sks, const uint32_t* __restrict__ msg_idx,
                                      const MsgEntry* __restrict__ hm, uint32_t n, uint8_t* __restrict__ sigs,
@@ -282,6 +233,7 @@ enum WsId {
   W_FBLINES,
   W_APK, W_APKST, W_ASIG, W_APR, W_ASR,          // folded aggregates (post-aggregate verification)
   W_TAPTS, W_TADST, W_TAMST, W_TADIG, W_TATAB, W_TAJ,  // ThresholdAggregate / Aggregate
+  W_SEGA, W_SEGB, W_SEGSTA, W_SEGSTB, W_VAPT, W_VAPV,  // VerifyAggregate key reduction
   W_COUNT_
 };
 
@@ -295,7 +247,7 @@ struct Ws {
 };
 
 // host-call staging buffers (inputs and outputs of the host-buffer entry points)
-enum IoId { I_PK, I_SIG, I_MSG, I_OFF, I_LEN, I_MIDX, I_HM, I_STAT, I_IDX, I_GOFF, I_OUT, I_SK, I_VGOFF, I_COUNT };
+enum IoId { I_PK, I_SIG, I_MSG, I_OFF, I_LEN, I_MIDX, I_HM, I_STAT, I_IDX, I_GOFF, I_OUT, I_SK, I_VGOFF, I_SEG, I_COUNT };
 
 constexpr int N_SIDE = 4;
 constexpr int N_WS = 2;
@@ -997,6 +949,106 @@ int verify_coalesced(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msg
 }
 
 // ---------------------------------------------------------------------------------------
+// VerifyAggregate (FastAggregateVerify, herumi.go:318-342) of n_groups groups whose public keys
+// are pks[goff[g] .. goff[g+1]) (goff on the HOST, goff[0] == 0): every key decompressed in
+// parallel (k_dec_pk), the keys of each group summed by a segmented tree reduction of segments of
+// VA_SEG points (k_seg_sum; planned here from goff: a 7M-key group takes 5 launches), the sums
+// paired with H(m_g) against the group's signature (k_pair3), herumi's checks applied in its
+// order (k_va_status).  hm: one hashed message (with lines) per group, written by hash_fn (if
+// given) on s while the side streams decompress: side 0 the keys and their reduction, side 1 the
+// signatures and their lines.
+// ---------------------------------------------------------------------------------------
+constexpr uint32_t VA_SEG = 32;
+
+int va_pipeline(Dev& d, Ws& w, const uint8_t* dpk, size_t np, const uint32_t* goff, size_t ng, const uint8_t* dsig,
+                const MsgEntry* hm, uint8_t* dst, hipStream_t s, const std::function<int()>& hash_fn) {
+  if (ng == 0) return 0;
+  if (np > 0xffffffffull || ng > 0x7fffffffull) return set_err("verify aggregate: too many keys");
+  // plan: boundaries of every pass, then the sum index of each group, then the identity map
+  std::vector<uint32_t> plan, lo(ng), hi(ng);
+  std::vector<size_t> pass_off, pass_n;
+  for (size_t g = 0; g < ng; g++) lo[g] = goff[g], hi[g] = goff[g + 1];
+  bool more = np > 0;
+  while (more) {
+    pass_off.push_back(plan.size());
+    plan.push_back(0);
+    uint32_t out = 0;
+    more = false;
+    for (size_t g = 0; g < ng; g++) {
+      if (hi[g] == lo[g]) continue;
+      const uint32_t first = out;
+      for (uint32_t b = lo[g]; b < hi[g]; b += VA_SEG) {
+        plan.push_back(std::min<uint32_t>(b + VA_SEG, hi[g]));
+        out++;
+      }
+      lo[g] = first;
+      hi[g] = out;
+      more |= out - first > 1;
+    }
+    pass_n.push_back(out);
+  }
+  const size_t sog_off = plan.size();
+  for (size_t g = 0; g < ng; g++) plan.push_back(hi[g] > lo[g] ? lo[g] : 0xffffffffu);
+  const size_t iota_off = plan.size();
+  for (size_t g = 0; g < ng; g++) plan.push_back((uint32_t)g);
+  uint32_t* dplan;
+  if (upload(d, I_SEG, plan.data(), plan.size(), &dplan)) return -1;
+  if (s != d.stream) {  // the upload ran on the library stream
+    HCHK(hipEventRecord(d.ev_fork, d.stream));
+    HCHK(hipStreamWaitEvent(s, d.ev_fork, 0));
+  }
+
+  G1AEntry *pts, *vapt;
+  uint8_t *mst, *sigst, *pv, *sta, *stb;
+  HmEntry* sigpt;
+  G1JEntry *sa, *sb;
+  LineEntry* lines;
+  const size_t na = pass_n.empty() ? 1 : pass_n[0], nb = pass_n.size() > 1 ? pass_n[1] : 1;
+  if (wsbuf(w, W_VPK, np, &pts) || wsbuf(w, W_VPKST, np, &mst) || wsbuf(w, W_VSIG, ng, &sigpt) ||
+      wsbuf(w, W_VSIGST, ng, &sigst) || wsbuf(w, W_FBLINES, ng * N_LINES, &lines) || wsbuf(w, W_SEGA, na, &sa) ||
+      wsbuf(w, W_SEGSTA, na, &sta) || wsbuf(w, W_SEGB, nb, &sb) || wsbuf(w, W_SEGSTB, nb, &stb) ||
+      wsbuf(w, W_VAPT, ng, &vapt) || wsbuf(w, W_VAPV, ng, &pv))
+    return -1;
+  hipStream_t s0 = d.side[0], s1 = d.side[1];
+  HCHK(hipEventRecord(d.ev_fork, s));
+  HCHK(hipStreamWaitEvent(s0, d.ev_fork, 0));
+  HCHK(hipStreamWaitEvent(s1, d.ev_fork, 0));
+  TIMED(d, "k_dec_sig_pt", s1, launch_dec_sig_pt(dsig, (uint32_t)ng, sigpt, sigst, s1));
+  TIMED(d, "k_sig_lines", s1, launch_sig_lines(sigpt, (uint32_t)ng, lines, (uint32_t)ng, s1));
+  HCHK(hipEventRecord(d.ev_side[1], s1));
+  if (hash_fn && hash_fn()) return -1;
+  if (np) TIMED(d, "k_dec_pk", s0, launch_dec_pk(dpk, (uint32_t)np, pts, mst, s0));
+  const void* in = pts;
+  const uint8_t* in_st = mst;
+  G1JEntry* out = sa;
+  uint8_t* out_st = sta;
+  for (size_t k = 0; k < pass_n.size(); k++) {
+    out = (k & 1) ? sb : sa;
+    out_st = (k & 1) ? stb : sta;
+    TIMED(d, "k_seg_sum", s0,
+          launch_seg_sum(k == 0, in, in_st, dplan + pass_off[k], (uint32_t)pass_n[k], out, out_st, s0));
+    in = out;
+    in_st = out_st;
+  }
+  HCHK(hipEventRecord(d.ev_side[0], s0));
+  HCHK(hipStreamWaitEvent(s, d.ev_side[0], 0));
+  HCHK(hipStreamWaitEvent(s, d.ev_side[1], 0));
+  TIMED(d, "k_va_point", s, launch_va_point(out, dplan + sog_off, (uint32_t)ng, vapt, s));
+  Pair3Args a{};
+  a.pk = vapt;
+  a.msg_idx = dplan + iota_off;
+  a.hm = hm;
+  a.sig_lines = lines;
+  a.stride = (uint32_t)ng;
+  a.n = (uint32_t)ng;
+  a.n_items = (uint32_t)ng;
+  a.status = pv;
+  TIMED(d, "k_pair3", s, launch_pair3(a, s));
+  TIMED(d, "k_va_status", s, launch_va_status(sigpt, sigst, out_st, dplan + sog_off, pv, (uint32_t)ng, dst, s));
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------
 // RCCL: one communicator per process (one GPU each) for the exchange of slot results
 // ---------------------------------------------------------------------------------------
 ncclComm_t g_comm = nullptr;
@@ -1064,23 +1116,18 @@ int hbls_verify_aggregate_batch(const uint8_t* pks, const uint32_t* grp_off, con
     }
     std::vector<uint32_t> goff(ng + 1);
     for (size_t g = 0; g <= ng; g++) goff[g] = grp_off[gb + g] - (uint32_t)pb;
-    MsgEntry* hm;
-    if (hash_table(d, t, &hm, false)) return -1;
     uint8_t *dpk, *dsig;
-    uint32_t* dgoff;
-    if (upload(d, I_PK, pks + 48 * pb, np * 48, &dpk) || upload(d, I_SIG, sigs + 96 * gb, ng * 96, &dsig) ||
-        upload(d, I_GOFF, goff.data(), ng + 1, &dgoff))
-      return -1;
-    Ws& w = ws_acquire(d, {d.stream});
-    G1AEntry* pts;
-    uint8_t *mst, *dst;
-    if (wsbuf(w, W_VPK, np, &pts) || wsbuf(w, W_VPKST, np, &mst)) return -1;
+    if (upload(d, I_PK, pks + 48 * pb, np * 48, &dpk) || upload(d, I_SIG, sigs + 96 * gb, ng * 96, &dsig)) return -1;
     void* p;
     if (ensure_buf(d.io[I_STAT], ng, &p)) return -1;
-    dst = (uint8_t*)p;
-    LAUNCH(k_g1_member, np, d.stream, dpk, (uint32_t)np, pts, mst);
-    LAUNCH(k_verify_aggregate, ng, d.stream, dgoff, (uint32_t)ng, (const G1AEntry*)pts, (const uint8_t*)mst, dsig,
-           (const MsgEntry*)hm, dst);
+    Ws& w = ws_acquire(d, {d.stream, d.side[0], d.side[1]});
+    uint8_t* dst = (uint8_t*)p;
+    void* hmp;  // the message table's buffer (hash_table fills the same one on the library stream)
+    if (ensure_buf(d.io[I_HM], ng * sizeof(MsgEntry), &hmp)) return -1;
+    MsgEntry* hm = (MsgEntry*)hmp;
+    if (va_pipeline(d, w, dpk, np, goff.data(), ng, dsig, hm, dst, d.stream,
+                    [&]() -> int { MsgEntry* h; return hash_table(d, t, &h, true); }))
+      return -1;
     if (ws_release(w, d.stream)) return -1;
     HCHK(hipMemcpyAsync(status + gb, dst, ng, hipMemcpyDeviceToHost, d.stream));
     HCHK(hipStreamSynchronize(d.stream));
@@ -1192,6 +1239,23 @@ int hbls_verify_device(const uint8_t* pks, const uint8_t* sigs, const uint32_t* 
   Ws& w = ws_acquire(*d, {s, d->side[0], d->side[1], d->side[3]});
   if (verify_pipeline(*d, w, pks, sigs, msg_idx, (const MsgEntry*)hm, n, vgrp_off, n_vgroups, status, s, nullptr,
                       nullptr))
+    return -1;
+  return ws_release(w, s);
+}
+
+int hbls_verify_aggregate_device(const uint8_t* pks, const uint32_t* grp_off, size_t n_groups, const uint8_t* sigs,
+                                 const void* hm, uint8_t* status, void* stream) {
+  Dev* d;
+  hipStream_t s = (hipStream_t)stream;
+  if (dev_of_stream(s, &d)) return -1;
+  if (n_groups == 0) return 0;
+  if (check_offsets(grp_off, n_groups)) return -1;
+  std::vector<uint32_t> goff(n_groups + 1);
+  for (size_t g = 0; g <= n_groups; g++) goff[g] = grp_off[g] - grp_off[0];
+  std::lock_guard<std::mutex> lk(d->mu);
+  Ws& w = ws_acquire(*d, {s, d->side[0], d->side[1]});
+  if (va_pipeline(*d, w, pks + 48ull * grp_off[0], goff[n_groups], goff.data(), n_groups, sigs, (const MsgEntry*)hm,
+                  status, s, nullptr))
     return -1;
   return ws_release(w, s);
 }

@@ -157,4 +157,14 @@ void launch_scatter(const ScatterArgs& a, hipStream_t s);
 void launch_fb_lines(const uint32_t* list, const uint32_t* count, uint32_t base, uint32_t cap, const HmEntry* sig,
                      const HmEntry* agg_sig, uint32_t n_items, LineEntry* lines, hipStream_t s);
 
+// FastAggregateVerify at scale (vbatch.hip): segmented G1 reduction, then the pairing kernel.
+void launch_seg_sum(bool affine, const void* pts, const uint8_t* st_in, const uint32_t* seg_off, uint32_t n_seg,
+                    G1JEntry* out, uint8_t* st_out, hipStream_t s);
+void launch_va_point(const G1JEntry* sums, const uint32_t* sum_of_group, uint32_t n_groups, G1AEntry* out,
+                     hipStream_t s);
+void launch_sig_lines(const HmEntry* sig, uint32_t n, LineEntry* lines, uint32_t stride, hipStream_t s);
+void launch_va_status(const HmEntry* sig, const uint8_t* sig_st, const uint8_t* key_bad,
+                      const uint32_t* sum_of_group, const uint8_t* pv, uint32_t n_groups, uint8_t* status,
+                      hipStream_t s);
+
 }  // namespace hb

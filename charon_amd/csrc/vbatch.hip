@@ -204,4 +204,108 @@ void launch_fb_lines(const uint32_t* list, const uint32_t* count, uint32_t base,
                        n_items, lines);
 }
 
+// ---------------------------------------------------------------------------------------
+// FastAggregateVerify at scale (tbls.VerifyAggregate, herumi.go:318-342; the startup check of
+// cluster/lock.go:185 runs it over every validator's every public share): the public keys of a
+// group are summed by a segmented tree reduction -- pass 1 sums segments of affine decompressed
+// keys, later passes sum segments of the previous pass's Jacobian partials -- so a group of 7M
+// keys takes a few launches of many lanes instead of one lane walking 7M points.
+// ---------------------------------------------------------------------------------------
+
+// One lane per segment [seg_off[s], seg_off[s+1]): sum of the points, OR of the bad flags.
+template <bool AFFINE>
+__global__ KB void k_seg_sum(const void* __restrict__ pts, const uint8_t* __restrict__ st_in,
+                             const uint32_t* __restrict__ seg_off, uint32_t n_seg, G1JEntry* __restrict__ out,
+                             uint8_t* __restrict__ st_out) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t sgi = blockIdx.x * blockDim.x + threadIdx.x;
+  if (sgi >= n_seg) return;
+  const uint32_t b = seg_off[sgi], e = seg_off[sgi + 1];
+  G1J acc = jac_infinity<Fp>();
+  uint8_t bad = 0;
+  for (uint32_t i = b; i < e; i++) {
+    bad |= st_in[i];
+    if (AFFINE) {
+      const G1AEntry q = reinterpret_cast<const G1AEntry*>(pts)[i];
+      acc = jac_add_aff(acc, G1A{q.x, q.y, q.inf != 0});
+    } else {
+      const G1JEntry q = reinterpret_cast<const G1JEntry*>(pts)[i];
+      acc = jac_add(acc, G1J{q.X, q.Y, q.Z});
+    }
+  }
+  out[sgi] = {acc.X, acc.Y, acc.Z};
+  st_out[sgi] = bad;
+#endif
+}
+
+// One lane per group: the reduced key sum (nullable for empty groups) -> affine, for the pairing.
+__global__ KB void k_va_point(const G1JEntry* __restrict__ sums, const uint32_t* __restrict__ sum_of_group,
+                              uint32_t n_groups, G1AEntry* __restrict__ out) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n_groups) return;
+  G1A a = {fp_zero(), fp_zero(), true};
+  const uint32_t k = sum_of_group[g];
+  if (k != 0xffffffffu) {
+    const G1JEntry q = sums[k];
+    a = jac_to_aff(G1J{q.X, q.Y, q.Z});
+  }
+  G1AEntry e;
+  e.x = a.x;
+  e.y = a.y;
+  e.inf = a.inf ? 1u : 0u;
+  e.pad[0] = e.pad[1] = e.pad[2] = 0;
+  out[g] = e;
+}
+
+// One lane per signature: its Miller lines evaluated at -g1 (lines[j * stride + i]).
+__global__ KB void k_sig_lines(const HmEntry* __restrict__ sig, uint32_t n, LineEntry* __restrict__ lines,
+                               uint32_t stride) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  line_chain<true>(hm_load(sig[i]), lines + i, stride);
+}
+
+// One lane per group: herumi's order of checks -- signature decoding, public key decoding, then
+// the pairing verdict (pv) of the aggregated key.  An empty group, and an identity signature
+// (verify_core, ops.h), never verify; the pairing kernel sees an identity key sum itself.
+__global__ KB void k_va_status(const HmEntry* __restrict__ sig, const uint8_t* __restrict__ sig_st,
+                               const uint8_t* __restrict__ key_bad, const uint32_t* __restrict__ sum_of_group,
+                               const uint8_t* __restrict__ pv, uint32_t n_groups, uint8_t* __restrict__ status) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n_groups) return;
+  const uint32_t k = sum_of_group[g];
+  uint8_t s;
+  if (sig_st[g]) s = ST_BAD_SIGNATURE;
+  else if (k != 0xffffffffu && key_bad[k]) s = ST_BAD_PUBKEY;
+  else if (k == 0xffffffffu || sig[g].inf) s = ST_NOT_VERIFIED;
+  else s = pv[g] == ST_OK ? ST_OK : ST_NOT_VERIFIED;
+  status[g] = s;
+}
+
+void launch_seg_sum(bool affine, const void* pts, const uint8_t* st_in, const uint32_t* seg_off, uint32_t n_seg,
+                    G1JEntry* out, uint8_t* st_out, hipStream_t s) {
+  if (!n_seg) return;
+  if (affine)
+    hipLaunchKernelGGL(k_seg_sum<true>, dim3(blocks_for(n_seg)), dim3(BLOCK), 0, s, pts, st_in, seg_off, n_seg, out,
+                       st_out);
+  else
+    hipLaunchKernelGGL(k_seg_sum<false>, dim3(blocks_for(n_seg)), dim3(BLOCK), 0, s, pts, st_in, seg_off, n_seg, out,
+                       st_out);
+}
+void launch_va_point(const G1JEntry* sums, const uint32_t* sum_of_group, uint32_t n_groups, G1AEntry* out,
+                     hipStream_t s) {
+  if (n_groups)
+    hipLaunchKernelGGL(k_va_point, dim3(blocks_for(n_groups)), dim3(BLOCK), 0, s, sums, sum_of_group, n_groups, out);
+}
+void launch_sig_lines(const HmEntry* sig, uint32_t n, LineEntry* lines, uint32_t stride, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_sig_lines, dim3(blocks_for(n)), dim3(BLOCK), 0, s, sig, n, lines, stride);
+}
+void launch_va_status(const HmEntry* sig, const uint8_t* sig_st, const uint8_t* key_bad,
+                      const uint32_t* sum_of_group, const uint8_t* pv, uint32_t n_groups, uint8_t* status,
+                      hipStream_t s) {
+  if (n_groups)
+    hipLaunchKernelGGL(k_va_status, dim3(blocks_for(n_groups)), dim3(BLOCK), 0, s, sig, sig_st, key_bad,
+                       sum_of_group, pv, n_groups, status);
+}
+
 }  // namespace hb

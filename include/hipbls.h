@@ -80,7 +80,9 @@ int hbls_aggregate_batch(const uint8_t* sigs, const uint32_t* grp_off, size_t n_
 
 /* VerifyAggregate (FastAggregateVerify): group g verifies sigs[g] on message g against the sum of
  * pks[grp_off[g] .. grp_off[g+1]).  tbls.VerifyAggregate / Herumi.VerifyAggregate
- * (tbls.go:133, herumi.go:318-342).  status in {OK, BAD_SIGNATURE, BAD_PUBKEY, NOT_VERIFIED}. */
+ * (tbls.go:133, herumi.go:318-342).  status in {OK, BAD_SIGNATURE, BAD_PUBKEY, NOT_VERIFIED}.
+ * The keys of a group are summed by a parallel segmented reduction, so one group may hold all
+ * public shares of a cluster lock (cluster/lock.go:185). */
 int hbls_verify_aggregate_batch(const uint8_t* pks, const uint32_t* grp_off, const uint8_t* sigs,
                                 const uint8_t* msgs, const uint64_t* msg_off, const uint32_t* msg_len,
                                 size_t n_groups, uint8_t* status);
@@ -118,6 +120,12 @@ int hbls_verify_device(const uint8_t* pks, const uint8_t* sigs, const uint32_t* 
 int hbls_threshold_aggregate_device(const uint8_t* sigs, const int64_t* idx, const uint32_t* grp_off,
                                     size_t n_groups, size_t n_partials, uint8_t* out, uint8_t* status,
                                     void* stream);
+
+/* VerifyAggregate on device buffers: pks (48 B each), sigs (96 B per group), hm (one hashed message
+ * per group, hbls_hash_to_g2_device), status (n_groups) are device pointers; grp_off is a HOST
+ * array of n_groups + 1 non-decreasing offsets into pks (the reduction is planned from it). */
+int hbls_verify_aggregate_device(const uint8_t* pks, const uint32_t* grp_off, size_t n_groups,
+                                 const uint8_t* sigs, const void* hm, uint8_t* status, void* stream);
 
 /* One attestation slot in one call: the batch entry point of SURVEY.md section 8b for
  * sigagg/parsigex (core/parsigex/parsigex.go:93-98, core/sigagg/sigagg.go:56-63,105,117).

@@ -326,3 +326,90 @@ def test_batched_groups_pass_without_fallback(L, hipbls, monkeypatch):
     assert st == [NOT_VERIFIED if i == 5 else OK for i in range(48)]
     d = [b - a for a, b in zip(s0, _stats(L))]
     assert d[2] == 16, d
+
+
+R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+
+
+def _rand_sks(rng, count):
+    """count random secret keys in [1, r) (32 B big-endian), vectorised."""
+    raw = np.frombuffer(rng.randbytes(32 * count), dtype=np.uint8).reshape(count, 32).copy()
+    raw[:, 0] &= 0x3F  # < 2^254 < r
+    raw[:, 31] |= 1    # nonzero
+    return raw.reshape(-1)
+
+
+def _sk_sum(sks):
+    return sum(int.from_bytes(bytes(sks[32 * i:32 * i + 32]), "big") for i in range(len(sks) // 32)) % R_ORDER
+
+
+def test_verify_aggregate_lock_scale(L):
+    """cluster/lock.go:185 at scale: one VerifyAggregate group holding 70 000 public shares (the
+    segmented key reduction runs 4 passes), beside the edge groups of FastAggregateVerify:
+    empty, single key, identity signature, undecodable signature over a group with a bad key
+    (signature checked first), a bad key, keys summing to the identity, wrong message.  Host and
+    device entry points must agree; small groups are checked against the oracle."""
+    import torch
+    rng = random.Random(77)
+    K = 70_000
+    sks = _rand_sks(rng, K + 1025 + 64 + 33 + 1)
+    pks = _pks(L, sks)
+    lock_hash = hashlib.sha256(b"cluster lock hash").digest()
+    other = hashlib.sha256(b"another root").digest()
+
+    def sig_of(lo, hi, msg):
+        s = _sk_sum(sks[32 * lo:32 * hi]).to_bytes(32, "big")
+        return bytes(_sign(L, np.frombuffer(s, dtype=np.uint8).copy(), np.frombuffer(msg, dtype=np.uint8).copy()))
+
+    o_big, o_1025, o_64, o_33, o_1 = 0, K, K + 1025, K + 1025 + 64, K + 1025 + 64 + 33
+    pk = lambda i: bytes(pks[48 * i:48 * i + 48])  # noqa: E731
+    bad_pk = bytes([0x9A]) + b"\xff" * 47
+    neg = bytearray(pk(o_1))
+    neg[0] ^= 0x20  # the negated key (sign flag flipped)
+    keys_1025 = [pk(o_1025 + j) for j in range(1025)]
+    keys_1025_bad = list(keys_1025)
+    keys_1025_bad[1000] = bad_pk
+    bad_sig = bytes([0x80]) + b"\xff" * 95  # x >= p
+    inf_sig = bytes([0xC0]) + bytes(95)
+    groups = [
+        ([pk(o_big + j) for j in range(K)], sig_of(o_big, o_big + K, lock_hash), lock_hash, OK),
+        ([], sig_of(o_1, o_1 + 1, lock_hash), lock_hash, NOT_VERIFIED),
+        ([pk(o_1)], sig_of(o_1, o_1 + 1, lock_hash), lock_hash, OK),
+        ([pk(o_33 + j) for j in range(33)], inf_sig, lock_hash, NOT_VERIFIED),
+        (keys_1025_bad, bad_sig, lock_hash, BAD_SIGNATURE),
+        (keys_1025_bad, sig_of(o_1025, o_1025 + 1025, lock_hash), lock_hash, BAD_PUBKEY),
+        ([pk(o_1), bytes(neg)], sig_of(o_1, o_1 + 1, lock_hash), lock_hash, NOT_VERIFIED),
+        ([pk(o_64 + j) for j in range(64)], sig_of(o_64, o_64 + 64, other), lock_hash, NOT_VERIFIED),
+        (keys_1025, sig_of(o_1025, o_1025 + 1025, lock_hash), lock_hash, OK),
+    ]
+    G = len(groups)
+    goff = np.zeros(G + 1, dtype=np.uint32)
+    for g, grp in enumerate(groups):
+        goff[g + 1] = goff[g] + len(grp[0])
+    allpk = np.frombuffer(b"".join(k for grp in groups for k in grp[0]), dtype=np.uint8).copy()
+    allsig = np.frombuffer(b"".join(grp[1] for grp in groups), dtype=np.uint8).copy()
+    mb = np.frombuffer(b"".join(grp[2] for grp in groups), dtype=np.uint8).copy()
+    moff = np.arange(G, dtype=np.uint64) * 32
+    mlen = np.full(G, 32, dtype=np.uint32)
+    st = np.full(G, 255, dtype=np.uint8)
+    _chk(L, L.hbls_verify_aggregate_batch(_p(allpk), _p(goff), _p(allsig), _p(mb), _p(moff), _p(mlen), G, _p(st)))
+    expect = [grp[3] for grp in groups]
+    assert list(st) == expect
+
+    # device entry point, same inputs
+    dev = torch.device("cuda", 0)
+    up = lambda a: torch.from_numpy(a).to(dev)  # noqa: E731
+    hm = torch.zeros(G * L.hbls_hm_entry_bytes(), dtype=torch.uint8, device=dev)
+    s = torch.cuda.Stream(device=dev)
+    sp = ctypes.c_void_p(s.cuda_stream)
+    dmb, dmo, dml = up(mb), up(moff.view(np.int64)), up(mlen.view(np.int32))
+    dpk, dsig = up(allpk), up(allsig)
+    dst = torch.full((G,), 255, dtype=torch.uint8, device=dev)
+    _chk(L, L.hbls_hash_to_g2_device(_p(dmb), _p(dmo), _p(dml), G, _p(hm), sp))
+    _chk(L, L.hbls_verify_aggregate_device(_p(dpk), _p(goff), G, _p(dsig), _p(hm), _p(dst), sp))
+    s.synchronize()
+    assert list(dst.cpu().numpy()) == expect
+
+    from oracle import bls12381 as B
+    for g in (1, 2, 3, 6):
+        assert B.verify_aggregate(groups[g][0], groups[g][1], groups[g][2]) == expect[g], g
