@@ -323,6 +323,8 @@ def main(argv=None):
     ap.add_argument("--aggregate-verify", type=int, default=1,
                     help="also time VerifyAggregate at scale (lock over all pubshares, sync-committee groups)")
     ap.add_argument("--host-api", action="store_true", help="also time the host-buffer (PCIe-inclusive) entry points")
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="slots in flight (each on its own stream and outputs); 1 = one slot at a time")
     ap.add_argument("--mode", default="slot", choices=["slot", "staged"],
                     help="slot: one hbls_slot_device call per step (stages overlap); staged: stage by stage")
     args = ap.parse_args(argv)
@@ -357,11 +359,15 @@ def main(argv=None):
     d_midx, d_pk, d_sig = up(d["midx"].view(np.int32)), up(d["pks"]), up(d["sigs"])
     d_tsrc, d_tidx, d_goff = up(d["ta_src"].view(np.int32)), up(d["ta_idx"]), up(d["grp_off"].view(np.int32))
     d_vgoff, d_dvpk, d_tsig = up(d["vgrp_off"].view(np.int32)), up(d["dv_pks"]), up(d["ta_sigs"])
-    d_hm = torch.zeros(M * L.hbls_hm_entry_bytes(), dtype=torch.uint8, device=dev)
-    d_vst = torch.full((NP,), 255, dtype=torch.uint8, device=dev)
-    d_tout = torch.zeros(V * 96, dtype=torch.uint8, device=dev)
-    d_tst = torch.full((V,), 255, dtype=torch.uint8, device=dev)
-    d_ast = torch.full((V,), 255, dtype=torch.uint8, device=dev)
+    # per in-flight slot: its own stream, hashed-message table and outputs (inputs are shared)
+    n_sets = max(1, args.inflight)
+    outs = [{"hm": torch.zeros(M * L.hbls_hm_entry_bytes(), dtype=torch.uint8, device=dev),
+             "vst": torch.full((NP,), 255, dtype=torch.uint8, device=dev),
+             "tout": torch.zeros(V * 96, dtype=torch.uint8, device=dev),
+             "tst": torch.full((V,), 255, dtype=torch.uint8, device=dev),
+             "ast": torch.full((V,), 255, dtype=torch.uint8, device=dev),
+             "stream": torch.cuda.Stream(device=dev)} for _ in range(n_sets)]
+    d_hm, d_vst, d_tout, d_tst, d_ast = (outs[0][k] for k in ("hm", "vst", "tout", "tst", "ast"))
 
     xchg = None
     if world > 1:
@@ -373,31 +379,53 @@ def main(argv=None):
         dist.broadcast_object_list(obj, src=0)
         idb = np.frombuffer(obj[0], dtype=np.uint8).copy()
         _chk(L, L.hbls_comm_init(world, rank, _p(idb)))
-        xchg = {"vst": torch.empty(world * NP, dtype=torch.uint8, device=dev),
-                "tout": torch.empty(world * V * 96, dtype=torch.uint8, device=dev),
-                "tst": torch.empty(world * V, dtype=torch.uint8, device=dev),
-                "ast": torch.empty(world * V, dtype=torch.uint8, device=dev)}
+        for o in outs:
+            o["xchg"] = {"vst": torch.empty(world * NP, dtype=torch.uint8, device=dev),
+                         "tout": torch.empty(world * V * 96, dtype=torch.uint8, device=dev),
+                         "tst": torch.empty(world * V, dtype=torch.uint8, device=dev),
+                         "ast": torch.empty(world * V, dtype=torch.uint8, device=dev)}
+        xchg = outs[0]["xchg"]
 
-    stream = torch.cuda.Stream(device=dev)
+    stream = outs[0]["stream"]
     sp = ctypes.c_void_p(stream.cuda_stream)
-    slot = _lib.HblsSlot(msgs=_p(d_msg).value, msg_off=_p(d_moff).value, msg_len=_p(d_mlen).value, n_msgs=M,
-                         hm=_p(d_hm).value, pks=_p(d_pk).value, sigs=_p(d_sig).value, msg_idx=_p(d_midx).value, n=NP,
-                         vgrp_off=_p(d_vgoff).value, n_vgroups=V, vstatus=_p(d_vst).value, ta_sigs=None,
-                         ta_src=_p(d_tsrc).value, ta_idx=_p(d_tidx).value, grp_off=_p(d_goff).value, n_groups=V,
-                         n_ta_partials=V * t, ta_out=_p(d_tout).value, ta_status=_p(d_tst).value,
-                         dv_pks=_p(d_dvpk).value, agg_vstatus=_p(d_ast).value)
+    for o in outs:
+        o["sp"] = ctypes.c_void_p(o["stream"].cuda_stream)
+        o["slot"] = _lib.HblsSlot(
+            msgs=_p(d_msg).value, msg_off=_p(d_moff).value, msg_len=_p(d_mlen).value, n_msgs=M, hm=_p(o["hm"]).value,
+            pks=_p(d_pk).value, sigs=_p(d_sig).value, msg_idx=_p(d_midx).value, n=NP, vgrp_off=_p(d_vgoff).value,
+            n_vgroups=V, vstatus=_p(o["vst"]).value, ta_sigs=None, ta_src=_p(d_tsrc).value, ta_idx=_p(d_tidx).value,
+            grp_off=_p(d_goff).value, n_groups=V, n_ta_partials=V * t, ta_out=_p(o["tout"]).value,
+            ta_status=_p(o["tst"]).value, dv_pks=_p(d_dvpk).value, agg_vstatus=_p(o["ast"]).value)
 
-    def exchange():  # all-gather verdicts + compressed aggregates to every rank (RCCL)
-        for src, dst in ((d_vst, "vst"), (d_tout, "tout"), (d_tst, "tst"), (d_ast, "ast")):
-            _chk(L, L.hbls_allgather_device(_p(src), _p(xchg[dst]), src.numel(), sp))
+    # the collectives of all in-flight slots go through ONE stream, so every rank issues them to
+    # the communicator in the same order and they never run concurrently
+    xs = torch.cuda.Stream(device=dev)
+    xsp = ctypes.c_void_p(xs.cuda_stream)
+
+    def exchange(o):  # all-gather verdicts + compressed aggregates to every rank (RCCL)
+        done = torch.cuda.Event()
+        done.record(o["stream"])
+        xs.wait_event(done)
+        for src, dst in ((o["vst"], "vst"), (o["tout"], "tout"), (o["tst"], "tst"), (o["ast"], "ast")):
+            _chk(L, L.hbls_allgather_device(_p(src), _p(o["xchg"][dst]), src.numel(), xsp))
+        back = torch.cuda.Event()
+        back.record(xs)
+        o["stream"].wait_event(back)  # the set's next slot overwrites the outputs only after the exchange
+
+    step_no = [0]
 
     def step_slot(ev):
-        ev[0].record(stream)
-        _chk(L, L.hbls_slot_device(ctypes.byref(slot), sp))
-        ev[1].record(stream)
+        # consecutive slots alternate between the in-flight sets: slot k+1's decompression and
+        # hashing run while slot k's pairings finish (the library orders its workspaces by events)
+        o = outs[step_no[0] % n_sets]
+        step_no[0] += 1
+        st = o["stream"]
+        ev[0].record(st)
+        _chk(L, L.hbls_slot_device(ctypes.byref(o["slot"]), o["sp"]))
+        ev[1].record(st)
         if world > 1:
-            exchange()
-        ev[2].record(stream)
+            exchange(o)
+        ev[2].record(st)
 
     def step_staged(ev):
         # the same work stage by stage (no overlap; the aggregation decompresses its own bytes)
@@ -442,13 +470,12 @@ def main(argv=None):
 
     # parity of the timed outputs: every partial verifies, every aggregate is byte-identical to the
     # root-key signature (tbls_test.go:72-97 property) and verifies under the DV key
-    vst = d_vst.cpu().numpy()
-    tst = d_tst.cpu().numpy()
-    tout = d_tout.cpu().numpy()
-    parity = {"verify_all_ok": bool((vst == 0).all()), "ta_all_ok": bool((tst == 0).all()),
-              "ta_equals_root_signature": bool(np.array_equal(tout, d["root_sigs"]))}
+    used = outs if not staged else outs[:1]
+    parity = {"verify_all_ok": all(bool((o["vst"] == 0).all().item()) for o in used),
+              "ta_all_ok": all(bool((o["tst"] == 0).all().item()) for o in used),
+              "ta_equals_root_signature": all(np.array_equal(o["tout"].cpu().numpy(), d["root_sigs"]) for o in used)}
     if not staged:
-        parity["aggregate_verify_all_ok"] = bool((d_ast.cpu().numpy() == 0).all())
+        parity["aggregate_verify_all_ok"] = all(bool((o["ast"] == 0).all().item()) for o in used)
     if world > 1:
         parity["allgather_ok"] = bool((xchg["vst"] == 0).all().item() and (xchg["tst"] == 0).all().item() and
                                       (xchg["ast"] == 0).all().item())

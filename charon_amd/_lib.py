@@ -96,8 +96,10 @@ def _declare(lib):
         fn.restype = res
 
 
-def load_library(path: str = LIB_PATH):
-    """Load the shared library without touching the GPU (safe on CPU-only hosts)."""
+def load_library(path: str = ""):
+    """Load the shared library without touching the GPU (safe on CPU-only hosts).  HBLS_LIBRARY
+    names a tuning variant built by charon_amd.build (default: the in-tree product library)."""
+    path = path or os.environ.get("HBLS_LIBRARY") or LIB_PATH
     global _lib
     with _lock:
         if _lib is None:

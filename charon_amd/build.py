@@ -28,7 +28,10 @@ def _newer(target, deps):
     return all(os.path.getmtime(d) <= t for d in deps)
 
 
-def build_library(force: bool = False, verbose: bool = True) -> str:
+def build_library(force: bool = False, verbose: bool = True, defines=(), out: str = LIB) -> str:
+    """defines / out: tuning variants (e.g. ("HB_OCC2=2",) -> charon_amd/lib/variants/...), used by
+    tools/ experiments through HBLS_LIBRARY; the product is the default build."""
+    LIB = out
     deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(ROOT, "include", "hipbls.h")]
     if not force and _newer(LIB, deps):
         return LIB
@@ -39,8 +42,8 @@ def build_library(force: bool = False, verbose: bool = True) -> str:
     for src in SOURCES:
         obj = os.path.join(os.path.dirname(LIB), os.path.splitext(src)[0] + ".o")
         objs.append(obj)
-        procs.append(subprocess.Popen([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-c",
-                                       os.path.join(CSRC, src), "-o", obj]))
+        procs.append(subprocess.Popen([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-c"] +
+                                      ["-D" + d for d in defines] + [os.path.join(CSRC, src), "-o", obj]))
     for p in procs:
         if p.wait(timeout=3000) != 0:
             raise RuntimeError("hipcc failed")

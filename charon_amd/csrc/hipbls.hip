@@ -233,23 +233,29 @@ enum WsId {
   W_FBLINES,
   W_APK, W_APKST, W_ASIG, W_APR, W_ASR,          // folded aggregates (post-aggregate verification)
   W_TAPTS, W_TADST, W_TAMST, W_TADIG, W_TATAB, W_TAJ,  // ThresholdAggregate / Aggregate
-  W_SEGA, W_SEGB, W_SEGSTA, W_SEGSTB, W_VAPT, W_VAPV,  // VerifyAggregate key reduction
+  W_SEGA, W_SEGB, W_SEGSTA, W_SEGSTB, W_VAPT, W_VAPV, W_PLAN,  // VerifyAggregate key reduction
   W_COUNT_
 };
 
 // A workspace set: grow-only device buffers plus the event recorded after the last kernel that
 // used them.  Every user waits on `free_ev` in each stream it launches on before touching the
 // set, so two calls never share a set concurrently, whatever streams they run on.
+//
+// Each set also owns the side streams its calls fork onto (decompression, hashing, aggregation)
+// and their fork/join events, so two calls in flight on different user streams -- consecutive
+// slots, say -- overlap instead of queueing behind each other on shared side streams.
+constexpr int N_SIDE = 4;
 struct Ws {
   DevBuf b[W_COUNT_];
   hipEvent_t free_ev = nullptr;
   bool used = false;
+  hipStream_t side[N_SIDE] = {};
+  hipEvent_t ev_fork = nullptr, ev_side[N_SIDE] = {}, ev_ta = nullptr;
 };
 
 // host-call staging buffers (inputs and outputs of the host-buffer entry points)
-enum IoId { I_PK, I_SIG, I_MSG, I_OFF, I_LEN, I_MIDX, I_HM, I_STAT, I_IDX, I_GOFF, I_OUT, I_SK, I_VGOFF, I_SEG, I_COUNT };
+enum IoId { I_PK, I_SIG, I_MSG, I_OFF, I_LEN, I_MIDX, I_HM, I_STAT, I_IDX, I_GOFF, I_OUT, I_SK, I_VGOFF, I_COUNT };
 
-constexpr int N_SIDE = 4;
 constexpr int N_WS = 2;
 
 struct Timed {
@@ -260,12 +266,15 @@ struct Timed {
 struct Dev {
   int ord = -1;
   hipStream_t stream = nullptr;  // the library stream of host-buffer calls
-  hipStream_t side[N_SIDE] = {};
-  hipEvent_t ev_fork = nullptr, ev_side[N_SIDE] = {}, ev_join = nullptr, ev_ta = nullptr;
   Ws ws[N_WS];
   unsigned next_ws = 0;
   DevBuf io[I_COUNT];
   std::mutex mu;  // one call at a time enqueues on this device
+  // end of the last verification's decompression stage: the next verification starts its own
+  // decompression after it, so consecutive slots in flight run staggered (one slot's
+  // decompression beside the previous slot's combinations and pairings) instead of in lockstep
+  hipEvent_t ev_dec = nullptr;
+  bool dec_valid = false;
   // timing (hbls_timing)
   bool timing = false;
   std::vector<Timed> tev;
@@ -300,11 +309,13 @@ int wsbuf(Ws& w, WsId id, size_t count, T** out) {
   return 0;
 }
 
-// Acquire a workspace set for a call whose kernels run on `streams`.
-Ws& ws_acquire(Dev& d, std::initializer_list<hipStream_t> streams) {
+// Acquire a workspace set for a call whose kernels run on `s` and the set's side streams.
+Ws& ws_acquire(Dev& d, hipStream_t s) {
   Ws& w = d.ws[d.next_ws++ % N_WS];
-  if (w.used)
-    for (hipStream_t s : streams) (void)hipStreamWaitEvent(s, w.free_ev, 0);
+  if (w.used) {
+    (void)hipStreamWaitEvent(s, w.free_ev, 0);
+    for (hipStream_t x : w.side) (void)hipStreamWaitEvent(x, w.free_ev, 0);
+  }
   return w;
 }
 int ws_release(Ws& w, hipStream_t last) {
@@ -356,14 +367,16 @@ int dev_create(int ord, Dev** out) {
   int prio_lo = 0, prio_hi = 0;
   HCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
   HCHK(hipStreamCreateWithPriority(&d->stream, hipStreamNonBlocking, prio_lo));
-  for (int k = 0; k < N_SIDE; k++) {
-    HCHK(hipStreamCreateWithPriority(&d->side[k], hipStreamNonBlocking, k == 3 ? prio_lo : prio_hi));
-    HCHK(hipEventCreateWithFlags(&d->ev_side[k], hipEventDisableTiming));
+  HCHK(hipEventCreateWithFlags(&d->ev_dec, hipEventDisableTiming));
+  for (auto& w : d->ws) {
+    HCHK(hipEventCreateWithFlags(&w.free_ev, hipEventDisableTiming));
+    for (int k = 0; k < N_SIDE; k++) {
+      HCHK(hipStreamCreateWithPriority(&w.side[k], hipStreamNonBlocking, k == 3 ? prio_lo : prio_hi));
+      HCHK(hipEventCreateWithFlags(&w.ev_side[k], hipEventDisableTiming));
+    }
+    HCHK(hipEventCreateWithFlags(&w.ev_fork, hipEventDisableTiming));
+    HCHK(hipEventCreateWithFlags(&w.ev_ta, hipEventDisableTiming));
   }
-  HCHK(hipEventCreateWithFlags(&d->ev_fork, hipEventDisableTiming));
-  HCHK(hipEventCreateWithFlags(&d->ev_join, hipEventDisableTiming));
-  HCHK(hipEventCreateWithFlags(&d->ev_ta, hipEventDisableTiming));
-  for (auto& w : d->ws) HCHK(hipEventCreateWithFlags(&w.free_ev, hipEventDisableTiming));
   *out = d;
   return 0;
 }
@@ -530,24 +543,25 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
   RlcKey key;
   if (rlc_key(key)) return -1;
 
-  // fork: decompression on the side streams
-  HCHK(hipEventRecord(d.ev_fork, s));
-  for (int k = 0; k < 2; k++) HCHK(hipStreamWaitEvent(d.side[k], d.ev_fork, 0));
-  TIMED(d, "k_dec_pk", d.side[0], launch_dec_pk(dpk, (uint32_t)n, vpk, vpkst, d.side[0]));
-  if (n_agg) TIMED(d, "k_dec_pk", d.side[0], launch_dec_pk(fold->dv_pks, (uint32_t)n_agg, apk, apkst, d.side[0]));
-  TIMED(d, "k_dec_sig_pt", d.side[1], launch_dec_sig_pt(dsig, (uint32_t)n, vsig, vsigst, d.side[1]));
-  HCHK(hipEventRecord(d.ev_side[0], d.side[0]));
-  HCHK(hipEventRecord(d.ev_side[1], d.side[1]));
+  // fork: decompression on the side streams (after the previous verification's decompression)
+  if (d.dec_valid) HCHK(hipStreamWaitEvent(s, d.ev_dec, 0));
+  HCHK(hipEventRecord(w.ev_fork, s));
+  for (int k = 0; k < 2; k++) HCHK(hipStreamWaitEvent(w.side[k], w.ev_fork, 0));
+  TIMED(d, "k_dec_pk", w.side[0], launch_dec_pk(dpk, (uint32_t)n, vpk, vpkst, w.side[0]));
+  if (n_agg) TIMED(d, "k_dec_pk", w.side[0], launch_dec_pk(fold->dv_pks, (uint32_t)n_agg, apk, apkst, w.side[0]));
+  TIMED(d, "k_dec_sig_pt", w.side[1], launch_dec_sig_pt(dsig, (uint32_t)n, vsig, vsigst, w.side[1]));
+  HCHK(hipEventRecord(w.ev_side[0], w.side[0]));
+  HCHK(hipEventRecord(w.ev_side[1], w.side[1]));
 
   // the slot's ThresholdAggregate on side 3 (needs the decompressed partials when it reuses them)
   const bool ta = fold && fold->n_groups;
   if (ta) {
-    hipStream_t st = d.side[3];
-    HCHK(hipStreamWaitEvent(st, d.ev_fork, 0));
+    hipStream_t st = w.side[3];
+    HCHK(hipStreamWaitEvent(st, w.ev_fork, 0));
     const HmEntry* pts = vsig;
     const uint8_t* mst_in = vsigst;
     if (fold->ta_src) {
-      HCHK(hipStreamWaitEvent(st, d.ev_side[1], 0));
+      HCHK(hipStreamWaitEvent(st, w.ev_side[1], 0));
     } else {  // the aggregation members come as their own bytes: decompress them here
       HmEntry* tpts;
       uint8_t* tdst;
@@ -559,16 +573,18 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
     if (ta_tail(d, w, pts, fold->ta_src, mst_in, fold->ta_idx, fold->grp_off, fold->n_groups, fold->n_partials, 0,
                 fold->ta_out, fold->ta_status, asig, st))
       return -1;
-    HCHK(hipEventRecord(d.ev_ta, st));
+    HCHK(hipEventRecord(w.ev_ta, st));
   }
 
   // random linear combinations per item, then per group
-  HCHK(hipStreamWaitEvent(s, d.ev_side[0], 0));
-  HCHK(hipStreamWaitEvent(s, d.ev_side[1], 0));
+  HCHK(hipStreamWaitEvent(s, w.ev_side[0], 0));
+  HCHK(hipStreamWaitEvent(s, w.ev_side[1], 0));
+  HCHK(hipEventRecord(d.ev_dec, s));
+  d.dec_valid = true;
   TIMED(d, "k_item_group", s, launch_item_group(dgoff, (uint32_t)n_groups, (uint32_t)n, igrp, s));
   TIMED(d, "k_rlc", s, launch_rlc(vpk, vpkst, vsig, vsigst, igrp, dgoff, 0, (uint32_t)n, 0, key, pr, sr, s));
   if (n_agg) {
-    HCHK(hipStreamWaitEvent(s, d.ev_ta, 0));
+    HCHK(hipStreamWaitEvent(s, w.ev_ta, 0));
     TIMED(d, "k_rlc", s,
           launch_rlc(apk, apkst, asig, fold->ta_status, nullptr, nullptr, 1, (uint32_t)n_agg, (uint32_t)n, key, apr,
                      asr, s));
@@ -658,7 +674,7 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
     TIMED(d, "k_pair3_fallback", s, launch_pair3(pa, s));
   }
   if (ta && !n_agg) {  // the aggregation ran beside the verification: join it
-    HCHK(hipStreamWaitEvent(s, d.ev_ta, 0));
+    HCHK(hipStreamWaitEvent(s, w.ev_ta, 0));
   }
   if (stats_on()) {  // HBLS_STATS=1: count the fallback items (synchronises; tests and diagnosis)
     uint32_t c = 0;
@@ -797,7 +813,7 @@ int verify_host(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msgs, co
     void* p;
     if (ensure_buf(d.io[I_STAT], m, &p)) return -1;
     dst = (uint8_t*)p;
-    Ws& w = ws_acquire(d, {d.stream, d.side[0], d.side[1], d.side[3]});
+    Ws& w = ws_acquire(d, d.stream);
     if (verify_pipeline(d, w, dpk, dsig, didx, hm, m, dgoff, ge - gb, dst, d.stream, nullptr, nullptr)) return -1;
     if (ws_release(w, d.stream)) return -1;
     std::vector<uint8_t> hst(m);
@@ -832,7 +848,7 @@ int group_op_host(const uint8_t* sigs, const int64_t* idx, const uint32_t* grp_o
     if (upload(d, I_GOFF, goff.data(), ng + 1, &dgoff)) return -1;
     void *dout, *dst;
     if (ensure_buf(d.io[I_OUT], ng * 96, &dout) || ensure_buf(d.io[I_STAT], ng, &dst)) return -1;
-    Ws& w = ws_acquire(d, {d.stream});
+    Ws& w = ws_acquire(d, d.stream);
     HmEntry* pts;
     uint8_t* mst0;
     if (wsbuf(w, W_TAPTS, np, &pts) || wsbuf(w, W_TADST, np, &mst0)) return -1;
@@ -991,12 +1007,9 @@ int va_pipeline(Dev& d, Ws& w, const uint8_t* dpk, size_t np, const uint32_t* go
   for (size_t g = 0; g < ng; g++) plan.push_back(hi[g] > lo[g] ? lo[g] : 0xffffffffu);
   const size_t iota_off = plan.size();
   for (size_t g = 0; g < ng; g++) plan.push_back((uint32_t)g);
-  uint32_t* dplan;
-  if (upload(d, I_SEG, plan.data(), plan.size(), &dplan)) return -1;
-  if (s != d.stream) {  // the upload ran on the library stream
-    HCHK(hipEventRecord(d.ev_fork, d.stream));
-    HCHK(hipStreamWaitEvent(s, d.ev_fork, 0));
-  }
+  uint32_t* dplan;  // in the workspace set (event-ordered), copied on the call's stream
+  if (wsbuf(w, W_PLAN, plan.size(), &dplan)) return -1;
+  HCHK(hipMemcpyAsync(dplan, plan.data(), plan.size() * sizeof(uint32_t), hipMemcpyHostToDevice, s));
 
   G1AEntry *pts, *vapt;
   uint8_t *mst, *sigst, *pv, *sta, *stb;
@@ -1009,13 +1022,13 @@ int va_pipeline(Dev& d, Ws& w, const uint8_t* dpk, size_t np, const uint32_t* go
       wsbuf(w, W_SEGSTA, na, &sta) || wsbuf(w, W_SEGB, nb, &sb) || wsbuf(w, W_SEGSTB, nb, &stb) ||
       wsbuf(w, W_VAPT, ng, &vapt) || wsbuf(w, W_VAPV, ng, &pv))
     return -1;
-  hipStream_t s0 = d.side[0], s1 = d.side[1];
-  HCHK(hipEventRecord(d.ev_fork, s));
-  HCHK(hipStreamWaitEvent(s0, d.ev_fork, 0));
-  HCHK(hipStreamWaitEvent(s1, d.ev_fork, 0));
+  hipStream_t s0 = w.side[0], s1 = w.side[1];
+  HCHK(hipEventRecord(w.ev_fork, s));
+  HCHK(hipStreamWaitEvent(s0, w.ev_fork, 0));
+  HCHK(hipStreamWaitEvent(s1, w.ev_fork, 0));
   TIMED(d, "k_dec_sig_pt", s1, launch_dec_sig_pt(dsig, (uint32_t)ng, sigpt, sigst, s1));
   TIMED(d, "k_sig_lines", s1, launch_sig_lines(sigpt, (uint32_t)ng, lines, (uint32_t)ng, s1));
-  HCHK(hipEventRecord(d.ev_side[1], s1));
+  HCHK(hipEventRecord(w.ev_side[1], s1));
   if (hash_fn && hash_fn()) return -1;
   if (np) TIMED(d, "k_dec_pk", s0, launch_dec_pk(dpk, (uint32_t)np, pts, mst, s0));
   const void* in = pts;
@@ -1030,9 +1043,9 @@ int va_pipeline(Dev& d, Ws& w, const uint8_t* dpk, size_t np, const uint32_t* go
     in = out;
     in_st = out_st;
   }
-  HCHK(hipEventRecord(d.ev_side[0], s0));
-  HCHK(hipStreamWaitEvent(s, d.ev_side[0], 0));
-  HCHK(hipStreamWaitEvent(s, d.ev_side[1], 0));
+  HCHK(hipEventRecord(w.ev_side[0], s0));
+  HCHK(hipStreamWaitEvent(s, w.ev_side[0], 0));
+  HCHK(hipStreamWaitEvent(s, w.ev_side[1], 0));
   TIMED(d, "k_va_point", s, launch_va_point(out, dplan + sog_off, (uint32_t)ng, vapt, s));
   Pair3Args a{};
   a.pk = vapt;
@@ -1120,7 +1133,7 @@ int hbls_verify_aggregate_batch(const uint8_t* pks, const uint32_t* grp_off, con
     if (upload(d, I_PK, pks + 48 * pb, np * 48, &dpk) || upload(d, I_SIG, sigs + 96 * gb, ng * 96, &dsig)) return -1;
     void* p;
     if (ensure_buf(d.io[I_STAT], ng, &p)) return -1;
-    Ws& w = ws_acquire(d, {d.stream, d.side[0], d.side[1]});
+    Ws& w = ws_acquire(d, d.stream);
     uint8_t* dst = (uint8_t*)p;
     void* hmp;  // the message table's buffer (hash_table fills the same one on the library stream)
     if (ensure_buf(d.io[I_HM], ng * sizeof(MsgEntry), &hmp)) return -1;
@@ -1236,7 +1249,7 @@ int hbls_verify_device(const uint8_t* pks, const uint8_t* sigs, const uint32_t* 
   if (dev_of_stream(s, &d)) return -1;
   if (n == 0) return 0;
   std::lock_guard<std::mutex> lk(d->mu);
-  Ws& w = ws_acquire(*d, {s, d->side[0], d->side[1], d->side[3]});
+  Ws& w = ws_acquire(*d, s);
   if (verify_pipeline(*d, w, pks, sigs, msg_idx, (const MsgEntry*)hm, n, vgrp_off, n_vgroups, status, s, nullptr,
                       nullptr))
     return -1;
@@ -1253,7 +1266,7 @@ int hbls_verify_aggregate_device(const uint8_t* pks, const uint32_t* grp_off, si
   std::vector<uint32_t> goff(n_groups + 1);
   for (size_t g = 0; g <= n_groups; g++) goff[g] = grp_off[g] - grp_off[0];
   std::lock_guard<std::mutex> lk(d->mu);
-  Ws& w = ws_acquire(*d, {s, d->side[0], d->side[1]});
+  Ws& w = ws_acquire(*d, s);
   if (va_pipeline(*d, w, pks + 48ull * grp_off[0], goff[n_groups], goff.data(), n_groups, sigs, (const MsgEntry*)hm,
                   status, s, nullptr))
     return -1;
@@ -1266,7 +1279,7 @@ int hbls_threshold_aggregate_device(const uint8_t* sigs, const int64_t* idx, con
   hipStream_t s = (hipStream_t)stream;
   if (dev_of_stream(s, &d)) return -1;
   std::lock_guard<std::mutex> lk(d->mu);
-  Ws& w = ws_acquire(*d, {s});
+  Ws& w = ws_acquire(*d, s);
   HmEntry* pts;
   uint8_t* mst0;
   if (wsbuf(w, W_TAPTS, n_partials, &pts) || wsbuf(w, W_TADST, n_partials, &mst0)) return -1;
@@ -1285,13 +1298,14 @@ int hbls_slot_device(const hbls_slot* a, void* stream) {
     return set_err("hbls_slot_device: the folded post-aggregate verification needs one verification group per "
                    "aggregation group");
   std::lock_guard<std::mutex> lk(d->mu);
-  Ws& w = ws_acquire(*d, {s, d->side[0], d->side[1], d->side[2], d->side[3]});
-  HCHK(hipEventRecord(d->ev_fork, s));
+  Ws& w = ws_acquire(*d, s);
+  if (d->dec_valid) HCHK(hipStreamWaitEvent(s, d->ev_dec, 0));  // staggered slots (Dev::ev_dec)
+  HCHK(hipEventRecord(w.ev_fork, s));
   // messages: hash + Miller lines (side 2)
-  hipStream_t sh = d->side[2];
-  HCHK(hipStreamWaitEvent(sh, d->ev_fork, 0));
+  hipStream_t sh = w.side[2];
+  HCHK(hipStreamWaitEvent(sh, w.ev_fork, 0));
   if (hash_messages(*d, a->msgs, a->msg_off, a->msg_len, a->n_msgs, (MsgEntry*)a->hm, sh)) return -1;
-  HCHK(hipEventRecord(d->ev_side[2], sh));
+  HCHK(hipEventRecord(w.ev_side[2], sh));
   TaFold fold{};
   fold.ta_sigs = a->ta_sigs;
   fold.ta_src = a->ta_src;
@@ -1304,9 +1318,9 @@ int hbls_slot_device(const hbls_slot* a, void* stream) {
   fold.dv_pks = a->dv_pks;
   fold.agg_status = a->agg_vstatus;
   if (verify_pipeline(*d, w, a->pks, a->sigs, a->msg_idx, (const MsgEntry*)a->hm, a->n, a->vgrp_off, a->n_vgroups,
-                      a->vstatus, s, d->ev_side[2], &fold))
+                      a->vstatus, s, w.ev_side[2], &fold))
     return -1;
-  HCHK(hipStreamWaitEvent(s, d->ev_side[2], 0));
+  HCHK(hipStreamWaitEvent(s, w.ev_side[2], 0));
   return ws_release(w, s);
 }
 

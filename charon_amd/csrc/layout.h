@@ -4,6 +4,35 @@
 #pragma once
 #include "ops.h"
 
+// Occupancy targets (waves per SIMD) of the heavy kernels: 1 lets the compiler use all 512
+// registers of a lane, 2 gives each wave 256, 3 gives 168 (spilling the rest to scratch).  Chosen
+// per kernel by measurement; tuning builds override them with -D.
+#ifndef HB_OCC_HASH
+#define HB_OCC_HASH 2
+#endif
+#ifndef HB_OCC_LINES
+#define HB_OCC_LINES 1
+#endif
+#ifndef HB_OCC_DECPK
+#define HB_OCC_DECPK 1
+#endif
+#ifndef HB_OCC_DECSIG
+#define HB_OCC_DECSIG 2
+#endif
+#ifndef HB_OCC_RLC
+#define HB_OCC_RLC 2
+#endif
+#ifndef HB_OCC_PREP
+#define HB_OCC_PREP 2
+#endif
+#ifndef HB_OCC_PAIR3
+#define HB_OCC_PAIR3 2
+#endif
+#ifndef HB_OCC_STRAUS
+#define HB_OCC_STRAUS 2
+#endif
+#define KB_OCC(n) __launch_bounds__(64, n)
+
 namespace hb {
 
 struct HmEntry {  // affine G2 point (Montgomery limbs) + infinity flag

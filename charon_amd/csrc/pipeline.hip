@@ -9,7 +9,6 @@
 
 namespace hb {
 
-#define KERNEL_BOUNDS __launch_bounds__(64)
 constexpr int BLOCK = 64;
 
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -27,7 +26,7 @@ __device__ __forceinline__ G2J xch_pair(const G2J& p) {  // the point of lane ^ 
 // Two lanes per distinct message: hash_to_curve G2 (RFC 9380, DST ..._POP_), affine.  Both lanes
 // expand the message; the even lane maps u0, the odd lane u1 (SSWU + 3-isogeny, the larger half
 // of the work, in parallel), then the even lane adds the pair and clears the cofactor.
-__global__ KERNEL_BOUNDS void k_hash_to_g2(const uint8_t* __restrict__ msgs, const uint64_t* __restrict__ off,
+__global__ KB_OCC(HB_OCC_HASH) void k_hash_to_g2(const uint8_t* __restrict__ msgs, const uint64_t* __restrict__ off,
                                            const uint32_t* __restrict__ len, uint32_t n, MsgEntry* __restrict__ hm) {
 #if defined(__HIP_DEVICE_COMPILE__)
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -52,7 +51,7 @@ __global__ KERNEL_BOUNDS void k_hash_to_g2(const uint8_t* __restrict__ msgs, con
 }
 
 // One lane per distinct message: the unevaluated line chain of H(m).
-__global__ KERNEL_BOUNDS void k_lines_msg(MsgEntry* __restrict__ hm, uint32_t n) {
+__global__ KB_OCC(HB_OCC_LINES) void k_lines_msg(MsgEntry* __restrict__ hm, uint32_t n) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   line_chain<false>(hm_load(hm[i].h), hm[i].lines, 1);
@@ -61,7 +60,7 @@ __global__ KERNEL_BOUNDS void k_lines_msg(MsgEntry* __restrict__ hm, uint32_t n)
 // THREE lanes per pairing (pair3.h): Miller loop over the streamed lines of (P, H(m)) and
 // (-g1, S), final exponentiation, verdict (herumi.go:299 VerifyByte).  Units and statuses as
 // described at Pair3Args (layout.h).
-__global__ __launch_bounds__(64, 2) void k_pair3(Pair3Args a) {
+__global__ KB_OCC(HB_OCC_PAIR3) void k_pair3(Pair3Args a) {
 #if defined(__HIP_DEVICE_COMPILE__)
   Grp g = grp_make();
   const int grp = (int)(threadIdx.x & 63u) / 3;

@@ -136,7 +136,7 @@ __device__ __forceinline__ void f2_select(Fp2& r, bool take_b, const Fp2& a, con
 // mixed additions, kept in global memory): 64 doublings + 64 table additions per partial, against
 // 4 x 64 of each for four independent ladders.  Uniform control flow: the table addition of
 // every step is computed and kept or dropped per lane by select.
-__global__ __launch_bounds__(64, 2) void k_ta_straus(const HmEntry* __restrict__ pts, const uint32_t* __restrict__ src,
+__global__ KB_OCC(HB_OCC_STRAUS) void k_ta_straus(const HmEntry* __restrict__ pts, const uint32_t* __restrict__ src,
                                                      const TaDigits* __restrict__ dig,
                                                      uint32_t n_partials, uint4* __restrict__ tab,
                                                      G2JEntry* __restrict__ out) {

@@ -45,7 +45,7 @@ __global__ KB void k_item_group(const uint32_t* __restrict__ grp_off, uint32_t n
 // One lane per partial: decompress + subgroup-check the public key (herumi.go:290
 // PublicKey.Deserialize).  A rejected key is replaced by g1 so later stages run the same
 // arithmetic on well-formed values; its status byte decides the verdict.
-__global__ KB void k_dec_pk(const uint8_t* __restrict__ pks, uint32_t n, G1AEntry* __restrict__ out,
+__global__ KB_OCC(HB_OCC_DECPK) void k_dec_pk(const uint8_t* __restrict__ pks, uint32_t n, G1AEntry* __restrict__ out,
                             uint8_t* __restrict__ st) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -64,7 +64,7 @@ __global__ KB void k_dec_pk(const uint8_t* __restrict__ pks, uint32_t n, G1AEntr
 // One lane per signature: decompress + subgroup-check (herumi.go:295 / :257 Sign.Deserialize),
 // affine point + status (1 = undecodable or off the subgroup).  Serves the verification and,
 // through index arrays, the ThresholdAggregate of the same partials.
-__global__ KB void k_dec_sig_pt(const uint8_t* __restrict__ sigs, uint32_t n, HmEntry* __restrict__ out,
+__global__ KB_OCC(HB_OCC_DECSIG) void k_dec_sig_pt(const uint8_t* __restrict__ sigs, uint32_t n, HmEntry* __restrict__ out,
                                 uint8_t* __restrict__ st) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -103,7 +103,7 @@ __device__ __forceinline__ bool item_usable(const G1AEntry& p, uint8_t pst, cons
 // P' = r pk, S' = r sig, written for every item so that the group sums need no branches: unusable
 // items (undecodable, infinity) contribute the point at infinity, items of singleton groups keep
 // r = 1 unless `always` (the folded aggregates).
-__global__ KB void k_rlc(const G1AEntry* __restrict__ pk, const uint8_t* __restrict__ pk_st,
+__global__ KB_OCC(HB_OCC_RLC) void k_rlc(const G1AEntry* __restrict__ pk, const uint8_t* __restrict__ pk_st,
                          const HmEntry* __restrict__ sig, const uint8_t* __restrict__ sig_st,
                          const uint32_t* __restrict__ item_grp, const uint32_t* __restrict__ grp_off, int always,
                          uint32_t n, uint32_t key_base, RlcKey key, G1JEntry* __restrict__ pout,
@@ -165,7 +165,7 @@ __global__ KB void k_scatter(ScatterArgs a) {
 }
 
 // Fallback: Miller lines at -g1 of the listed signatures, slot u = list position - base.
-__global__ KB void k_fb_lines(const uint32_t* __restrict__ list, const uint32_t* __restrict__ count, uint32_t base,
+__global__ KB_OCC(HB_OCC_LINES) void k_fb_lines(const uint32_t* __restrict__ list, const uint32_t* __restrict__ count, uint32_t base,
                               uint32_t cap, const HmEntry* __restrict__ sig, const HmEntry* __restrict__ agg_sig,
                               uint32_t n_items, LineEntry* __restrict__ lines) {
   const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
@@ -258,7 +258,7 @@ __global__ KB void k_va_point(const G1JEntry* __restrict__ sums, const uint32_t*
 }
 
 // One lane per signature: its Miller lines evaluated at -g1 (lines[j * stride + i]).
-__global__ KB void k_sig_lines(const HmEntry* __restrict__ sig, uint32_t n, LineEntry* __restrict__ lines,
+__global__ KB_OCC(HB_OCC_LINES) void k_sig_lines(const HmEntry* __restrict__ sig, uint32_t n, LineEntry* __restrict__ lines,
                                uint32_t stride) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;

@@ -16,7 +16,7 @@ __device__ __forceinline__ bool item_usable_g(const G1AEntry& p, uint8_t pst, co
 
 // One lane per verification group: sum the combined points of its usable items (plus the folded
 // aggregate), affine, and the Miller lines of the signature side evaluated at -g1.
-__global__ __launch_bounds__(64) void k_group_prep(GroupPrepArgs a) {
+__global__ KB_OCC(HB_OCC_PREP) void k_group_prep(GroupPrepArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
   const uint32_t lg = blockIdx.x * blockDim.x + threadIdx.x;
   if (lg >= a.ng) return;

@@ -1,8 +1,11 @@
-# GPU box: parity tests + bench (slot mode, no CPU baseline) + kernel-trace summary + staged bench.  $1 = tag
+# GPU box: one pytest selection + optional short C3 bench.  $1 = tag, $2 = pytest -k expr (or "all"), $3 = bench (1/0)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 TAG=${1:-q}
-timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/tests_$TAG.log 2>&1 &&
-timeout -k 10 300 python -u bench.py --cpu-seconds 0 --mode staged > gpurun_out/bench_staged_$TAG.json 2> gpurun_out/bench_staged_$TAG.err &&
-cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --cpu-seconds 0 > "$GRAFT_REPO_ROOT/gpurun_out/bench_$TAG.json" 2>&1
+K=${2:-all}
+if [ "$K" = "all" ]; then KARG=""; else KARG="-k $K"; fi
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread $KARG > gpurun_out/tests_$TAG.log 2>&1 &&
+if [ "${3:-1}" = "1" ]; then
+timeout -k 10 400 python -u bench.py --workload c3 --steps 3 --warmup 1 --cpu-seconds 0 --callers 0 > gpurun_out/bench_c3_$TAG.json 2> gpurun_out/bench_c3_$TAG.err
+fi

@@ -1,11 +1,17 @@
-"""Print one slot's kernel timeline from a rocprofv3 kernel trace: python tools/timeline.py <run_kernel_trace.csv>"""
+#!/usr/bin/env python3
+"""Print the kernel timeline of the last N slots of a rocprofv3 kernel trace (tools/gpu_trace.sh)."""
 import csv
 import sys
 
-rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
+rows = list(csv.DictReader(open(sys.argv[1])))
+rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+n = int(sys.argv[2]) if len(sys.argv) > 2 else 2
 idx = [i for i, r in enumerate(rows) if "k_hash_to_g2" in r["Kernel_Name"]]
-i0 = idx[-2]
-t0 = int(rows[i0]["Start_Timestamp"])
-for r in rows[i0:idx[-1]]:
-    s, e = int(r["Start_Timestamp"]) - t0, int(r["End_Timestamp"]) - t0
-    print(f"{r['Kernel_Name'][:28]:30s} q{r.get('Queue_Id', '?'):>3} start {s / 1e6:8.3f}  end {e / 1e6:8.3f}  dur {(e - s) / 1e6:7.3f}")
+sl = rows[idx[-n]:]
+t0 = int(sl[0]["Start_Timestamp"])
+for r in sl:
+    name = r["Kernel_Name"].split("(")[0].replace("hb::", "")
+    s = (int(r["Start_Timestamp"]) - t0) / 1e6
+    e = (int(r["End_Timestamp"]) - t0) / 1e6
+    if e - s > 0.05:
+        print("%-22s q%-3s %8.2f %8.2f %8.2f grid=%s" % (name[:22], r["Queue_Id"], s, e, e - s, r["Grid_Size_X"]))
