@@ -2,17 +2,20 @@
 """bench.py -- charon's BLS hot path on MI355X (BASELINE.json metric).
 
 One step = one attestation slot of BASELINE.json configs[2] ("C3", the largest single-GPU
-config): for V = 100 000 validators of a 10-operator threshold-7 cluster, each signing its own
-32-byte signing root,
-  1. hash the slot's 100 000 distinct signing roots to G2 (+ their Miller lines)
+config): for V = 100 000 validators of a 10-operator threshold-7 cluster, each attesting to its
+own AttestationData,
+  0. build the slot's 100 000 signing roots from the SSZ AttestationData on device
+     (eth2util/signing/signing.go:63-77 GetDataRoot; charon_amd/csrc/roots.hip)
+  1. hash them to G2 (+ their Miller lines)
   2. verify all V*n = 1 000 000 partial signatures            (tbls.Verify,
      /root/reference/tbls/herumi.go:288-304; callers core/parsigex/parsigex.go:93-98)
   3. threshold-aggregate every validator's first t = 7 partials  (tbls.ThresholdAggregate,
      herumi.go:249-286; caller core/sigagg/sigagg.go:105)
   4. verify every aggregate under the validator's DV public key (core/sigagg/sigagg.go:117).
-All of it is one hbls_slot_device call (include/hipbls.h).  Inputs (compressed pubshares, partial
-signatures, DV public keys, messages, share indices) are resident in HBM before the timed region;
-outputs are per-item status bytes and 96-byte aggregates in HBM.
+Steps 1-4 are one hbls_slot_device call (include/hipbls.h).  Inputs (compressed pubshares, partial
+signatures, DV public keys, AttestationData, share indices) are resident in HBM before the timed
+region; outputs are per-item status bytes and 96-byte aggregates in HBM.  Two consecutive slots
+are in flight (--inflight), each on its own stream with its own outputs.
 
 value = (verified partials + threshold aggregates) per second summed over all ranks; the
 post-aggregate verifications are extra work not counted in it.  Weak scaling: every rank owns
@@ -77,6 +80,27 @@ def _chk(L, rc):
         raise RuntimeError("hipbls: " + L.hbls_last_error().decode(errors="replace"))
 
 
+def attestation_data(roots, rank):
+    """One synthetic phase0.AttestationData per message, SSZ-encoded (128 B): slot, committee
+    index, beacon block root (the cluster's synthetic root), source and target checkpoints."""
+    out = np.zeros((len(roots), 128), dtype=np.uint8)
+    slot = 9_000_000 + rank
+    for i, r in enumerate(roots):
+        b = (slot.to_bytes(8, "little") + (i % 64).to_bytes(8, "little") + r +
+             (slot // 32 - 1).to_bytes(8, "little") + r[::-1] + (slot // 32).to_bytes(8, "little") + r[16:] + r[:16])
+        out[i] = np.frombuffer(b, dtype=np.uint8)
+    return out.reshape(-1)
+
+
+def attester_domain():
+    """compute_domain(DOMAIN_BEACON_ATTESTER, fork version, genesis validators root)
+    (eth2util/signing/signing.go:37-61 via the beacon node's Domain endpoint)."""
+    import hashlib
+    fork, gvr = bytes.fromhex("05000000"), hashlib.sha256(b"synthetic genesis").digest()
+    fork_data_root = hashlib.sha256(fork + bytes(28) + gvr).digest()
+    return np.frombuffer(bytes.fromhex("01000000") + fork_data_root[:28], dtype=np.uint8).copy()
+
+
 def setup_inputs(L, wl, V, rank):
     """Synthetic cluster -> host arrays; keys and signatures are derived on the GPU."""
     from charon_amd import synth
@@ -87,7 +111,12 @@ def setup_inputs(L, wl, V, rank):
     M = len(cl.msgs)
     msg_of_v = np.asarray(cl.msg_of_validator, dtype=np.uint32)
     midx = np.repeat(msg_of_v, n)
-    msgs = np.frombuffer(b"".join(cl.msgs), dtype=np.uint8).copy()
+    # the messages are attestation signing roots: M AttestationData (128-byte SSZ, fields from the
+    # cluster's synthetic roots) under the attester domain, rooted on the GPU (roots.hip)
+    att = attestation_data(cl.msgs, rank)
+    domain = attester_domain()
+    msgs = np.zeros(32 * M, dtype=np.uint8)
+    _chk(L, L.hbls_attestation_signing_roots(_p(att), M, _p(domain), 1, None, _p(msgs)))
     moff = (np.arange(M, dtype=np.uint64) * 32)
     mlen = np.full(M, 32, dtype=np.uint32)
     item_msgs = msgs.reshape(M, 32)[midx].reshape(-1).copy()
@@ -120,7 +149,7 @@ def setup_inputs(L, wl, V, rank):
     ta_idx = np.tile(np.arange(1, t + 1, dtype=np.int64), V)
     grp_off = (np.arange(V + 1, dtype=np.uint32) * t)
     vgrp_off = (np.arange(V + 1, dtype=np.uint32) * n)  # one verification group per validator
-    return dict(n=n, t=t, V=V, NP=NP, M=M, sks=sks, msgs=msgs, moff=moff, mlen=mlen, midx=midx, pks=pks, sigs=sigs,
+    return dict(n=n, t=t, V=V, NP=NP, M=M, sks=sks, att=att, domain=domain, msgs=msgs, moff=moff, mlen=mlen, midx=midx, pks=pks, sigs=sigs,
                 item_msgs=item_msgs, item_off=item_off, item_len=item_len, ta_sigs=ta_sigs, ta_src=ta_src,
                 ta_idx=ta_idx, grp_off=grp_off, vgrp_off=vgrp_off, root_sigs=root_sigs, dv_pks=dv_pks)
 
@@ -356,6 +385,7 @@ def main(argv=None):
         return torch.from_numpy(a).to(dev)
 
     d_msg, d_moff, d_mlen = up(d["msgs"]), up(d["moff"].view(np.int64)), up(d["mlen"].view(np.int32))
+    d_att, d_dom = up(d["att"]), up(d["domain"])
     d_midx, d_pk, d_sig = up(d["midx"].view(np.int32)), up(d["pks"]), up(d["sigs"])
     d_tsrc, d_tidx, d_goff = up(d["ta_src"].view(np.int32)), up(d["ta_idx"]), up(d["grp_off"].view(np.int32))
     d_vgoff, d_dvpk, d_tsig = up(d["vgrp_off"].view(np.int32)), up(d["dv_pks"]), up(d["ta_sigs"])
@@ -366,6 +396,7 @@ def main(argv=None):
              "tout": torch.zeros(V * 96, dtype=torch.uint8, device=dev),
              "tst": torch.full((V,), 255, dtype=torch.uint8, device=dev),
              "ast": torch.full((V,), 255, dtype=torch.uint8, device=dev),
+             "msg": torch.zeros(M * 32, dtype=torch.uint8, device=dev),
              "stream": torch.cuda.Stream(device=dev)} for _ in range(n_sets)]
     d_hm, d_vst, d_tout, d_tst, d_ast = (outs[0][k] for k in ("hm", "vst", "tout", "tst", "ast"))
 
@@ -391,7 +422,7 @@ def main(argv=None):
     for o in outs:
         o["sp"] = ctypes.c_void_p(o["stream"].cuda_stream)
         o["slot"] = _lib.HblsSlot(
-            msgs=_p(d_msg).value, msg_off=_p(d_moff).value, msg_len=_p(d_mlen).value, n_msgs=M, hm=_p(o["hm"]).value,
+            msgs=_p(o["msg"]).value, msg_off=_p(d_moff).value, msg_len=_p(d_mlen).value, n_msgs=M, hm=_p(o["hm"]).value,
             pks=_p(d_pk).value, sigs=_p(d_sig).value, msg_idx=_p(d_midx).value, n=NP, vgrp_off=_p(d_vgoff).value,
             n_vgroups=V, vstatus=_p(o["vst"]).value, ta_sigs=None, ta_src=_p(d_tsrc).value, ta_idx=_p(d_tidx).value,
             grp_off=_p(d_goff).value, n_groups=V, n_ta_partials=V * t, ta_out=_p(o["tout"]).value,
@@ -421,6 +452,8 @@ def main(argv=None):
         step_no[0] += 1
         st = o["stream"]
         ev[0].record(st)
+        # the slot's messages: attestation signing roots from the SSZ AttestationData (§8(f)3)
+        _chk(L, L.hbls_attestation_signing_roots_device(_p(d_att), M, _p(d_dom), 1, None, _p(o["msg"]), o["sp"]))
         _chk(L, L.hbls_slot_device(ctypes.byref(o["slot"]), o["sp"]))
         ev[1].record(st)
         if world > 1:

@@ -30,7 +30,8 @@ EXPORTS = (
     "hbls_verify_device", "hbls_threshold_aggregate_device", "hbls_verify_aggregate_device", "hbls_slot_device",
     "hbls_hm_entry_bytes", "hbls_sync",
     "hbls_timing", "hbls_timing_read", "hbls_comm_id_bytes", "hbls_comm_unique_id", "hbls_comm_init",
-    "hbls_allgather_device", "hbls_comm_destroy", "hbls_stats",
+    "hbls_allgather_device", "hbls_comm_destroy", "hbls_stats", "hbls_attestation_signing_roots",
+    "hbls_signing_roots", "hbls_attestation_signing_roots_device",
 )
 
 ALL_DEVICES = 0xFFFFFFFF
@@ -78,6 +79,9 @@ def _declare(lib):
         "hbls_verify_device": ([P, P, P, P, SZ, P, SZ, P, P], ctypes.c_int),
         "hbls_threshold_aggregate_device": ([P, P, P, SZ, SZ, P, P, P], ctypes.c_int),
         "hbls_verify_aggregate_device": ([P, P, SZ, P, P, P, P], ctypes.c_int),
+        "hbls_attestation_signing_roots": ([P, SZ, P, SZ, P, P], ctypes.c_int),
+        "hbls_signing_roots": ([P, SZ, P, SZ, P, P], ctypes.c_int),
+        "hbls_attestation_signing_roots_device": ([P, SZ, P, SZ, P, P, P], ctypes.c_int),
         "hbls_slot_device": ([ctypes.POINTER(HblsSlot), P], ctypes.c_int),
         "hbls_hm_entry_bytes": ([], SZ),
         "hbls_sync": ([P], ctypes.c_int),

@@ -1148,6 +1148,49 @@ int hbls_verify_aggregate_batch(const uint8_t* pks, const uint32_t* grp_off, con
   });
 }
 
+// Signing roots (roots.hip).  mode 0: data = 128-byte SSZ AttestationData; 1: data = 32-byte
+// object roots.  Host buffers; dom_idx nullable.
+static int roots_host(int mode, const uint8_t* data, size_t n, const uint8_t* domains, size_t n_domains,
+                      const uint32_t* dom_idx, uint8_t* roots) {
+  if (n_domains == 0) return set_err("signing roots: no domain");
+  if (dom_idx)
+    for (size_t i = 0; i < n; i++)
+      if (dom_idx[i] >= n_domains) return set_err("signing roots: domain index out of range");
+  const size_t item = mode == 0 ? 128 : 32;
+  return for_each_device(n, [&](Dev& d, size_t b, size_t e) -> int {
+    const size_t m = e - b;
+    uint8_t *dd, *ddom;
+    uint32_t* didx = nullptr;
+    if (upload(d, I_SIG, data + item * b, m * item, &dd) || upload(d, I_PK, domains, n_domains * 32, &ddom)) return -1;
+    if (dom_idx && upload(d, I_MIDX, dom_idx + b, m, &didx)) return -1;
+    void* out;
+    if (ensure_buf(d.io[I_OUT], m * 32, &out)) return -1;
+    if (mode == 0)
+      TIMED(d, "k_attestation_roots", d.stream,
+            launch_attestation_roots(dd, (uint32_t)m, ddom, (uint32_t)n_domains, didx, (uint8_t*)out, d.stream));
+    else
+      TIMED(d, "k_signing_roots", d.stream,
+            launch_signing_roots(dd, (uint32_t)m, ddom, (uint32_t)n_domains, didx, (uint8_t*)out, d.stream));
+    HCHK(hipMemcpyAsync(roots + 32 * b, out, m * 32, hipMemcpyDeviceToHost, d.stream));
+    HCHK(hipStreamSynchronize(d.stream));
+    return 0;
+  });
+}
+
+int hbls_attestation_signing_roots(const uint8_t* data, size_t n, const uint8_t* domains, size_t n_domains,
+                                   const uint32_t* dom_idx, uint8_t* roots) {
+  if (ensure_init()) return -1;
+  if (n == 0) return 0;
+  return roots_host(0, data, n, domains, n_domains, dom_idx, roots);
+}
+
+int hbls_signing_roots(const uint8_t* object_roots, size_t n, const uint8_t* domains, size_t n_domains,
+                       const uint32_t* dom_idx, uint8_t* roots) {
+  if (ensure_init()) return -1;
+  if (n == 0) return 0;
+  return roots_host(1, object_roots, n, domains, n_domains, dom_idx, roots);
+}
+
 int hbls_sign_batch(const uint8_t* sks, const uint8_t* msgs, const uint64_t* msg_off, const uint32_t* msg_len,
                     size_t n, uint8_t* sigs, uint8_t* status) {
   if (ensure_init()) return -1;
@@ -1254,6 +1297,20 @@ int hbls_verify_device(const uint8_t* pks, const uint8_t* sigs, const uint32_t* 
                       nullptr))
     return -1;
   return ws_release(w, s);
+}
+
+int hbls_attestation_signing_roots_device(const uint8_t* data, size_t n, const uint8_t* domains, size_t n_domains,
+                                          const uint32_t* dom_idx, uint8_t* roots, void* stream) {
+  Dev* d;
+  hipStream_t s = (hipStream_t)stream;
+  if (dev_of_stream(s, &d)) return -1;
+  if (n == 0) return 0;
+  if (n_domains == 0) return set_err("signing roots: no domain");
+  if (n > 0xffffffffull) return set_err("signing roots: too many items");
+  std::lock_guard<std::mutex> lk(d->mu);
+  TIMED(*d, "k_attestation_roots", s,
+        launch_attestation_roots(data, (uint32_t)n, domains, (uint32_t)n_domains, dom_idx, roots, s));
+  return 0;
 }
 
 int hbls_verify_aggregate_device(const uint8_t* pks, const uint32_t* grp_off, size_t n_groups, const uint8_t* sigs,

@@ -186,6 +186,12 @@ void launch_scatter(const ScatterArgs& a, hipStream_t s);
 void launch_fb_lines(const uint32_t* list, const uint32_t* count, uint32_t base, uint32_t cap, const HmEntry* sig,
                      const HmEntry* agg_sig, uint32_t n_items, LineEntry* lines, hipStream_t s);
 
+// Signing roots (roots.hip): SSZ AttestationData -> GetDataRoot, and SigningData of object roots.
+void launch_attestation_roots(const uint8_t* data, uint32_t n, const uint8_t* domains, uint32_t n_domains,
+                              const uint32_t* dom_idx, uint8_t* roots, hipStream_t s);
+void launch_signing_roots(const uint8_t* obj, uint32_t n, const uint8_t* domains, uint32_t n_domains,
+                          const uint32_t* dom_idx, uint8_t* roots, hipStream_t s);
+
 // FastAggregateVerify at scale (vbatch.hip): segmented G1 reduction, then the pairing kernel.
 void launch_seg_sum(bool affine, const void* pts, const uint8_t* st_in, const uint32_t* seg_off, uint32_t n_seg,
                     G1JEntry* out, uint8_t* st_out, hipStream_t s);

@@ -1,0 +1,123 @@
+// roots.hip: the 32-byte signing roots of a slot's attestations, on device.
+//
+// charon builds every message it verifies as GetDataRoot(domain, object root)
+// (eth2util/signing/signing.go:63-77: SSZ SigningData{object_root, domain}); for attestations the
+// object root is phase0.AttestationData.HashTreeRoot (core/signeddata.go Attestation.MessageRoot,
+// consensus-specs AttestationData{slot, index, beacon_block_root, source, target}).  Here one lane
+// takes one AttestationData in its 128-byte SSZ encoding and writes its signing root, so the
+// messages of a slot go from the wire format to hash-to-G2 without a host round trip.
+//
+// Merkleisation of the 5-field container (8 leaves, 3 zero):
+//   c0 = slot, c1 = index, c2 = beacon_block_root, c3 = H(src.epoch, src.root), c4 = H(tgt...)
+//   root = H(H(H(c0, c1), H(c2, c3)), H(H(c4, 0), Z1))      Z1 = H(0, 0)
+//   signing root = H(root, domain)
+// H(l, r) = SHA-256 of the 64 bytes l || r: two compressions (data block + the constant padding
+// block).  8 H per attestation, i.e. 16 SHA-256 compressions: integer VALU work, negligible next
+// to the pairing path (k_attestation_roots in DESIGN.md §4).
+#include "layout.h"
+#include "sha256.h"
+
+namespace hb {
+
+// a 32-byte chunk as 8 big-endian words (the SHA-256 message word order)
+struct Chunk {
+  uint32_t w[8];
+};
+
+__device__ __forceinline__ Chunk chunk_load(const uint8_t* p) {
+  Chunk c;
+  HB_UNROLL for (int i = 0; i < 8; i++)
+    c.w[i] = ((uint32_t)p[4 * i] << 24) | ((uint32_t)p[4 * i + 1] << 16) | ((uint32_t)p[4 * i + 2] << 8) |
+             (uint32_t)p[4 * i + 3];
+  return c;
+}
+
+// uint64 little-endian in the first 8 bytes of a chunk, zero padded
+__device__ __forceinline__ Chunk chunk_u64(const uint8_t* p) {
+  Chunk c;
+  HB_UNROLL for (int i = 0; i < 8; i++) c.w[i] = 0;
+  c.w[0] = ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | (uint32_t)p[3];
+  c.w[1] = ((uint32_t)p[4] << 24) | ((uint32_t)p[5] << 16) | ((uint32_t)p[6] << 8) | (uint32_t)p[7];
+  return c;
+}
+
+__device__ __forceinline__ Chunk chunk_zero() {
+  Chunk c;
+  HB_UNROLL for (int i = 0; i < 8; i++) c.w[i] = 0;
+  return c;
+}
+
+// H(l || r): SHA-256 of one 64-byte message
+__device__ __forceinline__ Chunk h2(const Chunk& l, const Chunk& r) {
+  uint32_t blk[16];
+  HB_UNROLL for (int i = 0; i < 8; i++) {
+    blk[i] = l.w[i];
+    blk[8 + i] = r.w[i];
+  }
+  Sha256State st = sha256_init();
+  sha256_compress(st, blk);
+  HB_UNROLL for (int i = 0; i < 16; i++) blk[i] = 0;
+  blk[0] = 0x80000000u;
+  blk[15] = 512;  // message length in bits
+  sha256_compress(st, blk);
+  Chunk o;
+  HB_UNROLL for (int i = 0; i < 8; i++) o.w[i] = st.h[i];
+  return o;
+}
+
+__device__ __forceinline__ void chunk_store(uint8_t* p, const Chunk& c) {
+  HB_UNROLL for (int i = 0; i < 8; i++) {
+    p[4 * i] = (uint8_t)(c.w[i] >> 24);
+    p[4 * i + 1] = (uint8_t)(c.w[i] >> 16);
+    p[4 * i + 2] = (uint8_t)(c.w[i] >> 8);
+    p[4 * i + 3] = (uint8_t)c.w[i];
+  }
+}
+
+// One lane per attestation: data[i] (128 B SSZ) -> roots[i] = GetDataRoot(domains[dom_idx[i]], HTR)
+__global__ __launch_bounds__(64) void k_attestation_roots(const uint8_t* __restrict__ data, uint32_t n,
+                                                         const uint8_t* __restrict__ domains, uint32_t n_domains,
+                                                         const uint32_t* __restrict__ dom_idx,
+                                                         uint8_t* __restrict__ roots) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint8_t* a = data + 128ull * i;
+  const Chunk z = chunk_zero();
+  const Chunk src = h2(chunk_u64(a + 48), chunk_load(a + 56));
+  const Chunk tgt = h2(chunk_u64(a + 88), chunk_load(a + 96));
+  const Chunk n01 = h2(chunk_u64(a + 0), chunk_u64(a + 8));
+  const Chunk n23 = h2(chunk_load(a + 16), src);
+  const Chunk n45 = h2(tgt, z);
+  const Chunk n67 = h2(z, z);
+  const Chunk root = h2(h2(n01, n23), h2(n45, n67));
+  uint32_t d = dom_idx ? dom_idx[i] : 0u;
+  if (d >= n_domains) d = 0;  // validated on the host for host-buffer calls
+  chunk_store(roots + 32ull * i, h2(root, chunk_load(domains + 32ull * d)));
+}
+
+// One lane per object root: roots[i] = SigningData{object_roots[i], domains[dom_idx[i]]}.HTR
+__global__ __launch_bounds__(64) void k_signing_roots(const uint8_t* __restrict__ obj, uint32_t n,
+                                                     const uint8_t* __restrict__ domains, uint32_t n_domains,
+                                                     const uint32_t* __restrict__ dom_idx,
+                                                     uint8_t* __restrict__ roots) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t d = dom_idx ? dom_idx[i] : 0u;
+  if (d >= n_domains) d = 0;
+  chunk_store(roots + 32ull * i, h2(chunk_load(obj + 32ull * i), chunk_load(domains + 32ull * d)));
+}
+
+void launch_attestation_roots(const uint8_t* data, uint32_t n, const uint8_t* domains, uint32_t n_domains,
+                              const uint32_t* dom_idx, uint8_t* roots, hipStream_t s) {
+  if (n)
+    hipLaunchKernelGGL(k_attestation_roots, dim3((n + 63) / 64), dim3(64), 0, s, data, n, domains, n_domains,
+                       dom_idx, roots);
+}
+void launch_signing_roots(const uint8_t* obj, uint32_t n, const uint8_t* domains, uint32_t n_domains,
+                          const uint32_t* dom_idx, uint8_t* roots, hipStream_t s) {
+  if (n)
+    hipLaunchKernelGGL(k_signing_roots, dim3((n + 63) / 64), dim3(64), 0, s, obj, n, domains, n_domains, dom_idx,
+                       roots);
+}
+
+}  // namespace hb

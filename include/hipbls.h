@@ -87,6 +87,18 @@ int hbls_verify_aggregate_batch(const uint8_t* pks, const uint32_t* grp_off, con
                                 const uint8_t* msgs, const uint64_t* msg_off, const uint32_t* msg_len,
                                 size_t n_groups, uint8_t* status);
 
+/* Signing roots (eth2util/signing/signing.go:63-77 GetDataRoot = SSZ SigningData{object_root,
+ * domain}.HashTreeRoot), the 32-byte messages every verification hashes to G2.
+ *   attestation: data[i] is the 128-byte SSZ encoding of a phase0.AttestationData (object root =
+ *                its hash-tree-root, core/signeddata.go Attestation.MessageRoot);
+ *   generic:     object_roots[i] is a 32-byte object root computed by the caller.
+ * domains: n_domains 32-byte domains (signing.GetDomain); item i uses domains[dom_idx[i]]
+ * (dom_idx NULL: domain 0).  roots: n x 32 bytes. */
+int hbls_attestation_signing_roots(const uint8_t* data, size_t n, const uint8_t* domains, size_t n_domains,
+                                   const uint32_t* dom_idx, uint8_t* roots);
+int hbls_signing_roots(const uint8_t* object_roots, size_t n, const uint8_t* domains, size_t n_domains,
+                       const uint32_t* dom_idx, uint8_t* roots);
+
 /* Sign (herumi.go:306-316) and SecretToPublicKey (herumi.go:66-79), batched.
  * Sign status in {OK, BAD_SECRET}; SecretToPublicKey additionally rejects the zero key. */
 int hbls_sign_batch(const uint8_t* sks, const uint8_t* msgs, const uint64_t* msg_off,
@@ -120,6 +132,12 @@ int hbls_verify_device(const uint8_t* pks, const uint8_t* sigs, const uint32_t* 
 int hbls_threshold_aggregate_device(const uint8_t* sigs, const int64_t* idx, const uint32_t* grp_off,
                                     size_t n_groups, size_t n_partials, uint8_t* out, uint8_t* status,
                                     void* stream);
+
+/* Attestation signing roots on device buffers (see hbls_attestation_signing_roots); dom_idx
+ * entries must be < n_domains (out-of-range entries use domain 0).  Writes the messages a slot
+ * then hashes (hbls_hash_to_g2_device / hbls_slot_device msgs). */
+int hbls_attestation_signing_roots_device(const uint8_t* data, size_t n, const uint8_t* domains, size_t n_domains,
+                                          const uint32_t* dom_idx, uint8_t* roots, void* stream);
 
 /* VerifyAggregate on device buffers: pks (48 B each), sigs (96 B per group), hm (one hashed message
  * per group, hbls_hash_to_g2_device), status (n_groups) are device pointers; grp_off is a HOST

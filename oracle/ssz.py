@@ -69,3 +69,32 @@ def deposit_message_root(pubkey: bytes, withdrawal_credentials: bytes, amount: i
 
 DOMAIN_APPLICATION_BUILDER = bytes.fromhex("00000001")
 DOMAIN_DEPOSIT = bytes.fromhex("03000000")
+
+
+# ---- attestations (the slot's hot message): core/signeddata.go Attestation.MessageRoot ->
+# phase0.AttestationData.HashTreeRoot (go-eth2-client's generated SSZ, consensus-specs container
+# AttestationData{slot, index, beacon_block_root, source: Checkpoint, target: Checkpoint}).
+DOMAIN_BEACON_ATTESTER = bytes.fromhex("01000000")
+ATTESTATION_DATA_SSZ_LEN = 128
+
+
+def checkpoint_root(epoch: int, root: bytes) -> bytes:
+    return merkleize([htr_uint64(epoch), root])
+
+
+def parse_attestation_data(b: bytes):
+    """SSZ bytes (fixed layout, 128 B) -> (slot, index, beacon_block_root, (src_epoch, src_root),
+    (tgt_epoch, tgt_root))."""
+    assert len(b) == ATTESTATION_DATA_SSZ_LEN
+    u = lambda o: int.from_bytes(b[o:o + 8], "little")  # noqa: E731
+    return u(0), u(8), b[16:48], (u(48), b[56:88]), (u(88), b[96:128])
+
+
+def attestation_data_root(b: bytes) -> bytes:
+    slot, index, bbr, (se, sr), (te, tr) = parse_attestation_data(b)
+    return merkleize([htr_uint64(slot), htr_uint64(index), bbr, checkpoint_root(se, sr), checkpoint_root(te, tr)])
+
+
+def attestation_signing_root(b: bytes, domain: bytes) -> bytes:
+    """GetDataRoot (signing.go:63-77) of an attestation: SigningData{HTR(data), domain}."""
+    return signing_root(attestation_data_root(b), domain)

@@ -9,6 +9,10 @@ Sources:
   * eth2util/signing/signing_test.go:24-74  (teku-produced registration; sk, pk, sig, domain)
   * eth2util/deposit/deposit_test.go:215-259 + testdata/TestMarshalDepositData.golden
   * cluster/examples/cluster-lock-00{0..3}.json  (cluster/cluster_test.go:242-260 TestExamples)
+  * core/testdata/TestSSZSerialisation_AttestationData.ssz.golden + the .json.golden of the same
+    value (core/ssz_test.go): the SSZ bytes of one phase0.AttestationData, cross-checked field by
+    field against the JSON; its hash-tree-root is re-derived with oracle/ssz.py (no reference
+    file states one)
 """
 
 from __future__ import annotations
@@ -103,8 +107,23 @@ def lock_kats():
     return out
 
 
+def attestation_data_kat():
+    raw = open(os.path.join(REF, "core/testdata/TestSSZSerialisation_AttestationData.ssz.golden"), "rb").read()
+    js = json.load(open(os.path.join(REF, "core/testdata/TestJSONSerialisation_AttestationData.json.golden")))
+    ad = js["attestation_data"]
+    off = int.from_bytes(raw[0:4], "little")  # core.AttestationData{Data, Duty}: offset of Data
+    data = raw[off:off + ssz.ATTESTATION_DATA_SSZ_LEN]
+    slot, index, bbr, (se, sr), (te, tr) = ssz.parse_attestation_data(data)
+    assert (slot, index) == (int(ad["slot"]), int(ad["index"]))
+    assert bbr == _b(ad["beacon_block_root"])
+    assert (se, sr) == (int(ad["source"]["epoch"]), _b(ad["source"]["root"]))
+    assert (te, tr) == (int(ad["target"]["epoch"]), _b(ad["target"]["root"]))
+    return {"ssz": data.hex(), "htr_oracle": ssz.attestation_data_root(data).hex()}
+
+
 def main():
-    kats = {"registration": registration_kat(), "deposit": deposit_kats(), "locks": lock_kats()}
+    kats = {"registration": registration_kat(), "deposit": deposit_kats(), "locks": lock_kats(),
+            "attestation_data": attestation_data_kat()}
     with open(os.path.join(HERE, "kat_reference.json"), "w") as f:
         json.dump(kats, f, indent=1)
     print("wrote", os.path.join(HERE, "kat_reference.json"))
