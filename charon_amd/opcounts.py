@@ -22,9 +22,9 @@ PEAK_MAD_TOPS_NOMINAL = 39.3
 # hc_count_blocks, in its order
 BLOCK_NAMES = ("f12_sqr", "f12_mul_line", "final_exp", "fp_inv", "g1_dec", "g2_dec", "rlc_g1", "rlc_g2",
                "jac_add_g1", "jac_add_g2", "to_aff_g1", "to_aff_g2", "lines_eval", "lines_uneval", "jac_dbl_g2",
-               "jac_add_aff_g2", "cyclo_sqr", "f12_mul", "g2_compress")
+               "jac_add_aff_g2", "cyclo_sqr", "f12_mul", "g2_compress", "jac_add_aff_g1")
 BLOCKS = dict(zip(BLOCK_NAMES, (36, 39, 8288, 610, 1665, 2486, 732, 1880, 16, 43, 614, 625, 1843, 1571, 16, 29, 18,
-                                54, 4)))
+                                54, 4, 11)))
 
 N_LINES = 68      # Miller-loop lines (63 doublings + 5 additions)
 N_SQR = 62        # Fp12 squarings of the Miller loop
@@ -69,6 +69,11 @@ def per_unit(b=BLOCKS, group_size=1, t=1):
         "k_group_sum": (gsum,) * 2,
         "k_hash_to_g2": (HASH_TO_G2,) * 2,
         "k_lines_msg": (b["lines_uneval"],) * 2,
+        # VerifyAggregate at scale (vbatch.hip): per key one mixed addition in pass 1 (later passes
+        # add 1/32 as many Jacobian partials), per group the affine sum and the signature's lines
+        "k_seg_sum": (b["jac_add_aff_g1"],) * 2,
+        "k_va_point": (b["to_aff_g1"],) * 2,
+        "k_sig_lines": (b["lines_eval"],) * 2,
     }
     return out
 
@@ -76,7 +81,11 @@ def per_unit(b=BLOCKS, group_size=1, t=1):
 UNITS = {"k_pair3": "pairing check", "k_pair3_fallback": "pairing check", "k_dec_pk": "public key",
          "k_dec_sig_pt": "signature", "k_rlc": "partial", "k_group_prep": "verification group",
          "k_fb_lines": "partial", "k_ta_straus": "aggregation member", "k_group_sum": "aggregation group",
-         "k_hash_to_g2": "message", "k_lines_msg": "message"}
+         "k_hash_to_g2": "message", "k_lines_msg": "message", "k_seg_sum": "public key (pass 1)",
+         "k_va_point": "aggregation group", "k_sig_lines": "signature"}
+
+# SHA-256 compressions per attestation signing root (roots.hip: 8 two-block hashes)
+SHA256_PER_ATTESTATION_ROOT = 16
 
 # The herumi-equivalent per-item work of r01 (frozen): one Verify = G1 + G2 decompression with
 # subgroup checks + a 2-pair Miller loop with line construction + final exponentiation, counted
