@@ -200,6 +200,105 @@ HD void fp_sqr_core(uint32_t* out, const uint32_t* aw) {
   fp_join28(out, r);
 }
 
+// Fp2 products without intermediate reductions (xi = -1 + ... tower: u^2 = -1):
+//   real = (a0 b0 - a1 b1) / R   imag = (a0 b1 + a1 b0) / R
+// one product-scanning pass per output coefficient, both in the same column loop (two independent
+// multiply-add chains).  The real part's negative terms are signed multiply-adds against negated
+// limbs (two's complement in the same 64-bit accumulator, arithmetic carry shifts); its result lies
+// in (-p, 2p) and is moved to [0, 2p) by one conditional addition of p.  Same multiply-add count as
+// three Montgomery products (Karatsuba) but no Fp additions/subtractions around them, two operand
+// splits fewer and one output conversion fewer.
+#define HB_MONT28_TAIL_S(acc, m, k, r)                                                   \
+  if ((k) < 14) {                                                                       \
+    m[(k)] = ((uint32_t)(acc) * HB_P_N0_28) & 0x0FFFFFFFu;                               \
+    acc += (uint64_t)m[(k)] * P28[0];                                                    \
+  } else {                                                                              \
+    r[(k) - 14] = (uint32_t)(acc) & 0x0FFFFFFFu;                                          \
+  }                                                                                     \
+  acc = (uint64_t)((int64_t)(acc) >> 28);
+
+HD void fp2_fix_neg(uint32_t* out, const uint32_t* r, bool neg) {  // r (mod 2^384) + p if neg
+  uint32_t w[12], s[12];
+  fp_join28(w, r);
+  unsigned c = 0;
+  HB_UNROLL for (int i = 0; i < 12; i++) {
+    uint64_t t = (uint64_t)w[i] + P_RAW[i] + c;
+    s[i] = (uint32_t)t;
+    c = (unsigned)(t >> 32);
+  }
+  HB_UNROLL for (int i = 0; i < 12; i++) out[i] = neg ? s[i] : w[i];
+}
+
+HD void fp2_mul_core(uint32_t* o0, uint32_t* o1, const uint32_t* a0w, const uint32_t* a1w, const uint32_t* b0w,
+                     const uint32_t* b1w) {
+  uint32_t a0[14], a1[14], b0[14], b1[14], m0[14], m1[14], r0[14], r1[14];
+  int32_t na1[14];
+  fp_split28(a0, a0w);
+  fp_split28(a1, a1w);
+  fp_split28(b0, b0w);
+  fp_split28(b1, b1w);
+  HB_UNROLL for (int j = 0; j < 14; j++) na1[j] = -(int32_t)a1[j];
+  uint64_t ar = 0, ai = 0;
+  HB_UNROLL for (int k = 0; k < 27; k++) {
+    const int lo = k < 14 ? 0 : k - 13, hi = k < 14 ? k : 13;
+    HB_UNROLL for (int j = lo; j <= hi; j++) {
+      ar += (uint64_t)a0[j] * b0[k - j];
+      ar += (uint64_t)((int64_t)na1[j] * (int64_t)(int32_t)b1[k - j]);
+      ai += (uint64_t)a0[j] * b1[k - j];
+      ai += (uint64_t)a1[j] * b0[k - j];
+    }
+    HB_UNROLL for (int j = lo; j <= hi; j++)
+      if (j < k || k >= 14) {
+        ar += (uint64_t)m0[j] * P28[k - j];
+        ai += (uint64_t)m1[j] * P28[k - j];
+      }
+    HB_MONT28_TAIL_S(ar, m0, k, r0)
+    HB_MONT28_TAIL(ai, m1, k, r1)
+  }
+  r0[13] = (uint32_t)ar;
+  r1[13] = (uint32_t)ai;
+  fp2_fix_neg(o0, r0, (int64_t)ar < 0);
+  fp_join28(o1, r1);
+}
+
+// (a0 + a1 u)^2 = (a0^2 - a1^2) + 2 a0 a1 u, squares with the doubled-limb cross products
+HD void fp2_sqr_core(uint32_t* o0, uint32_t* o1, const uint32_t* a0w, const uint32_t* a1w) {
+  uint32_t a0[14], a1[14], d0[14], m0[14], m1[14], r0[14], r1[14];
+  int32_t na1[14], nd1[14];
+  fp_split28(a0, a0w);
+  fp_split28(a1, a1w);
+  HB_UNROLL for (int j = 0; j < 14; j++) {
+    d0[j] = a0[j] << 1;
+    na1[j] = -(int32_t)a1[j];
+    nd1[j] = -(int32_t)(a1[j] << 1);
+  }
+  uint64_t ar = 0, ai = 0;
+  HB_UNROLL for (int k = 0; k < 27; k++) {
+    const int lo = k < 14 ? 0 : k - 13, hi = k < 14 ? k : 13;
+    HB_UNROLL for (int j = lo; j <= hi; j++) {
+      if (2 * j < k) {
+        ar += (uint64_t)d0[j] * a0[k - j];
+        ar += (uint64_t)((int64_t)nd1[j] * (int64_t)(int32_t)a1[k - j]);
+      } else if (2 * j == k) {
+        ar += (uint64_t)a0[j] * a0[j];
+        ar += (uint64_t)((int64_t)na1[j] * (int64_t)(int32_t)a1[j]);
+      }
+      ai += (uint64_t)d0[j] * a1[k - j];
+    }
+    HB_UNROLL for (int j = lo; j <= hi; j++)
+      if (j < k || k >= 14) {
+        ar += (uint64_t)m0[j] * P28[k - j];
+        ai += (uint64_t)m1[j] * P28[k - j];
+      }
+    HB_MONT28_TAIL_S(ar, m0, k, r0)
+    HB_MONT28_TAIL(ai, m1, k, r1)
+  }
+  r0[13] = (uint32_t)ar;
+  r1[13] = (uint32_t)ai;
+  fp2_fix_neg(o0, r0, (int64_t)ar < 0);
+  fp_join28(o1, r1);
+}
+
 #if defined(__HIP_DEVICE_COMPILE__)
 // Device: one out-of-line copy per code object (standard calling convention: the operands travel
 // in VGPRs as 12-wide vectors; struct arguments would go through scratch).  Everything around it
@@ -224,6 +323,63 @@ __device__ __noinline__ static u32x12 fp_sqr_leaf(u32x12 a) {
   HB_UNROLL for (int i = 0; i < 12; i++) o[i] = r[i];
   return o;
 }
+typedef uint32_t u32x24 __attribute__((ext_vector_type(24)));
+__device__ __noinline__ static u32x24 fp2_mul_leaf(u32x24 a, u32x24 b) {
+  uint32_t x0[12], x1[12], y0[12], y1[12], r0[12], r1[12];
+  HB_UNROLL for (int i = 0; i < 12; i++) {
+    x0[i] = a[i];
+    x1[i] = a[12 + i];
+    y0[i] = b[i];
+    y1[i] = b[12 + i];
+  }
+  fp2_mul_core(r0, r1, x0, x1, y0, y1);
+  u32x24 o;
+  HB_UNROLL for (int i = 0; i < 12; i++) {
+    o[i] = r0[i];
+    o[12 + i] = r1[i];
+  }
+  return o;
+}
+__device__ __noinline__ static u32x24 fp2_sqr_leaf(u32x24 a) {
+  uint32_t x0[12], x1[12], r0[12], r1[12];
+  HB_UNROLL for (int i = 0; i < 12; i++) {
+    x0[i] = a[i];
+    x1[i] = a[12 + i];
+  }
+  fp2_sqr_core(r0, r1, x0, x1);
+  u32x24 o;
+  HB_UNROLL for (int i = 0; i < 12; i++) {
+    o[i] = r0[i];
+    o[12 + i] = r1[i];
+  }
+  return o;
+}
+HD void fp2_mul_pair(Fp& r0, Fp& r1, const Fp& a0, const Fp& a1, const Fp& b0, const Fp& b1) {
+  u32x24 av, bv;
+  HB_UNROLL for (int i = 0; i < NL; i++) {
+    av[i] = a0.v[i];
+    av[12 + i] = a1.v[i];
+    bv[i] = b0.v[i];
+    bv[12 + i] = b1.v[i];
+  }
+  u32x24 rv = fp2_mul_leaf(av, bv);
+  HB_UNROLL for (int i = 0; i < NL; i++) {
+    r0.v[i] = rv[i];
+    r1.v[i] = rv[12 + i];
+  }
+}
+HD void fp2_sqr_pair(Fp& r0, Fp& r1, const Fp& a0, const Fp& a1) {
+  u32x24 av;
+  HB_UNROLL for (int i = 0; i < NL; i++) {
+    av[i] = a0.v[i];
+    av[12 + i] = a1.v[i];
+  }
+  u32x24 rv = fp2_sqr_leaf(av);
+  HB_UNROLL for (int i = 0; i < NL; i++) {
+    r0.v[i] = rv[i];
+    r1.v[i] = rv[12 + i];
+  }
+}
 HD Fp fp_mul(const Fp& a, const Fp& b) {
   HB_COUNT_FP_MUL();
   u32x12 av, bv;
@@ -246,6 +402,10 @@ HD Fp fp_sqr(const Fp& a) {
   return r;
 }
 #else
+HD void fp2_mul_pair(Fp& r0, Fp& r1, const Fp& a0, const Fp& a1, const Fp& b0, const Fp& b1) {
+  fp2_mul_core(r0.v, r1.v, a0.v, a1.v, b0.v, b1.v);
+}
+HD void fp2_sqr_pair(Fp& r0, Fp& r1, const Fp& a0, const Fp& a1) { fp2_sqr_core(r0.v, r1.v, a0.v, a1.v); }
 HD Fp fp_mul(const Fp& a, const Fp& b) {
   HB_COUNT_FP_MUL();
   Fp r;

@@ -71,6 +71,30 @@ HD Fp2 f2_neg(const Fp2& a) { return f2_sub(f2_zero(), a); }
 HD Fp2 f2_dbl(const Fp2& a) { return f2_add(a, a); }
 HD Fp2 f2_conj(const Fp2& a) { return {a.c0, fp_neg(a.c1)}; }
 
+// Fp2 product and square as single lazily reduced passes (fp.h fp2_mul_core / fp2_sqr_core), or
+// (HB_F2_LAZY=0) as Karatsuba / complex squaring over Fp products.  Counted as 3 and 2 Fp products
+// either way, the unit of the op counts (charon_amd/opcounts.py).
+#ifndef HB_F2_LAZY
+#define HB_F2_LAZY 1
+#endif
+#if HB_F2_LAZY
+HD Fp2 f2_mul(const Fp2& a, const Fp2& b) {
+  HB_COUNT_FP_MUL();
+  HB_COUNT_FP_MUL();
+  HB_COUNT_FP_MUL();
+  Fp2 r;
+  fp2_mul_pair(r.c0, r.c1, a.c0, a.c1, b.c0, b.c1);
+  return r;
+}
+
+HD Fp2 f2_sqr(const Fp2& a) {
+  HB_COUNT_FP_MUL();
+  HB_COUNT_FP_MUL();
+  Fp2 r;
+  fp2_sqr_pair(r.c0, r.c1, a.c0, a.c1);
+  return r;
+}
+#else
 HD Fp2 f2_mul(const Fp2& a, const Fp2& b) {
   Fp t0 = fp_mul(a.c0, b.c0);
   Fp t1 = fp_mul(a.c1, b.c1);
@@ -83,6 +107,7 @@ HD Fp2 f2_sqr(const Fp2& a) {
   Fp t1 = fp_mul(a.c0, a.c1);
   return {t0, fp_dbl(t1)};
 }
+#endif
 
 HD Fp2 f2_mul_fp(const Fp2& a, const Fp& b) { return {fp_mul(a.c0, b), fp_mul(a.c1, b)}; }
 
