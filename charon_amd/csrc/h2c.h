@@ -144,7 +144,7 @@ HDNI void sswu_map(Fp2& x, Fp2& y, const Fp2& u) {
   Fp2 x2 = f2_mul(zu2, x1);
   Fp2 gx2 = f2_add(f2_mul(f2_add(f2_sqr(x2), A), x2), B);
   Fp n1 = fp_add(fp_sqr(gx1.c0), fp_sqr(gx1.c1));
-  Fp s1 = fp_pow_const(n1, EXP_SQRT, 379);
+  Fp s1 = fp_pow_win(n1, WIN_SQRT, WIN_SQRT_N);
   const bool sq1 = fp_eq(fp_sqr(s1), n1);
   Fp nu = fp_add(fp_sqr(u.c0), fp_sqr(u.c1));
   Fp s2 = fp_mul(fp_mul(s1, fp_mul(fp_sqr(nu), nu)), fp_from_const(SSWU_SQRT_MNZ3));
@@ -154,7 +154,7 @@ HDNI void sswu_map(Fp2& x, Fp2& y, const Fp2& u) {
   Fp inv2 = fp_from_const(FP_INV2);
   Fp c = fp_mul(fp_add(a.c0, s), inv2);
   if (fp_is_zero(c)) c = fp_mul(fp_sub(a.c0, s), inv2);
-  Fp t = fp_pow_const(c, EXP_P_M3_4, 378);
+  Fp t = fp_pow_win(c, WIN_P_M3_4, WIN_P_M3_4_N);
   Fp y0 = fp_mul(c, t);
   Fp h = fp_mul(fp_mul(a.c1, t), inv2);
   if (fp_eq(fp_sqr(y0), c)) {

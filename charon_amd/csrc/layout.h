@@ -14,7 +14,7 @@
 #define HB_OCC_LINES 1
 #endif
 #ifndef HB_OCC_DECPK
-#define HB_OCC_DECPK 1
+#define HB_OCC_DECPK 2
 #endif
 #ifndef HB_OCC_DECSIG
 #define HB_OCC_DECSIG 2

@@ -144,7 +144,7 @@ HDNI bool f2_sqrt(Fp2& x, const Fp2& a) {
   Fp inv2 = fp_from_const(FP_INV2);
   Fp c = fp_mul(fp_add(a.c0, s), inv2);
   if (fp_is_zero(c)) c = fp_mul(fp_sub(a.c0, s), inv2);
-  Fp t = fp_pow_const(c, EXP_P_M3_4, 378);
+  Fp t = fp_pow_win(c, WIN_P_M3_4, WIN_P_M3_4_N);
   Fp y = fp_mul(c, t);
   Fp h = fp_mul(fp_mul(a.c1, t), inv2);
   if (fp_eq(fp_sqr(y), c)) {
