@@ -277,6 +277,7 @@ struct Dev {
   bool dec_valid = false;
   // timing (hbls_timing)
   bool timing = false;
+  bool serial = false;  // timing mode 2: every timed launch completes before the next is enqueued
   std::vector<Timed> tev;
   size_t tev_used = 0;
 };
@@ -340,8 +341,11 @@ int timed_begin(Dev& d, const char* name, hipStream_t s, Timed** t) {
   *t = &x;
   return 0;
 }
-int timed_end(Timed* t, hipStream_t s) {
-  if (t) HCHK(hipEventRecord(t->b, s));
+int timed_end(Dev& d, Timed* t, hipStream_t s) {
+  if (t) {
+    HCHK(hipEventRecord(t->b, s));
+    if (d.serial) HCHK(hipEventSynchronize(t->b));  // the kernel ran alone on the device
+  }
   return 0;
 }
 #define TIMED(dev, name, s, call)                  \
@@ -350,7 +354,7 @@ int timed_end(Timed* t, hipStream_t s) {
     if (timed_begin((dev), (name), (s), &_t)) return -1; \
     call;                                          \
     HCHK(hipGetLastError());                       \
-    if (timed_end(_t, (s))) return -1;             \
+    if (timed_end((dev), _t, (s))) return -1;      \
   } while (0)
 
 int dev_create(int ord, Dev** out) {
@@ -1386,6 +1390,7 @@ int hbls_timing(int enable) {
   for (Dev* d : g_devs) {
     std::lock_guard<std::mutex> lk(d->mu);
     d->timing = enable != 0;
+    d->serial = enable == 2;
     d->tev_used = 0;
   }
   return 0;

@@ -189,7 +189,9 @@ size_t hbls_hm_entry_bytes(void);
 /* Measurement: with timing enabled (which also resets the record), every kernel launch of the
  * verification, aggregation and hashing paths is bracketed by HIP events on the stream it runs
  * on; hbls_timing_read returns kernel names (static strings) and durations in milliseconds, in
- * launch order. */
+ * launch order.  enable: 0 off, 1 on, 2 on and serialised (each timed launch completes before
+ * the call enqueues the next one, so every duration is the kernel alone on the device: the
+ * per-kernel roofline; calls then block). */
 int hbls_timing(int enable);
 int hbls_timing_read(const char** names, float* ms, size_t max_n, size_t* n_out);
 /* Verification statistics, collected only with HBLS_STATS=1 in the environment (each call then
