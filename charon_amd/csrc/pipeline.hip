@@ -1,5 +1,5 @@
-// pipeline.hip: message hashing and the pairing kernel of libhipbls.so (tbls.Verify,
-// herumi.go:288-304).
+// pipeline.hip: the Miller lines of the hashed messages and the pairing kernel of libhipbls.so
+// (tbls.Verify, herumi.go:288-304).  Message hashing is in hash.hip.
 //
 // Compiled with HB_FAST_FPMUL: every field / curve / tower function is inlined; the Fp product and
 // square are the only calls (fp.h fp_mul_leaf / fp_sqr_leaf, compiler-visible C++).
@@ -10,45 +10,6 @@
 namespace hb {
 
 constexpr int BLOCK = 64;
-
-#if defined(__HIP_DEVICE_COMPILE__)
-__device__ __forceinline__ G2J xch_pair(const G2J& p) {  // the point of lane ^ 1
-  G2J r;
-  const uint32_t* s = reinterpret_cast<const uint32_t*>(&p);
-  uint32_t* d = reinterpret_cast<uint32_t*>(&r);
-  const int addr = (int)((threadIdx.x ^ 1u) << 2);
-  HB_UNROLL for (int k = 0; k < (int)(sizeof(G2J) / 4); k++)
-    d[k] = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)s[k]);
-  return r;
-}
-#endif
-
-// Two lanes per distinct message: hash_to_curve G2 (RFC 9380, DST ..._POP_), affine.  Both lanes
-// expand the message; the even lane maps u0, the odd lane u1 (SSWU + 3-isogeny, the larger half
-// of the work, in parallel), then the even lane adds the pair and clears the cofactor.
-__global__ KB_OCC(HB_OCC_HASH) void k_hash_to_g2(const uint8_t* __restrict__ msgs, const uint64_t* __restrict__ off,
-                                           const uint32_t* __restrict__ len, uint32_t n, MsgEntry* __restrict__ hm) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t i = t >> 1;
-  const bool odd = (t & 1u) != 0;
-  const uint32_t ii = i < n ? i : n - 1;  // every lane takes part in the exchange
-  Fp2 u0, u1;
-  hash_to_field_fp2(u0, u1, msgs + off[ii], len[ii]);
-  Fp2 x, y;
-  sswu_map(x, y, odd ? u1 : u0);
-  const G2J q = iso3_map(x, y);
-  const G2J q1 = xch_pair(q);
-  if (odd || i >= n) return;
-  G2A h = jac_to_aff(g2_clear_cofactor(jac_add(q, q1)));
-  HmEntry e;
-  e.x = h.x;
-  e.y = h.y;
-  e.inf = h.inf ? 1u : 0u;
-  e.pad[0] = e.pad[1] = e.pad[2] = 0;
-  hm[i].h = e;
-#endif
-}
 
 // One lane per distinct message: the unevaluated line chain of H(m).
 __global__ KB_OCC(HB_OCC_LINES) void k_lines_msg(MsgEntry* __restrict__ hm, uint32_t n) {
@@ -115,10 +76,6 @@ __global__ KB_OCC(HB_OCC_PAIR3) void k_pair3(Pair3Args a) {
 
 static inline unsigned blocks_for(size_t n) { return (unsigned)((n + BLOCK - 1) / BLOCK); }
 
-void launch_hash_to_g2(const uint8_t* msgs, const uint64_t* off, const uint32_t* len, uint32_t n, MsgEntry* hm,
-                       hipStream_t s) {
-  if (n) hipLaunchKernelGGL(k_hash_to_g2, dim3(blocks_for(2 * (size_t)n)), dim3(BLOCK), 0, s, msgs, off, len, n, hm);
-}
 void launch_lines_msg(MsgEntry* hm, uint32_t n, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_lines_msg, dim3(blocks_for(n)), dim3(BLOCK), 0, s, hm, n);
 }
