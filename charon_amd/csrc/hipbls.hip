@@ -221,6 +221,8 @@ size_t env_size(const char* name, size_t dflt) {
 // fallback items per pass (HBLS_GROUP_CHUNK / HBLS_FALLBACK_CHUNK).  Host-buffer calls build
 // groups of at most GMAX items over one message (HBLS_GROUP_MAX).
 size_t g_gcap = 131072, g_fbcap = 65536, g_gmax = 16;
+// HBLS_RLC_MSM=0: one ladder per item (k_rlc) instead of shared-doubling chunks (k_rlc_msm)
+bool g_rlc_msm = true;
 
 struct DevBuf {
   void* p = nullptr;
@@ -234,6 +236,7 @@ enum WsId {
   W_APK, W_APKST, W_ASIG, W_APR, W_ASR,          // folded aggregates (post-aggregate verification)
   W_TAPTS, W_TADST, W_TAMST, W_TADIG, W_TATAB, W_TAJ,  // ThresholdAggregate / Aggregate
   W_SEGA, W_SEGB, W_SEGSTA, W_SEGSTB, W_VAPT, W_VAPV, W_PLAN,  // VerifyAggregate key reduction
+  W_PCNT, W_PCOFF, W_PCFIRST, W_PCCOUNT, W_COEF, W_RT1, W_RT2,  // chunk plan + multi-scalar RLC
   W_COUNT_
 };
 
@@ -407,6 +410,7 @@ int init_mask(uint32_t mask) {
   g_gcap = env_size("HBLS_GROUP_CHUNK", g_gcap);
   g_fbcap = env_size("HBLS_FALLBACK_CHUNK", g_fbcap);
   g_gmax = std::max<size_t>(1, env_size("HBLS_GROUP_MAX", g_gmax));
+  g_rlc_msm = env_size("HBLS_RLC_MSM", 1) != 0;
   std::vector<Dev*> devs;
   for (int k = 0; k < 32; k++)
     if (mask & (1u << k)) {
@@ -586,7 +590,37 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
   HCHK(hipEventRecord(d.ev_dec, s));
   d.dec_valid = true;
   TIMED(d, "k_item_group", s, launch_item_group(dgoff, (uint32_t)n_groups, (uint32_t)n, igrp, s));
-  TIMED(d, "k_rlc", s, launch_rlc(vpk, vpkst, vsig, vsigst, igrp, dgoff, 0, (uint32_t)n, 0, key, pr, sr, s));
+  if (dgoff && g_rlc_msm) {
+    // chunks of at most RLC_CHUNK items of a group share their ladders' doublings (k_rlc_msm)
+    const size_t max_chunks = n / RLC_CHUNK + n_groups;
+    uint32_t *pcnt, *pcoff, *pcf, *pcc;
+    uint2* coef;
+    G1J* t1;
+    G2J* t2;
+    if (wsbuf(w, W_PCNT, n_groups, &pcnt) || wsbuf(w, W_PCOFF, n_groups + 1, &pcoff) ||
+        wsbuf(w, W_PCFIRST, max_chunks, &pcf) || wsbuf(w, W_PCCOUNT, max_chunks, &pcc) ||
+        wsbuf(w, W_COEF, n, &coef) || wsbuf(w, W_RT1, 3 * n, &t1) || wsbuf(w, W_RT2, 3 * n, &t2))
+      return -1;
+    TIMED(d, "k_plan", s, launch_plan(dgoff, (uint32_t)n_groups, RLC_CHUNK, pcnt, pcoff, pcf, pcc, s));
+    RlcMsmArgs ra{};
+    ra.pk = vpk;
+    ra.pk_st = vpkst;
+    ra.sig = vsig;
+    ra.sig_st = vsigst;
+    ra.cfirst = pcf;
+    ra.ccount = pcc;
+    ra.total = pcoff + n_groups;
+    ra.key_base = 0;
+    ra.key = key;
+    ra.coef = coef;
+    ra.t1 = t1;
+    ra.t2 = t2;
+    ra.pout = pr;
+    ra.sout = sr;
+    TIMED(d, "k_rlc", s, launch_rlc_msm(ra, (uint32_t)max_chunks, s));
+  } else {
+    TIMED(d, "k_rlc", s, launch_rlc(vpk, vpkst, vsig, vsigst, igrp, dgoff, 0, (uint32_t)n, 0, key, pr, sr, s));
+  }
   if (n_agg) {
     HCHK(hipStreamWaitEvent(s, w.ev_ta, 0));
     TIMED(d, "k_rlc", s,

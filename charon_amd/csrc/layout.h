@@ -133,6 +133,27 @@ void launch_pair3(const Pair3Args& a, hipStream_t s);
 void launch_item_group(const uint32_t* grp_off, uint32_t n_groups, uint32_t n, uint32_t* item_grp, hipStream_t s);
 void launch_dec_pk(const uint8_t* pks, uint32_t n, G1AEntry* out, uint8_t* st, hipStream_t s);
 void launch_dec_sig_pt(const uint8_t* sigs, uint32_t n, HmEntry* out, uint8_t* st, hipStream_t s);
+// Chunk plans and the multi-scalar random linear combination (vbatch.hip k_plan_*, k_rlc_msm).
+constexpr uint32_t RLC_CHUNK = 16;  // items per lane of k_rlc_msm
+struct RlcMsmArgs {
+  const G1AEntry* pk;
+  const uint8_t* pk_st;
+  const HmEntry* sig;
+  const uint8_t* sig_st;
+  const uint32_t* cfirst;
+  const uint32_t* ccount;
+  const uint32_t* total;  // device: number of chunks
+  uint32_t key_base;
+  RlcKey key;
+  uint2* coef;    // per item
+  G1J* t1;        // 3 per item
+  G2J* t2;        // 3 per item
+  G1JEntry* pout;
+  G2JEntry* sout;
+};
+void launch_plan(const uint32_t* grp_off, uint32_t ng, uint32_t cmax, uint32_t* cnt, uint32_t* coff,
+                 uint32_t* cfirst, uint32_t* ccount, hipStream_t s);
+void launch_rlc_msm(const RlcMsmArgs& a, uint32_t max_chunks, hipStream_t s);
 void launch_rlc(const G1AEntry* pk, const uint8_t* pk_st, const HmEntry* sig, const uint8_t* sig_st,
                 const uint32_t* item_grp, const uint32_t* grp_off, int always, uint32_t n, uint32_t key_base,
                 const RlcKey& key, G1JEntry* pout, G2JEntry* sout, hipStream_t s);

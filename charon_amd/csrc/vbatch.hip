@@ -134,6 +134,150 @@ __global__ KB_OCC(HB_OCC_RLC) void k_rlc(const G1AEntry* __restrict__ pk, const 
 #endif
 }
 
+// ---------------------------------------------------------------------------------------
+// Chunk plans: the items of every group [grp_off[g], grp_off[g+1]) cut into chunks of at most
+// cmax consecutive items (group g's chunks are coff[g] .. coff[g+1]-1; chunk c covers
+// cfirst[c] .. cfirst[c] + (ccount[c] & 0x7fffffff) - 1; bit 31 of ccount marks a group of ONE
+// item).  A chunk is one lane of the multi-scalar kernels below, which share the doublings of a
+// ladder over the chunk's items.
+// ---------------------------------------------------------------------------------------
+__global__ KB void k_plan_count(const uint32_t* __restrict__ grp_off, uint32_t ng, uint32_t cmax,
+                                uint32_t* __restrict__ cnt) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= ng) return;
+  cnt[g] = (grp_off[g + 1] - grp_off[g] + cmax - 1) / cmax;
+}
+
+// one workgroup: exclusive scan of cnt[0..ng) into coff[0..ng], coff[ng] = total
+__global__ __launch_bounds__(1024) void k_plan_scan(const uint32_t* __restrict__ cnt, uint32_t ng,
+                                                    uint32_t* __restrict__ coff) {
+  __shared__ uint32_t part[1024];
+  const uint32_t t = threadIdx.x, per = (ng + 1023u) / 1024u;
+  const uint32_t b = t * per < ng ? t * per : ng, e = b + per < ng ? b + per : ng;
+  uint32_t sum = 0;
+  for (uint32_t i = b; i < e; i++) sum += cnt[i];
+  part[t] = sum;
+  __syncthreads();
+  for (uint32_t off = 1; off < 1024u; off <<= 1) {
+    const uint32_t v = t >= off ? part[t - off] : 0u;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  uint32_t run = part[t] - sum;
+  for (uint32_t i = b; i < e; i++) {
+    coff[i] = run;
+    run += cnt[i];
+  }
+  if (t == 1023u) coff[ng] = part[1023];
+}
+
+__global__ KB void k_plan_fill(const uint32_t* __restrict__ grp_off, uint32_t ng, uint32_t cmax,
+                               const uint32_t* __restrict__ coff, uint32_t* __restrict__ cfirst,
+                               uint32_t* __restrict__ ccount) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= ng) return;
+  const uint32_t b = grp_off[g], sz = grp_off[g + 1] - b, c0 = coff[g], nc = coff[g + 1] - c0;
+  for (uint32_t k = 0; k < nc; k++) {
+    cfirst[c0 + k] = b + k * cmax;
+    const uint32_t left = sz - k * cmax;
+    ccount[c0 + k] = (left < cmax ? left : cmax) | (sz == 1 ? 0x80000000u : 0u);
+  }
+}
+
+// One lane per chunk of a verification group: sum_i [r_i] pk_i and sum_i [r_i] sig_i over the
+// chunk's items with r_i = a_i + b_i lambda (rlc.h), as ONE joint 32-step ladder per side whose
+// doublings all items share (32 doublings + 32 additions per item before: 32 doublings per chunk
+// + 32 additions per item now).  Each item's three ladder points {T1, phi(T1), T1 + phi(T1)} go to
+// the workspace as Jacobian records and are read back by the step's selection; unusable items
+// contribute nothing; a group of one item keeps r = 1.  The chunk's sum is written at its first
+// item, infinity at the others, so k_group_prep sums the items as before.
+template <class F>
+__device__ __forceinline__ Jac<F> msm_ladder(const Jac<F>* __restrict__ tab, const uint2* __restrict__ coef,
+                                             uint32_t first, uint32_t cnt) {
+  Jac<F> R = jac_infinity<F>();
+  HB_NOUNROLL for (int bit = 31; bit >= 0; bit--) {
+    R = jac_dbl(R);
+    HB_NOUNROLL for (uint32_t k = 0; k < cnt; k++) {
+      const uint32_t i = first + k;
+      const uint2 ab = coef[i];
+      const uint32_t sel = ((ab.x >> bit) & 1u) | (((ab.y >> bit) & 1u) << 1);
+      const Jac<F> T = tab[3ull * i + (sel ? sel - 1u : 0u)];
+      const Jac<F> S = jac_add(R, T);
+      R = jac_select(sel != 0, R, S);
+    }
+  }
+  return R;
+}
+
+__global__ KB_OCC(HB_OCC_RLC) void k_rlc_msm(RlcMsmArgs a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= *a.total) return;
+  const uint32_t first = a.cfirst[c], cc = a.ccount[c], cnt = cc & 0x7fffffffu;
+  const bool single = (cc & 0x80000000u) != 0;
+  if (single) {  // r = 1
+    const uint32_t i = first;
+    const bool usable = !a.pk_st[i] && !a.sig_st[i] && !a.pk[i].inf && !a.sig[i].inf;
+    const G1AEntry pe = a.pk[i];
+    const G1J rp = usable ? jac_from_aff(G1A{pe.x, pe.y, false}) : jac_infinity<Fp>();
+    a.pout[i] = {rp.X, rp.Y, rp.Z};
+    const HmEntry se = a.sig[i];
+    const G2J rs = usable ? jac_from_aff(G2A{se.x, se.y, false}) : jac_infinity<Fp2>();
+    a.sout[i] = {rs.X, rs.Y, rs.Z};
+    return;
+  }
+  // coefficients and the G1 ladder points of the chunk's items
+  HB_NOUNROLL for (uint32_t k = 0; k < cnt; k++) {
+    const uint32_t i = first + k;
+    const bool usable = !a.pk_st[i] && !a.sig_st[i] && !a.pk[i].inf && !a.sig[i].inf;
+    uint32_t ca = 0, cb = 0;
+    if (usable) rlc_coeffs(a.key, a.key_base + i, ca, cb);
+    a.coef[i] = make_uint2(ca, cb);
+    const G1AEntry pe = a.pk[i];
+    const G1A P = {pe.x, pe.y, false};
+    const G1A P2 = {fp_mul(P.x, fp_from_const(G1_BETA)), P.y, false};
+    const G1J J1 = jac_from_aff(P), J2 = jac_from_aff(P2), J3 = jac_add_aff(J1, P2);
+    a.t1[3ull * i] = J1;
+    a.t1[3ull * i + 1] = J2;
+    a.t1[3ull * i + 2] = J3;
+  }
+  const G1J rp = msm_ladder<Fp>(a.t1, a.coef, first, cnt);
+  a.pout[first] = {rp.X, rp.Y, rp.Z};
+  // the G2 ladder points, then the G2 ladder
+  HB_NOUNROLL for (uint32_t k = 0; k < cnt; k++) {
+    const uint32_t i = first + k;
+    const HmEntry se = a.sig[i];
+    const G2A S = {se.x, se.y, false};
+    const G2A S2 = {f2_mul(S.x, f2_from_const(PSI2_CX)), f2_neg(f2_mul(S.y, f2_from_const(PSI2_CY))), false};
+    const G2J J1 = jac_from_aff(S), J2 = jac_from_aff(S2), J3 = jac_add_aff(J1, S2);
+    a.t2[3ull * i] = J1;
+    a.t2[3ull * i + 1] = J2;
+    a.t2[3ull * i + 2] = J3;
+  }
+  const G2J rs = msm_ladder<Fp2>(a.t2, a.coef, first, cnt);
+  a.sout[first] = {rs.X, rs.Y, rs.Z};
+  const G1J zi = jac_infinity<Fp>();
+  const G2J zs = jac_infinity<Fp2>();
+  for (uint32_t k = 1; k < cnt; k++) {
+    a.pout[first + k] = {zi.X, zi.Y, zi.Z};
+    a.sout[first + k] = {zs.X, zs.Y, zs.Z};
+  }
+#endif
+}
+
+void launch_plan(const uint32_t* grp_off, uint32_t ng, uint32_t cmax, uint32_t* cnt, uint32_t* coff,
+                 uint32_t* cfirst, uint32_t* ccount, hipStream_t s) {
+  if (!ng) return;
+  const unsigned nb = (ng + BLOCK - 1) / BLOCK;
+  hipLaunchKernelGGL(k_plan_count, dim3(nb), dim3(BLOCK), 0, s, grp_off, ng, cmax, cnt);
+  hipLaunchKernelGGL(k_plan_scan, dim3(1), dim3(1024), 0, s, cnt, ng, coff);
+  hipLaunchKernelGGL(k_plan_fill, dim3(nb), dim3(BLOCK), 0, s, grp_off, ng, cmax, coff, cfirst, ccount);
+}
+void launch_rlc_msm(const RlcMsmArgs& a, uint32_t max_chunks, hipStream_t s) {
+  if (max_chunks) hipLaunchKernelGGL(k_rlc_msm, dim3((max_chunks + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, a);
+}
+
 // One lane per item (then per folded aggregate): final status, or a place in the fallback list.
 __global__ KB void k_scatter(ScatterArgs a) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
