@@ -532,7 +532,12 @@ def main(argv=None):
 
     per_unit = opcounts.per_unit(group_size=n, t=t)
     ta_units = V * t
-    units = {"k_pair3": (V, per_unit["k_pair3"]), "k_rlc": (NP + (0 if staged else V), per_unit["k_rlc"]),
+    # k_rlc: the partials as multi-scalar chunks (one per validator), the folded aggregates (slot
+    # mode) one ladder each
+    rlc_item = opcounts.BLOCKS["rlc_g1"] + opcounts.BLOCKS["rlc_g2"]
+    n_rlc = NP + (0 if staged else V)
+    rlc_avg = (NP * per_unit["k_rlc"][0] + (0 if staged else V) * rlc_item) / n_rlc
+    units = {"k_pair3": (V, per_unit["k_pair3"]), "k_rlc": (n_rlc, (rlc_avg, rlc_avg)),
              "k_dec_pk": (NP + (0 if staged else V), per_unit["k_dec_pk"]),
              "k_dec_sig_pt": (NP + (ta_units if staged else 0), per_unit["k_dec_sig_pt"]),
              "k_group_prep": (V, opcounts.per_unit(group_size=n + (0 if staged else 1), t=t)["k_group_prep"]),

@@ -223,6 +223,12 @@ size_t env_size(const char* name, size_t dflt) {
 size_t g_gcap = 131072, g_fbcap = 65536, g_gmax = 16;
 // HBLS_RLC_MSM=0: one ladder per item (k_rlc) instead of shared-doubling chunks (k_rlc_msm)
 bool g_rlc_msm = true;
+// HBLS_TA_MSM=1: the aggregation as shared-doubling chunks (k_ta_msm) instead of one Straus ladder
+// per member (k_ta_straus).  Off: measured slower at C3 (per-member tables read across lanes
+// uncoalesced; fewer, longer lanes) -- 222.8 ms/slot with per-member ladders vs 224.2-227.8 with
+// chunks of 2, 4 or 8 members.
+bool g_ta_msm = false;
+size_t g_ta_chunk = 4;   // HBLS_TA_CHUNK: members per lane of k_ta_msm (<= TA_CHUNK)
 
 struct DevBuf {
   void* p = nullptr;
@@ -237,6 +243,7 @@ enum WsId {
   W_TAPTS, W_TADST, W_TAMST, W_TADIG, W_TATAB, W_TAJ,  // ThresholdAggregate / Aggregate
   W_SEGA, W_SEGB, W_SEGSTA, W_SEGSTB, W_VAPT, W_VAPV, W_PLAN,  // VerifyAggregate key reduction
   W_PCNT, W_PCOFF, W_PCFIRST, W_PCCOUNT, W_COEF, W_RT1, W_RT2,  // chunk plan + multi-scalar RLC
+  W_TPCNT, W_TPCOFF, W_TPCFIRST, W_TPCCOUNT,                    // chunk plan of the aggregation
   W_COUNT_
 };
 
@@ -411,6 +418,8 @@ int init_mask(uint32_t mask) {
   g_fbcap = env_size("HBLS_FALLBACK_CHUNK", g_fbcap);
   g_gmax = std::max<size_t>(1, env_size("HBLS_GROUP_MAX", g_gmax));
   g_rlc_msm = env_size("HBLS_RLC_MSM", 1) != 0;
+  g_ta_msm = env_size("HBLS_TA_MSM", 0) != 0;
+  g_ta_chunk = std::min<size_t>(TA_CHUNK, std::max<size_t>(1, env_size("HBLS_TA_CHUNK", g_ta_chunk)));
   std::vector<Dev*> devs;
   for (int k = 0; k < 32; k++)
     if (mask & (1u << k)) {
@@ -510,7 +519,20 @@ int ta_tail(Dev& d, Ws& w, const HmEntry* pts, const uint32_t* src, const uint8_
     else HCHK(hipMemcpyAsync(mst, mst_in, np, hipMemcpyDeviceToDevice, s));
     HCHK(hipGetLastError());
     TIMED(d, "k_ta_lambda", s, launch_ta_lambda(didx, dgoff, (uint32_t)n_groups, (uint32_t)np, mode, dig, mst, s));
-    TIMED(d, "k_ta_straus", s, launch_ta_straus(pts, src, dig, (uint32_t)np, tab, pj, s));
+    if (g_ta_msm && n_groups) {
+      // chunks of at most TA_CHUNK members share their ladder's doublings (k_ta_msm)
+      const size_t max_chunks = np / g_ta_chunk + n_groups;
+      uint32_t *pcnt, *pcoff, *pcf, *pcc;
+      if (wsbuf(w, W_TPCNT, n_groups, &pcnt) || wsbuf(w, W_TPCOFF, n_groups + 1, &pcoff) ||
+          wsbuf(w, W_TPCFIRST, max_chunks, &pcf) || wsbuf(w, W_TPCCOUNT, max_chunks, &pcc))
+        return -1;
+      TIMED(d, "k_plan", s, launch_plan(dgoff, (uint32_t)n_groups, (uint32_t)g_ta_chunk, pcnt, pcoff, pcf, pcc, s));
+      if (mode == 0) TIMED(d, "k_ta_table", s, launch_ta_table(pts, src, (uint32_t)np, tab, s));
+      TIMED(d, "k_ta_straus", s,
+            launch_ta_msm(pts, src, dig, tab, pcf, pcc, pcoff + n_groups, (uint32_t)max_chunks, mode, pj, s));
+    } else {
+      TIMED(d, "k_ta_straus", s, launch_ta_straus(pts, src, dig, (uint32_t)np, tab, pj, s));
+    }
   }
   TIMED(d, "k_group_sum", s,
         LAUNCH(k_group_sum, n_groups, s, dgoff, (uint32_t)n_groups, mode, (const G2JEntry*)pj, (const uint8_t*)mst,

@@ -181,6 +181,82 @@ __global__ KB_OCC(HB_OCC_STRAUS) void k_ta_straus(const HmEntry* __restrict__ pt
 #endif
 }
 
+// The same aggregation as multi-scalar ladders over chunks of up to TA_CHUNK members of a group
+// (k_plan_* chunk plan, vbatch.hip): k_ta_table builds every member's 15-entry subset table (the
+// first half of k_ta_straus), then one lane per chunk runs ONE 64-step ladder whose doublings the
+// chunk's members share (64 doublings per chunk + 64 additions per member, instead of 64 + 64 per
+// member).  The chunk's sum goes to its first member's slot of `out`, infinity to the others, so
+// k_group_sum adds the members as before.  mode 1 (Aggregate, lambda = 1): a plain sum.
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ uint4* member_tab(uint4* tab, uint32_t m) {
+  return tab + (size_t)(m >> 6) * 15 * TA_TAB_QUADS * 64 + (m & 63u);
+}
+#endif
+
+__global__ KB_OCC(HB_OCC_STRAUS) void k_ta_table(const HmEntry* __restrict__ pts, const uint32_t* __restrict__ src,
+                                                    uint32_t n_partials, uint4* __restrict__ tab) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t m = blockIdx.x * 64 + (threadIdx.x & 63u);
+  if (m >= n_partials) return;
+  uint4* wt = member_tab(tab, m);
+  {
+    const HmEntry e = pts[src ? src[m] : m];
+    G2A P0 = {e.x, e.y, e.inf != 0};
+    G2A P1 = {f2_mul(f2_conj(e.x), f2_from_const(PSI_CX)), f2_neg(f2_mul(f2_conj(e.y), f2_from_const(PSI_CY))), P0.inf};
+    G2A P2 = {f2_mul(e.x, f2_from_const(PSI2_CX)), f2_mul(e.y, f2_from_const(PSI2_CY)), P0.inf};
+    G2A P3 = {f2_mul(f2_conj(P2.x), f2_from_const(PSI_CX)), f2_neg(f2_mul(f2_conj(P2.y), f2_from_const(PSI_CY))), P0.inf};
+    tab_store(wt, 0, jac_from_aff(P0));
+    tab_store(wt, 1, jac_from_aff(P1));
+    tab_store(wt, 3, jac_from_aff(P2));
+    tab_store(wt, 7, jac_from_aff(P3));
+  }
+  HB_NOUNROLL for (int sidx = 3; sidx < 16; sidx++) {
+    const int hi = sidx >= 8 ? 8 : (sidx >= 4 ? 4 : 2);
+    if (sidx == hi) continue;
+    const G2J h = tab_load(wt, hi - 1);
+    const G2A ha = {h.X, h.Y, f2_is_zero(h.Z)};
+    tab_store(wt, sidx - 1, jac_add_aff(tab_load(wt, sidx - hi - 1), ha));
+  }
+#endif
+}
+
+__global__ KB_OCC(HB_OCC_STRAUS) void k_ta_msm(const HmEntry* __restrict__ pts, const uint32_t* __restrict__ src,
+                                                  const TaDigits* __restrict__ dig, uint4* __restrict__ tab,
+                                                  const uint32_t* __restrict__ cfirst,
+                                                  const uint32_t* __restrict__ ccount,
+                                                  const uint32_t* __restrict__ total, int mode,
+                                                  G2JEntry* __restrict__ out) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= *total) return;
+  const uint32_t first = cfirst[c], cnt = ccount[c] & 0x7fffffffu;
+  G2J R = jac_infinity<Fp2>();
+  if (mode == 1) {
+    HB_NOUNROLL for (uint32_t k = 0; k < cnt; k++) {
+      const HmEntry e = pts[src ? src[first + k] : first + k];
+      R = jac_add(R, jac_from_aff(G2A{e.x, e.y, e.inf != 0}));
+    }
+  } else {
+    HB_NOUNROLL for (int b = 63; b >= 0; b--) {
+      R = jac_dbl(R);
+      HB_NOUNROLL for (uint32_t k = 0; k < cnt; k++) {
+        const uint32_t m = first + k;
+        const TaDigits d = dig[m];
+        const uint32_t sel = (uint32_t)((d.a[0] >> b) & 1) | ((uint32_t)((d.a[1] >> b) & 1) << 1) |
+                             ((uint32_t)((d.a[2] >> b) & 1) << 2) | ((uint32_t)((d.a[3] >> b) & 1) << 3);
+        const G2J S = jac_add(R, tab_load(member_tab(tab, m), sel == 0 ? 0 : (int)sel - 1));
+        f2_select(R.X, sel != 0, R.X, S.X);
+        f2_select(R.Y, sel != 0, R.Y, S.Y);
+        f2_select(R.Z, sel != 0, R.Z, S.Z);
+      }
+    }
+  }
+  out[first] = {R.X, R.Y, R.Z};
+  const G2J z = jac_infinity<Fp2>();
+  for (uint32_t k = 1; k < cnt; k++) out[first + k] = {z.X, z.Y, z.Z};
+#endif
+}
+
 static inline unsigned blocks_of(size_t n, unsigned per) { return (unsigned)((n + per - 1) / per); }
 
 void launch_ta_lambda(const int64_t* idx, const uint32_t* grp_off, uint32_t n_groups,
@@ -191,6 +267,18 @@ void launch_ta_lambda(const int64_t* idx, const uint32_t* grp_off, uint32_t n_gr
 }
 
 size_t ta_table_bytes(uint32_t n_partials) { return (size_t)blocks_of(n_partials, 64) * 15 * sizeof(G2JEntry) * 64; }
+
+void launch_ta_table(const HmEntry* pts, const uint32_t* src, uint32_t n_partials, void* tab, hipStream_t s) {
+  if (n_partials)
+    hipLaunchKernelGGL(k_ta_table, dim3(blocks_of(n_partials, 64)), dim3(64), 0, s, pts, src, n_partials, (uint4*)tab);
+}
+void launch_ta_msm(const HmEntry* pts, const uint32_t* src, const TaDigits* dig, void* tab, const uint32_t* cfirst,
+                   const uint32_t* ccount, const uint32_t* total, uint32_t max_chunks, int mode, G2JEntry* out,
+                   hipStream_t s) {
+  if (max_chunks)
+    hipLaunchKernelGGL(k_ta_msm, dim3(blocks_of(max_chunks, 64)), dim3(64), 0, s, pts, src, dig, (uint4*)tab, cfirst,
+                       ccount, total, mode, out);
+}
 
 void launch_ta_straus(const HmEntry* pts, const uint32_t* src, const TaDigits* dig, uint32_t n_partials, void* tab,
                       G2JEntry* out, hipStream_t s) {

@@ -22,9 +22,9 @@ PEAK_MAD_TOPS_NOMINAL = 39.3
 # hc_count_blocks, in its order
 BLOCK_NAMES = ("f12_sqr", "f12_mul_line", "final_exp", "fp_inv", "g1_dec", "g2_dec", "rlc_g1", "rlc_g2",
                "jac_add_g1", "jac_add_g2", "to_aff_g1", "to_aff_g2", "lines_eval", "lines_uneval", "jac_dbl_g2",
-               "jac_add_aff_g2", "cyclo_sqr", "f12_mul", "g2_compress", "jac_add_aff_g1")
+               "jac_add_aff_g2", "cyclo_sqr", "f12_mul", "g2_compress", "jac_add_aff_g1", "jac_dbl_g1")
 BLOCKS = dict(zip(BLOCK_NAMES, (36, 39, 8141, 463, 1517, 2192, 732, 1880, 16, 43, 467, 478, 1843, 1571, 16, 29, 18,
-                                54, 4, 11)))
+                                54, 4, 11, 7)))
 
 N_LINES = 68      # Miller-loop lines (63 doublings + 5 additions)
 N_SQR = 62        # Fp12 squarings of the Miller loop
@@ -50,22 +50,40 @@ def pair3(b=BLOCKS):
     return alg, exe
 
 
+RLC_CHUNK = 16   # items per lane of k_rlc_msm (layout.h)
+TA_CHUNK = 8     # members per lane of k_ta_msm (layout.h)
+
+
+def rlc_msm(b=BLOCKS, chunk=1):
+    """k_rlc_msm per item of a chunk of `chunk` items: the ladder points (phi + one mixed addition
+    per side), 32 shared doublings per chunk, 32 additions per item."""
+    g1 = 1 + b["jac_add_aff_g1"] + 32 * b["jac_add_g1"] + 32 * b["jac_dbl_g1"] / chunk
+    g2 = 6 + b["jac_add_aff_g2"] + 32 * b["jac_add_g2"] + 32 * b["jac_dbl_g2"] / chunk
+    return g1 + g2
+
+
+def ta_msm(b=BLOCKS, chunk=1):
+    """k_ta_table + k_ta_msm per member of a chunk of `chunk` members: the 15-entry subset table,
+    64 shared doublings per chunk, 64 additions per member."""
+    return 18 + 11 * b["jac_add_aff_g2"] + 64 * b["jac_add_g2"] + 64 * b["jac_dbl_g2"] / chunk
+
+
 def per_unit(b=BLOCKS, group_size=1, t=1):
     """{kernel: (alg, exec)} Fp products per unit (unit named in UNITS)."""
     p = pair3(b)
     k = group_size
     prep = (b["lines_eval"] if k == 1 else
             (k - 1) * (b["jac_add_g1"] + b["jac_add_g2"]) + b["to_aff_g1"] + b["to_aff_g2"] + b["lines_eval"])
-    straus = 18 + 11 * b["jac_add_aff_g2"] + 64 * (b["jac_dbl_g2"] + b["jac_add_g2"])
     gsum = t * b["jac_add_g2"] + b["to_aff_g2"] + b["g2_compress"]
     out = {
         "k_pair3": p, "k_pair3_fallback": p,
         "k_dec_pk": (b["g1_dec"],) * 2,
         "k_dec_sig_pt": (b["g2_dec"],) * 2,
-        "k_rlc": (b["rlc_g1"] + b["rlc_g2"],) * 2,
+        # one chunk per verification group of <= RLC_CHUNK items (the slot's groups of n + 1)
+        "k_rlc": (rlc_msm(b, min(group_size, RLC_CHUNK)),) * 2,
         "k_group_prep": (prep,) * 2,
         "k_fb_lines": (b["lines_eval"],) * 2,
-        "k_ta_straus": (straus,) * 2,
+        "k_ta_straus": (ta_msm(b, 1),) * 2,  # one ladder per member (HBLS_TA_MSM off)
         "k_group_sum": (gsum,) * 2,
         "k_hash_to_g2": (HASH_TO_G2,) * 2,
         "k_lines_msg": (b["lines_uneval"],) * 2,

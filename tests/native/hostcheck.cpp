@@ -350,6 +350,7 @@ extern "C" int hc_count_blocks(const uint8_t* pk48, const uint8_t* sig96, unsign
   uint8_t buf[96];
   cnt(18, [&] { g2_compress(buf, q); });
   cnt(19, [&] { pj2 = jac_add_aff(pj2, p); });
+  cnt(20, [&] { pj2 = jac_dbl(pj2); });
   (void)r;
   (void)t;
   return 0;
