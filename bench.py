@@ -314,6 +314,41 @@ def aggregate_verify(L, d, d_pk, dev, sp, reps: int = 3, sync_size: int = 512):
     return out
 
 
+def key_table_slots(L, d_pk, d_dvpk, outs, NP, V, steps, step, mk, items):
+    """The same slots with the public keys taken from decompressed-key tables made once
+    (hbls_decompress_pubkeys_device; pubshares are static per cluster lock): the
+    steady state of a node, reported beside the headline, which decompresses every key."""
+    import torch
+    E = L.hbls_pk_entry_bytes()
+    dev = d_pk.device
+    tab = torch.zeros(NP * E, dtype=torch.uint8, device=dev)
+    tst = torch.full((NP,), 255, dtype=torch.uint8, device=dev)
+    dtab = torch.zeros(V * E, dtype=torch.uint8, device=dev)
+    dst = torch.full((V,), 255, dtype=torch.uint8, device=dev)
+    s0 = ctypes.c_void_p(outs[0]["stream"].cuda_stream)
+    t0 = time.perf_counter()
+    _chk(L, L.hbls_decompress_pubkeys_device(_p(d_pk), NP, _p(tab), _p(tst), s0))
+    _chk(L, L.hbls_decompress_pubkeys_device(_p(d_dvpk), V, _p(dtab), _p(dst), s0))
+    torch.cuda.synchronize()
+    build_ms = (time.perf_counter() - t0) * 1e3
+    for o in outs:
+        o["slot"].pk_table, o["slot"].pk_table_st = _p(tab).value, _p(tst).value
+        o["slot"].dv_pk_table, o["slot"].dv_pk_table_st = _p(dtab).value, _p(dst).value
+    step(mk())
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step(mk())
+    torch.cuda.synchronize()
+    el = (time.perf_counter() - t0) / steps
+    ok = all(bool((o["vst"] == 0).all().item()) and bool((o["tst"] == 0).all().item()) and
+             bool((o["ast"] == 0).all().item()) for o in outs)
+    for o in outs:
+        o["slot"].pk_table = o["slot"].pk_table_st = o["slot"].dv_pk_table = o["slot"].dv_pk_table_st = None
+    return {"items_per_s": round(items / el, 1), "ms_per_step": round(el * 1e3, 3), "steps": steps,
+            "table_build_ms": round(build_ms, 3), "all_ok": ok}
+
+
 def _lib_timing(L):
     from charon_amd import _lib
     return _lib.timing_read(L)
@@ -351,6 +386,8 @@ def main(argv=None):
     ap.add_argument("--callers-seconds", type=float, default=4.0)
     ap.add_argument("--aggregate-verify", type=int, default=1,
                     help="also time VerifyAggregate at scale (lock over all pubshares, sync-committee groups)")
+    ap.add_argument("--key-tables", type=int, default=1,
+                    help="also time the slot with decompressed-key tables built once (steady state)")
     ap.add_argument("--host-api", action="store_true", help="also time the host-buffer (PCIe-inclusive) entry points")
     ap.add_argument("--inflight", type=int, default=2,
                     help="slots in flight (each on its own stream and outputs); 1 = one slot at a time")
@@ -606,6 +643,9 @@ def main(argv=None):
         out["host_buffer_items_per_s"] = round((NP + V) / (time.perf_counter() - t0), 1)
         out["host_buffer_parity"] = bool((st == 0).all() and (tst_h == 0).all() and
                                          np.array_equal(tout_h, d["root_sigs"]))
+
+    if rank == 0 and world == 1 and args.key_tables and not staged:
+        out["with_key_tables"] = key_table_slots(L, d_pk, d_dvpk, outs, NP, V, args.steps, step_slot, mk, items)
 
     if rank == 0 and world == 1 and args.aggregate_verify:
         out["verify_aggregate"] = aggregate_verify(L, d, d_pk, dev, sp)

@@ -31,7 +31,8 @@ EXPORTS = (
     "hbls_hm_entry_bytes", "hbls_sync",
     "hbls_timing", "hbls_timing_read", "hbls_comm_id_bytes", "hbls_comm_unique_id", "hbls_comm_init",
     "hbls_allgather_device", "hbls_comm_destroy", "hbls_stats", "hbls_attestation_signing_roots",
-    "hbls_signing_roots", "hbls_attestation_signing_roots_device",
+    "hbls_signing_roots", "hbls_attestation_signing_roots_device", "hbls_pk_entry_bytes",
+    "hbls_decompress_pubkeys_device",
 )
 
 ALL_DEVICES = 0xFFFFFFFF
@@ -43,7 +44,8 @@ class HblsSlot(ctypes.Structure):
         ("msgs", "p"), ("msg_off", "p"), ("msg_len", "p"), ("n_msgs", "s"), ("hm", "p"),
         ("pks", "p"), ("sigs", "p"), ("msg_idx", "p"), ("n", "s"), ("vgrp_off", "p"), ("n_vgroups", "s"),
         ("vstatus", "p"), ("ta_sigs", "p"), ("ta_src", "p"), ("ta_idx", "p"), ("grp_off", "p"), ("n_groups", "s"),
-        ("n_ta_partials", "s"), ("ta_out", "p"), ("ta_status", "p"), ("dv_pks", "p"), ("agg_vstatus", "p"))]
+        ("n_ta_partials", "s"), ("ta_out", "p"), ("ta_status", "p"), ("dv_pks", "p"), ("agg_vstatus", "p"),
+        ("pk_table", "p"), ("pk_table_st", "p"), ("dv_pk_table", "p"), ("dv_pk_table_st", "p"))]
 
 
 class HipBlsUnavailable(RuntimeError):
@@ -82,6 +84,8 @@ def _declare(lib):
         "hbls_attestation_signing_roots": ([P, SZ, P, SZ, P, P], ctypes.c_int),
         "hbls_signing_roots": ([P, SZ, P, SZ, P, P], ctypes.c_int),
         "hbls_attestation_signing_roots_device": ([P, SZ, P, SZ, P, P, P], ctypes.c_int),
+        "hbls_pk_entry_bytes": ([], SZ),
+        "hbls_decompress_pubkeys_device": ([P, SZ, P, P, P], ctypes.c_int),
         "hbls_slot_device": ([ctypes.POINTER(HblsSlot), P], ctypes.c_int),
         "hbls_hm_entry_bytes": ([], SZ),
         "hbls_sync": ([P], ctypes.c_int),

@@ -501,6 +501,12 @@ struct TaFold {
   // post-aggregate verification (nullable): DV public key per group, verdict per group
   const uint8_t* dv_pks;
   uint8_t* agg_status;
+  // decompressed-key tables (hbls_decompress_pubkeys_device; nullable): used instead of
+  // decompressing pks / dv_pks in this call
+  const G1AEntry* pk_table;
+  const uint8_t* pk_table_st;
+  const G1AEntry* dv_pk_table;
+  const uint8_t* dv_pk_table_st;
 };
 
 // ThresholdAggregate (mode 0) / Aggregate (mode 1) of groups whose members are already
@@ -577,8 +583,20 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
   if (d.dec_valid) HCHK(hipStreamWaitEvent(s, d.ev_dec, 0));
   HCHK(hipEventRecord(w.ev_fork, s));
   for (int k = 0; k < 2; k++) HCHK(hipStreamWaitEvent(w.side[k], w.ev_fork, 0));
-  TIMED(d, "k_dec_pk", w.side[0], launch_dec_pk(dpk, (uint32_t)n, vpk, vpkst, w.side[0]));
-  if (n_agg) TIMED(d, "k_dec_pk", w.side[0], launch_dec_pk(fold->dv_pks, (uint32_t)n_agg, apk, apkst, w.side[0]));
+  // public keys: from the caller's decompressed-key tables when given (static per cluster lock:
+  // decompressed and subgroup-checked once), else decompressed here
+  if (fold && fold->pk_table) {
+    vpk = const_cast<G1AEntry*>(fold->pk_table);
+    vpkst = const_cast<uint8_t*>(fold->pk_table_st);
+  } else {
+    TIMED(d, "k_dec_pk", w.side[0], launch_dec_pk(dpk, (uint32_t)n, vpk, vpkst, w.side[0]));
+  }
+  if (n_agg && fold->dv_pk_table) {
+    apk = const_cast<G1AEntry*>(fold->dv_pk_table);
+    apkst = const_cast<uint8_t*>(fold->dv_pk_table_st);
+  } else if (n_agg) {
+    TIMED(d, "k_dec_pk", w.side[0], launch_dec_pk(fold->dv_pks, (uint32_t)n_agg, apk, apkst, w.side[0]));
+  }
   TIMED(d, "k_dec_sig_pt", w.side[1], launch_dec_sig_pt(dsig, (uint32_t)n, vsig, vsigst, w.side[1]));
   HCHK(hipEventRecord(w.ev_side[0], w.side[0]));
   HCHK(hipEventRecord(w.ev_side[1], w.side[1]));
@@ -1359,6 +1377,19 @@ int hbls_verify_device(const uint8_t* pks, const uint8_t* sigs, const uint32_t* 
   return ws_release(w, s);
 }
 
+size_t hbls_pk_entry_bytes(void) { return sizeof(G1AEntry); }
+
+int hbls_decompress_pubkeys_device(const uint8_t* pks, size_t n, void* table, uint8_t* status, void* stream) {
+  Dev* d;
+  hipStream_t s = (hipStream_t)stream;
+  if (dev_of_stream(s, &d)) return -1;
+  if (n == 0) return 0;
+  if (n > 0xffffffffull) return set_err("decompress pubkeys: too many keys");
+  std::lock_guard<std::mutex> lk(d->mu);
+  TIMED(*d, "k_dec_pk", s, launch_dec_pk(pks, (uint32_t)n, (G1AEntry*)table, status, s));
+  return 0;
+}
+
 int hbls_attestation_signing_roots_device(const uint8_t* data, size_t n, const uint8_t* domains, size_t n_domains,
                                           const uint32_t* dom_idx, uint8_t* roots, void* stream) {
   Dev* d;
@@ -1434,6 +1465,13 @@ int hbls_slot_device(const hbls_slot* a, void* stream) {
   fold.ta_status = a->ta_status;
   fold.dv_pks = a->dv_pks;
   fold.agg_status = a->agg_vstatus;
+  if ((a->pk_table != nullptr) != (a->pk_table_st != nullptr) ||
+      (a->dv_pk_table != nullptr) != (a->dv_pk_table_st != nullptr))
+    return set_err("hbls_slot_device: a key table needs its status array");
+  fold.pk_table = (const G1AEntry*)a->pk_table;
+  fold.pk_table_st = a->pk_table_st;
+  fold.dv_pk_table = (const G1AEntry*)a->dv_pk_table;
+  fold.dv_pk_table_st = a->dv_pk_table_st;
   if (verify_pipeline(*d, w, a->pks, a->sigs, a->msg_idx, (const MsgEntry*)a->hm, a->n, a->vgrp_off, a->n_vgroups,
                       a->vstatus, s, w.ev_side[2], &fold))
     return -1;

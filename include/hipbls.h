@@ -139,6 +139,12 @@ int hbls_threshold_aggregate_device(const uint8_t* sigs, const int64_t* idx, con
 int hbls_attestation_signing_roots_device(const uint8_t* data, size_t n, const uint8_t* domains, size_t n_domains,
                                           const uint32_t* dom_idx, uint8_t* roots, void* stream);
 
+/* Decompressed-key tables for hbls_slot pk_table / dv_pk_table: n compressed public keys ->
+ * n entries of hbls_pk_entry_bytes() (library layout) + a status byte each (0 = valid, else the
+ * key is undecodable or outside G1 and every partial under it gets HBLS_BAD_PUBKEY). */
+size_t hbls_pk_entry_bytes(void);
+int hbls_decompress_pubkeys_device(const uint8_t* pks, size_t n, void* table, uint8_t* status, void* stream);
+
 /* VerifyAggregate on device buffers: pks (48 B each), sigs (96 B per group), hm (one hashed message
  * per group, hbls_hash_to_g2_device), status (n_groups) are device pointers; grp_off is a HOST
  * array of n_groups + 1 non-decreasing offsets into pks (the reduction is planned from it). */
@@ -182,6 +188,14 @@ typedef struct hbls_slot {
   uint8_t* ta_status;
   const uint8_t* dv_pks;
   uint8_t* agg_vstatus;
+  /* Optional decompressed-key tables (hbls_decompress_pubkeys_device): when non-NULL the slot
+   * reads entry i of pk_table (status pk_table_st[i]) instead of decompressing pks[i], and
+   * entry g of dv_pk_table instead of dv_pks[g].  Pubshares are static per cluster lock, so a
+   * node decompresses and subgroup-checks them once (SURVEY.md 8e pubshare cache). */
+  const void* pk_table;
+  const uint8_t* pk_table_st;
+  const void* dv_pk_table;
+  const uint8_t* dv_pk_table_st;
 } hbls_slot;
 int hbls_slot_device(const hbls_slot* args, void* stream);
 /* Bytes of the `hm` table entry per message. */

@@ -82,7 +82,10 @@ def _pks(L, sks):
     return out
 
 
-def test_slot_adversarial_c2(L):
+@pytest.mark.parametrize("key_tables", [False, True], ids=["decompress", "key_tables"])
+def test_slot_adversarial_c2(L, key_tables):
+    """key_tables: the public keys come from tables made once by hbls_decompress_pubkeys_device
+    (the slot's pk_table / dv_pk_table) -- same verdicts and aggregates."""
     import torch
     from charon_amd import synth
     V, n, t = 10_000, 4, 3
@@ -174,6 +177,17 @@ def test_slot_adversarial_c2(L):
                          ta_out=_p(tout).value, ta_status=_p(tst).value, dv_pks=_p(d["dvpk"]).value,
                          agg_vstatus=_p(ast).value)
     s = torch.cuda.Stream(device=dev)
+    if key_tables:
+        E = L.hbls_pk_entry_bytes()
+        tabs = {"pk": torch.zeros(NP * E, dtype=torch.uint8, device=dev),
+                "pkst": torch.full((NP,), 255, dtype=torch.uint8, device=dev),
+                "dv": torch.zeros(V * E, dtype=torch.uint8, device=dev),
+                "dvst": torch.full((V,), 255, dtype=torch.uint8, device=dev)}
+        sp0 = ctypes.c_void_p(s.cuda_stream)
+        _chk(L, L.hbls_decompress_pubkeys_device(_p(d["pks"]), NP, _p(tabs["pk"]), _p(tabs["pkst"]), sp0))
+        _chk(L, L.hbls_decompress_pubkeys_device(_p(d["dvpk"]), V, _p(tabs["dv"]), _p(tabs["dvst"]), sp0))
+        slot.pk_table, slot.pk_table_st = _p(tabs["pk"]).value, _p(tabs["pkst"]).value
+        slot.dv_pk_table, slot.dv_pk_table_st = _p(tabs["dv"]).value, _p(tabs["dvst"]).value
     _chk(L, L.hbls_slot_device(ctypes.byref(slot), ctypes.c_void_p(s.cuda_stream)))
     s.synchronize()
     got = vst.cpu().numpy()
