@@ -32,7 +32,7 @@ EXPORTS = (
     "hbls_timing", "hbls_timing_read", "hbls_comm_id_bytes", "hbls_comm_unique_id", "hbls_comm_init",
     "hbls_allgather_device", "hbls_comm_destroy", "hbls_stats", "hbls_attestation_signing_roots",
     "hbls_signing_roots", "hbls_attestation_signing_roots_device", "hbls_pk_entry_bytes",
-    "hbls_decompress_pubkeys_device",
+    "hbls_decompress_pubkeys_device", "hbls_pubkey_cache_add", "hbls_pubkey_cache_clear", "hbls_pubkey_cache_size",
 )
 
 ALL_DEVICES = 0xFFFFFFFF
@@ -86,6 +86,9 @@ def _declare(lib):
         "hbls_attestation_signing_roots_device": ([P, SZ, P, SZ, P, P, P], ctypes.c_int),
         "hbls_pk_entry_bytes": ([], SZ),
         "hbls_decompress_pubkeys_device": ([P, SZ, P, P, P], ctypes.c_int),
+        "hbls_pubkey_cache_add": ([P, SZ], ctypes.c_int),
+        "hbls_pubkey_cache_clear": ([], ctypes.c_int),
+        "hbls_pubkey_cache_size": ([], SZ),
         "hbls_slot_device": ([ctypes.POINTER(HblsSlot), P], ctypes.c_int),
         "hbls_hm_entry_bytes": ([], SZ),
         "hbls_sync": ([P], ctypes.c_int),

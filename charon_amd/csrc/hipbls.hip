@@ -223,6 +223,10 @@ size_t env_size(const char* name, size_t dflt) {
 size_t g_gcap = 131072, g_fbcap = 65536, g_gmax = 16;
 // HBLS_RLC_MSM=0: one ladder per item (k_rlc) instead of shared-doubling chunks (k_rlc_msm)
 bool g_rlc_msm = true;
+// public-key cache: compressed key -> entry index (the same on every device)
+std::mutex g_kc_mu;
+std::unordered_map<std::string, uint32_t> g_kc_map;
+size_t g_kc_n = 0;
 // HBLS_TA_MSM=1: the aggregation as shared-doubling chunks (k_ta_msm) instead of one Straus ladder
 // per member (k_ta_straus).  Off: measured slower at C3 (per-member tables read across lanes
 // uncoalesced; fewer, longer lanes) -- 222.8 ms/slot with per-member ladders vs 224.2-227.8 with
@@ -264,7 +268,7 @@ struct Ws {
 };
 
 // host-call staging buffers (inputs and outputs of the host-buffer entry points)
-enum IoId { I_PK, I_SIG, I_MSG, I_OFF, I_LEN, I_MIDX, I_HM, I_STAT, I_IDX, I_GOFF, I_OUT, I_SK, I_VGOFF, I_COUNT };
+enum IoId { I_PK, I_SIG, I_MSG, I_OFF, I_LEN, I_MIDX, I_HM, I_STAT, I_IDX, I_GOFF, I_OUT, I_SK, I_VGOFF, I_KC, I_COUNT };
 
 constexpr int N_WS = 2;
 
@@ -285,6 +289,9 @@ struct Dev {
   // decompression beside the previous slot's combinations and pairings) instead of in lockstep
   hipEvent_t ev_dec = nullptr;
   bool dec_valid = false;
+  // public-key cache (hbls_pubkey_cache_add): decompressed entries + statuses, every device holds
+  // all g_kc_n of them
+  DevBuf kc_tab, kc_st;
   // timing (hbls_timing)
   bool timing = false;
   bool serial = false;  // timing mode 2: every timed launch completes before the next is enqueued
@@ -548,7 +555,7 @@ int ta_tail(Dev& d, Ws& w, const HmEntry* pts, const uint32_t* src, const uint8_
 
 int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, const uint32_t* didx,
                     const MsgEntry* hm, size_t n, const uint32_t* dgoff, size_t n_groups, uint8_t* dst,
-                    hipStream_t s, hipEvent_t hm_ready, const TaFold* fold) {
+                    hipStream_t s, hipEvent_t hm_ready, const TaFold* fold, const uint32_t* kc_idx = nullptr) {
   if (!dgoff) n_groups = n;
   G1AEntry* vpk;
   HmEntry* vsig;
@@ -588,6 +595,10 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
   if (fold && fold->pk_table) {
     vpk = const_cast<G1AEntry*>(fold->pk_table);
     vpkst = const_cast<uint8_t*>(fold->pk_table_st);
+  } else if (kc_idx) {  // host-buffer call with the key cache: cached entries, the rest decompressed
+    TIMED(d, "k_dec_pk", w.side[0],
+          launch_pk_gather(dpk, kc_idx, (const G1AEntry*)d.kc_tab.p, (const uint8_t*)d.kc_st.p, (uint32_t)n, vpk,
+                           vpkst, w.side[0]));
   } else {
     TIMED(d, "k_dec_pk", w.side[0], launch_dec_pk(dpk, (uint32_t)n, vpk, vpkst, w.side[0]));
   }
@@ -855,6 +866,23 @@ int for_each_device(size_t n_units, const std::function<int(Dev&, size_t, size_t
 
 // Verify n host-buffer items (tbls.Verify per item): items are ordered by message and grouped
 // (at most g_gmax per group), the groups sharded over the devices, statuses scattered back.
+// Cache indices of m packed compressed keys (0xffffffff: not cached).  false when the cache is
+// empty or holds none of them (the call then decompresses every key).
+bool kc_lookup(const uint8_t* pks, size_t m, std::vector<uint32_t>& idx) {
+  std::lock_guard<std::mutex> lk(g_kc_mu);
+  if (g_kc_map.empty()) return false;
+  idx.assign(m, 0xffffffffu);
+  bool any = false;
+  for (size_t k = 0; k < m; k++) {
+    auto it = g_kc_map.find(std::string((const char*)pks + 48 * k, 48));
+    if (it != g_kc_map.end()) {
+      idx[k] = it->second;
+      any = true;
+    }
+  }
+  return any;
+}
+
 int verify_host(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msgs, const uint64_t* msg_off,
                 const uint32_t* msg_len, size_t n, uint8_t* status) {
   if (n == 0) return 0;
@@ -884,15 +912,18 @@ int verify_host(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msgs, co
     MsgEntry* hm;
     if (hash_table(d, t, &hm, true)) return -1;
     uint8_t *dpk, *dsig, *dst;
-    uint32_t *didx, *dgoff;
+    uint32_t *didx, *dgoff, *dkc = nullptr;
     if (upload(d, I_PK, hpk.data(), hpk.size(), &dpk) || upload(d, I_SIG, hsig.data(), hsig.size(), &dsig) ||
         upload(d, I_MIDX, t.idx.data(), m, &didx) || upload(d, I_VGOFF, goff.data(), goff.size(), &dgoff))
       return -1;
+    std::vector<uint32_t> kc;
+    if (kc_lookup(hpk.data(), m, kc) && upload(d, I_KC, kc.data(), m, &dkc)) return -1;
     void* p;
     if (ensure_buf(d.io[I_STAT], m, &p)) return -1;
     dst = (uint8_t*)p;
     Ws& w = ws_acquire(d, d.stream);
-    if (verify_pipeline(d, w, dpk, dsig, didx, hm, m, dgoff, ge - gb, dst, d.stream, nullptr, nullptr)) return -1;
+    if (verify_pipeline(d, w, dpk, dsig, didx, hm, m, dgoff, ge - gb, dst, d.stream, nullptr, nullptr, dkc))
+      return -1;
     if (ws_release(w, d.stream)) return -1;
     std::vector<uint8_t> hst(m);
     HCHK(hipMemcpyAsync(hst.data(), dst, m, hipMemcpyDeviceToHost, d.stream));
@@ -1378,6 +1409,62 @@ int hbls_verify_device(const uint8_t* pks, const uint8_t* sigs, const uint32_t* 
 }
 
 size_t hbls_pk_entry_bytes(void) { return sizeof(G1AEntry); }
+
+int hbls_pubkey_cache_add(const uint8_t* pks, size_t n) {
+  if (ensure_init()) return -1;
+  std::lock_guard<std::mutex> lk(g_kc_mu);
+  std::vector<uint8_t> fresh;
+  std::unordered_map<std::string, uint32_t> add;
+  for (size_t k = 0; k < n; k++) {
+    std::string key((const char*)pks + 48 * k, 48);
+    if (g_kc_map.count(key) || add.count(key)) continue;
+    add.emplace(key, (uint32_t)(g_kc_n + add.size()));
+    fresh.insert(fresh.end(), pks + 48 * k, pks + 48 * k + 48);
+  }
+  const size_t m = add.size();
+  if (m == 0) return 0;
+  if (g_kc_n + m > 0xffffffffull) return set_err("pubkey cache full");
+  for (Dev* dp : g_devs) {
+    Dev& d = *dp;
+    std::lock_guard<std::mutex> dl(d.mu);
+    HCHK(hipSetDevice(d.ord));
+    const size_t tot = g_kc_n + m;
+    if (d.kc_tab.cap < tot * sizeof(G1AEntry) || d.kc_st.cap < tot) {  // grow, keeping the old entries
+      DevBuf nt, ns;
+      void* p;
+      if (ensure_buf(nt, tot * sizeof(G1AEntry), &p) || ensure_buf(ns, tot, &p)) return -1;
+      if (g_kc_n) {
+        HCHK(hipMemcpyAsync(nt.p, d.kc_tab.p, g_kc_n * sizeof(G1AEntry), hipMemcpyDeviceToDevice, d.stream));
+        HCHK(hipMemcpyAsync(ns.p, d.kc_st.p, g_kc_n, hipMemcpyDeviceToDevice, d.stream));
+        HCHK(hipStreamSynchronize(d.stream));
+      }
+      if (d.kc_tab.p) HCHK(hipFree(d.kc_tab.p));
+      if (d.kc_st.p) HCHK(hipFree(d.kc_st.p));
+      d.kc_tab = nt;
+      d.kc_st = ns;
+    }
+    uint8_t* dpk;
+    if (upload(d, I_PK, fresh.data(), fresh.size(), &dpk)) return -1;
+    TIMED(d, "k_dec_pk", d.stream,
+          launch_dec_pk(dpk, (uint32_t)m, (G1AEntry*)d.kc_tab.p + g_kc_n, (uint8_t*)d.kc_st.p + g_kc_n, d.stream));
+    HCHK(hipStreamSynchronize(d.stream));
+  }
+  for (auto& kv : add) g_kc_map.emplace(kv.first, kv.second);
+  g_kc_n += m;
+  return 0;
+}
+
+int hbls_pubkey_cache_clear(void) {
+  std::lock_guard<std::mutex> lk(g_kc_mu);
+  g_kc_map.clear();
+  g_kc_n = 0;
+  return 0;
+}
+
+size_t hbls_pubkey_cache_size(void) {
+  std::lock_guard<std::mutex> lk(g_kc_mu);
+  return g_kc_n;
+}
 
 int hbls_decompress_pubkeys_device(const uint8_t* pks, size_t n, void* table, uint8_t* status, void* stream) {
   Dev* d;

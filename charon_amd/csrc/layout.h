@@ -138,6 +138,8 @@ void launch_pair3(const Pair3Args& a, hipStream_t s);
 void launch_item_group(const uint32_t* grp_off, uint32_t n_groups, uint32_t n, uint32_t* item_grp, hipStream_t s);
 void launch_dec_pk(const uint8_t* pks, uint32_t n, G1AEntry* out, uint8_t* st, hipStream_t s);
 void launch_dec_sig_pt(const uint8_t* sigs, uint32_t n, HmEntry* out, uint8_t* st, hipStream_t s);
+void launch_pk_gather(const uint8_t* pks, const uint32_t* idx, const G1AEntry* tab, const uint8_t* tst, uint32_t n,
+                      G1AEntry* out, uint8_t* st, hipStream_t s);
 // Chunk plans and the multi-scalar random linear combination (vbatch.hip k_plan_*, k_rlc_msm).
 constexpr uint32_t RLC_CHUNK = 16;  // items per lane of k_rlc_msm
 struct RlcMsmArgs {

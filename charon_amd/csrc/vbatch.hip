@@ -80,6 +80,31 @@ __global__ KB_OCC(HB_OCC_DECSIG) void k_dec_sig_pt(const uint8_t* __restrict__ s
   st[i] = bad;
 }
 
+// One lane per public key of a host-buffer call with a key cache (hbls_pubkey_cache_add): the
+// cached entry when idx[i] names one, else decompressed here like k_dec_pk.
+__global__ KB_OCC(HB_OCC_DECPK) void k_pk_gather(const uint8_t* __restrict__ pks, const uint32_t* __restrict__ idx,
+                                                 const G1AEntry* __restrict__ tab, const uint8_t* __restrict__ tst,
+                                                 uint32_t n, G1AEntry* __restrict__ out, uint8_t* __restrict__ st) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t k = idx[i];
+  if (k != 0xffffffffu) {
+    out[i] = tab[k];
+    st[i] = tst[k];
+    return;
+  }
+  G1A p;
+  uint8_t bad = g1_decompress(p, pks + 48ull * i);
+  if (bad) p = {fp_zero(), fp_zero(), true};
+  G1AEntry e;
+  e.x = p.x;
+  e.y = p.y;
+  e.inf = p.inf ? 1u : 0u;
+  e.pad[0] = e.pad[1] = e.pad[2] = 0;
+  out[i] = e;
+  st[i] = bad;
+}
+
 // the random coefficient r = a + b lambda of entry `item` (SHA-256 of key || item, one block)
 __device__ __forceinline__ void rlc_coeffs(const RlcKey& key, uint32_t item, uint32_t& a, uint32_t& b) {
   uint32_t w[16];
@@ -326,6 +351,10 @@ void launch_item_group(const uint32_t* grp_off, uint32_t n_groups, uint32_t n, u
 }
 void launch_dec_pk(const uint8_t* pks, uint32_t n, G1AEntry* out, uint8_t* st, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_dec_pk, dim3(blocks_for(n)), dim3(BLOCK), 0, s, pks, n, out, st);
+}
+void launch_pk_gather(const uint8_t* pks, const uint32_t* idx, const G1AEntry* tab, const uint8_t* tst, uint32_t n,
+                      G1AEntry* out, uint8_t* st, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_pk_gather, dim3(blocks_for(n)), dim3(BLOCK), 0, s, pks, idx, tab, tst, n, out, st);
 }
 void launch_dec_sig_pt(const uint8_t* sigs, uint32_t n, HmEntry* out, uint8_t* st, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_dec_sig_pt, dim3(blocks_for(n)), dim3(BLOCK), 0, s, sigs, n, out, st);

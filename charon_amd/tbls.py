@@ -157,6 +157,18 @@ class HIPBLS:
             raise TblsError("cannot recover full private key from partial keys")
         return out.raw
 
+    def cache_pubkeys(self, pks: Sequence[bytes]) -> int:
+        """Add public keys to the library's key cache (hbls_pubkey_cache_add): later verifications
+        take them decompressed and subgroup-checked from it.  charon would add its cluster lock's
+        pubshares at startup.  Returns the number of cached keys."""
+        blob = b"".join(_need(p, PUBKEY_LEN, "public key") for p in pks)
+        if blob:
+            check(self._L.hbls_pubkey_cache_add(_buf(blob), len(pks)))
+        return int(self._L.hbls_pubkey_cache_size())
+
+    def clear_pubkey_cache(self) -> None:
+        check(self._L.hbls_pubkey_cache_clear())
+
     # ------------------------------------------------------------------ signatures
     def sign(self, private_key: bytes, data: bytes) -> bytes:
         """herumi.go:306-316."""

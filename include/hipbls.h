@@ -99,6 +99,15 @@ int hbls_attestation_signing_roots(const uint8_t* data, size_t n, const uint8_t*
 int hbls_signing_roots(const uint8_t* object_roots, size_t n, const uint8_t* domains, size_t n_domains,
                        const uint32_t* dom_idx, uint8_t* roots);
 
+/* Public-key cache for the host-buffer verification (hbls_verify_batch): keys added here are
+ * decompressed and subgroup-checked once, on every device of the mask; later calls take cached
+ * keys from the cache and decompress only the others.  charon adds every pubshare of its cluster
+ * lock at startup (cluster/lock.go; the keys never change while it runs).  Statuses and verdicts
+ * are unchanged: an undecodable cached key still yields HBLS_BAD_PUBKEY. */
+int hbls_pubkey_cache_add(const uint8_t* pks, size_t n);
+int hbls_pubkey_cache_clear(void);
+size_t hbls_pubkey_cache_size(void);
+
 /* Sign (herumi.go:306-316) and SecretToPublicKey (herumi.go:66-79), batched.
  * Sign status in {OK, BAD_SECRET}; SecretToPublicKey additionally rejects the zero key. */
 int hbls_sign_batch(const uint8_t* sks, const uint8_t* msgs, const uint64_t* msg_off,

@@ -427,3 +427,29 @@ def test_verify_aggregate_lock_scale(L):
     from oracle import bls12381 as B
     for g in (1, 2, 3, 6):
         assert B.verify_aggregate(groups[g][0], groups[g][1], groups[g][2]) == expect[g], g
+
+
+def test_pubkey_cache_same_verdicts(hipbls):
+    """Verification with the key cache (hbls_pubkey_cache_add) gives the verdicts of the uncached
+    path: cached valid keys, cached undecodable / off-curve keys, uncached keys, mixed in one batch."""
+    rng = random.Random(31)
+    keys = [hipbls.generate_secret_key() for _ in range(40)]
+    msgs = [hashlib.sha256(b"cache %d" % (k % 4)).digest() for k in range(40)]
+    sigs = hipbls.sign_batch(keys, msgs)
+    pks = [hipbls.secret_to_public_key(k) for k in keys]
+    bad_x = bytes([0x9A]) + b"\xff" * 47           # x >= p
+    bad_flag = bytes([0x1A]) + pks[3][1:]           # compression flag missing
+    items = [(pks[i], msgs[i], sigs[i]) for i in range(40)]
+    items[5] = (bad_x, msgs[5], sigs[5])
+    items[6] = (bad_flag, msgs[6], sigs[6])
+    items[7] = (pks[8], msgs[7], sigs[7])            # wrong key
+    items[9] = (pks[9], msgs[9], sigs[10])           # wrong signature
+    rng.shuffle(items)
+    P, M, S = zip(*items)
+    hipbls.clear_pubkey_cache()
+    plain = hipbls.verify_batch(P, M, S)
+    assert hipbls.cache_pubkeys(pks[:25] + [bad_x, bad_flag]) == 27
+    cached = hipbls.verify_batch(P, M, S)
+    hipbls.clear_pubkey_cache()
+    assert cached == plain
+    assert sorted(plain).count(0) == 36
