@@ -223,6 +223,7 @@ size_t env_size(const char* name, size_t dflt) {
 size_t g_gcap = 131072, g_fbcap = 65536, g_gmax = 16;
 // HBLS_RLC_MSM=0: one ladder per item (k_rlc) instead of shared-doubling chunks (k_rlc_msm)
 bool g_rlc_msm = true;
+size_t g_rlc_lanes = 65536;   // HBLS_RLC_LANES: lanes the chunk size aims to keep busy
 // public-key cache: compressed key -> entry index (the same on every device)
 std::mutex g_kc_mu;
 std::unordered_map<std::string, uint32_t> g_kc_map;
@@ -425,6 +426,7 @@ int init_mask(uint32_t mask) {
   g_fbcap = env_size("HBLS_FALLBACK_CHUNK", g_fbcap);
   g_gmax = std::max<size_t>(1, env_size("HBLS_GROUP_MAX", g_gmax));
   g_rlc_msm = env_size("HBLS_RLC_MSM", 1) != 0;
+  g_rlc_lanes = std::max<size_t>(1, env_size("HBLS_RLC_LANES", g_rlc_lanes));
   g_ta_msm = env_size("HBLS_TA_MSM", 0) != 0;
   g_ta_chunk = std::min<size_t>(TA_CHUNK, std::max<size_t>(1, env_size("HBLS_TA_CHUNK", g_ta_chunk)));
   std::vector<Dev*> devs;
@@ -641,9 +643,12 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
   HCHK(hipEventRecord(d.ev_dec, s));
   d.dec_valid = true;
   TIMED(d, "k_item_group", s, launch_item_group(dgoff, (uint32_t)n_groups, (uint32_t)n, igrp, s));
-  if (dgoff && g_rlc_msm) {
-    // chunks of at most RLC_CHUNK items of a group share their ladders' doublings (k_rlc_msm)
-    const size_t max_chunks = n / RLC_CHUNK + n_groups;
+  const uint32_t rlc_cmax = (uint32_t)std::min<size_t>(RLC_CHUNK, std::max<size_t>(1, n / g_rlc_lanes));
+  if (dgoff && g_rlc_msm && rlc_cmax > 1) {
+    // chunks of a group's items share their ladders' doublings (k_rlc_msm); the chunk size keeps
+    // about g_rlc_lanes lanes busy (at most RLC_CHUNK items, one item per lane for small calls)
+    const uint32_t cmax = rlc_cmax;
+    const size_t max_chunks = n / cmax + n_groups;
     uint32_t *pcnt, *pcoff, *pcf, *pcc;
     uint2* coef;
     G1J* t1;
@@ -652,7 +657,7 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
         wsbuf(w, W_PCFIRST, max_chunks, &pcf) || wsbuf(w, W_PCCOUNT, max_chunks, &pcc) ||
         wsbuf(w, W_COEF, n, &coef) || wsbuf(w, W_RT1, 3 * n, &t1) || wsbuf(w, W_RT2, 3 * n, &t2))
       return -1;
-    TIMED(d, "k_plan", s, launch_plan(dgoff, (uint32_t)n_groups, RLC_CHUNK, pcnt, pcoff, pcf, pcc, s));
+    TIMED(d, "k_plan", s, launch_plan(dgoff, (uint32_t)n_groups, cmax, pcnt, pcoff, pcf, pcc, s));
     RlcMsmArgs ra{};
     ra.pk = vpk;
     ra.pk_st = vpkst;

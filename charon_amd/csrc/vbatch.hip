@@ -160,8 +160,8 @@ __global__ KB_OCC(HB_OCC_RLC) void k_rlc(const G1AEntry* __restrict__ pk, const 
 }
 
 // ---------------------------------------------------------------------------------------
-// Chunk plans: the items of every group [grp_off[g], grp_off[g+1]) cut into chunks of at most
-// cmax consecutive items (group g's chunks are coff[g] .. coff[g+1]-1; chunk c covers
+// Chunk plans: the items of every group [grp_off[g], grp_off[g+1]) cut into ceil(size / cmax)
+// nearly equal chunks of consecutive items (group g's chunks are coff[g] .. coff[g+1]-1; chunk c covers
 // cfirst[c] .. cfirst[c] + (ccount[c] & 0x7fffffff) - 1; bit 31 of ccount marks a group of ONE
 // item).  A chunk is one lane of the multi-scalar kernels below, which share the doublings of a
 // ladder over the chunk's items.
@@ -202,11 +202,12 @@ __global__ KB void k_plan_fill(const uint32_t* __restrict__ grp_off, uint32_t ng
                                uint32_t* __restrict__ ccount) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= ng) return;
+  // the group's items split into nc nearly equal chunks (a wave's lanes then run equal loops)
   const uint32_t b = grp_off[g], sz = grp_off[g + 1] - b, c0 = coff[g], nc = coff[g + 1] - c0;
   for (uint32_t k = 0; k < nc; k++) {
-    cfirst[c0 + k] = b + k * cmax;
-    const uint32_t left = sz - k * cmax;
-    ccount[c0 + k] = (left < cmax ? left : cmax) | (sz == 1 ? 0x80000000u : 0u);
+    const uint32_t lo = (uint32_t)((uint64_t)k * sz / nc), hi = (uint32_t)((uint64_t)(k + 1) * sz / nc);
+    cfirst[c0 + k] = b + lo;
+    ccount[c0 + k] = (hi - lo) | (sz == 1 ? 0x80000000u : 0u);
   }
 }
 
