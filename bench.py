@@ -573,7 +573,13 @@ def main(argv=None):
     # mode) one ladder each
     rlc_item = opcounts.BLOCKS["rlc_g1"] + opcounts.BLOCKS["rlc_g2"]
     n_rlc = NP + (0 if staged else V)
-    rlc_avg = (NP * per_unit["k_rlc"][0] + (0 if staged else V) * rlc_item) / n_rlc
+    cmax = min(opcounts.RLC_CHUNK, max(1, NP // int(os.environ.get("HBLS_RLC_LANES", "65536"))))
+    if cmax > 1:  # the library's chunking (hipbls.hip verify_pipeline): balanced chunks of a group
+        n_chunks = -(-n // cmax)
+        rlc_partial = opcounts.rlc_msm(chunk=n / n_chunks)
+    else:
+        rlc_partial = rlc_item
+    rlc_avg = (NP * rlc_partial + (0 if staged else V) * rlc_item) / n_rlc
     units = {"k_pair3": (V, per_unit["k_pair3"]), "k_rlc": (n_rlc, (rlc_avg, rlc_avg)),
              "k_dec_pk": (NP + (0 if staged else V), per_unit["k_dec_pk"]),
              "k_dec_sig_pt": (NP + (ta_units if staged else 0), per_unit["k_dec_sig_pt"]),
