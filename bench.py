@@ -354,6 +354,16 @@ def _lib_timing(L):
     return _lib.timing_read(L)
 
 
+def traffic_of(kernel):
+    """HBM bytes per launch of `kernel` (FETCH_SIZE x2 + WRITE_SIZE) from the committed PMC pass,
+    or None (rocprofv3 counters cannot be read from inside the timed run)."""
+    try:
+        k = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))["kernels"].get(kernel)
+        return round(k["bytes_per_launch"]) if k else None
+    except (OSError, ValueError, KeyError):
+        return None
+
+
 def roofline_from_timing(recs, steps, units):
     """Per-kernel totals over the timed steps; the dominant kernel's roofline entry."""
     tot, cnt = {}, {}
@@ -538,16 +548,6 @@ def main(argv=None):
     recs_overlapped = _lib.timing_read(L)
     _chk(L, L.hbls_timing(0))
 
-    # per-kernel roofline: the same slot once more with every kernel ALONE on the device (timing
-    # mode 2 serialises the launches), after the timed region -- overlapped launches of two slots
-    # in flight share the chip and their durations say nothing about one kernel
-    torch.cuda.synchronize()
-    _chk(L, L.hbls_timing(2))
-    step(mk())
-    torch.cuda.synchronize()
-    recs = _lib.timing_read(L)
-    _chk(L, L.hbls_timing(0))
-
     # parity of the timed outputs: every partial verifies, every aggregate is byte-identical to the
     # root-key signature (tbls_test.go:72-97 property) and verifies under the DV key
     used = outs if not staged else outs[:1]
@@ -567,50 +567,64 @@ def main(argv=None):
     ms_per_step = elapsed / args.steps * 1e3
     value = items / (elapsed / args.steps)
 
-    per_unit = opcounts.per_unit(group_size=n, t=t)
-    ta_units = V * t
-    # k_rlc: the partials as multi-scalar chunks (one per validator), the folded aggregates (slot
-    # mode) one ladder each
-    rlc_item = opcounts.BLOCKS["rlc_g1"] + opcounts.BLOCKS["rlc_g2"]
-    n_rlc = NP + (0 if staged else V)
-    cmax = min(opcounts.RLC_CHUNK, max(1, NP // int(os.environ.get("HBLS_RLC_LANES", "65536"))))
-    if cmax > 1:  # the library's chunking (hipbls.hip verify_pipeline): balanced chunks of a group
-        n_chunks = -(-n // cmax)
-        rlc_partial = opcounts.rlc_msm(chunk=n / n_chunks)
-    else:
-        rlc_partial = rlc_item
-    rlc_avg = (NP * rlc_partial + (0 if staged else V) * rlc_item) / n_rlc
-    units = {"k_pair3": (V, per_unit["k_pair3"]), "k_rlc": (n_rlc, (rlc_avg, rlc_avg)),
-             "k_dec_pk": (NP + (0 if staged else V), per_unit["k_dec_pk"]),
-             "k_dec_sig_pt": (NP + (ta_units if staged else 0), per_unit["k_dec_sig_pt"]),
-             "k_group_prep": (V, opcounts.per_unit(group_size=n + (0 if staged else 1), t=t)["k_group_prep"]),
-             "k_ta_straus": (ta_units, per_unit["k_ta_straus"]), "k_group_sum": (V, per_unit["k_group_sum"]),
-             "k_hash_to_g2": (M, per_unit["k_hash_to_g2"]), "k_lines_msg": (M, per_unit["k_lines_msg"])}
-    dom, per = roofline_from_timing(recs, 1, units)
-    # the whole slot: every kernel's algorithmic work over the measured step time
-    slot_fpmul = sum(u * w[0] for u, w in units.values())
-    slot_tops = slot_fpmul * opcounts.MAC_PER_FPMUL / (elapsed / args.steps) / 1e12
-    pair = per.get("k_pair3")
-    roofline = None
-    if dom:
-        x = per[dom]
-        roofline = {"bound": "valu", "kernel": dom, "unit_of_work": opcounts.UNITS.get(dom),
-                    "achieved": x["achieved_Tops_alg"], "peak": opcounts.PEAK_MAD_TOPS,
-                    "unit": "Tops/s (32-bit multiply-add lane-ops, v_mad_u64_u32)",
-                    "frac": round(x["achieved_Tops_alg"] / opcounts.PEAK_MAD_TOPS, 4),
-                    "frac_executed": round(x["achieved_Tops_exec"] / opcounts.PEAK_MAD_TOPS, 4),
-                    "frac_vs_nominal_clock": round(x["achieved_Tops_alg"] / opcounts.PEAK_MAD_TOPS_NOMINAL, 4),
-                    "traffic": None,
-                    "algorithmic_work": f"{x['units_per_step']} units x {x['fpmul_per_unit_alg']} Fp-mul x "
-                                        f"{opcounts.MAC_PER_FPMUL} MAC per step (executed {x['fpmul_per_unit_exec']} "
-                                        f"Fp-mul per unit)",
-                    "kernel_ms_alone": x["ms_per_step"],
-                    "timing": "HIP events around each launch on its stream, kernels serialised (one extra "
-                              "slot after the timed region, library timing mode 2)",
-                    "slot": {"fpmul_alg_per_step": slot_fpmul, "achieved": round(slot_tops, 3),
-                             "frac": round(slot_tops / opcounts.PEAK_MAD_TOPS, 4),
-                             "note": "all kernels' algorithmic work over ms_per_step (two slots in flight)"},
-                    "k_pair3": pair}
+    def kernel_roofline():
+        # per-kernel roofline: the same slot once more with every kernel ALONE on the device
+        # (timing mode 2 serialises the launches), after every other measurement -- overlapped
+        # launches of two slots in flight share the chip and their durations say nothing about one
+        # kernel; as the last slot of the run it is also the last one in a rocprofv3 trace
+        torch.cuda.synchronize()
+        _chk(L, L.hbls_timing(2))
+        step(mk())
+        torch.cuda.synchronize()
+        recs = _lib.timing_read(L)
+        _chk(L, L.hbls_timing(0))
+        per_unit = opcounts.per_unit(group_size=n, t=t)
+        ta_units = V * t
+        # k_rlc: the partials as multi-scalar chunks (one per validator), the folded aggregates (slot
+        # mode) one ladder each
+        rlc_item = opcounts.BLOCKS["rlc_g1"] + opcounts.BLOCKS["rlc_g2"]
+        n_rlc = NP + (0 if staged else V)
+        cmax = min(opcounts.RLC_CHUNK, max(1, NP // int(os.environ.get("HBLS_RLC_LANES", "65536"))))
+        if cmax > 1:  # the library's chunking (hipbls.hip verify_pipeline): balanced chunks of a group
+            n_chunks = -(-n // cmax)
+            rlc_partial = opcounts.rlc_msm(chunk=n / n_chunks)
+        else:
+            rlc_partial = rlc_item
+        rlc_avg = (NP * rlc_partial + (0 if staged else V) * rlc_item) / n_rlc
+        units = {"k_pair3": (V, per_unit["k_pair3"]), "k_rlc": (n_rlc, (rlc_avg, rlc_avg)),
+                 "k_dec_pk": (NP + (0 if staged else V), per_unit["k_dec_pk"]),
+                 "k_dec_sig_pt": (NP + (ta_units if staged else 0), per_unit["k_dec_sig_pt"]),
+                 "k_group_prep": (V, opcounts.per_unit(group_size=n + (0 if staged else 1), t=t)["k_group_prep"]),
+                 "k_ta_straus": (ta_units, per_unit["k_ta_straus"]), "k_group_sum": (V, per_unit["k_group_sum"]),
+                 "k_hash_to_g2": (M, per_unit["k_hash_to_g2"]), "k_lines_msg": (M, per_unit["k_lines_msg"])}
+        dom, per = roofline_from_timing(recs, 1, units)
+        # the whole slot: every kernel's algorithmic work over the measured step time
+        slot_fpmul = sum(u * w[0] for u, w in units.values())
+        slot_tops = slot_fpmul * opcounts.MAC_PER_FPMUL / (elapsed / args.steps) / 1e12
+        pair = per.get("k_pair3")
+        roofline = None
+        if dom:
+            x = per[dom]
+            roofline = {"bound": "valu", "kernel": dom, "unit_of_work": opcounts.UNITS.get(dom),
+                        "achieved": x["achieved_Tops_alg"], "peak": opcounts.PEAK_MAD_TOPS,
+                        "unit": "Tops/s (32-bit multiply-add lane-ops, v_mad_u64_u32)",
+                        "frac": round(x["achieved_Tops_alg"] / opcounts.PEAK_MAD_TOPS, 4),
+                        "frac_executed": round(x["achieved_Tops_exec"] / opcounts.PEAK_MAD_TOPS, 4),
+                        "frac_vs_nominal_clock": round(x["achieved_Tops_alg"] / opcounts.PEAK_MAD_TOPS_NOMINAL, 4),
+                        "traffic": traffic_of(dom),
+                        "traffic_source": "profiles/pmc_traffic.json (PMC pass of this build, per launch)",
+                        "algorithmic_work": f"{x['units_per_step']} units x {x['fpmul_per_unit_alg']} Fp-mul x "
+                                            f"{opcounts.MAC_PER_FPMUL} MAC per step (executed {x['fpmul_per_unit_exec']} "
+                                            f"Fp-mul per unit)",
+                        "kernel_ms_alone": x["ms_per_step"],
+                        "timing": "HIP events around each launch on its stream, kernels serialised (one extra "
+                                  "slot after the timed region, library timing mode 2)",
+                        "slot": {"fpmul_alg_per_step": slot_fpmul, "achieved": round(slot_tops, 3),
+                                 "frac": round(slot_tops / opcounts.PEAK_MAD_TOPS, 4),
+                                 "note": "all kernels' algorithmic work over ms_per_step (two slots in flight)"},
+                        "k_pair3": pair}
+        return per, roofline
+
     # whole-slot effective rate against the r01 (herumi-equivalent, one pairing per partial) work
     verify_effective = world * NP * opcounts.FPMUL_PER_ITEM_R01["verify"] * opcounts.MAC_PER_FPMUL / \
         (elapsed / args.steps) / 1e12
@@ -633,8 +647,8 @@ def main(argv=None):
                       "threshold_aggregate": round(k_ms[2], 3)} if staged else
                      {"slot": round(k_ms[0], 3), "allgather": round(k_ms[1], 3)}),
         "verify_whole_effective_Tops_vs_r01_work": round(verify_effective, 3),
-        "kernels": per,
-        "parity": parity, "roofline": roofline, "cpu_baseline": None,
+        "kernels": None,
+        "parity": parity, "roofline": None, "cpu_baseline": None,
     }
 
     if args.host_api and rank == 0:
@@ -652,6 +666,8 @@ def main(argv=None):
 
     if rank == 0 and world == 1 and args.key_tables and not staged:
         out["with_key_tables"] = key_table_slots(L, d_pk, d_dvpk, outs, NP, V, args.steps, step_slot, mk, items)
+
+    out["kernels"], out["roofline"] = kernel_roofline()
 
     if rank == 0 and world == 1 and args.aggregate_verify:
         out["verify_aggregate"] = aggregate_verify(L, d, d_pk, dev, sp)
