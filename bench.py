@@ -355,11 +355,11 @@ def _lib_timing(L):
 
 
 def traffic_of(kernel):
-    """HBM bytes per launch of `kernel` (FETCH_SIZE x2 + WRITE_SIZE) from the committed PMC pass,
-    or None (rocprofv3 counters cannot be read from inside the timed run)."""
+    """HBM bytes per slot of `kernel` (all its launches, FETCH_SIZE x2 + WRITE_SIZE) from the
+    committed PMC pass, or None (rocprofv3 counters cannot be read from inside the timed run)."""
     try:
         k = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))["kernels"].get(kernel)
-        return round(k["bytes_per_launch"]) if k else None
+        return round(k["bytes_per_slot"]) if k else None
     except (OSError, ValueError, KeyError):
         return None
 
@@ -612,7 +612,8 @@ def main(argv=None):
                         "frac_executed": round(x["achieved_Tops_exec"] / opcounts.PEAK_MAD_TOPS, 4),
                         "frac_vs_nominal_clock": round(x["achieved_Tops_alg"] / opcounts.PEAK_MAD_TOPS_NOMINAL, 4),
                         "traffic": traffic_of(dom),
-                        "traffic_source": "profiles/pmc_traffic.json (PMC pass of this build, per launch)",
+                        "traffic_source": "profiles/pmc_traffic.json (PMC pass of this build; bytes per step, "
+                                          "like achieved)",
                         "algorithmic_work": f"{x['units_per_step']} units x {x['fpmul_per_unit_alg']} Fp-mul x "
                                             f"{opcounts.MAC_PER_FPMUL} MAC per step (executed {x['fpmul_per_unit_exec']} "
                                             f"Fp-mul per unit)",
