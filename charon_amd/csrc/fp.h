@@ -324,13 +324,24 @@ __device__ __noinline__ static u32x12 fp_sqr_leaf(u32x12 a) {
   return o;
 }
 typedef uint32_t u32x24 __attribute__((ext_vector_type(24)));
-__device__ __noinline__ static u32x24 fp2_mul_leaf(u32x24 a, u32x24 b) {
+// The Fp2 product has 48 argument dwords; the calling convention passes 32 in VGPRs and the rest
+// on the scratch stack (dword stores and loads around every call).  The second operand therefore
+// travels through this per-lane LDS slot instead (k-major pairs: conflict-free 64-bit accesses).
+// Every kernel runs 64-lane workgroups, one wave each (BLOCK / dim3(64) at every launch).
+__shared__ uint2 hb_fp2_arg[12 * 64];
+__device__ __noinline__ static u32x24 fp2_mul_leaf(u32x24 a) {
   uint32_t x0[12], x1[12], y0[12], y1[12], r0[12], r1[12];
+  const uint32_t lane = threadIdx.x & 63u;
+  HB_UNROLL for (int k = 0; k < 6; k++) {
+    const uint2 v = hb_fp2_arg[k * 64 + lane], w = hb_fp2_arg[(6 + k) * 64 + lane];
+    y0[2 * k] = v.x;
+    y0[2 * k + 1] = v.y;
+    y1[2 * k] = w.x;
+    y1[2 * k + 1] = w.y;
+  }
   HB_UNROLL for (int i = 0; i < 12; i++) {
     x0[i] = a[i];
     x1[i] = a[12 + i];
-    y0[i] = b[i];
-    y1[i] = b[12 + i];
   }
   fp2_mul_core(r0, r1, x0, x1, y0, y1);
   u32x24 o;
@@ -355,14 +366,17 @@ __device__ __noinline__ static u32x24 fp2_sqr_leaf(u32x24 a) {
   return o;
 }
 HD void fp2_mul_pair(Fp& r0, Fp& r1, const Fp& a0, const Fp& a1, const Fp& b0, const Fp& b1) {
-  u32x24 av, bv;
+  u32x24 av;
   HB_UNROLL for (int i = 0; i < NL; i++) {
     av[i] = a0.v[i];
     av[12 + i] = a1.v[i];
-    bv[i] = b0.v[i];
-    bv[12 + i] = b1.v[i];
   }
-  u32x24 rv = fp2_mul_leaf(av, bv);
+  const uint32_t lane = threadIdx.x & 63u;
+  HB_UNROLL for (int k = 0; k < 6; k++) {
+    hb_fp2_arg[k * 64 + lane] = make_uint2(b0.v[2 * k], b0.v[2 * k + 1]);
+    hb_fp2_arg[(6 + k) * 64 + lane] = make_uint2(b1.v[2 * k], b1.v[2 * k + 1]);
+  }
+  u32x24 rv = fp2_mul_leaf(av);
   HB_UNROLL for (int i = 0; i < NL; i++) {
     r0.v[i] = rv[i];
     r1.v[i] = rv[12 + i];
