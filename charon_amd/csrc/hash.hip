@@ -8,6 +8,8 @@
 // exhausted the device's scratch with two slots in flight.
 #include "layout.h"
 
+#include <stdlib.h>
+
 namespace hb {
 
 constexpr int BLOCK = 64;
@@ -52,10 +54,41 @@ __global__ KB_OCC(HB_OCC_HASH) void k_hash_to_g2(const uint8_t* __restrict__ msg
 }
 
 
+// One lane per distinct message (hash_to_g2, h2c.h): the same result with no idle partner lane
+// during the cofactor clearing and no duplicated expand_message -- fewer lane-cycles per
+// message, half the lanes.  Used when the call has enough messages to fill the chip.
+__global__ KB_OCC(HB_OCC_HASH) void k_hash_to_g2_1(const uint8_t* __restrict__ msgs, const uint64_t* __restrict__ off,
+                                                   const uint32_t* __restrict__ len, uint32_t n,
+                                                   MsgEntry* __restrict__ hm) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  G2A h = jac_to_aff(hash_to_g2(msgs + off[i], len[i]));
+  HmEntry e;
+  e.x = h.x;
+  e.y = h.y;
+  e.inf = h.inf ? 1u : 0u;
+  e.pad[0] = e.pad[1] = e.pad[2] = 0;
+  hm[i].h = e;
+}
+
+// messages from which one lane per message fills the chip (HBLS_HASH_ONE_LANE, default 65536)
+static size_t hash_one_lane_min() {
+  static const size_t v = [] {
+    const char* e = getenv("HBLS_HASH_ONE_LANE");
+    return e ? (size_t)strtoull(e, nullptr, 0) : (size_t)65536;
+  }();
+  return v;
+}
+
 void launch_hash_to_g2(const uint8_t* msgs, const uint64_t* off, const uint32_t* len, uint32_t n, MsgEntry* hm,
                        hipStream_t s) {
-  if (n) hipLaunchKernelGGL(k_hash_to_g2, dim3((unsigned)((2 * (size_t)n + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s,
-                            msgs, off, len, n, hm);
+  if (!n) return;
+  if (n >= hash_one_lane_min())
+    hipLaunchKernelGGL(k_hash_to_g2_1, dim3((unsigned)((n + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s, msgs, off, len,
+                       n, hm);
+  else
+    hipLaunchKernelGGL(k_hash_to_g2, dim3((unsigned)((2 * (size_t)n + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s,
+                       msgs, off, len, n, hm);
 }
 
 }  // namespace hb
