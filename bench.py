@@ -101,6 +101,28 @@ def attester_domain():
     return np.frombuffer(bytes.fromhex("01000000") + fork_data_root[:28], dtype=np.uint8).copy()
 
 
+def ta_share_positions(n, t):
+    """The share positions (0-based) of the aggregated partials: a fixed pseudo-random t-subset of
+    the n operators whose Lagrange coefficients at 0 are not all integers (runs of consecutive
+    indices give integer coefficients, binomials, which shorten the aggregation ladders)."""
+    import itertools
+    import random
+    from fractions import Fraction
+    rng = random.Random(1000 * n + t)
+    subsets = list(itertools.combinations(range(n), t))
+    rng.shuffle(subsets)
+    for pos in subsets:
+        ids = [p + 1 for p in pos]
+        lam = [Fraction(1)] * t
+        for a, i in enumerate(ids):
+            for j in ids:
+                if j != i:
+                    lam[a] *= Fraction(j, j - i)
+        if any(x.denominator != 1 for x in lam):
+            return list(pos)
+    return list(range(t))
+
+
 def setup_inputs(L, wl, V, rank):
     """Synthetic cluster -> host arrays; keys and signatures are derived on the GPU."""
     from charon_amd import synth
@@ -142,11 +164,16 @@ def setup_inputs(L, wl, V, rank):
     assert not stv.any(), "root signing failed"
     _chk(L, L.hbls_secret_to_public_key_batch(_p(root_sks), V, _p(dv_pks), _p(stv)))
     assert not stv.any(), "DV key derivation failed"
-    # ThresholdAggregate input: shares 1..t of every validator (parsigdb fires with exactly t,
-    # core/parsigdb/memory.go:218-221), given as indices of the verified partials
-    ta_src = (np.arange(V)[:, None] * n + np.arange(t)[None, :]).reshape(-1).astype(np.uint32)
+    # ThresholdAggregate input: t shares of every validator (parsigdb fires with exactly t,
+    # core/parsigdb/memory.go:218-221), given as indices of the verified partials.  The set is
+    # that of the t operators whose partials arrived first -- the same for every validator of the
+    # duty (parsigex exchanges whole sets per peer), a fixed pseudo-random t-subset here rather
+    # than 1..t, whose Lagrange coefficients would be small integers (binomials) and flatter the
+    # aggregation ladders
+    shares = ta_share_positions(n, t)
+    ta_src = (np.arange(V)[:, None] * n + np.asarray(shares)[None, :]).reshape(-1).astype(np.uint32)
     ta_sigs = sigs.reshape(NP, 96)[ta_src].reshape(-1).copy()
-    ta_idx = np.tile(np.arange(1, t + 1, dtype=np.int64), V)
+    ta_idx = np.tile(np.asarray(shares, dtype=np.int64) + 1, V)
     grp_off = (np.arange(V + 1, dtype=np.uint32) * t)
     vgrp_off = (np.arange(V + 1, dtype=np.uint32) * n)  # one verification group per validator
     return dict(n=n, t=t, V=V, NP=NP, M=M, sks=sks, att=att, domain=domain, msgs=msgs, moff=moff, mlen=mlen, midx=midx, pks=pks, sigs=sigs,
@@ -639,6 +666,7 @@ def main(argv=None):
         "data": "synthetic: SHA-256-derived keys, Shamir shares and signing roots (charon_amd/synth.py); "
                 "pubshares and signatures produced on device",
         "config": {"workload": wl["desc"], "validators_per_gpu": V, "operators": n, "threshold": t,
+                   "aggregated_share_indices": [int(x) + 1 for x in ta_share_positions(n, t)],
                    "distinct_messages": M, "partials_per_gpu": NP, "parallelism": f"validator-sharded x{world}"},
         "verify_per_s": round(world * NP / (elapsed / args.steps), 1),
         "threshold_aggregate_per_s": round(world * V / (elapsed / args.steps), 1),

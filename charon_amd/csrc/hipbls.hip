@@ -546,7 +546,7 @@ int ta_tail(Dev& d, Ws& w, const HmEntry* pts, const uint32_t* src, const uint8_
       TIMED(d, "k_ta_straus", s,
             launch_ta_msm(pts, src, dig, tab, pcf, pcc, pcoff + n_groups, (uint32_t)max_chunks, mode, pj, s));
     } else {
-      TIMED(d, "k_ta_straus", s, launch_ta_straus(pts, src, dig, (uint32_t)np, tab, pj, s));
+      TIMED(d, "k_ta_straus", s, launch_ta_straus(pts, src, dig, (uint32_t)np, (uint32_t)n_groups, tab, pj, s));
     }
   }
   TIMED(d, "k_group_sum", s,

@@ -96,8 +96,8 @@ void launch_ta_msm(const HmEntry* pts, const uint32_t* src, const TaDigits* dig,
                    const uint32_t* ccount, const uint32_t* total, uint32_t max_chunks, int mode, G2JEntry* out,
                    hipStream_t s);
 size_t ta_table_bytes(uint32_t n_partials);
-void launch_ta_straus(const HmEntry* pts, const uint32_t* src, const TaDigits* dig, uint32_t n_partials, void* tab,
-                      G2JEntry* out, hipStream_t s);
+void launch_ta_straus(const HmEntry* pts, const uint32_t* src, const TaDigits* dig, uint32_t n_partials,
+                      uint32_t n_groups, void* tab, G2JEntry* out, hipStream_t s);
 void launch_ta_member_status(const uint8_t* sig_st, const uint32_t* src, uint32_t n_partials, uint8_t* mstat,
                              hipStream_t s);
 

@@ -138,46 +138,115 @@ __device__ __forceinline__ void f2_select(Fp2& r, bool take_b, const Fp2& a, con
 // every step is computed and kept or dropped per lane by select.
 __global__ KB_OCC(HB_OCC_STRAUS) void k_ta_straus(const HmEntry* __restrict__ pts, const uint32_t* __restrict__ src,
                                                      const TaDigits* __restrict__ dig,
-                                                     uint32_t n_partials, uint4* __restrict__ tab,
-                                                     G2JEntry* __restrict__ out) {
+                                                     uint32_t n_partials, uint32_t n_groups, uint32_t t_uniform,
+                                                     uint4* __restrict__ tab, G2JEntry* __restrict__ out) {
 #if defined(__HIP_DEVICE_COMPILE__)
+  __shared__ int8_t naf[4][66];
+  __shared__ int naf_top;
   const int lane = (int)(threadIdx.x & 63u);
   const uint32_t item = blockIdx.x * 64 + (uint32_t)lane;
   const bool valid = item < n_partials;
   const uint32_t it = valid ? item : n_partials - 1;
-  uint4* wt = tab + (size_t)blockIdx.x * 15 * TA_TAB_QUADS * 64 + lane;
-  const TaDigits d = dig[it];
-  {
-    const HmEntry e = pts[src ? src[it] : it];
-    // psi (x, y) = (conj(x) c1x, conj(y) c1y); psi^2 (x, y) = (x c2x, y c2y)
-    G2A P0 = {e.x, e.y, e.inf != 0};
-    G2A P1 = {f2_mul(f2_conj(e.x), f2_from_const(PSI_CX)), f2_neg(f2_mul(f2_conj(e.y), f2_from_const(PSI_CY))), P0.inf};
-    G2A P2 = {f2_mul(e.x, f2_from_const(PSI2_CX)), f2_mul(e.y, f2_from_const(PSI2_CY)), P0.inf};
-    G2A P3 = {f2_mul(f2_conj(P2.x), f2_from_const(PSI_CX)), f2_neg(f2_mul(f2_conj(P2.y), f2_from_const(PSI_CY))), P0.inf};
-    tab_store(wt, 0, jac_from_aff(P0));
-    tab_store(wt, 1, jac_from_aff(P1));
-    tab_store(wt, 3, jac_from_aff(P2));
-    tab_store(wt, 7, jac_from_aff(P3));
+  // member of this lane: with t members in every group, lane L takes member j = L / n_groups of
+  // validator v = L % n_groups, so a wave holds the same share position of 64 validators -- whose
+  // Lagrange digits agree whenever the validators' index sets do (the common slot)
+  const uint32_t m = t_uniform ? (it % n_groups) * t_uniform + it / n_groups : it;
+  uint4* wt = tab + (size_t)blockIdx.x * 16 * TA_TAB_QUADS * 64 + lane;
+  const TaDigits d = dig[m];
+  bool same = true;
+  HB_UNROLL for (int k = 0; k < 4; k++) {
+    const uint32_t lo = (uint32_t)d.a[k], hi = (uint32_t)(d.a[k] >> 32);
+    same = same && lo == (uint32_t)__builtin_amdgcn_readfirstlane((int)lo) &&
+           hi == (uint32_t)__builtin_amdgcn_readfirstlane((int)hi);
   }
-  // T[s] (entry s - 1) = T[s - hi] + T[hi], hi the top bit of s; T[hi] is affine (Z = 1 or infinity)
-  HB_NOUNROLL for (int s = 3; s < 16; s++) {
-    const int hi = s >= 8 ? 8 : (s >= 4 ? 4 : 2);
-    if (s == hi) continue;
-    const G2J h = tab_load(wt, hi - 1);
-    const G2A ha = {h.X, h.Y, f2_is_zero(h.Z)};
-    tab_store(wt, s - 1, jac_add_aff(tab_load(wt, s - hi - 1), ha));
-  }
+  const HmEntry e = pts[src ? src[m] : m];
+  const G2A P0 = {e.x, e.y, e.inf != 0};
   G2J R = jac_infinity<Fp2>();
-  HB_NOUNROLL for (int b = 63; b >= 0; b--) {
-    R = jac_dbl(R);
-    const uint32_t sel = (uint32_t)((d.a[0] >> b) & 1) | ((uint32_t)((d.a[1] >> b) & 1) << 1) |
-                         ((uint32_t)((d.a[2] >> b) & 1) << 2) | ((uint32_t)((d.a[3] >> b) & 1) << 3);
-    const G2J S = jac_add(R, tab_load(wt, sel == 0 ? 0 : (int)sel - 1));
-    f2_select(R.X, sel != 0, R.X, S.X);
-    f2_select(R.Y, sel != 0, R.Y, S.Y);
-    f2_select(R.Z, sel != 0, R.Z, S.Z);
+  if (__all(same)) {
+    // wave-uniform digits: signed width-4 NAF of each digit (one shared schedule, uniform
+    // branches) over the odd multiples {1, 3, 5, 7} of the four bases B_k = P0, -psi(P0),
+    // psi^2(P0), -psi^3(P0): ~13 additions per 64-bit digit instead of one per ladder step
+    if (lane == 0) {
+      int top = 0;
+      HB_UNROLL for (int k = 0; k < 4; k++) {
+        uint64_t v = d.a[k];  // < |x| < 2^64 - 7: v + 7 cannot overflow
+        for (int i = 0; i < 66; i++) {
+          int dg = 0;
+          if (v & 1u) {
+            dg = (int)(v & 15u);
+            if (dg >= 8) dg -= 16;
+            v = dg > 0 ? v - (uint64_t)dg : v + (uint64_t)(-dg);
+          }
+          naf[k][i] = (int8_t)dg;
+          if (dg && i > top) top = i;
+          v >>= 1;
+        }
+      }
+      naf_top = top;
+    }
+    __syncthreads();
+    const G2J J1 = jac_from_aff(P0);
+    const G2J J2 = jac_dbl(J1);
+    const G2J J3 = jac_add_aff(J2, P0);
+    const G2J J5 = jac_add(J3, J2);
+    const G2J J7 = jac_add(J5, J2);
+    const Fp2 cx = f2_from_const(PSI_CX), cy = f2_from_const(PSI_CY);
+    const Fp2 c2x = f2_from_const(PSI2_CX), c2y = f2_from_const(PSI2_CY);
+    HB_NOUNROLL for (int j = 0; j < 4; j++) {
+      const G2J J = j == 0 ? J1 : j == 1 ? J3 : j == 2 ? J5 : J7;
+      tab_store(wt, j, J);
+      // -psi: (conj(X) cx, -conj(Y) cy, conj(Z));  psi^2: (X c2x, Y c2y, Z)
+      const G2J N1 = {f2_mul(f2_conj(J.X), cx), f2_neg(f2_mul(f2_conj(J.Y), cy)), f2_conj(J.Z)};
+      const G2J N2 = {f2_mul(J.X, c2x), f2_mul(J.Y, c2y), J.Z};
+      const G2J N3 = {f2_mul(f2_conj(N2.X), cx), f2_neg(f2_mul(f2_conj(N2.Y), cy)), f2_conj(N2.Z)};
+      tab_store(wt, 4 + j, N1);
+      tab_store(wt, 8 + j, N2);
+      tab_store(wt, 12 + j, N3);
+    }
+    const int top = naf_top;
+    HB_NOUNROLL for (int i = top; i >= 0; i--) {
+      R = jac_dbl(R);
+      HB_NOUNROLL for (int k = 0; k < 4; k++) {
+        const int dg = naf[k][i];
+        if (dg != 0) {  // wave-uniform
+          G2J T = tab_load(wt, 4 * k + ((dg < 0 ? -dg : dg) >> 1));
+          if (dg < 0) T.Y = f2_neg(T.Y);
+          R = jac_add(R, T);
+        }
+      }
+    }
+  } else {
+    // general case: one joint 64-step ladder over the 15-entry subset table of the four bases
+    {
+      G2A P1 = {f2_mul(f2_conj(e.x), f2_from_const(PSI_CX)), f2_neg(f2_mul(f2_conj(e.y), f2_from_const(PSI_CY))),
+                P0.inf};
+      G2A P2 = {f2_mul(e.x, f2_from_const(PSI2_CX)), f2_mul(e.y, f2_from_const(PSI2_CY)), P0.inf};
+      G2A P3 = {f2_mul(f2_conj(P2.x), f2_from_const(PSI_CX)), f2_neg(f2_mul(f2_conj(P2.y), f2_from_const(PSI_CY))),
+                P0.inf};
+      tab_store(wt, 0, jac_from_aff(P0));
+      tab_store(wt, 1, jac_from_aff(P1));
+      tab_store(wt, 3, jac_from_aff(P2));
+      tab_store(wt, 7, jac_from_aff(P3));
+    }
+    // T[s] (entry s - 1) = T[s - hi] + T[hi], hi the top bit of s; T[hi] is affine (Z = 1 or infinity)
+    HB_NOUNROLL for (int sidx = 3; sidx < 16; sidx++) {
+      const int hi = sidx >= 8 ? 8 : (sidx >= 4 ? 4 : 2);
+      if (sidx == hi) continue;
+      const G2J h = tab_load(wt, hi - 1);
+      const G2A ha = {h.X, h.Y, f2_is_zero(h.Z)};
+      tab_store(wt, sidx - 1, jac_add_aff(tab_load(wt, sidx - hi - 1), ha));
+    }
+    HB_NOUNROLL for (int b = 63; b >= 0; b--) {
+      R = jac_dbl(R);
+      const uint32_t sel = (uint32_t)((d.a[0] >> b) & 1) | ((uint32_t)((d.a[1] >> b) & 1) << 1) |
+                           ((uint32_t)((d.a[2] >> b) & 1) << 2) | ((uint32_t)((d.a[3] >> b) & 1) << 3);
+      const G2J S = jac_add(R, tab_load(wt, sel == 0 ? 0 : (int)sel - 1));
+      f2_select(R.X, sel != 0, R.X, S.X);
+      f2_select(R.Y, sel != 0, R.Y, S.Y);
+      f2_select(R.Z, sel != 0, R.Z, S.Z);
+    }
   }
-  if (valid) out[item] = {R.X, R.Y, R.Z};
+  if (valid) out[m] = {R.X, R.Y, R.Z};
 #endif
 }
 
@@ -189,7 +258,7 @@ __global__ KB_OCC(HB_OCC_STRAUS) void k_ta_straus(const HmEntry* __restrict__ pt
 // k_group_sum adds the members as before.  mode 1 (Aggregate, lambda = 1): a plain sum.
 #if defined(__HIP_DEVICE_COMPILE__)
 __device__ __forceinline__ uint4* member_tab(uint4* tab, uint32_t m) {
-  return tab + (size_t)(m >> 6) * 15 * TA_TAB_QUADS * 64 + (m & 63u);
+  return tab + (size_t)(m >> 6) * 16 * TA_TAB_QUADS * 64 + (m & 63u);
 }
 #endif
 
@@ -266,7 +335,7 @@ void launch_ta_lambda(const int64_t* idx, const uint32_t* grp_off, uint32_t n_gr
                      n_partials, mode, dig, mstat);
 }
 
-size_t ta_table_bytes(uint32_t n_partials) { return (size_t)blocks_of(n_partials, 64) * 15 * sizeof(G2JEntry) * 64; }
+size_t ta_table_bytes(uint32_t n_partials) { return (size_t)blocks_of(n_partials, 64) * 16 * sizeof(G2JEntry) * 64; }
 
 void launch_ta_table(const HmEntry* pts, const uint32_t* src, uint32_t n_partials, void* tab, hipStream_t s) {
   if (n_partials)
@@ -280,11 +349,13 @@ void launch_ta_msm(const HmEntry* pts, const uint32_t* src, const TaDigits* dig,
                        ccount, total, mode, out);
 }
 
-void launch_ta_straus(const HmEntry* pts, const uint32_t* src, const TaDigits* dig, uint32_t n_partials, void* tab,
-                      G2JEntry* out, hipStream_t s) {
-  if (n_partials)
-    hipLaunchKernelGGL(k_ta_straus, dim3(blocks_of(n_partials, 64)), dim3(64), 0, s, pts, src, dig, n_partials,
-                       (uint4*)tab, out);
+void launch_ta_straus(const HmEntry* pts, const uint32_t* src, const TaDigits* dig, uint32_t n_partials,
+                      uint32_t n_groups, void* tab, G2JEntry* out, hipStream_t s) {
+  if (!n_partials) return;
+  // members laid out share-position-major when every group has the same size t
+  const uint32_t t = (n_groups && n_partials % n_groups == 0) ? n_partials / n_groups : 0;
+  hipLaunchKernelGGL(k_ta_straus, dim3(blocks_of(n_partials, 64)), dim3(64), 0, s, pts, src, dig, n_partials,
+                     n_groups, t, (uint4*)tab, out);
 }
 
 // Member statuses of a ThresholdAggregate whose partials were decompressed by the verification
