@@ -618,11 +618,13 @@ def main(argv=None):
         else:
             rlc_partial = rlc_item
         rlc_avg = (NP * rlc_partial + (0 if staged else V) * rlc_item) / n_rlc
+        ta_w = opcounts.ta_uniform([x + 1 for x in ta_share_positions(n, t)])
         units = {"k_pair3": (V, per_unit["k_pair3"]), "k_rlc": (n_rlc, (rlc_avg, rlc_avg)),
                  "k_dec_pk": (NP + (0 if staged else V), per_unit["k_dec_pk"]),
                  "k_dec_sig_pt": (NP + (ta_units if staged else 0), per_unit["k_dec_sig_pt"]),
                  "k_group_prep": (V, opcounts.per_unit(group_size=n + (0 if staged else 1), t=t)["k_group_prep"]),
-                 "k_ta_straus": (ta_units, per_unit["k_ta_straus"]), "k_group_sum": (V, per_unit["k_group_sum"]),
+                 # the aggregation ladders: the uniform-digit schedule of the aggregated index set
+                 "k_ta_straus": (ta_units, (ta_w, ta_w)), "k_group_sum": (V, per_unit["k_group_sum"]),
                  "k_hash_to_g2": (M, per_unit["k_hash_to_g2"]), "k_lines_msg": (M, per_unit["k_lines_msg"])}
         dom, per = roofline_from_timing(recs, 1, units)
         # the whole slot: every kernel's algorithmic work over the measured step time

@@ -68,6 +68,48 @@ def ta_msm(b=BLOCKS, chunk=1):
     return 18 + 11 * b["jac_add_aff_g2"] + 64 * b["jac_add_g2"] + 64 * b["jac_dbl_g2"] / chunk
 
 
+R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+X_ABS = 0xD201000000010000
+
+
+def _naf4(v):
+    """Signed width-4 NAF digits of v (least significant first), as k_ta_straus builds them."""
+    out = []
+    while v:
+        d = 0
+        if v & 1:
+            d = v & 15
+            if d >= 8:
+                d -= 16
+            v -= d
+        out.append(d)
+        v >>= 1
+    return out
+
+
+def ta_uniform(ids, b=BLOCKS):
+    """k_ta_straus per member when a wave's Lagrange digits agree (every validator aggregates the
+    share indices `ids`): the odd-multiple table (a doubling, three additions, the psi images),
+    then top + 1 doublings and one addition per nonzero NAF digit of the four base-|x| digits of
+    lambda_j(0).  Returns the mean over the members."""
+    tot = 0
+    for i in ids:
+        lam = 1
+        for j in ids:
+            if j != i:
+                lam = lam * j % R_ORDER * pow(j - i, -1, R_ORDER) % R_ORDER
+        digits = []
+        for _ in range(4):
+            digits.append(lam % X_ABS)
+            lam //= X_ABS
+        nafs = [_naf4(a) for a in digits]
+        top = max((len(n) for n in nafs), default=1)
+        adds = sum(1 for n in nafs for d in n if d)
+        table = b["jac_dbl_g2"] + b["jac_add_aff_g2"] + 2 * b["jac_add_g2"] + 4 * 24
+        tot += table + top * b["jac_dbl_g2"] + adds * b["jac_add_g2"]
+    return tot / len(ids)
+
+
 def per_unit(b=BLOCKS, group_size=1, t=1):
     """{kernel: (alg, exec)} Fp products per unit (unit named in UNITS)."""
     p = pair3(b)
