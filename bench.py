@@ -607,8 +607,8 @@ def main(argv=None):
         _chk(L, L.hbls_timing(0))
         per_unit = opcounts.per_unit(group_size=n, t=t)
         ta_units = V * t
-        # k_rlc: the partials as multi-scalar chunks (one per validator), the folded aggregates (slot
-        # mode) one ladder each
+        # k_rlc: the partials as multi-scalar chunks (one per validator); the folded aggregates
+        # (slot mode) keep r = 1
         rlc_item = opcounts.BLOCKS["rlc_g1"] + opcounts.BLOCKS["rlc_g2"]
         n_rlc = NP + (0 if staged else V)
         cmax = min(opcounts.RLC_CHUNK, max(1, NP // int(os.environ.get("HBLS_RLC_LANES", "65536"))))
@@ -617,7 +617,7 @@ def main(argv=None):
             rlc_partial = opcounts.rlc_msm(chunk=n / n_chunks)
         else:
             rlc_partial = rlc_item
-        rlc_avg = (NP * rlc_partial + (0 if staged else V) * rlc_item) / n_rlc
+        rlc_avg = NP * rlc_partial / n_rlc  # the folded aggregates keep r = 1 (no ladder)
         ta_w = opcounts.ta_uniform([x + 1 for x in ta_share_positions(n, t)])
         units = {"k_pair3": (V, per_unit["k_pair3"]), "k_rlc": (n_rlc, (rlc_avg, rlc_avg)),
                  "k_dec_pk": (NP + (0 if staged else V), per_unit["k_dec_pk"]),

@@ -678,9 +678,12 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
     TIMED(d, "k_rlc", s, launch_rlc(vpk, vpkst, vsig, vsigst, igrp, dgoff, 0, (uint32_t)n, 0, key, pr, sr, s));
   }
   if (n_agg) {
+    // the folded aggregate keeps r = 1: one coefficient per combination may be fixed without
+    // losing soundness (an invalid aggregate alone fails the combined check exactly; with an
+    // invalid partial j beside it the check passes for one value of the random r_j only)
     HCHK(hipStreamWaitEvent(s, w.ev_ta, 0));
     TIMED(d, "k_rlc", s,
-          launch_rlc(apk, apkst, asig, fold->ta_status, nullptr, nullptr, 1, (uint32_t)n_agg, (uint32_t)n, key, apr,
+          launch_rlc(apk, apkst, asig, fold->ta_status, nullptr, nullptr, 0, (uint32_t)n_agg, (uint32_t)n, key, apr,
                      asr, s));
   }
   if (hm_ready) HCHK(hipStreamWaitEvent(s, hm_ready, 0));
