@@ -607,8 +607,8 @@ def main(argv=None):
         _chk(L, L.hbls_timing(0))
         per_unit = opcounts.per_unit(group_size=n, t=t)
         ta_units = V * t
-        # k_rlc: the partials as multi-scalar chunks (one per validator); the folded aggregates
-        # (slot mode) keep r = 1
+        # k_rlc: the partials as multi-scalar chunks (one per validator), then the folded
+        # aggregates (slot mode)
         rlc_item = opcounts.BLOCKS["rlc_g1"] + opcounts.BLOCKS["rlc_g2"]
         n_rlc = NP + (0 if staged else V)
         cmax = min(opcounts.RLC_CHUNK, max(1, NP // int(os.environ.get("HBLS_RLC_LANES", "65536"))))
@@ -617,20 +617,32 @@ def main(argv=None):
             rlc_partial = opcounts.rlc_msm(chunk=n / n_chunks)
         else:
             rlc_partial = rlc_item
-        rlc_avg = NP * rlc_partial / n_rlc  # the folded aggregates keep r = 1 (no ladder)
+        # batched final exponentiation (the library's setting; verifications of >= fe_min groups):
+        # every folded aggregate then takes a random coefficient (one ladder each), else r = 1
+        fe_min = L.hbls_fe_batch(0)
+        L.hbls_fe_batch(fe_min)
+        bfe = fe_min and V >= fe_min
+        rlc_avg = (NP * rlc_partial + (0 if staged or not bfe else V * rlc_item)) / n_rlc
         ta_w = opcounts.ta_uniform([x + 1 for x in ta_share_positions(n, t)])
-        units = {"k_pair3": (V, per_unit["k_pair3"]), "k_rlc": (n_rlc, (rlc_avg, rlc_avg)),
+        prep_units = opcounts.per_unit(group_size=n + (0 if staged else 1), t=t)
+        units = {"k_rlc": (n_rlc, (rlc_avg, rlc_avg)),
                  "k_dec_pk": (NP + (0 if staged else V), per_unit["k_dec_pk"]),
                  "k_dec_sig_pt": (NP + (ta_units if staged else 0), per_unit["k_dec_sig_pt"]),
-                 "k_group_prep": (V, opcounts.per_unit(group_size=n + (0 if staged else 1), t=t)["k_group_prep"]),
                  # the aggregation ladders: the uniform-digit schedule of the aggregated index set
                  "k_ta_straus": (ta_units, (ta_w, ta_w)), "k_group_sum": (V, per_unit["k_group_sum"]),
                  "k_hash_to_g2": (M, per_unit["k_hash_to_g2"]), "k_lines_msg": (M, per_unit["k_lines_msg"])}
+        if bfe:
+            nb = -(-V // opcounts.FE_BATCH)
+            units.update({"k_group_prep": (V, prep_units["k_group_prep_b"]),
+                          "k_pair3_ml": (V, per_unit["k_pair3_ml"]), "k_pair3_fin": (nb, per_unit["k_pair3_fin"]),
+                          "k_slines": (nb, per_unit["k_slines"])})
+        else:
+            units.update({"k_group_prep": (V, prep_units["k_group_prep"]), "k_pair3": (V, per_unit["k_pair3"])})
         dom, per = roofline_from_timing(recs, 1, units)
         # the whole slot: every kernel's algorithmic work over the measured step time
         slot_fpmul = sum(u * w[0] for u, w in units.values())
         slot_tops = slot_fpmul * opcounts.MAC_PER_FPMUL / (elapsed / args.steps) / 1e12
-        pair = per.get("k_pair3")
+        pair = per.get("k_pair3") or {k: per.get(k) for k in ("k_pair3_ml", "k_pair3_fin")}
         roofline = None
         if dom:
             x = per[dom]

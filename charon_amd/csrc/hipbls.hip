@@ -234,6 +234,9 @@ size_t g_kc_n = 0;
 // chunks of 2, 4 or 8 members.
 bool g_ta_msm = false;
 size_t g_ta_chunk = 4;   // HBLS_TA_CHUNK: members per lane of k_ta_msm (<= TA_CHUNK)
+// HBLS_FE_BATCH: verifications of at least this many groups check FE_BATCH groups per final
+// exponentiation (vgroup.hip; 0 = one final exponentiation per group)
+std::atomic<size_t> g_fe_batch_min{2 * FE_BATCH};
 
 struct DevBuf {
   void* p = nullptr;
@@ -249,6 +252,7 @@ enum WsId {
   W_SEGA, W_SEGB, W_SEGSTA, W_SEGSTB, W_VAPT, W_VAPV, W_PLAN,  // VerifyAggregate key reduction
   W_PCNT, W_PCOFF, W_PCFIRST, W_PCCOUNT, W_COEF, W_RT1, W_RT2,  // chunk plan + multi-scalar RLC
   W_TPCNT, W_TPCOFF, W_TPCFIRST, W_TPCCOUNT,                    // chunk plan of the aggregation
+  W_FBUF, W_GS, W_BS, W_BLINES, W_BBAD, W_BVER, W_GLIST, W_GCOUNT,  // batched final exponentiation
   W_COUNT_
 };
 
@@ -429,6 +433,7 @@ int init_mask(uint32_t mask) {
   g_rlc_lanes = std::max<size_t>(1, env_size("HBLS_RLC_LANES", g_rlc_lanes));
   g_ta_msm = env_size("HBLS_TA_MSM", 0) != 0;
   g_ta_chunk = std::min<size_t>(TA_CHUNK, std::max<size_t>(1, env_size("HBLS_TA_CHUNK", g_ta_chunk)));
+  g_fe_batch_min = env_size("HBLS_FE_BATCH", g_fe_batch_min.load());
   std::vector<Dev*> devs;
   for (int k = 0; k < 32; k++)
     if (mask & (1u << k)) {
@@ -492,7 +497,7 @@ int rlc_key(RlcKey& k) {
 // post-aggregate verification under the DV keys (sigagg.go:117) into the same groups.
 // ---------------------------------------------------------------------------------------
 // verification statistics (HBLS_STATS=1): items, groups, items re-checked alone
-std::atomic<uint64_t> g_stats[3];
+std::atomic<uint64_t> g_stats[4];
 bool stats_on() {
   const char* v = getenv("HBLS_STATS");
   return v && v[0] == '1';
@@ -587,6 +592,22 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
     return -1;
   RlcKey key;
   if (rlc_key(key)) return -1;
+  // Batched final exponentiation: FE_BATCH groups share one final exponentiation and one Miller
+  // loop of the signature side, checking prod_g e(P_g, H(m_g)) * e(-g1, sum_g S_g) == 1.  Every
+  // item (singletons and folded aggregates included) then takes a random coefficient: with two
+  // fixed coefficients in one combination, errors of two items could cancel.
+  const size_t fe_min = g_fe_batch_min.load();
+  const bool bfe = fe_min && n_groups >= fe_min;
+  const size_t nbcap = (gcap + FE_BATCH - 1) / FE_BATCH;
+  Fp4Entry* fbuf = nullptr;
+  G2JEntry *gS = nullptr, *bS = nullptr;
+  LineEntry* blines = nullptr;
+  uint8_t *bbad = nullptr, *bver = nullptr;
+  uint32_t *glist = nullptr, *gcount = nullptr;
+  if (bfe && (wsbuf(w, W_FBUF, 3 * gcap, &fbuf) || wsbuf(w, W_GS, gcap, &gS) || wsbuf(w, W_BS, nbcap, &bS) ||
+              wsbuf(w, W_BLINES, nbcap * N_LINES, &blines) || wsbuf(w, W_BBAD, nbcap, &bbad) ||
+              wsbuf(w, W_BVER, nbcap, &bver) || wsbuf(w, W_GLIST, gcap, &glist) || wsbuf(w, W_GCOUNT, 1, &gcount)))
+    return -1;
 
   // fork: decompression on the side streams (after the previous verification's decompression)
   if (d.dec_valid) HCHK(hipStreamWaitEvent(s, d.ev_dec, 0));
@@ -673,18 +694,21 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
     ra.t2 = t2;
     ra.pout = pr;
     ra.sout = sr;
+    ra.always = bfe ? 1 : 0;
     TIMED(d, "k_rlc", s, launch_rlc_msm(ra, (uint32_t)max_chunks, s));
   } else {
-    TIMED(d, "k_rlc", s, launch_rlc(vpk, vpkst, vsig, vsigst, igrp, dgoff, 0, (uint32_t)n, 0, key, pr, sr, s));
+    TIMED(d, "k_rlc", s,
+          launch_rlc(vpk, vpkst, vsig, vsigst, igrp, dgoff, bfe ? 1 : 0, (uint32_t)n, 0, key, pr, sr, s));
   }
   if (n_agg) {
-    // the folded aggregate keeps r = 1: one coefficient per combination may be fixed without
-    // losing soundness (an invalid aggregate alone fails the combined check exactly; with an
-    // invalid partial j beside it the check passes for one value of the random r_j only)
+    // without the batched final exponentiation the folded aggregate keeps r = 1: one coefficient
+    // per combination may be fixed without losing soundness (an invalid aggregate alone fails the
+    // combined check exactly; with an invalid partial j beside it the check passes for one value
+    // of the random r_j only)
     HCHK(hipStreamWaitEvent(s, w.ev_ta, 0));
     TIMED(d, "k_rlc", s,
-          launch_rlc(apk, apkst, asig, fold->ta_status, nullptr, nullptr, 0, (uint32_t)n_agg, (uint32_t)n, key, apr,
-                     asr, s));
+          launch_rlc(apk, apkst, asig, fold->ta_status, nullptr, nullptr, bfe ? 1 : 0, (uint32_t)n_agg, (uint32_t)n,
+                     key, apr, asr, s));
   }
   if (hm_ready) HCHK(hipStreamWaitEvent(s, hm_ready, 0));
   for (size_t g0 = 0; g0 < n_groups; g0 += gcap) {
@@ -713,6 +737,52 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
     ga.gmsg = gmsg;
     ga.gst = gst;
     ga.glines = glines;
+    if (bfe) {
+      ga.gS = gS;
+      ga.bS = bS;
+      TIMED(d, "k_group_prep", s, launch_group_prep(ga, s));
+      const uint32_t nb = (ng + FE_BATCH - 1) / FE_BATCH;
+      // the (P_g, H(m_g)) Miller loops, stored unexponentiated
+      Pair3Args pm{};
+      pm.pk = gP;
+      pm.pk_st = gst;
+      pm.msg_idx = gmsg + g0;
+      pm.hm = hm;
+      pm.sig_lines = glines;
+      pm.stride = ng;
+      pm.n = ng;
+      pm.f_out = fbuf;
+      TIMED(d, "k_pair3_ml", s, launch_pair3_ml(pm, s));
+      // per batch: the lines of sum_g S_g, one Miller loop times the batch's stored loops, one
+      // final exponentiation
+      TIMED(d, "k_slines", s, launch_slines(bS, nullptr, nullptr, nb, blines, nb, bbad, s));
+      Pair3Args pf{};
+      pf.pk_st = bbad;
+      pf.sig_lines = blines;
+      pf.stride = nb;
+      pf.n = nb;
+      pf.f_in = fbuf;
+      pf.f_range = FE_BATCH;
+      pf.f_n = ng;
+      pf.status = bver;
+      TIMED(d, "k_pair3_fin", s, launch_pair3_fin(pf, s));
+      // groups of a failing batch: checked one by one (their stored loop, their own S lines)
+      HCHK(hipMemsetAsync(gcount, 0, sizeof(uint32_t), s));
+      TIMED(d, "k_batch_verdict", s, launch_batch_verdict(gst, bver, ng, gver + g0, glist, gcount, s));
+      TIMED(d, "k_slines", s, launch_slines(gS, glist, gcount, ng, glines, ng, nullptr, s));
+      Pair3Args pg{};
+      pg.sig_lines = glines;
+      pg.stride = ng;
+      pg.n = ng;
+      pg.list = glist;
+      pg.count = gcount;
+      pg.f_in = fbuf;
+      pg.f_range = 1;
+      pg.f_n = ng;
+      pg.status = gver + g0;
+      TIMED(d, "k_pair3_fin", s, launch_pair3_fin(pg, s));
+      continue;
+    }
     TIMED(d, "k_group_prep", s, launch_group_prep(ga, s));
     Pair3Args pa{};
     pa.pk = gP;
@@ -780,6 +850,11 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
     g_stats[0] += n + n_agg;
     g_stats[1] += n_groups;
     g_stats[2] += c;
+    if (bfe) {  // only the last chunk's count is still in gcount: enough for the tests' sizes
+      HCHK(hipMemcpyAsync(&c, gcount, sizeof(c), hipMemcpyDeviceToHost, s));
+      HCHK(hipStreamSynchronize(s));
+      g_stats[3] += c;
+    }
   }
   return 0;
 }
@@ -1604,9 +1679,11 @@ int hbls_timing_read(const char** names, float* ms, size_t max_n, size_t* n_out)
 }
 
 int hbls_stats(uint64_t* out, size_t n) {
-  for (size_t k = 0; k < n && k < 3; k++) out[k] = g_stats[k].load();
+  for (size_t k = 0; k < n && k < 4; k++) out[k] = g_stats[k].load();
   return stats_on() ? 0 : set_err("statistics are collected only with HBLS_STATS=1");
 }
+
+size_t hbls_fe_batch(size_t min_groups) { return g_fe_batch_min.exchange(min_groups); }
 
 int hbls_sync(void* stream) {
   HCHK(hipStreamSynchronize((hipStream_t)stream));

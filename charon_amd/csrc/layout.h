@@ -59,6 +59,10 @@ struct LineEntry {  // one Miller-loop line: (a0, c1, c2) unevaluated or (a0, a1
   Fp2 a0, a1, b1;
 };
 
+struct Fp4Entry {  // one lane's third of an Fp12 value in the lane-group form of pair3.h
+  Fp2 x, y;
+};
+
 // Per distinct message: H(m) and the 68 unevaluated lines of its Miller chain (pairing.h
 // miller_dbl_c / miller_add_c), shared by every partial signed over that message.
 struct MsgEntry {
@@ -113,6 +117,12 @@ void launch_lines_msg(MsgEntry* hm, uint32_t n, hipStream_t s);
 // entries e >= n_items denote the folded aggregate of validator e - n_items (agg_pk, agg_msg,
 // agg_status).  Statuses: a nonzero pk_st / sig_st byte (nullable arrays) decides the verdict
 // without the pairing; otherwise OK iff the product of the two pairings is one.
+//
+// Batched final exponentiation (launch_pair3_ml / launch_pair3_fin): the ML launch runs only the
+// Miller loop of (P, H(m)) of entry e and stores it, unexponentiated, at f_out[3 e .. 3 e + 2] (one
+// where pk_st[e] is nonzero).  The FIN launch runs the Miller loop of (-g1, S) from sig_lines,
+// multiplies in the stored values f_in of entries [e f_range, min((e + 1) f_range, f_n)), then
+// exponentiates: status[e] = nonzero pk_st[e] ? 1 : (OK iff the product is one).
 struct Pair3Args {
   const G1AEntry* pk;
   const uint8_t* pk_st;
@@ -131,8 +141,13 @@ struct Pair3Args {
   const uint32_t* agg_msg;
   uint8_t* status;
   uint8_t* agg_status;
+  Fp4Entry* f_out;
+  const Fp4Entry* f_in;
+  uint32_t f_range, f_n;
 };
 void launch_pair3(const Pair3Args& a, hipStream_t s);
+void launch_pair3_ml(const Pair3Args& a, hipStream_t s);
+void launch_pair3_fin(const Pair3Args& a, hipStream_t s);
 
 // Batched verification (vbatch.hip).
 void launch_item_group(const uint32_t* grp_off, uint32_t n_groups, uint32_t n, uint32_t* item_grp, hipStream_t s);
@@ -157,6 +172,7 @@ struct RlcMsmArgs {
   G2J* t2;        // 3 per item
   G1JEntry* pout;
   G2JEntry* sout;
+  int always;     // random r for groups of one item too (batched final exponentiation)
 };
 void launch_plan(const uint32_t* grp_off, uint32_t ng, uint32_t cmax, uint32_t* cnt, uint32_t* coff,
                  uint32_t* cfirst, uint32_t* ccount, hipStream_t s);
@@ -186,8 +202,21 @@ struct GroupPrepArgs {
   uint32_t* gmsg;    // [n_groups] (indexed by g)
   uint8_t* gst;      // [ng]
   LineEntry* glines; // [N_LINES][ng]
+  // batched final exponentiation (non-null): no lines; the group's S (Jacobian, infinity unless
+  // READY) and the sum over each batch of FE_BATCH consecutive groups
+  G2JEntry* gS;      // [ng]
+  G2JEntry* bS;      // [ceil(ng / FE_BATCH)]
 };
+constexpr uint32_t FE_BATCH = 64;  // groups per batched final exponentiation (one wave of k_group_prep)
 void launch_group_prep(const GroupPrepArgs& a, hipStream_t s);
+// lines at -g1 of the affine images of pts[e], e = list ? list[u] (u < *count) : u, into
+// lines[j * stride + u]; bad[u] (nullable) = the point is infinity
+void launch_slines(const G2JEntry* pts, const uint32_t* list, const uint32_t* count, uint32_t n, LineEntry* lines,
+                   uint32_t stride, uint8_t* bad, hipStream_t s);
+// group verdicts from the batch verdicts: not READY -> 1, READY in a passing batch -> 0, else the
+// group joins list (its verdict comes from the per-group check)
+void launch_batch_verdict(const uint8_t* gst, const uint8_t* bver, uint32_t ng, uint8_t* gver, uint32_t* list,
+                          uint32_t* count, hipStream_t s);
 struct ScatterArgs {
   uint32_t n;
   const uint32_t* item_grp;

@@ -20,7 +20,14 @@ __global__ KB_OCC(HB_OCC_LINES) void k_lines_msg(MsgEntry* __restrict__ hm, uint
 
 // THREE lanes per pairing (pair3.h): Miller loop over the streamed lines of (P, H(m)) and
 // (-g1, S), final exponentiation, verdict (herumi.go:299 VerifyByte).  Units and statuses as
-// described at Pair3Args (layout.h).
+// described at Pair3Args (layout.h).  MODE: P3_FULL as just said; P3_ML the (P, H(m)) loop only,
+// stored unexponentiated; P3_FIN the (-g1, S) loop times stored values, exponentiated (the batched
+// final exponentiation of vgroup.hip).
+enum { P3_FULL = 0, P3_ML = 1, P3_FIN = 2 };
+
+__device__ __forceinline__ Fp4 f4_load(const Fp4Entry& e) { return {e.x, e.y}; }
+
+template <int MODE>
 __global__ KB_OCC(HB_OCC_PAIR3) void k_pair3(Pair3Args a) {
 #if defined(__HIP_DEVICE_COMPILE__)
   Grp g = grp_make();
@@ -36,10 +43,15 @@ __global__ KB_OCC(HB_OCC_PAIR3) void k_pair3(Pair3Args a) {
   const bool valid = grp < GROUPS_PER_WAVE && unit < avail;
   const uint32_t u = valid ? unit : avail - 1;  // idle lanes shadow a real unit (no divergence)
   uint32_t e = a.list ? a.list[a.base + u] : u;
-  const bool agg = e >= a.n_items;
-  const G1AEntry P = agg ? a.agg_pk[e - a.n_items] : a.pk[e];
-  const uint32_t m = agg ? a.agg_msg[e - a.n_items] : a.msg_idx[e];
-  const LineEntry* ml = a.hm[m].lines;
+  const bool agg = MODE == P3_FULL && e >= a.n_items;
+  G1AEntry P{};
+  uint32_t m = 0;
+  const LineEntry* ml = nullptr;
+  if (MODE != P3_FIN) {
+    P = agg ? a.agg_pk[e - a.n_items] : a.pk[e];
+    m = agg ? a.agg_msg[e - a.n_items] : a.msg_idx[e];
+    ml = a.hm[m].lines;
+  }
   const LineEntry* sl = a.sig_lines + u;
   // Lines in loop order: for each bit i = 62..0 of |x| a doubling line (preceded by f^2 except
   // at the top) and, if bit i is set, an addition line.  One copy of the line products.
@@ -49,10 +61,14 @@ __global__ KB_OCC(HB_OCC_PAIR3) void k_pair3(Pair3Args a) {
   HB_NOUNROLL for (int j = 0; j < N_LINES; j++) {
     const bool dbl = !pending_add;
     if (dbl && j > 0) f = g_sqr(g, f);
-    LineEntry L = ml[j];
-    f = g_mul_line(g, f, L.a0, f2_mul_fp(L.a1, P.x), f2_mul_fp(L.b1, P.y));
-    LineEntry S = sl[(size_t)j * a.stride];
-    f = g_mul_line(g, f, S.a0, S.a1, S.b1);
+    if (MODE != P3_FIN) {
+      LineEntry L = ml[j];
+      f = g_mul_line(g, f, L.a0, f2_mul_fp(L.a1, P.x), f2_mul_fp(L.b1, P.y));
+    }
+    if (MODE != P3_ML) {
+      LineEntry S = sl[(size_t)j * a.stride];
+      f = g_mul_line(g, f, S.a0, S.a1, S.b1);
+    }
     if (dbl) {
       pending_add = ((HB_X_ABS >> bit) & 1) != 0;
       bit--;
@@ -60,11 +76,28 @@ __global__ KB_OCC(HB_OCC_PAIR3) void k_pair3(Pair3Args a) {
       pending_add = false;
     }
   }
+  if (MODE == P3_ML) {
+    Fp4 r;
+    f4_select(r, a.pk_st && a.pk_st[e], f, g_one(g));
+    if (valid) a.f_out[3ull * e + g.k] = Fp4Entry{r.x, r.y};
+    return;
+  }
+  if (MODE == P3_FIN) {  // times the stored Miller loops of entries [e f_range, ...) (wave-uniform trip count)
+    const uint32_t first = e * a.f_range;
+    const uint32_t cnt = first < a.f_n ? min(a.f_range, a.f_n - first) : 0u;
+    HB_NOUNROLL for (uint32_t j = 0; j < a.f_range; j++) {
+      const uint32_t idx = j < cnt ? first + j : 0u;
+      Fp4 t;
+      f4_select(t, j >= cnt, f4_load(a.f_in[3ull * idx + g.k]), g_one(g));
+      f = g_mul(g, f, t);
+    }
+  }
   f = g_final_exp(g, f);
   const bool one = g_is_one(g, f);
   if (valid && g.k == 0) {
     uint8_t s;
-    if (!agg && a.pk_st && a.pk_st[e]) s = ST_BAD_PUBKEY;
+    if (MODE == P3_FIN) s = (a.pk_st && a.pk_st[e]) ? (uint8_t)1 : (one ? ST_OK : ST_NOT_VERIFIED);
+    else if (!agg && a.pk_st && a.pk_st[e]) s = ST_BAD_PUBKEY;
     else if (!agg && a.sig_st && a.sig_st[e]) s = ST_BAD_SIGNATURE;
     else if (P.inf || (!agg && a.sig_inf && a.sig_inf[e]) || a.hm[m].h.inf) s = ST_NOT_VERIFIED;  // verify_core
     else s = one ? ST_OK : ST_NOT_VERIFIED;
@@ -79,10 +112,14 @@ static inline unsigned blocks_for(size_t n) { return (unsigned)((n + BLOCK - 1) 
 void launch_lines_msg(MsgEntry* hm, uint32_t n, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_lines_msg, dim3(blocks_for(n)), dim3(BLOCK), 0, s, hm, n);
 }
-void launch_pair3(const Pair3Args& a, hipStream_t s) {
+template <int MODE>
+static void pair3_launch(const Pair3Args& a, hipStream_t s) {
   if (!a.n) return;
   unsigned grid = (unsigned)((a.n + GROUPS_PER_WAVE - 1) / GROUPS_PER_WAVE);
-  hipLaunchKernelGGL(k_pair3, dim3(grid), dim3(64), 0, s, a);
+  hipLaunchKernelGGL(k_pair3<MODE>, dim3(grid), dim3(64), 0, s, a);
 }
+void launch_pair3(const Pair3Args& a, hipStream_t s) { pair3_launch<P3_FULL>(a, s); }
+void launch_pair3_ml(const Pair3Args& a, hipStream_t s) { pair3_launch<P3_ML>(a, s); }
+void launch_pair3_fin(const Pair3Args& a, hipStream_t s) { pair3_launch<P3_FIN>(a, s); }
 
 }  // namespace hb

@@ -241,7 +241,7 @@ __global__ KB_OCC(HB_OCC_RLC) void k_rlc_msm(RlcMsmArgs a) {
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= *a.total) return;
   const uint32_t first = a.cfirst[c], cc = a.ccount[c], cnt = cc & 0x7fffffffu;
-  const bool single = (cc & 0x80000000u) != 0;
+  const bool single = (cc & 0x80000000u) != 0 && !a.always;
   if (single) {  // r = 1
     const uint32_t i = first;
     const bool usable = !a.pk_st[i] && !a.sig_st[i] && !a.pk[i].inf && !a.sig[i].inf;

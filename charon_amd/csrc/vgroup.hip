@@ -7,6 +7,7 @@
 // subroutine is gone; the kernel is compiled like the other fast units.
 #define HB_FAST_FPMUL 1
 #include "lines.h"
+#include "pair3.h"
 
 namespace hb {
 
@@ -14,12 +15,11 @@ __device__ __forceinline__ bool item_usable_g(const G1AEntry& p, uint8_t pst, co
   return !pst && !sst && !p.inf && !s.inf;
 }
 
-// One lane per verification group: sum the combined points of its usable items (plus the folded
-// aggregate), affine, and the Miller lines of the signature side evaluated at -g1.
-__global__ KB_OCC(HB_OCC_PREP) void k_group_prep(GroupPrepArgs a) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  const uint32_t lg = blockIdx.x * blockDim.x + threadIdx.x;
-  if (lg >= a.ng) return;
+// The group's state; when READY, P = its combined public key (affine, finite) and its combined
+// signature as S (Jacobian; BATCH) or Sa (affine).  Group sizes of one without an aggregate keep
+// r = 1 (k_rlc) and take the decoded points directly unless BATCH (random r for every item).
+template <bool BATCH>
+__device__ __forceinline__ uint8_t group_scan(const GroupPrepArgs& a, uint32_t lg, G1A& P, G2J& S, G2A& Sa) {
   const uint32_t g = a.g0 + lg;
   const uint32_t b = a.grp_off ? a.grp_off[g] : g, e = a.grp_off ? a.grp_off[g + 1] : g + 1;
   uint32_t cnt = 0, first = b, m = 0;
@@ -39,56 +39,133 @@ __global__ KB_OCC(HB_OCC_PREP) void k_group_prep(GroupPrepArgs a) {
                         cnt > 0;  // the aggregate takes its message from the group's partials
   if (cnt == 0 && e > b) m = a.msg_idx[b];  // the folded aggregate's message (a fallback may need it)
   a.gmsg[g] = m;
-  if (cnt == 0 || a.hm[m].h.inf) {
-    a.gst[lg] = G_EMPTY;
-    return;
-  }
-  if (!consistent) {
-    a.gst[lg] = G_FALLBACK;
-    return;
-  }
-  G1A P;
-  G2A S;
-  if (cnt == 1 && !with_agg) {
+  if (cnt == 0 || a.hm[m].h.inf) return G_EMPTY;
+  if (!consistent) return G_FALLBACK;
+  if (!BATCH && cnt == 1 && !with_agg) {
     P = g1a_load(a.pk[first]);
-    S = hm_load(a.sig[first]);
+    Sa = hm_load(a.sig[first]);
+    return G_READY;
+  }
+  // unusable items hold the point at infinity (k_rlc): a plain sum
+  G1J pacc = jac_infinity<Fp>();
+  G2J sacc = jac_infinity<Fp2>();
+  for (uint32_t i = b; i < e; i++) {
+    const G1JEntry pj = a.pr[i];
+    const G2JEntry sj = a.sr[i];
+    pacc = jac_add(pacc, G1J{pj.X, pj.Y, pj.Z});
+    sacc = jac_add(sacc, G2J{sj.X, sj.Y, sj.Z});
+  }
+  if (with_agg) {
+    const G1JEntry pj = a.agg_pr[g];
+    const G2JEntry sj = a.agg_sr[g];
+    pacc = jac_add(pacc, G1J{pj.X, pj.Y, pj.Z});
+    sacc = jac_add(sacc, G2J{sj.X, sj.Y, sj.Z});
+  }
+  P = jac_to_aff(pacc);
+  bool s_inf;
+  if (BATCH) {
+    S = sacc;
+    s_inf = jac_is_inf(sacc);
   } else {
-    // unusable items hold the point at infinity (k_rlc): a plain sum
-    G1J pacc = jac_infinity<Fp>();
-    G2J sacc = jac_infinity<Fp2>();
-    for (uint32_t i = b; i < e; i++) {
-      const G1JEntry pj = a.pr[i];
-      const G2JEntry sj = a.sr[i];
-      pacc = jac_add(pacc, G1J{pj.X, pj.Y, pj.Z});
-      sacc = jac_add(sacc, G2J{sj.X, sj.Y, sj.Z});
-    }
-    if (with_agg) {
-      const G1JEntry pj = a.agg_pr[g];
-      const G2JEntry sj = a.agg_sr[g];
-      pacc = jac_add(pacc, G1J{pj.X, pj.Y, pj.Z});
-      sacc = jac_add(sacc, G2J{sj.X, sj.Y, sj.Z});
-    }
-    P = jac_to_aff(pacc);
-    S = jac_to_aff(sacc);
+    Sa = jac_to_aff(sacc);
+    s_inf = Sa.inf;
   }
-  if (P.inf || S.inf) {  // a degenerate combination (probability ~2^-64): check every item alone
-    a.gst[lg] = G_FALLBACK;
-    return;
-  }
+  // a degenerate combination (probability ~2^-64): check every item alone
+  return (P.inf || s_inf) ? G_FALLBACK : G_READY;
+}
+
+__device__ __forceinline__ void store_gp(G1AEntry* out, const G1A& P) {
   G1AEntry pe;
   pe.x = P.x;
   pe.y = P.y;
   pe.inf = 0;
   pe.pad[0] = pe.pad[1] = pe.pad[2] = 0;
-  a.gP[lg] = pe;
-  a.gst[lg] = G_READY;
-  line_chain<true>(S, a.glines + lg, a.ng);
+  *out = pe;
+}
+
+// One lane per verification group: sum the combined points of its usable items (plus the folded
+// aggregate), affine, and the Miller lines of the signature side evaluated at -g1.
+__global__ KB_OCC(HB_OCC_PREP) void k_group_prep(GroupPrepArgs a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t lg = blockIdx.x * blockDim.x + threadIdx.x;
+  if (lg >= a.ng) return;
+  G1A P;
+  G2J S;
+  G2A Sa;
+  const uint8_t st = group_scan<false>(a, lg, P, S, Sa);
+  a.gst[lg] = st;
+  if (st != G_READY) return;
+  store_gp(a.gP + lg, P);
+  line_chain<true>(Sa, a.glines + lg, a.ng);
 #endif
 }
 
+// Batched final exponentiation: one lane per group as above but no lines; the group's S is kept
+// (gS) and the 64 groups of the wave -- one batch -- sum their S into bS (butterfly over the wave).
+__global__ KB_OCC(HB_OCC_PREP) void k_group_prep_b(GroupPrepArgs a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t lg = blockIdx.x * blockDim.x + threadIdx.x;
+  G2J S = jac_infinity<Fp2>();
+  if (lg < a.ng) {
+    G1A P;
+    G2J Sg;
+    G2A Sa;
+    const uint8_t st = group_scan<true>(a, lg, P, Sg, Sa);
+    a.gst[lg] = st;
+    if (st == G_READY) {
+      store_gp(a.gP + lg, P);
+      S = Sg;
+    }
+    a.gS[lg] = {S.X, S.Y, S.Z};
+  }
+  const int lane = (int)(threadIdx.x & 63u);
+  HB_NOUNROLL for (int off = 32; off; off >>= 1) {
+    const int addr = (lane ^ off) << 2;
+    const G2J T = {xch(S.X, addr), xch(S.Y, addr), xch(S.Z, addr)};
+    S = jac_add(S, T);
+  }
+  if (lane == 0) a.bS[blockIdx.x] = {S.X, S.Y, S.Z};
+#endif
+}
+
+__global__ KB_OCC(HB_OCC_LINES) void k_slines(const G2JEntry* __restrict__ pts, const uint32_t* __restrict__ list,
+                                             const uint32_t* __restrict__ count, uint32_t n,
+                                             LineEntry* __restrict__ lines, uint32_t stride, uint8_t* __restrict__ bad) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t avail = list ? min(*count, n) : n;
+  if (u >= avail) return;
+  const uint32_t e = list ? list[u] : u;
+  const G2JEntry pe = pts[e];
+  const G2A S = jac_to_aff(G2J{pe.X, pe.Y, pe.Z});
+  if (bad) bad[u] = S.inf ? 1 : 0;
+  if (S.inf) return;  // the verdict comes from bad[u]; the lines are never used
+  line_chain<true>(S, lines + u, stride);
+#endif
+}
+
+__global__ __launch_bounds__(64) void k_batch_verdict(const uint8_t* __restrict__ gst, const uint8_t* __restrict__ bver, uint32_t ng,
+                                   uint8_t* __restrict__ gver, uint32_t* __restrict__ list,
+                                   uint32_t* __restrict__ count) {
+  const uint32_t lg = blockIdx.x * blockDim.x + threadIdx.x;
+  if (lg >= ng) return;
+  if (gst[lg] != G_READY) gver[lg] = 1;
+  else if (bver[lg / FE_BATCH] == 0) gver[lg] = 0;
+  else list[atomicAdd(count, 1u)] = lg;
+}
 
 void launch_group_prep(const GroupPrepArgs& a, hipStream_t s) {
-  if (a.ng) hipLaunchKernelGGL(k_group_prep, dim3((a.ng + 63) / 64), dim3(64), 0, s, a);
+  if (!a.ng) return;
+  if (a.gS) hipLaunchKernelGGL(k_group_prep_b, dim3((a.ng + FE_BATCH - 1) / FE_BATCH), dim3(FE_BATCH), 0, s, a);
+  else hipLaunchKernelGGL(k_group_prep, dim3((a.ng + 63) / 64), dim3(64), 0, s, a);
+}
+void launch_slines(const G2JEntry* pts, const uint32_t* list, const uint32_t* count, uint32_t n, LineEntry* lines,
+                   uint32_t stride, uint8_t* bad, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_slines, dim3((n + 63) / 64), dim3(64), 0, s, pts, list, count, n, lines, stride, bad);
+}
+void launch_batch_verdict(const uint8_t* gst, const uint8_t* bver, uint32_t ng, uint8_t* gver, uint32_t* list,
+                          uint32_t* count, hipStream_t s) {
+  if (ng) hipLaunchKernelGGL(k_batch_verdict, dim3((ng + 63) / 64), dim3(64), 0, s, gst, bver, ng, gver, list, count);
 }
 
 }  // namespace hb

@@ -50,6 +50,24 @@ def pair3(b=BLOCKS):
     return alg, exe
 
 
+FE_BATCH = 64    # groups per batched final exponentiation (layout.h)
+
+
+def pair3_ml(b=BLOCKS):
+    """k_pair3_ml, per verification group: the Miller loop of (P, H(m)) alone, stored."""
+    alg = N_SQR * b["f12_sqr"] + N_LINES * b["f12_mul_line"] + N_LINES * 4
+    exe = N_SQR * 36 + N_LINES * 45 + N_LINES * 12
+    return alg, exe
+
+
+def pair3_fin(b=BLOCKS, batch=FE_BATCH):
+    """k_pair3_fin, per batch of `batch` groups: the Miller loop of (-g1, sum S), times the stored
+    loops, one final exponentiation."""
+    alg = N_SQR * b["f12_sqr"] + N_LINES * b["f12_mul_line"] + batch * b["f12_mul"] + b["final_exp"]
+    exe = N_SQR * 36 + N_LINES * 45 + batch * 54 + 3 * _pair3_exec_per_lane(b)
+    return alg, exe
+
+
 RLC_CHUNK = 16   # items per lane of k_rlc_msm (layout.h)
 TA_CHUNK = 8     # members per lane of k_ta_msm (layout.h)
 
@@ -134,6 +152,14 @@ def per_unit(b=BLOCKS, group_size=1, t=1):
         "k_seg_sum": (b["jac_add_aff_g1"],) * 2,
         "k_va_point": (b["to_aff_g1"],) * 2,
         "k_sig_lines": (b["lines_eval"],) * 2,
+        # batched final exponentiation (vgroup.hip): per group the sums, the affine key, one share
+        # of the batch sum (executed: the six-level butterfly in every lane) and the stored loop;
+        # per batch the lines of the summed signature side and the shared exponentiation
+        "k_group_prep_b": ((k - 1) * (b["jac_add_g1"] + b["jac_add_g2"]) + b["to_aff_g1"] + b["jac_add_g2"],
+                           (k - 1) * (b["jac_add_g1"] + b["jac_add_g2"]) + b["to_aff_g1"] + 6 * b["jac_add_g2"]),
+        "k_pair3_ml": pair3_ml(b),
+        "k_pair3_fin": pair3_fin(b),
+        "k_slines": (b["to_aff_g2"] + b["lines_eval"],) * 2,
     }
     return out
 
@@ -142,7 +168,9 @@ UNITS = {"k_pair3": "pairing check", "k_pair3_fallback": "pairing check", "k_dec
          "k_dec_sig_pt": "signature", "k_rlc": "partial", "k_group_prep": "verification group",
          "k_fb_lines": "partial", "k_ta_straus": "aggregation member", "k_group_sum": "aggregation group",
          "k_hash_to_g2": "message", "k_lines_msg": "message", "k_seg_sum": "public key (pass 1)",
-         "k_va_point": "aggregation group", "k_sig_lines": "signature"}
+         "k_va_point": "aggregation group", "k_sig_lines": "signature", "k_group_prep_b": "verification group",
+         "k_pair3_ml": "verification group", "k_pair3_fin": "batch of 64 groups",
+         "k_slines": "batch of 64 groups"}
 
 # SHA-256 compressions per attestation signing root (roots.hip: 8 two-block hashes)
 SHA256_PER_ATTESTATION_ROOT = 16

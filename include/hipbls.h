@@ -219,8 +219,13 @@ int hbls_timing(int enable);
 int hbls_timing_read(const char** names, float* ms, size_t max_n, size_t* n_out);
 /* Verification statistics, collected only with HBLS_STATS=1 in the environment (each call then
  * synchronises): out[0] items verified, out[1] verification groups, out[2] items re-checked
- * alone because their group's combined check failed. */
+ * alone because their group's combined check failed, out[3] groups checked alone because their
+ * batch's shared final exponentiation failed. */
 int hbls_stats(uint64_t* out, size_t n);
+/* Tuning: verifications of at least min_groups groups share one final exponentiation among 64
+ * groups (0 = one per group; default 128, HBLS_FE_BATCH).  Returns the previous value.  Verdicts
+ * do not depend on it. */
+size_t hbls_fe_batch(size_t min_groups);
 /* Wait for all work the library queued on `stream`. */
 int hbls_sync(void* stream);
 

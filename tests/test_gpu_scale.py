@@ -82,10 +82,20 @@ def _pks(L, sks):
     return out
 
 
+@pytest.fixture
+def fe_mode(L, request):
+    """Batched final exponentiation on (the default at these sizes) or off for the test."""
+    prev = L.hbls_fe_batch(128 if request.param == "fe_batch" else 0)
+    yield request.param
+    L.hbls_fe_batch(prev)
+
+
+@pytest.mark.parametrize("fe_mode", ["fe_batch", "fe_per_group"], indirect=True)
 @pytest.mark.parametrize("key_tables", [False, True], ids=["decompress", "key_tables"])
-def test_slot_adversarial_c2(L, key_tables):
+def test_slot_adversarial_c2(L, key_tables, fe_mode):
     """key_tables: the public keys come from tables made once by hbls_decompress_pubkeys_device
-    (the slot's pk_table / dv_pk_table) -- same verdicts and aggregates."""
+    (the slot's pk_table / dv_pk_table) -- same verdicts and aggregates.  fe_mode: 64 groups per
+    final exponentiation, or one per group -- same verdicts."""
     import torch
     from charon_amd import synth
     V, n, t = 10_000, 4, 3
@@ -315,9 +325,37 @@ def test_device_call_and_host_call_do_not_race(L, hipbls):
 
 
 def _stats(L):
-    out = (ctypes.c_uint64 * 3)()
-    assert L.hbls_stats(out, 3) == 0
+    out = (ctypes.c_uint64 * 4)()
+    assert L.hbls_stats(out, 4) == 0
     return list(out)
+
+
+def test_batched_fe_rejects_cancelling_errors(L, hipbls, monkeypatch):
+    """300 items over distinct messages (300 groups of one: 5 batches of 64 groups share their
+    final exponentiations).  Two signatures carry opposite errors, sig0 + D and sig1 - D: the
+    plain sum of the batch is unchanged, so the batch check must weigh every item by its own
+    random coefficient (groups of one included) to reject them -- and it does, exactly those two.
+    A clean run of the same size needs no per-group check."""
+    from oracle import bls12381 as B
+    monkeypatch.setenv("HBLS_STATS", "1")
+    n = 300
+    keys = [hipbls.generate_secret_key() for _ in range(n)]
+    msgs = [hashlib.sha256(b"duty %d" % k).digest() for k in range(n)]
+    sigs = hipbls.sign_batch(keys, msgs)
+    pks = [hipbls.secret_to_public_key(k) for k in keys]
+    s0 = _stats(L)
+    assert hipbls.verify_batch(pks, msgs, sigs) == [OK] * n
+    d = [b - a for a, b in zip(s0, _stats(L))]
+    assert d[1] == n and d[2] == 0 and d[3] == 0, d
+    D = B.g2_decompress(sigs[7])
+    bad = list(sigs)
+    bad[0] = B.g2_compress(B.g2_add(B.g2_decompress(sigs[0]), D))
+    bad[1] = B.g2_compress(B.g2_add(B.g2_decompress(sigs[1]), B.g2_neg(D)))
+    s0 = _stats(L)
+    st = hipbls.verify_batch(pks, msgs, bad)
+    assert st == [NOT_VERIFIED if i < 2 else OK for i in range(n)]
+    d = [b - a for a, b in zip(s0, _stats(L))]
+    assert d[3] >= 1 and d[2] == 2, d  # the failing batch's groups checked alone, then the two items
 
 
 def test_batched_groups_pass_without_fallback(L, hipbls, monkeypatch):
