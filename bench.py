@@ -192,6 +192,7 @@ def cpu_baseline(d, seconds: float):
     hc = ctypes.CDLL(build_hostcheck(verbose=False))
     n, t = d["n"], d["t"]
     midx = np.ascontiguousarray(d["midx"], dtype=np.uint32)
+    ta_idx = np.ascontiguousarray(d["ta_idx"], dtype=np.int64)  # the aggregated share indices, per validator
     try:
         threads = max(1, min(16, len(os.sched_getaffinity(0))))
     except AttributeError:
@@ -200,7 +201,7 @@ def cpu_baseline(d, seconds: float):
     def run(units, th):
         t0 = time.perf_counter()
         bad = hc.hc_cpu_slot(th, units, n, t, _p(d["pks"]), _p(d["sigs"]), _p(d["msgs"]), _p(midx),
-                             _p(d["ta_sigs"]), _p(d["root_sigs"]))
+                             _p(d["ta_sigs"]), _p(d["root_sigs"]), _p(ta_idx))
         return time.perf_counter() - t0, bad
 
     per_unit, bad = run(1, 1)
