@@ -610,19 +610,25 @@ def main(argv=None):
         ta_units = V * t
         # k_rlc: the partials as multi-scalar chunks (one per validator), then the folded
         # aggregates (slot mode)
-        rlc_item = opcounts.BLOCKS["rlc_g1"] + opcounts.BLOCKS["rlc_g2"]
-        n_rlc = NP + (0 if staged else V)
-        cmax = min(opcounts.RLC_CHUNK, max(1, NP // int(os.environ.get("HBLS_RLC_LANES", "65536"))))
-        if cmax > 1:  # the library's chunking (hipbls.hip verify_pipeline): balanced chunks of a group
-            n_chunks = -(-n // cmax)
-            rlc_partial = opcounts.rlc_msm(chunk=n / n_chunks)
-        else:
-            rlc_partial = rlc_item
         # batched final exponentiation (the library's setting; verifications of >= fe_min groups):
         # every folded aggregate then takes a random coefficient (one ladder each), else r = 1
         fe_min = L.hbls_fe_batch(0)
         L.hbls_fe_batch(fe_min)
         bfe = fe_min and V >= fe_min
+        # slot-wide check (the library's setting): the signature side as one MSM, so the
+        # combination kernels compute the public-key side only
+        s_min = L.hbls_slot_msm(0)
+        L.hbls_slot_msm(s_min)
+        n_rlc = NP + (0 if staged else V)
+        smsm = bool(bfe and s_min and n_rlc >= s_min)
+        sides = 1 if smsm else 3
+        rlc_item = opcounts.BLOCKS["rlc_g1"] + (opcounts.BLOCKS["rlc_g2"] if sides & 2 else 0)
+        cmax = min(opcounts.RLC_CHUNK, max(1, NP // int(os.environ.get("HBLS_RLC_LANES", "65536"))))
+        if cmax > 1:  # the library's chunking (hipbls.hip verify_pipeline): balanced chunks of a group
+            n_chunks = -(-n // cmax)
+            rlc_partial = opcounts.rlc_msm(chunk=n / n_chunks, sides=sides)
+        else:
+            rlc_partial = rlc_item
         rlc_avg = (NP * rlc_partial + (0 if staged or not bfe else V * rlc_item)) / n_rlc
         ta_w = opcounts.ta_uniform([x + 1 for x in ta_share_positions(n, t)])
         prep_units = opcounts.per_unit(group_size=n + (0 if staged else 1), t=t)
@@ -632,7 +638,18 @@ def main(argv=None):
                  # the aggregation ladders: the uniform-digit schedule of the aggregated index set
                  "k_ta_straus": (ta_units, (ta_w, ta_w)), "k_group_sum": (V, per_unit["k_group_sum"]),
                  "k_hash_to_g2": (M, per_unit["k_hash_to_g2"]), "k_lines_msg": (M, per_unit["k_lines_msg"])}
-        if bfe:
+        if smsm:
+            nb1 = -(-V // opcounts.FE_BATCH)
+            nb2 = -(-nb1 // opcounts.FE_BATCH)
+            fin = opcounts.pair3_fin(batch=nb2)
+            units.update({"k_group_prep": (V, prep_units["k_group_prep_p"]),
+                          "k_pair3_ml": (V, per_unit["k_pair3_ml"]),
+                          "k_pair3_prod": (V + nb1, per_unit["k_pair3_prod"]),
+                          "k_pair3_fin": (1, fin), "k_slines": (1, per_unit["k_slines"]),
+                          "k_msm_bucket": (opcounts.MSM_ENTRIES_PER_ITEM * n_rlc, per_unit["k_msm_bucket"]),
+                          "k_msm_reduce": (opcounts.MSM_PARTS, per_unit["k_msm_reduce"]),
+                          "k_msm_sum": (opcounts.MSM_PARTS + opcounts.MSM_PARTS // 128, per_unit["k_msm_sum"])})
+        elif bfe:
             nb = -(-V // opcounts.FE_BATCH)
             units.update({"k_group_prep": (V, prep_units["k_group_prep_b"]),
                           "k_pair3_ml": (V, per_unit["k_pair3_ml"]), "k_pair3_fin": (nb, per_unit["k_pair3_fin"]),

@@ -223,7 +223,7 @@ size_t env_size(const char* name, size_t dflt) {
 size_t g_gcap = 131072, g_fbcap = 65536, g_gmax = 16;
 // HBLS_RLC_MSM=0: one ladder per item (k_rlc) instead of shared-doubling chunks (k_rlc_msm)
 bool g_rlc_msm = true;
-size_t g_rlc_lanes = 65536;   // HBLS_RLC_LANES: lanes the chunk size aims to keep busy
+std::atomic<size_t> g_rlc_lanes{65536};   // HBLS_RLC_LANES: lanes the chunk size aims to keep busy
 // public-key cache: compressed key -> entry index (the same on every device)
 std::mutex g_kc_mu;
 std::unordered_map<std::string, uint32_t> g_kc_map;
@@ -237,6 +237,11 @@ size_t g_ta_chunk = 4;   // HBLS_TA_CHUNK: members per lane of k_ta_msm (<= TA_C
 // HBLS_FE_BATCH: verifications of at least this many groups check FE_BATCH groups per final
 // exponentiation (vgroup.hip; 0 = one final exponentiation per group)
 std::atomic<size_t> g_fe_batch_min{2 * FE_BATCH};
+// HBLS_SLOT_MSM: batched verifications of at least this many items (partials + folded aggregates,
+// one chunk of groups) check every group at once -- the signature side as one multi-scalar
+// multiplication (msm.hip), one final exponentiation for the call -- and fall back to the
+// per-batch check when that fails (0 = never)
+std::atomic<size_t> g_slot_msm_min{65536};
 
 struct DevBuf {
   void* p = nullptr;
@@ -253,6 +258,7 @@ enum WsId {
   W_PCNT, W_PCOFF, W_PCFIRST, W_PCCOUNT, W_COEF, W_RT1, W_RT2,  // chunk plan + multi-scalar RLC
   W_TPCNT, W_TPCOFF, W_TPCFIRST, W_TPCCOUNT,                    // chunk plan of the aggregation
   W_FBUF, W_GS, W_BS, W_BLINES, W_BBAD, W_BVER, W_GLIST, W_GCOUNT,  // batched final exponentiation
+  W_MCNT, W_MOFF, W_MCUR, W_MENT, W_MBUCKET, W_MPART, W_MPART2, W_MTOT, W_PBUF1, W_PBUF2, W_SFAIL,  // slot-wide check
   W_COUNT_
 };
 
@@ -269,7 +275,7 @@ struct Ws {
   hipEvent_t free_ev = nullptr;
   bool used = false;
   hipStream_t side[N_SIDE] = {};
-  hipEvent_t ev_fork = nullptr, ev_side[N_SIDE] = {}, ev_ta = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_side[N_SIDE] = {}, ev_ta = nullptr, ev_msm = nullptr;
 };
 
 // host-call staging buffers (inputs and outputs of the host-buffer entry points)
@@ -402,6 +408,7 @@ int dev_create(int ord, Dev** out) {
     }
     HCHK(hipEventCreateWithFlags(&w.ev_fork, hipEventDisableTiming));
     HCHK(hipEventCreateWithFlags(&w.ev_ta, hipEventDisableTiming));
+    HCHK(hipEventCreateWithFlags(&w.ev_msm, hipEventDisableTiming));
   }
   *out = d;
   return 0;
@@ -430,10 +437,11 @@ int init_mask(uint32_t mask) {
   g_fbcap = env_size("HBLS_FALLBACK_CHUNK", g_fbcap);
   g_gmax = std::max<size_t>(1, env_size("HBLS_GROUP_MAX", g_gmax));
   g_rlc_msm = env_size("HBLS_RLC_MSM", 1) != 0;
-  g_rlc_lanes = std::max<size_t>(1, env_size("HBLS_RLC_LANES", g_rlc_lanes));
+  g_rlc_lanes = std::max<size_t>(1, env_size("HBLS_RLC_LANES", g_rlc_lanes.load()));
   g_ta_msm = env_size("HBLS_TA_MSM", 0) != 0;
   g_ta_chunk = std::min<size_t>(TA_CHUNK, std::max<size_t>(1, env_size("HBLS_TA_CHUNK", g_ta_chunk)));
   g_fe_batch_min = env_size("HBLS_FE_BATCH", g_fe_batch_min.load());
+  g_slot_msm_min = env_size("HBLS_SLOT_MSM", g_slot_msm_min.load());
   std::vector<Dev*> devs;
   for (int k = 0; k < 32; k++)
     if (mask & (1u << k)) {
@@ -497,7 +505,7 @@ int rlc_key(RlcKey& k) {
 // post-aggregate verification under the DV keys (sigagg.go:117) into the same groups.
 // ---------------------------------------------------------------------------------------
 // verification statistics (HBLS_STATS=1): items, groups, items re-checked alone
-std::atomic<uint64_t> g_stats[4];
+std::atomic<uint64_t> g_stats[6];
 bool stats_on() {
   const char* v = getenv("HBLS_STATS");
   return v && v[0] == '1';
@@ -608,6 +616,23 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
               wsbuf(w, W_BLINES, nbcap * N_LINES, &blines) || wsbuf(w, W_BBAD, nbcap, &bbad) ||
               wsbuf(w, W_BVER, nbcap, &bver) || wsbuf(w, W_GLIST, gcap, &glist) || wsbuf(w, W_GCOUNT, 1, &gcount)))
     return -1;
+  // Slot-wide check (msm.hip): every group of the call at once, the signature side as one
+  // multi-scalar multiplication; the per-batch path below runs only if it fails (its kernels wait
+  // on the device flag sfail).  Needs all groups in one chunk.
+  const size_t smin = g_slot_msm_min.load();
+  const bool smsm = bfe && smin && n_groups <= gcap && n + n_agg >= smin;
+  const size_t nb1 = (gcap + FE_BATCH - 1) / FE_BATCH, nb2 = (nb1 + FE_BATCH - 1) / FE_BATCH;
+  G2MsmArgs ma{};
+  Fp4Entry *pbuf1 = nullptr, *pbuf2 = nullptr;
+  uint8_t* sfail = nullptr;
+  if (smsm && (wsbuf(w, W_MCNT, MSM_KEYS, &ma.cnt) || wsbuf(w, W_MOFF, MSM_KEYS + 1, &ma.off) ||
+               wsbuf(w, W_MCUR, MSM_KEYS, &ma.cur) || wsbuf(w, W_MENT, 2 * MSM_WINDOWS * (n + n_agg), &ma.ent) ||
+               wsbuf(w, W_MBUCKET, MSM_KEYS, &ma.bucket) || wsbuf(w, W_MPART, MSM_PARTS, &ma.part) ||
+               wsbuf(w, W_MPART2, MSM_PARTS / 128, &ma.part2) || wsbuf(w, W_MTOT, 1, &ma.total) ||
+               wsbuf(w, W_PBUF1, 3 * nb1, &pbuf1) || wsbuf(w, W_PBUF2, 3 * nb2, &pbuf2) ||
+               wsbuf(w, W_SFAIL, 1, &sfail)))
+    return -1;
+  const int sides1 = smsm ? 1 : 3;  // first pass: the public-key side only when the MSM takes the other
 
   // fork: decompression on the side streams (after the previous verification's decompression)
   if (d.dec_valid) HCHK(hipStreamWaitEvent(s, d.ev_dec, 0));
@@ -664,7 +689,10 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
   HCHK(hipEventRecord(d.ev_dec, s));
   d.dec_valid = true;
   TIMED(d, "k_item_group", s, launch_item_group(dgoff, (uint32_t)n_groups, (uint32_t)n, igrp, s));
-  const uint32_t rlc_cmax = (uint32_t)std::min<size_t>(RLC_CHUNK, std::max<size_t>(1, n / g_rlc_lanes));
+  const uint32_t rlc_cmax = (uint32_t)std::min<size_t>(RLC_CHUNK, std::max<size_t>(1, n / g_rlc_lanes.load()));
+  RlcMsmArgs rlc_fallback{};
+  uint32_t rlc_fallback_chunks = 0;
+  uint2* coef_pi = nullptr;  // per-item path's coefficients (slot-wide check)
   if (dgoff && g_rlc_msm && rlc_cmax > 1) {
     // chunks of a group's items share their ladders' doublings (k_rlc_msm); the chunk size keeps
     // about g_rlc_lanes lanes busy (at most RLC_CHUNK items, one item per lane for small calls)
@@ -676,7 +704,7 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
     G2J* t2;
     if (wsbuf(w, W_PCNT, n_groups, &pcnt) || wsbuf(w, W_PCOFF, n_groups + 1, &pcoff) ||
         wsbuf(w, W_PCFIRST, max_chunks, &pcf) || wsbuf(w, W_PCCOUNT, max_chunks, &pcc) ||
-        wsbuf(w, W_COEF, n, &coef) || wsbuf(w, W_RT1, 3 * n, &t1) || wsbuf(w, W_RT2, 3 * n, &t2))
+        wsbuf(w, W_COEF, n + n_agg, &coef) || wsbuf(w, W_RT1, 3 * n, &t1) || wsbuf(w, W_RT2, 3 * n, &t2))
       return -1;
     TIMED(d, "k_plan", s, launch_plan(dgoff, (uint32_t)n_groups, cmax, pcnt, pcoff, pcf, pcc, s));
     RlcMsmArgs ra{};
@@ -695,10 +723,19 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
     ra.pout = pr;
     ra.sout = sr;
     ra.always = bfe ? 1 : 0;
+    ra.sides = sides1;
     TIMED(d, "k_rlc", s, launch_rlc_msm(ra, (uint32_t)max_chunks, s));
+    if (smsm) {  // the per-item signature side, only if the slot-wide check fails
+      ra.sides = 2;
+      ra.guard = sfail;
+      rlc_fallback = ra;
+      rlc_fallback_chunks = (uint32_t)max_chunks;
+    }
   } else {
+    if (smsm && wsbuf(w, W_COEF, n + n_agg, &coef_pi)) return -1;
     TIMED(d, "k_rlc", s,
-          launch_rlc(vpk, vpkst, vsig, vsigst, igrp, dgoff, bfe ? 1 : 0, (uint32_t)n, 0, key, pr, sr, s));
+          launch_rlc(vpk, vpkst, vsig, vsigst, igrp, dgoff, bfe ? 1 : 0, (uint32_t)n, 0, key, pr, sr, s, coef_pi,
+                     sides1));
   }
   if (n_agg) {
     // without the batched final exponentiation the folded aggregate keeps r = 1: one coefficient
@@ -706,9 +743,10 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
     // combined check exactly; with an invalid partial j beside it the check passes for one value
     // of the random r_j only)
     HCHK(hipStreamWaitEvent(s, w.ev_ta, 0));
+    uint2* acoef = smsm ? (coef_pi ? coef_pi : rlc_fallback.coef) + n : nullptr;
     TIMED(d, "k_rlc", s,
           launch_rlc(apk, apkst, asig, fold->ta_status, nullptr, nullptr, bfe ? 1 : 0, (uint32_t)n_agg, (uint32_t)n,
-                     key, apr, asr, s));
+                     key, apr, asr, s, acoef, sides1));
   }
   if (hm_ready) HCHK(hipStreamWaitEvent(s, hm_ready, 0));
   for (size_t g0 = 0; g0 < n_groups; g0 += gcap) {
@@ -738,11 +776,7 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
     ga.gst = gst;
     ga.glines = glines;
     if (bfe) {
-      ga.gS = gS;
-      ga.bS = bS;
-      TIMED(d, "k_group_prep", s, launch_group_prep(ga, s));
       const uint32_t nb = (ng + FE_BATCH - 1) / FE_BATCH;
-      // the (P_g, H(m_g)) Miller loops, stored unexponentiated
       Pair3Args pm{};
       pm.pk = gP;
       pm.pk_st = gst;
@@ -752,10 +786,81 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
       pm.stride = ng;
       pm.n = ng;
       pm.f_out = fbuf;
-      TIMED(d, "k_pair3_ml", s, launch_pair3_ml(pm, s));
+      if (smsm) {
+        // the groups' public-key sides and states; then beside each other: the (P_g, H(m_g))
+        // Miller loops and their product tree (s), the MSM of the signature side and its lines (side 0)
+        ga.p_only = 1;
+        TIMED(d, "k_group_prep", s, launch_group_prep(ga, s));
+        HCHK(hipEventRecord(w.ev_msm, s));
+        hipStream_t sm = w.side[0];
+        HCHK(hipStreamWaitEvent(sm, w.ev_msm, 0));
+        ma.sig = vsig;
+        ma.agg_sig = asig;
+        ma.coef = coef_pi ? coef_pi : rlc_fallback.coef;
+        ma.igrp = igrp;
+        ma.gst = gst;
+        ma.n = (uint32_t)n;
+        ma.n_agg = (uint32_t)n_agg;
+        HCHK(hipMemsetAsync(ma.cnt, 0, MSM_KEYS * sizeof(uint32_t), sm));
+        HCHK(hipMemsetAsync(ma.cur, 0, MSM_KEYS * sizeof(uint32_t), sm));
+        TIMED(d, "k_msm_count", sm, launch_msm_count(ma, sm));
+        TIMED(d, "k_msm_scan", sm, launch_scan(ma.cnt, MSM_KEYS, ma.off, sm));
+        TIMED(d, "k_msm_fill", sm, launch_msm_fill(ma, sm));
+        TIMED(d, "k_msm_bucket", sm, launch_msm_bucket(ma, sm));
+        TIMED(d, "k_msm_reduce", sm, launch_msm_reduce(ma, sm));
+        TIMED(d, "k_msm_sum", sm, launch_msm_sum(ma, sm));
+        TIMED(d, "k_slines", sm, launch_slines(ma.total, nullptr, nullptr, 1, blines, 1, bbad, sm));
+        HCHK(hipEventRecord(w.ev_side[0], sm));
+        TIMED(d, "k_pair3_ml", s, launch_pair3_ml(pm, s));
+        Pair3Args pp{};
+        pp.n = (uint32_t)((ng + FE_BATCH - 1) / FE_BATCH);
+        pp.f_in = fbuf;
+        pp.f_range = FE_BATCH;
+        pp.f_n = ng;
+        pp.f_out = pbuf1;
+        TIMED(d, "k_pair3_prod", s, launch_pair3_prod(pp, s));
+        const uint32_t n1 = pp.n;
+        pp.n = (n1 + FE_BATCH - 1) / FE_BATCH;
+        pp.f_in = pbuf1;
+        pp.f_n = n1;
+        pp.f_out = pbuf2;
+        TIMED(d, "k_pair3_prod", s, launch_pair3_prod(pp, s));
+        HCHK(hipStreamWaitEvent(s, w.ev_side[0], 0));
+        Pair3Args pf{};
+        pf.pk_st = bbad;
+        pf.sig_lines = blines;
+        pf.stride = 1;
+        pf.n = 1;
+        pf.f_in = pbuf2;
+        pf.f_range = pp.n;
+        pf.f_n = pp.n;
+        pf.status = sfail;
+        TIMED(d, "k_pair3_fin", s, launch_pair3_fin(pf, s));
+        TIMED(d, "k_slot_verdict", s, launch_slot_verdict(gst, sfail, ng, gver + g0, s));
+        // the slot-wide check failed: the per-batch check (signature sides per item and group)
+        if (rlc_fallback_chunks) {
+          TIMED(d, "k_rlc", s, launch_rlc_msm(rlc_fallback, rlc_fallback_chunks, s));
+        } else {
+          TIMED(d, "k_rlc", s,
+                launch_rlc(vpk, vpkst, vsig, vsigst, igrp, dgoff, 1, (uint32_t)n, 0, key, pr, sr, s, coef_pi, 2,
+                           sfail));
+        }
+        if (n_agg)
+          TIMED(d, "k_rlc", s,
+                launch_rlc(apk, apkst, asig, fold->ta_status, nullptr, nullptr, 1, (uint32_t)n_agg, (uint32_t)n, key,
+                           apr, asr, s, const_cast<uint2*>(ma.coef) + n, 2, sfail));
+        ga.p_only = 0;
+        ga.guard = sfail;
+      }
+      ga.gS = gS;
+      ga.bS = bS;
+      TIMED(d, "k_group_prep", s, launch_group_prep(ga, s));
+      // the (P_g, H(m_g)) Miller loops, stored unexponentiated
+      if (!smsm) TIMED(d, "k_pair3_ml", s, launch_pair3_ml(pm, s));
       // per batch: the lines of sum_g S_g, one Miller loop times the batch's stored loops, one
       // final exponentiation
-      TIMED(d, "k_slines", s, launch_slines(bS, nullptr, nullptr, nb, blines, nb, bbad, s));
+      const uint8_t* guard = smsm ? sfail : nullptr;
+      TIMED(d, "k_slines", s, launch_slines(bS, nullptr, nullptr, nb, blines, nb, bbad, s, guard));
       Pair3Args pf{};
       pf.pk_st = bbad;
       pf.sig_lines = blines;
@@ -765,10 +870,11 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
       pf.f_range = FE_BATCH;
       pf.f_n = ng;
       pf.status = bver;
+      pf.guard = guard;
       TIMED(d, "k_pair3_fin", s, launch_pair3_fin(pf, s));
       // groups of a failing batch: checked one by one (their stored loop, their own S lines)
       HCHK(hipMemsetAsync(gcount, 0, sizeof(uint32_t), s));
-      TIMED(d, "k_batch_verdict", s, launch_batch_verdict(gst, bver, ng, gver + g0, glist, gcount, s));
+      TIMED(d, "k_batch_verdict", s, launch_batch_verdict(gst, bver, ng, gver + g0, glist, gcount, s, guard));
       TIMED(d, "k_slines", s, launch_slines(gS, glist, gcount, ng, glines, ng, nullptr, s));
       Pair3Args pg{};
       pg.sig_lines = glines;
@@ -854,6 +960,13 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
       HCHK(hipMemcpyAsync(&c, gcount, sizeof(c), hipMemcpyDeviceToHost, s));
       HCHK(hipStreamSynchronize(s));
       g_stats[3] += c;
+    }
+    if (smsm) {
+      uint8_t f = 0;
+      HCHK(hipMemcpyAsync(&f, sfail, 1, hipMemcpyDeviceToHost, s));
+      HCHK(hipStreamSynchronize(s));
+      g_stats[4] += 1;
+      g_stats[5] += f ? 1 : 0;
     }
   }
   return 0;
@@ -1679,11 +1792,13 @@ int hbls_timing_read(const char** names, float* ms, size_t max_n, size_t* n_out)
 }
 
 int hbls_stats(uint64_t* out, size_t n) {
-  for (size_t k = 0; k < n && k < 4; k++) out[k] = g_stats[k].load();
+  for (size_t k = 0; k < n && k < 6; k++) out[k] = g_stats[k].load();
   return stats_on() ? 0 : set_err("statistics are collected only with HBLS_STATS=1");
 }
 
 size_t hbls_fe_batch(size_t min_groups) { return g_fe_batch_min.exchange(min_groups); }
+size_t hbls_slot_msm(size_t min_items) { return g_slot_msm_min.exchange(min_items); }
+size_t hbls_rlc_lanes(size_t lanes) { return g_rlc_lanes.exchange(lanes ? lanes : 65536); }
 
 int hbls_sync(void* stream) {
   HCHK(hipStreamSynchronize((hipStream_t)stream));

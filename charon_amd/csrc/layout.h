@@ -144,10 +144,13 @@ struct Pair3Args {
   Fp4Entry* f_out;
   const Fp4Entry* f_in;
   uint32_t f_range, f_n;
+  const uint8_t* guard;  // nullable: the launch does nothing unless *guard != 0 (slot-wide check failed)
 };
 void launch_pair3(const Pair3Args& a, hipStream_t s);
 void launch_pair3_ml(const Pair3Args& a, hipStream_t s);
 void launch_pair3_fin(const Pair3Args& a, hipStream_t s);
+// PROD: f_out[e] = product of the stored values f_in of entries [e f_range, min((e + 1) f_range, f_n))
+void launch_pair3_prod(const Pair3Args& a, hipStream_t s);
 
 // Batched verification (vbatch.hip).
 void launch_item_group(const uint32_t* grp_off, uint32_t n_groups, uint32_t n, uint32_t* item_grp, hipStream_t s);
@@ -173,13 +176,19 @@ struct RlcMsmArgs {
   G1JEntry* pout;
   G2JEntry* sout;
   int always;     // random r for groups of one item too (batched final exponentiation)
+  int sides;      // 1: public-key side only (coef written); 2: signature side only (coef read); 3: both
+  const uint8_t* guard;  // nullable: nothing unless *guard != 0
 };
 void launch_plan(const uint32_t* grp_off, uint32_t ng, uint32_t cmax, uint32_t* cnt, uint32_t* coff,
                  uint32_t* cfirst, uint32_t* ccount, hipStream_t s);
 void launch_rlc_msm(const RlcMsmArgs& a, uint32_t max_chunks, hipStream_t s);
+// per item; coef (nullable) as RlcMsmArgs::coef with `sides`, guard as RlcMsmArgs::guard
 void launch_rlc(const G1AEntry* pk, const uint8_t* pk_st, const HmEntry* sig, const uint8_t* sig_st,
                 const uint32_t* item_grp, const uint32_t* grp_off, int always, uint32_t n, uint32_t key_base,
-                const RlcKey& key, G1JEntry* pout, G2JEntry* sout, hipStream_t s);
+                const RlcKey& key, G1JEntry* pout, G2JEntry* sout, hipStream_t s, uint2* coef = nullptr,
+                int sides = 3, const uint8_t* guard = nullptr);
+// exclusive scan of cnt[0..n) into off[0..n], off[n] = total (one workgroup)
+void launch_scan(const uint32_t* cnt, uint32_t n, uint32_t* off, hipStream_t s);
 struct GroupPrepArgs {
   const uint32_t* grp_off;  // nullable: group g = item g
   uint32_t g0, ng;          // groups [g0, g0 + ng) of this launch
@@ -206,17 +215,51 @@ struct GroupPrepArgs {
   // READY) and the sum over each batch of FE_BATCH consecutive groups
   G2JEntry* gS;      // [ng]
   G2JEntry* bS;      // [ceil(ng / FE_BATCH)]
+  int p_only;        // slot-wide check (msm.hip): the public-key side and the state only, no S
+  const uint8_t* guard;  // nullable: nothing unless *guard != 0
 };
 constexpr uint32_t FE_BATCH = 64;  // groups per batched final exponentiation (one wave of k_group_prep)
 void launch_group_prep(const GroupPrepArgs& a, hipStream_t s);
 // lines at -g1 of the affine images of pts[e], e = list ? list[u] (u < *count) : u, into
 // lines[j * stride + u]; bad[u] (nullable) = the point is infinity
 void launch_slines(const G2JEntry* pts, const uint32_t* list, const uint32_t* count, uint32_t n, LineEntry* lines,
-                   uint32_t stride, uint8_t* bad, hipStream_t s);
+                   uint32_t stride, uint8_t* bad, hipStream_t s, const uint8_t* guard = nullptr);
 // group verdicts from the batch verdicts: not READY -> 1, READY in a passing batch -> 0, else the
 // group joins list (its verdict comes from the per-group check)
 void launch_batch_verdict(const uint8_t* gst, const uint8_t* bver, uint32_t ng, uint8_t* gver, uint32_t* list,
-                          uint32_t* count, hipStream_t s);
+                          uint32_t* count, hipStream_t s, const uint8_t* guard = nullptr);
+// slot-wide check passed (*sfail == 0): gver[g] = (gst[g] != READY); else nothing (the per-group
+// path decides)
+void launch_slot_verdict(const uint8_t* gst, const uint8_t* sfail, uint32_t ng, uint8_t* gver, hipStream_t s);
+
+// The signature side of a whole verification as one multi-scalar multiplication (msm.hip):
+// S = sum over the items i of READY groups of [a_i] sig_i + [b_i] (-psi^2 sig_i), bucket method
+// with MSM_WINDOWS windows of MSM_C bits.
+constexpr uint32_t MSM_C = 16, MSM_WINDOWS = 2, MSM_MASK = (1u << MSM_C) - 1;
+constexpr uint32_t MSM_KEYS = MSM_WINDOWS << MSM_C;  // buckets (window, digit); digit 0 unused
+constexpr uint32_t MSM_CHUNK = 16;                   // buckets per lane of the weighing pass
+constexpr uint32_t MSM_PARTS = MSM_KEYS / MSM_CHUNK;
+struct G2MsmArgs {
+  const HmEntry* sig;      // items [0, n)
+  const HmEntry* agg_sig;  // items [n, n + n_agg): the folded aggregates (group i - n)
+  const uint2* coef;       // [n + n_agg]; (0, 0) = the item is not in the combination
+  const uint32_t* igrp;    // [n] item -> group
+  const uint8_t* gst;      // [groups] group state (G_READY ones enter)
+  uint32_t n, n_agg;
+  uint32_t* cnt;           // [MSM_KEYS] zeroed
+  uint32_t* off;           // [MSM_KEYS + 1]
+  uint32_t* cur;           // [MSM_KEYS] zeroed
+  uint32_t* ent;           // [2 MSM_WINDOWS (n + n_agg)]
+  G2JEntry* bucket;        // [MSM_KEYS]
+  G2JEntry* part;          // [MSM_PARTS]
+  G2JEntry* part2;         // [MSM_PARTS / 128]
+  G2JEntry* total;         // [1]
+};
+void launch_msm_count(const G2MsmArgs& a, hipStream_t s);
+void launch_msm_fill(const G2MsmArgs& a, hipStream_t s);
+void launch_msm_bucket(const G2MsmArgs& a, hipStream_t s);
+void launch_msm_reduce(const G2MsmArgs& a, hipStream_t s);
+void launch_msm_sum(const G2MsmArgs& a, hipStream_t s);
 struct ScatterArgs {
   uint32_t n;
   const uint32_t* item_grp;

@@ -23,13 +23,16 @@ __global__ KB_OCC(HB_OCC_LINES) void k_lines_msg(MsgEntry* __restrict__ hm, uint
 // described at Pair3Args (layout.h).  MODE: P3_FULL as just said; P3_ML the (P, H(m)) loop only,
 // stored unexponentiated; P3_FIN the (-g1, S) loop times stored values, exponentiated (the batched
 // final exponentiation of vgroup.hip).
-enum { P3_FULL = 0, P3_ML = 1, P3_FIN = 2 };
+// P3_PROD: no lines, no exponentiation -- the product of a range of stored values (the
+// slot-wide check's product tree).
+enum { P3_FULL = 0, P3_ML = 1, P3_FIN = 2, P3_PROD = 3 };
 
 __device__ __forceinline__ Fp4 f4_load(const Fp4Entry& e) { return {e.x, e.y}; }
 
 template <int MODE>
 __global__ KB_OCC(HB_OCC_PAIR3) void k_pair3(Pair3Args a) {
 #if defined(__HIP_DEVICE_COMPILE__)
+  if (a.guard && *a.guard == 0) return;
   Grp g = grp_make();
   const int grp = (int)(threadIdx.x & 63u) / 3;
   const uint32_t unit = blockIdx.x * GROUPS_PER_WAVE + (uint32_t)grp;
@@ -47,6 +50,19 @@ __global__ KB_OCC(HB_OCC_PAIR3) void k_pair3(Pair3Args a) {
   G1AEntry P{};
   uint32_t m = 0;
   const LineEntry* ml = nullptr;
+  if (MODE == P3_PROD) {  // wave-uniform trip count; idle lanes multiply by one
+    const uint32_t first = e * a.f_range;
+    const uint32_t cnt = first < a.f_n ? min(a.f_range, a.f_n - first) : 0u;
+    Fp4 f = g_one(g);
+    HB_NOUNROLL for (uint32_t j = 0; j < a.f_range; j++) {
+      const uint32_t idx = j < cnt ? first + j : 0u;
+      Fp4 t;
+      f4_select(t, j >= cnt, f4_load(a.f_in[3ull * idx + g.k]), g_one(g));
+      f = g_mul(g, f, t);
+    }
+    if (valid) a.f_out[3ull * e + g.k] = Fp4Entry{f.x, f.y};
+    return;
+  }
   if (MODE != P3_FIN) {
     P = agg ? a.agg_pk[e - a.n_items] : a.pk[e];
     m = agg ? a.agg_msg[e - a.n_items] : a.msg_idx[e];
@@ -121,5 +137,6 @@ static void pair3_launch(const Pair3Args& a, hipStream_t s) {
 void launch_pair3(const Pair3Args& a, hipStream_t s) { pair3_launch<P3_FULL>(a, s); }
 void launch_pair3_ml(const Pair3Args& a, hipStream_t s) { pair3_launch<P3_ML>(a, s); }
 void launch_pair3_fin(const Pair3Args& a, hipStream_t s) { pair3_launch<P3_FIN>(a, s); }
+void launch_pair3_prod(const Pair3Args& a, hipStream_t s) { pair3_launch<P3_PROD>(a, s); }
 
 }  // namespace hb

@@ -127,13 +127,16 @@ __device__ __forceinline__ bool item_usable(const G1AEntry& p, uint8_t pst, cons
 // One lane per item (key_base + i is the item's index in the coefficient stream):
 // P' = r pk, S' = r sig, written for every item so that the group sums need no branches: unusable
 // items (undecodable, infinity) contribute the point at infinity, items of singleton groups keep
-// r = 1 unless `always` (the folded aggregates).
+// r = 1 unless `always` (the folded aggregates).  coef (nullable): the item's (a, b), (0, 0) when
+// unusable; sides 1 computes P' only and writes coef, sides 2 computes S' only from coef.
 __global__ KB_OCC(HB_OCC_RLC) void k_rlc(const G1AEntry* __restrict__ pk, const uint8_t* __restrict__ pk_st,
                          const HmEntry* __restrict__ sig, const uint8_t* __restrict__ sig_st,
                          const uint32_t* __restrict__ item_grp, const uint32_t* __restrict__ grp_off, int always,
                          uint32_t n, uint32_t key_base, RlcKey key, G1JEntry* __restrict__ pout,
-                         G2JEntry* __restrict__ sout) {
+                         G2JEntry* __restrict__ sout, uint2* __restrict__ coef, int sides,
+                         const uint8_t* __restrict__ guard) {
 #if defined(__HIP_DEVICE_COMPILE__)
+  if (guard && *guard == 0) return;
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const G1AEntry pe = pk[i];
@@ -142,20 +145,28 @@ __global__ KB_OCC(HB_OCC_RLC) void k_rlc(const G1AEntry* __restrict__ pk, const 
   const G2A S = {se.x, se.y, false};
   G1J rp;
   G2J rs;
+  uint32_t a = 0, b = 0;
   if (!item_usable(pe, pk_st[i], se, sig_st[i])) {
     rp = jac_infinity<Fp>();
     rs = jac_infinity<Fp2>();
   } else if (!always && (!grp_off || grp_off[item_grp[i] + 1] - grp_off[item_grp[i]] <= 1)) {
+    a = 1;
     rp = jac_from_aff(P);
     rs = jac_from_aff(S);
   } else {
-    uint32_t a, b;
-    rlc_coeffs(key, key_base + i, a, b);
-    rp = rlc_g1(P, a, b);
-    rs = rlc_g2(S, a, b);
+    if (sides == 2) {
+      const uint2 ab = coef[i];
+      a = ab.x;
+      b = ab.y;
+    } else {
+      rlc_coeffs(key, key_base + i, a, b);
+    }
+    if (sides & 1) rp = rlc_g1(P, a, b);
+    if (sides & 2) rs = rlc_g2(S, a, b);
   }
-  pout[i] = {rp.X, rp.Y, rp.Z};
-  sout[i] = {rs.X, rs.Y, rs.Z};
+  if (sides & 1) pout[i] = {rp.X, rp.Y, rp.Z};
+  if (sides & 2) sout[i] = {rs.X, rs.Y, rs.Z};
+  if (coef && sides != 2) coef[i] = make_uint2(a, b);
 #endif
 }
 
@@ -238,6 +249,7 @@ __device__ __forceinline__ Jac<F> msm_ladder(const Jac<F>* __restrict__ tab, con
 
 __global__ KB_OCC(HB_OCC_RLC) void k_rlc_msm(RlcMsmArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
+  if (a.guard && *a.guard == 0) return;
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= *a.total) return;
   const uint32_t first = a.cfirst[c], cc = a.ccount[c], cnt = cc & 0x7fffffffu;
@@ -246,31 +258,41 @@ __global__ KB_OCC(HB_OCC_RLC) void k_rlc_msm(RlcMsmArgs a) {
     const uint32_t i = first;
     const bool usable = !a.pk_st[i] && !a.sig_st[i] && !a.pk[i].inf && !a.sig[i].inf;
     const G1AEntry pe = a.pk[i];
-    const G1J rp = usable ? jac_from_aff(G1A{pe.x, pe.y, false}) : jac_infinity<Fp>();
-    a.pout[i] = {rp.X, rp.Y, rp.Z};
-    const HmEntry se = a.sig[i];
-    const G2J rs = usable ? jac_from_aff(G2A{se.x, se.y, false}) : jac_infinity<Fp2>();
-    a.sout[i] = {rs.X, rs.Y, rs.Z};
+    if (a.sides & 1) {
+      const G1J rp = usable ? jac_from_aff(G1A{pe.x, pe.y, false}) : jac_infinity<Fp>();
+      a.pout[i] = {rp.X, rp.Y, rp.Z};
+      a.coef[i] = make_uint2(usable ? 1u : 0u, 0u);
+    }
+    if (a.sides & 2) {
+      const HmEntry se = a.sig[i];
+      const G2J rs = usable ? jac_from_aff(G2A{se.x, se.y, false}) : jac_infinity<Fp2>();
+      a.sout[i] = {rs.X, rs.Y, rs.Z};
+    }
     return;
   }
-  // coefficients and the G1 ladder points of the chunk's items
-  HB_NOUNROLL for (uint32_t k = 0; k < cnt; k++) {
-    const uint32_t i = first + k;
-    const bool usable = !a.pk_st[i] && !a.sig_st[i] && !a.pk[i].inf && !a.sig[i].inf;
-    uint32_t ca = 0, cb = 0;
-    if (usable) rlc_coeffs(a.key, a.key_base + i, ca, cb);
-    a.coef[i] = make_uint2(ca, cb);
-    const G1AEntry pe = a.pk[i];
-    const G1A P = {pe.x, pe.y, false};
-    const G1A P2 = {fp_mul(P.x, fp_from_const(G1_BETA)), P.y, false};
-    const G1J J1 = jac_from_aff(P), J2 = jac_from_aff(P2), J3 = jac_add_aff(J1, P2);
-    a.t1[3ull * i] = J1;
-    a.t1[3ull * i + 1] = J2;
-    a.t1[3ull * i + 2] = J3;
+  if (a.sides & 1) {
+    // coefficients and the G1 ladder points of the chunk's items
+    HB_NOUNROLL for (uint32_t k = 0; k < cnt; k++) {
+      const uint32_t i = first + k;
+      const bool usable = !a.pk_st[i] && !a.sig_st[i] && !a.pk[i].inf && !a.sig[i].inf;
+      uint32_t ca = 0, cb = 0;
+      if (usable) rlc_coeffs(a.key, a.key_base + i, ca, cb);
+      a.coef[i] = make_uint2(ca, cb);
+      const G1AEntry pe = a.pk[i];
+      const G1A P = {pe.x, pe.y, false};
+      const G1A P2 = {fp_mul(P.x, fp_from_const(G1_BETA)), P.y, false};
+      const G1J J1 = jac_from_aff(P), J2 = jac_from_aff(P2), J3 = jac_add_aff(J1, P2);
+      a.t1[3ull * i] = J1;
+      a.t1[3ull * i + 1] = J2;
+      a.t1[3ull * i + 2] = J3;
+    }
+    const G1J rp = msm_ladder<Fp>(a.t1, a.coef, first, cnt);
+    a.pout[first] = {rp.X, rp.Y, rp.Z};
+    const G1J zi = jac_infinity<Fp>();
+    for (uint32_t k = 1; k < cnt; k++) a.pout[first + k] = {zi.X, zi.Y, zi.Z};
   }
-  const G1J rp = msm_ladder<Fp>(a.t1, a.coef, first, cnt);
-  a.pout[first] = {rp.X, rp.Y, rp.Z};
-  // the G2 ladder points, then the G2 ladder
+  if (!(a.sides & 2)) return;
+  // the G2 ladder points, then the G2 ladder (coefficients from the workspace)
   HB_NOUNROLL for (uint32_t k = 0; k < cnt; k++) {
     const uint32_t i = first + k;
     const HmEntry se = a.sig[i];
@@ -283,12 +305,8 @@ __global__ KB_OCC(HB_OCC_RLC) void k_rlc_msm(RlcMsmArgs a) {
   }
   const G2J rs = msm_ladder<Fp2>(a.t2, a.coef, first, cnt);
   a.sout[first] = {rs.X, rs.Y, rs.Z};
-  const G1J zi = jac_infinity<Fp>();
   const G2J zs = jac_infinity<Fp2>();
-  for (uint32_t k = 1; k < cnt; k++) {
-    a.pout[first + k] = {zi.X, zi.Y, zi.Z};
-    a.sout[first + k] = {zs.X, zs.Y, zs.Z};
-  }
+  for (uint32_t k = 1; k < cnt; k++) a.sout[first + k] = {zs.X, zs.Y, zs.Z};
 #endif
 }
 
@@ -299,6 +317,9 @@ void launch_plan(const uint32_t* grp_off, uint32_t ng, uint32_t cmax, uint32_t* 
   hipLaunchKernelGGL(k_plan_count, dim3(nb), dim3(BLOCK), 0, s, grp_off, ng, cmax, cnt);
   hipLaunchKernelGGL(k_plan_scan, dim3(1), dim3(1024), 0, s, cnt, ng, coff);
   hipLaunchKernelGGL(k_plan_fill, dim3(nb), dim3(BLOCK), 0, s, grp_off, ng, cmax, coff, cfirst, ccount);
+}
+void launch_scan(const uint32_t* cnt, uint32_t n, uint32_t* off, hipStream_t s) {
+  hipLaunchKernelGGL(k_plan_scan, dim3(1), dim3(1024), 0, s, cnt, n, off);
 }
 void launch_rlc_msm(const RlcMsmArgs& a, uint32_t max_chunks, hipStream_t s) {
   if (max_chunks) hipLaunchKernelGGL(k_rlc_msm, dim3((max_chunks + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, a);
@@ -362,10 +383,11 @@ void launch_dec_sig_pt(const uint8_t* sigs, uint32_t n, HmEntry* out, uint8_t* s
 }
 void launch_rlc(const G1AEntry* pk, const uint8_t* pk_st, const HmEntry* sig, const uint8_t* sig_st,
                 const uint32_t* item_grp, const uint32_t* grp_off, int always, uint32_t n, uint32_t key_base,
-                const RlcKey& key, G1JEntry* pout, G2JEntry* sout, hipStream_t s) {
+                const RlcKey& key, G1JEntry* pout, G2JEntry* sout, hipStream_t s, uint2* coef, int sides,
+                const uint8_t* guard) {
   if (n)
     hipLaunchKernelGGL(k_rlc, dim3(blocks_for(n)), dim3(BLOCK), 0, s, pk, pk_st, sig, sig_st, item_grp, grp_off,
-                       always, n, key_base, key, pout, sout);
+                       always, n, key_base, key, pout, sout, coef, sides, guard);
 }
 void launch_scatter(const ScatterArgs& a, hipStream_t s) {
   const size_t tot = (size_t)a.n + a.n_agg;

@@ -18,7 +18,9 @@ __device__ __forceinline__ bool item_usable_g(const G1AEntry& p, uint8_t pst, co
 // The group's state; when READY, P = its combined public key (affine, finite) and its combined
 // signature as S (Jacobian; BATCH) or Sa (affine).  Group sizes of one without an aggregate keep
 // r = 1 (k_rlc) and take the decoded points directly unless BATCH (random r for every item).
-template <bool BATCH>
+// P_ONLY (the slot-wide check, msm.hip): no signature side at all; a degenerate S is caught by
+// the slot-wide check failing.
+template <bool BATCH, bool P_ONLY = false>
 __device__ __forceinline__ uint8_t group_scan(const GroupPrepArgs& a, uint32_t lg, G1A& P, G2J& S, G2A& Sa) {
   const uint32_t g = a.g0 + lg;
   const uint32_t b = a.grp_off ? a.grp_off[g] : g, e = a.grp_off ? a.grp_off[g + 1] : g + 1;
@@ -51,19 +53,25 @@ __device__ __forceinline__ uint8_t group_scan(const GroupPrepArgs& a, uint32_t l
   G2J sacc = jac_infinity<Fp2>();
   for (uint32_t i = b; i < e; i++) {
     const G1JEntry pj = a.pr[i];
-    const G2JEntry sj = a.sr[i];
     pacc = jac_add(pacc, G1J{pj.X, pj.Y, pj.Z});
-    sacc = jac_add(sacc, G2J{sj.X, sj.Y, sj.Z});
+    if (!P_ONLY) {
+      const G2JEntry sj = a.sr[i];
+      sacc = jac_add(sacc, G2J{sj.X, sj.Y, sj.Z});
+    }
   }
   if (with_agg) {
     const G1JEntry pj = a.agg_pr[g];
-    const G2JEntry sj = a.agg_sr[g];
     pacc = jac_add(pacc, G1J{pj.X, pj.Y, pj.Z});
-    sacc = jac_add(sacc, G2J{sj.X, sj.Y, sj.Z});
+    if (!P_ONLY) {
+      const G2JEntry sj = a.agg_sr[g];
+      sacc = jac_add(sacc, G2J{sj.X, sj.Y, sj.Z});
+    }
   }
   P = jac_to_aff(pacc);
   bool s_inf;
-  if (BATCH) {
+  if (P_ONLY) {
+    s_inf = false;
+  } else if (BATCH) {
     S = sacc;
     s_inf = jac_is_inf(sacc);
   } else {
@@ -104,6 +112,7 @@ __global__ KB_OCC(HB_OCC_PREP) void k_group_prep(GroupPrepArgs a) {
 // (gS) and the 64 groups of the wave -- one batch -- sum their S into bS (butterfly over the wave).
 __global__ KB_OCC(HB_OCC_PREP) void k_group_prep_b(GroupPrepArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
+  if (a.guard && *a.guard == 0) return;
   const uint32_t lg = blockIdx.x * blockDim.x + threadIdx.x;
   G2J S = jac_infinity<Fp2>();
   if (lg < a.ng) {
@@ -128,10 +137,27 @@ __global__ KB_OCC(HB_OCC_PREP) void k_group_prep_b(GroupPrepArgs a) {
 #endif
 }
 
+// Slot-wide check (msm.hip): one lane per verification group, its combined public key and state
+// only (the signature side is one multi-scalar multiplication over the whole call).
+__global__ KB_OCC(HB_OCC_PREP) void k_group_prep_p(GroupPrepArgs a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t lg = blockIdx.x * blockDim.x + threadIdx.x;
+  if (lg >= a.ng) return;
+  G1A P;
+  G2J Sg;
+  G2A Sa;
+  const uint8_t st = group_scan<true, true>(a, lg, P, Sg, Sa);
+  a.gst[lg] = st;
+  if (st == G_READY) store_gp(a.gP + lg, P);
+#endif
+}
+
 __global__ KB_OCC(HB_OCC_LINES) void k_slines(const G2JEntry* __restrict__ pts, const uint32_t* __restrict__ list,
                                              const uint32_t* __restrict__ count, uint32_t n,
-                                             LineEntry* __restrict__ lines, uint32_t stride, uint8_t* __restrict__ bad) {
+                                             LineEntry* __restrict__ lines, uint32_t stride, uint8_t* __restrict__ bad,
+                                             const uint8_t* __restrict__ guard) {
 #if defined(__HIP_DEVICE_COMPILE__)
+  if (guard && *guard == 0) return;
   const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t avail = list ? min(*count, n) : n;
   if (u >= avail) return;
@@ -146,7 +172,8 @@ __global__ KB_OCC(HB_OCC_LINES) void k_slines(const G2JEntry* __restrict__ pts, 
 
 __global__ __launch_bounds__(64) void k_batch_verdict(const uint8_t* __restrict__ gst, const uint8_t* __restrict__ bver, uint32_t ng,
                                    uint8_t* __restrict__ gver, uint32_t* __restrict__ list,
-                                   uint32_t* __restrict__ count) {
+                                   uint32_t* __restrict__ count, const uint8_t* __restrict__ guard) {
+  if (guard && *guard == 0) return;
   const uint32_t lg = blockIdx.x * blockDim.x + threadIdx.x;
   if (lg >= ng) return;
   if (gst[lg] != G_READY) gver[lg] = 1;
@@ -154,18 +181,31 @@ __global__ __launch_bounds__(64) void k_batch_verdict(const uint8_t* __restrict_
   else list[atomicAdd(count, 1u)] = lg;
 }
 
+__global__ __launch_bounds__(64) void k_slot_verdict(const uint8_t* __restrict__ gst, const uint8_t* __restrict__ sfail,
+                                                      uint32_t ng, uint8_t* __restrict__ gver) {
+  if (*sfail != 0) return;
+  const uint32_t lg = blockIdx.x * blockDim.x + threadIdx.x;
+  if (lg < ng) gver[lg] = gst[lg] != G_READY ? 1 : 0;
+}
+
 void launch_group_prep(const GroupPrepArgs& a, hipStream_t s) {
   if (!a.ng) return;
-  if (a.gS) hipLaunchKernelGGL(k_group_prep_b, dim3((a.ng + FE_BATCH - 1) / FE_BATCH), dim3(FE_BATCH), 0, s, a);
+  if (a.p_only) hipLaunchKernelGGL(k_group_prep_p, dim3((a.ng + 63) / 64), dim3(64), 0, s, a);
+  else if (a.gS) hipLaunchKernelGGL(k_group_prep_b, dim3((a.ng + FE_BATCH - 1) / FE_BATCH), dim3(FE_BATCH), 0, s, a);
   else hipLaunchKernelGGL(k_group_prep, dim3((a.ng + 63) / 64), dim3(64), 0, s, a);
 }
 void launch_slines(const G2JEntry* pts, const uint32_t* list, const uint32_t* count, uint32_t n, LineEntry* lines,
-                   uint32_t stride, uint8_t* bad, hipStream_t s) {
-  if (n) hipLaunchKernelGGL(k_slines, dim3((n + 63) / 64), dim3(64), 0, s, pts, list, count, n, lines, stride, bad);
+                   uint32_t stride, uint8_t* bad, hipStream_t s, const uint8_t* guard) {
+  if (n)
+    hipLaunchKernelGGL(k_slines, dim3((n + 63) / 64), dim3(64), 0, s, pts, list, count, n, lines, stride, bad, guard);
 }
 void launch_batch_verdict(const uint8_t* gst, const uint8_t* bver, uint32_t ng, uint8_t* gver, uint32_t* list,
-                          uint32_t* count, hipStream_t s) {
-  if (ng) hipLaunchKernelGGL(k_batch_verdict, dim3((ng + 63) / 64), dim3(64), 0, s, gst, bver, ng, gver, list, count);
+                          uint32_t* count, hipStream_t s, const uint8_t* guard) {
+  if (ng)
+    hipLaunchKernelGGL(k_batch_verdict, dim3((ng + 63) / 64), dim3(64), 0, s, gst, bver, ng, gver, list, count, guard);
+}
+void launch_slot_verdict(const uint8_t* gst, const uint8_t* sfail, uint32_t ng, uint8_t* gver, hipStream_t s) {
+  if (ng) hipLaunchKernelGGL(k_slot_verdict, dim3((ng + 63) / 64), dim3(64), 0, s, gst, sfail, ng, gver);
 }
 
 }  // namespace hb

@@ -72,12 +72,34 @@ RLC_CHUNK = 16   # items per lane of k_rlc_msm (layout.h)
 TA_CHUNK = 8     # members per lane of k_ta_msm (layout.h)
 
 
-def rlc_msm(b=BLOCKS, chunk=1):
+def rlc_msm(b=BLOCKS, chunk=1, sides=3):
     """k_rlc_msm per item of a chunk of `chunk` items: the ladder points (phi + one mixed addition
-    per side), 32 shared doublings per chunk, 32 additions per item."""
+    per side), 32 shared doublings per chunk, 32 additions per item.  sides: 1 the public-key side
+    only (the slot-wide check takes the signature side as one MSM), 3 both."""
     g1 = 1 + b["jac_add_aff_g1"] + 32 * b["jac_add_g1"] + 32 * b["jac_dbl_g1"] / chunk
     g2 = 6 + b["jac_add_aff_g2"] + 32 * b["jac_add_g2"] + 32 * b["jac_dbl_g2"] / chunk
-    return g1 + g2
+    return g1 + (g2 if sides & 2 else 0)
+
+
+# The slot-wide check's multi-scalar multiplication of the signature side (msm.hip): two windows of
+# 16 bits over the two 32-bit halves of every coefficient, i.e. 4 bucket entries per item.
+MSM_C, MSM_WINDOWS, MSM_CHUNK = 16, 2, 16
+MSM_KEYS = MSM_WINDOWS << MSM_C
+MSM_PARTS = MSM_KEYS // MSM_CHUNK
+MSM_ENTRIES_PER_ITEM = 2 * MSM_WINDOWS
+
+
+def msm_bucket(b=BLOCKS):
+    """k_msm_bucket per entry: one mixed G2 addition; half the entries first map the point through
+    -psi^2 (two Fp2-by-Fp products)."""
+    return b["jac_add_aff_g2"] + 2
+
+
+def msm_reduce(b=BLOCKS):
+    """k_msm_reduce per chunk of MSM_CHUNK buckets: running sums (2 additions per bucket), one
+    16-bit multiple (16 doublings, 16 additions), the window shift (16 doublings for window 1)."""
+    return 2 * MSM_CHUNK * b["jac_add_g2"] + 16 * (b["jac_dbl_g2"] + b["jac_add_g2"]) + \
+        16 * b["jac_dbl_g2"] * (MSM_WINDOWS - 1) / MSM_WINDOWS
 
 
 def ta_msm(b=BLOCKS, chunk=1):
@@ -160,6 +182,13 @@ def per_unit(b=BLOCKS, group_size=1, t=1):
         "k_pair3_ml": pair3_ml(b),
         "k_pair3_fin": pair3_fin(b),
         "k_slines": (b["to_aff_g2"] + b["lines_eval"],) * 2,
+        # slot-wide check (msm.hip): per group the key sum alone; the product tree of the stored
+        # loops (one Fp12 product per stored value); the MSM kernels per entry / chunk / point
+        "k_group_prep_p": ((k - 1) * b["jac_add_g1"] + b["to_aff_g1"],) * 2,
+        "k_pair3_prod": (b["f12_mul"], 3 * 18),
+        "k_msm_bucket": (msm_bucket(b),) * 2,
+        "k_msm_reduce": (msm_reduce(b),) * 2,
+        "k_msm_sum": (b["jac_add_g2"],) * 2,
     }
     return out
 
@@ -170,7 +199,9 @@ UNITS = {"k_pair3": "pairing check", "k_pair3_fallback": "pairing check", "k_dec
          "k_hash_to_g2": "message", "k_lines_msg": "message", "k_seg_sum": "public key (pass 1)",
          "k_va_point": "aggregation group", "k_sig_lines": "signature", "k_group_prep_b": "verification group",
          "k_pair3_ml": "verification group", "k_pair3_fin": "batch of 64 groups",
-         "k_slines": "batch of 64 groups"}
+         "k_slines": "batch of 64 groups", "k_group_prep_p": "verification group",
+         "k_pair3_prod": "stored Miller loop", "k_msm_bucket": "bucket entry", "k_msm_reduce": "chunk of 16 buckets",
+         "k_msm_sum": "point"}
 
 # SHA-256 compressions per attestation signing root (roots.hip: 8 two-block hashes)
 SHA256_PER_ATTESTATION_ROOT = 16

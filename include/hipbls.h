@@ -220,12 +220,23 @@ int hbls_timing_read(const char** names, float* ms, size_t max_n, size_t* n_out)
 /* Verification statistics, collected only with HBLS_STATS=1 in the environment (each call then
  * synchronises): out[0] items verified, out[1] verification groups, out[2] items re-checked
  * alone because their group's combined check failed, out[3] groups checked alone because their
- * batch's shared final exponentiation failed. */
+ * batch's shared final exponentiation failed, out[4] slot-wide checks run, out[5] slot-wide
+ * checks that failed (the call then took the per-batch check).  n <= 6. */
 int hbls_stats(uint64_t* out, size_t n);
 /* Tuning: verifications of at least min_groups groups share one final exponentiation among 64
  * groups (0 = one per group; default 128, HBLS_FE_BATCH).  Returns the previous value.  Verdicts
  * do not depend on it. */
 size_t hbls_fe_batch(size_t min_groups);
+/* Tuning: batched verifications of at least min_items items (partials + folded aggregates) first
+ * check every group at once -- the signature side as one multi-scalar multiplication, one final
+ * exponentiation for the call -- and take the per-batch check only if that fails (0 = never;
+ * default 65536, HBLS_SLOT_MSM).  Returns the previous value.  Verdicts do not depend on it. */
+size_t hbls_slot_msm(size_t min_items);
+/* Tuning: the random linear combination's public-key side groups a verification group's items
+ * into shared-doubling chunks sized to keep about `lanes` lanes busy (at most 16 items per chunk;
+ * calls of fewer than 2 lanes' worth keep one ladder per item).  0 restores the default 65536
+ * (HBLS_RLC_LANES).  Returns the previous value.  Verdicts do not depend on it. */
+size_t hbls_rlc_lanes(size_t lanes);
 /* Wait for all work the library queued on `stream`. */
 int hbls_sync(void* stream);
 

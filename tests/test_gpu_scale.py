@@ -84,13 +84,21 @@ def _pks(L, sks):
 
 @pytest.fixture
 def fe_mode(L, request):
-    """Batched final exponentiation on (the default at these sizes) or off for the test."""
-    prev = L.hbls_fe_batch(128 if request.param == "fe_batch" else 0)
+    """Batched final exponentiation on (the default at these sizes) or off for the test; slot_msm:
+    first the slot-wide check (one multi-scalar multiplication for the signature side, one final
+    exponentiation for the call), the per-batch check only when it fails."""
+    prev = L.hbls_fe_batch(0 if request.param == "fe_per_group" else 128)
+    prev_s = L.hbls_slot_msm(1 if request.param.startswith("slot_msm") else 0)
+    # slot_msm_chunks: the combination's public-key side as shared-doubling chunks (k_rlc_msm, a
+    # validator's partials per lane) as at C3, instead of one ladder per item
+    prev_l = L.hbls_rlc_lanes(4096 if request.param == "slot_msm_chunks" else 0)
     yield request.param
     L.hbls_fe_batch(prev)
+    L.hbls_slot_msm(prev_s)
+    L.hbls_rlc_lanes(prev_l)
 
 
-@pytest.mark.parametrize("fe_mode", ["fe_batch", "fe_per_group"], indirect=True)
+@pytest.mark.parametrize("fe_mode", ["fe_batch", "fe_per_group", "slot_msm", "slot_msm_chunks"], indirect=True)
 @pytest.mark.parametrize("key_tables", [False, True], ids=["decompress", "key_tables"])
 def test_slot_adversarial_c2(L, key_tables, fe_mode):
     """key_tables: the public keys come from tables made once by hbls_decompress_pubkeys_device
@@ -325,8 +333,8 @@ def test_device_call_and_host_call_do_not_race(L, hipbls):
 
 
 def _stats(L):
-    out = (ctypes.c_uint64 * 4)()
-    assert L.hbls_stats(out, 4) == 0
+    out = (ctypes.c_uint64 * 6)()
+    assert L.hbls_stats(out, 6) == 0
     return list(out)
 
 
@@ -356,6 +364,37 @@ def test_batched_fe_rejects_cancelling_errors(L, hipbls, monkeypatch):
     assert st == [NOT_VERIFIED if i < 2 else OK for i in range(n)]
     d = [b - a for a, b in zip(s0, _stats(L))]
     assert d[3] >= 1 and d[2] == 2, d  # the failing batch's groups checked alone, then the two items
+
+
+def test_slot_msm_clean_and_cancelling_errors(L, hipbls, monkeypatch):
+    """The slot-wide check (HBLS_SLOT_MSM) on 300 groups of one: a clean call passes it with no
+    per-batch or per-item check; two signatures with opposite errors (sig0 + D, sig1 - D) make it
+    fail, and the per-batch check then rejects exactly those two."""
+    from oracle import bls12381 as B
+    monkeypatch.setenv("HBLS_STATS", "1")
+    prev_f, prev_s = L.hbls_fe_batch(128), L.hbls_slot_msm(1)
+    try:
+        n = 300
+        keys = [hipbls.generate_secret_key() for _ in range(n)]
+        msgs = [hashlib.sha256(b"slot duty %d" % k).digest() for k in range(n)]
+        sigs = hipbls.sign_batch(keys, msgs)
+        pks = [hipbls.secret_to_public_key(k) for k in keys]
+        s0 = _stats(L)
+        assert hipbls.verify_batch(pks, msgs, sigs) == [OK] * n
+        d = [b - a for a, b in zip(s0, _stats(L))]
+        assert d[1] == n and d[2] == 0 and d[3] == 0 and d[4] == 1 and d[5] == 0, d
+        D = B.g2_decompress(sigs[11])
+        bad = list(sigs)
+        bad[0] = B.g2_compress(B.g2_add(B.g2_decompress(sigs[0]), D))
+        bad[1] = B.g2_compress(B.g2_add(B.g2_decompress(sigs[1]), B.g2_neg(D)))
+        s0 = _stats(L)
+        st = hipbls.verify_batch(pks, msgs, bad)
+        assert st == [NOT_VERIFIED if i < 2 else OK for i in range(n)]
+        d = [b - a for a, b in zip(s0, _stats(L))]
+        assert d[4] == 1 and d[5] == 1 and d[3] >= 1 and d[2] == 2, d
+    finally:
+        L.hbls_fe_batch(prev_f)
+        L.hbls_slot_msm(prev_s)
 
 
 def test_batched_groups_pass_without_fallback(L, hipbls, monkeypatch):
