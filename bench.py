@@ -608,6 +608,8 @@ def main(argv=None):
         _chk(L, L.hbls_timing(0))
         per_unit = opcounts.per_unit(group_size=n, t=t)
         ta_units = V * t
+        jc_knob = L.hbls_ta_joint(0)
+        L.hbls_ta_joint(jc_knob)
         # k_rlc: the partials as multi-scalar chunks (one per validator), then the folded
         # aggregates (slot mode)
         # batched final exponentiation (the library's setting; verifications of >= fe_min groups):
@@ -630,7 +632,9 @@ def main(argv=None):
         else:
             rlc_partial = rlc_item
         rlc_avg = (NP * rlc_partial + (0 if staged or not bfe else V * rlc_item)) / n_rlc
-        ta_w = opcounts.ta_uniform([x + 1 for x in ta_share_positions(n, t)])
+        ta_ids = [x + 1 for x in ta_share_positions(n, t)]
+        jc = opcounts.ta_joint_chunk(t, ta_units, jc_knob)
+        ta_w = opcounts.ta_joint(ta_ids, jc) if jc else opcounts.ta_uniform(ta_ids)
         prep_units = opcounts.per_unit(group_size=n + (0 if staged else 1), t=t)
         units = {"k_rlc": (n_rlc, (rlc_avg, rlc_avg)),
                  "k_dec_pk": (NP + (0 if staged else V), per_unit["k_dec_pk"]),

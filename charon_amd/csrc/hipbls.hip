@@ -234,6 +234,11 @@ size_t g_kc_n = 0;
 // chunks of 2, 4 or 8 members.
 bool g_ta_msm = false;
 size_t g_ta_chunk = 4;   // HBLS_TA_CHUNK: members per lane of k_ta_msm (<= TA_CHUNK)
+// HBLS_TA_JOINT: members per lane of the joint aggregation ladders (k_ta_joint) when every group has
+// the same size t; 0 = auto (about TA_JOINT_LANES lanes, at most t and 8), 1 = one ladder per member
+// (k_ta_straus)
+std::atomic<size_t> g_ta_joint{0};
+constexpr size_t TA_JOINT_LANES = 98304;
 // HBLS_FE_BATCH: verifications of at least this many groups check FE_BATCH groups per final
 // exponentiation (vgroup.hip; 0 = one final exponentiation per group)
 std::atomic<size_t> g_fe_batch_min{2 * FE_BATCH};
@@ -440,6 +445,7 @@ int init_mask(uint32_t mask) {
   g_rlc_lanes = std::max<size_t>(1, env_size("HBLS_RLC_LANES", g_rlc_lanes.load()));
   g_ta_msm = env_size("HBLS_TA_MSM", 0) != 0;
   g_ta_chunk = std::min<size_t>(TA_CHUNK, std::max<size_t>(1, env_size("HBLS_TA_CHUNK", g_ta_chunk)));
+  g_ta_joint = std::min<size_t>(8, env_size("HBLS_TA_JOINT", g_ta_joint.load()));
   g_fe_batch_min = env_size("HBLS_FE_BATCH", g_fe_batch_min.load());
   g_slot_msm_min = env_size("HBLS_SLOT_MSM", g_slot_msm_min.load());
   std::vector<Dev*> devs;
@@ -541,7 +547,18 @@ int ta_tail(Dev& d, Ws& w, const HmEntry* pts, const uint32_t* src, const uint8_
   void* tab;
   G2JEntry* pj;
   if (wsbuf(w, W_TAMST, np, &mst) || wsbuf(w, W_TADIG, np, &dig) || wsbuf(w, W_TAJ, np, &pj)) return -1;
-  if (wsbuf(w, W_TATAB, ta_table_bytes((uint32_t)np), (uint8_t**)&tab)) return -1;
+  // joint ladders over chunks of a validator's members (k_ta_joint) when every group has t members
+  const size_t t_u = (n_groups && np % n_groups == 0) ? np / n_groups : 0;
+  size_t jc = 0;
+  if (mode == 0 && t_u > 1 && !g_ta_msm) {
+    const size_t knob = g_ta_joint.load();
+    jc = knob ? knob : np / TA_JOINT_LANES;
+    jc = std::min<size_t>(std::min<size_t>(jc, t_u), 8);
+    if (jc <= 1) jc = 0;
+  }
+  const size_t tab_bytes = jc ? ta_joint_table_bytes((uint32_t)n_groups, (uint32_t)t_u, (uint32_t)jc)
+                              : ta_table_bytes((uint32_t)np);
+  if (wsbuf(w, W_TATAB, tab_bytes, (uint8_t**)&tab)) return -1;
   if (np) {
     if (src) launch_ta_member_status(mst_in, src, (uint32_t)np, mst, s);
     else HCHK(hipMemcpyAsync(mst, mst_in, np, hipMemcpyDeviceToDevice, s));
@@ -558,6 +575,9 @@ int ta_tail(Dev& d, Ws& w, const HmEntry* pts, const uint32_t* src, const uint8_
       if (mode == 0) TIMED(d, "k_ta_table", s, launch_ta_table(pts, src, (uint32_t)np, tab, s));
       TIMED(d, "k_ta_straus", s,
             launch_ta_msm(pts, src, dig, tab, pcf, pcc, pcoff + n_groups, (uint32_t)max_chunks, mode, pj, s));
+    } else if (jc) {
+      TIMED(d, "k_ta_straus", s,
+            launch_ta_joint(pts, src, dig, (uint32_t)n_groups, (uint32_t)t_u, (uint32_t)jc, tab, pj, s));
     } else {
       TIMED(d, "k_ta_straus", s, launch_ta_straus(pts, src, dig, (uint32_t)np, (uint32_t)n_groups, tab, pj, s));
     }
@@ -1798,6 +1818,7 @@ int hbls_stats(uint64_t* out, size_t n) {
 
 size_t hbls_fe_batch(size_t min_groups) { return g_fe_batch_min.exchange(min_groups); }
 size_t hbls_slot_msm(size_t min_items) { return g_slot_msm_min.exchange(min_items); }
+size_t hbls_ta_joint(size_t members) { return g_ta_joint.exchange(std::min<size_t>(members, 8)); }
 size_t hbls_rlc_lanes(size_t lanes) { return g_rlc_lanes.exchange(lanes ? lanes : 65536); }
 
 int hbls_sync(void* stream) {

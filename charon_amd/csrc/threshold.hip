@@ -250,6 +250,159 @@ __global__ KB_OCC(HB_OCC_STRAUS) void k_ta_straus(const HmEntry* __restrict__ pt
 #endif
 }
 
+#if defined(__HIP_DEVICE_COMPILE__)
+// The odd multiples {1, 3, 5, 7} of the four bases B_k = P0, -psi(P0), psi^2(P0), -psi^3(P0) of
+// one member: table entries e0 + 4 k + (|d| >> 1).
+__device__ __forceinline__ void odd_table(uint4* wt, int e0, const G2A& P0) {
+  const G2J J1 = jac_from_aff(P0);
+  const G2J J2 = jac_dbl(J1);
+  const G2J J3 = jac_add_aff(J2, P0);
+  const G2J J5 = jac_add(J3, J2);
+  const G2J J7 = jac_add(J5, J2);
+  const Fp2 cx = f2_from_const(PSI_CX), cy = f2_from_const(PSI_CY);
+  const Fp2 c2x = f2_from_const(PSI2_CX), c2y = f2_from_const(PSI2_CY);
+  HB_NOUNROLL for (int j = 0; j < 4; j++) {
+    const G2J J = j == 0 ? J1 : j == 1 ? J3 : j == 2 ? J5 : J7;
+    tab_store(wt, e0 + j, J);
+    const G2J N1 = {f2_mul(f2_conj(J.X), cx), f2_neg(f2_mul(f2_conj(J.Y), cy)), f2_conj(J.Z)};
+    const G2J N2 = {f2_mul(J.X, c2x), f2_mul(J.Y, c2y), J.Z};
+    const G2J N3 = {f2_mul(f2_conj(N2.X), cx), f2_neg(f2_mul(f2_conj(N2.Y), cy)), f2_conj(N2.Z)};
+    tab_store(wt, e0 + 4 + j, N1);
+    tab_store(wt, e0 + 8 + j, N2);
+    tab_store(wt, e0 + 12 + j, N3);
+  }
+}
+
+// signed width-4 NAF of a 64-bit digit (< |x| < 2^64 - 7, so v + 7 cannot overflow) into out[66];
+// returns the top nonzero position (0 if none)
+__device__ __forceinline__ int naf4_digits(uint64_t v, int8_t* out) {
+  int top = 0;
+  for (int i = 0; i < 66; i++) {
+    int dg = 0;
+    if (v & 1u) {
+      dg = (int)(v & 15u);
+      if (dg >= 8) dg -= 16;
+      v = dg > 0 ? v - (uint64_t)dg : v + (uint64_t)(-dg);
+    }
+    out[i] = (int8_t)dg;
+    if (dg && i > top) top = i;
+    v >>= 1;
+  }
+  return top;
+}
+
+// lambda sigma for one member with arbitrary digits: the joint 64-step ladder over its 15-entry
+// subset table (entries e0 .. e0 + 14)
+__device__ __forceinline__ G2J member_general(uint4* wt, int e0, const HmEntry& e, const TaDigits& d) {
+  const G2A P0 = {e.x, e.y, e.inf != 0};
+  {
+    G2A P1 = {f2_mul(f2_conj(e.x), f2_from_const(PSI_CX)), f2_neg(f2_mul(f2_conj(e.y), f2_from_const(PSI_CY))),
+              P0.inf};
+    G2A P2 = {f2_mul(e.x, f2_from_const(PSI2_CX)), f2_mul(e.y, f2_from_const(PSI2_CY)), P0.inf};
+    G2A P3 = {f2_mul(f2_conj(P2.x), f2_from_const(PSI_CX)), f2_neg(f2_mul(f2_conj(P2.y), f2_from_const(PSI_CY))),
+              P0.inf};
+    tab_store(wt, e0 + 0, jac_from_aff(P0));
+    tab_store(wt, e0 + 1, jac_from_aff(P1));
+    tab_store(wt, e0 + 3, jac_from_aff(P2));
+    tab_store(wt, e0 + 7, jac_from_aff(P3));
+  }
+  HB_NOUNROLL for (int sidx = 3; sidx < 16; sidx++) {
+    const int hi = sidx >= 8 ? 8 : (sidx >= 4 ? 4 : 2);
+    if (sidx == hi) continue;
+    const G2J h = tab_load(wt, e0 + hi - 1);
+    const G2A ha = {h.X, h.Y, f2_is_zero(h.Z)};
+    tab_store(wt, e0 + sidx - 1, jac_add_aff(tab_load(wt, e0 + sidx - hi - 1), ha));
+  }
+  G2J R = jac_infinity<Fp2>();
+  HB_NOUNROLL for (int b = 63; b >= 0; b--) {
+    R = jac_dbl(R);
+    const uint32_t sel = (uint32_t)((d.a[0] >> b) & 1) | ((uint32_t)((d.a[1] >> b) & 1) << 1) |
+                         ((uint32_t)((d.a[2] >> b) & 1) << 2) | ((uint32_t)((d.a[3] >> b) & 1) << 3);
+    const G2J S = jac_add(R, tab_load(wt, e0 + (sel == 0 ? 0 : (int)sel - 1)));
+    f2_select(R.X, sel != 0, R.X, S.X);
+    f2_select(R.Y, sel != 0, R.Y, S.Y);
+    f2_select(R.Z, sel != 0, R.Z, S.Z);
+  }
+  return R;
+}
+#endif
+
+// Joint aggregation ladders: one lane per CHUNK of c members of one validator (the validator's t
+// members in ceil(t / c) chunks), lane L taking chunk q = L / n_groups of validator v = L % n_groups
+// so that a wave holds the same members of 64 validators.  When their Lagrange digits agree
+// across the wave (every validator aggregates the same share indices -- the common slot), ONE
+// signed width-4 NAF schedule runs over all c members' odd-multiple tables: top + 1 doublings for
+// the chunk instead of per member, one addition per nonzero digit as before.  Otherwise each member
+// takes the general 15-entry ladder.  The chunk's sum goes to its first member's slot of `out`,
+// infinity to the others (k_group_sum adds a group's t slots).
+constexpr int TA_JOINT_MAX = 8;
+__global__ KB_OCC(HB_OCC_STRAUS) void k_ta_joint(const HmEntry* __restrict__ pts, const uint32_t* __restrict__ src,
+                                                    const TaDigits* __restrict__ dig, uint32_t n_groups, uint32_t t,
+                                                    uint32_t c, uint4* __restrict__ tab, G2JEntry* __restrict__ out) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __shared__ int8_t naf[TA_JOINT_MAX][4][66];
+  __shared__ int naf_top;
+  const int lane = (int)(threadIdx.x & 63u);
+  const uint32_t n_chunks = (t + c - 1) / c, n_lanes = n_groups * n_chunks;
+  const uint32_t L = blockIdx.x * 64 + (uint32_t)lane;
+  const bool valid = L < n_lanes;
+  const uint32_t Lc = valid ? L : n_lanes - 1;
+  const uint32_t q = Lc / n_groups, v = Lc % n_groups;
+  const uint32_t j0 = q * c, cnt = min(c, t - j0);
+  const uint32_t m0 = v * t + j0;
+  uint4* wt = tab + (size_t)blockIdx.x * (16 * c) * TA_TAB_QUADS * 64 + lane;
+  bool same = cnt == (uint32_t)__builtin_amdgcn_readfirstlane((int)cnt);
+  HB_NOUNROLL for (uint32_t k = 0; k < c; k++) {
+    const TaDigits d = dig[m0 + (k < cnt ? k : 0)];
+    HB_UNROLL for (int i = 0; i < 4; i++) {
+      const uint32_t lo = (uint32_t)d.a[i], hi = (uint32_t)(d.a[i] >> 32);
+      same = same && lo == (uint32_t)__builtin_amdgcn_readfirstlane((int)lo) &&
+             hi == (uint32_t)__builtin_amdgcn_readfirstlane((int)hi);
+    }
+  }
+  G2J R = jac_infinity<Fp2>();
+  if (__all(same)) {
+    if (lane == 0) {
+      int top = 0;
+      for (uint32_t k = 0; k < cnt; k++) {
+        const TaDigits d = dig[m0 + k];
+        for (int i = 0; i < 4; i++) top = max(top, naf4_digits(d.a[i], naf[k][i]));
+      }
+      naf_top = top;
+    }
+    __syncthreads();
+    HB_NOUNROLL for (uint32_t k = 0; k < cnt; k++) {
+      const HmEntry e = pts[src ? src[m0 + k] : m0 + k];
+      odd_table(wt, 16 * (int)k, G2A{e.x, e.y, e.inf != 0});
+    }
+    const int top = naf_top;
+    HB_NOUNROLL for (int i = top; i >= 0; i--) {
+      R = jac_dbl(R);
+      HB_NOUNROLL for (uint32_t k = 0; k < cnt; k++) {
+        HB_NOUNROLL for (int b = 0; b < 4; b++) {
+          const int dg = naf[k][b][i];
+          if (dg != 0) {  // wave-uniform
+            G2J T = tab_load(wt, 16 * (int)k + 4 * b + ((dg < 0 ? -dg : dg) >> 1));
+            if (dg < 0) T.Y = f2_neg(T.Y);
+            R = jac_add(R, T);
+          }
+        }
+      }
+    }
+  } else {
+    HB_NOUNROLL for (uint32_t k = 0; k < cnt; k++) {
+      const HmEntry e = pts[src ? src[m0 + k] : m0 + k];
+      R = jac_add(R, member_general(wt, 0, e, dig[m0 + k]));
+    }
+  }
+  if (valid) {
+    out[m0] = {R.X, R.Y, R.Z};
+    const G2J z = jac_infinity<Fp2>();
+    for (uint32_t k = 1; k < cnt; k++) out[m0 + k] = {z.X, z.Y, z.Z};
+  }
+#endif
+}
+
 // The same aggregation as multi-scalar ladders over chunks of up to TA_CHUNK members of a group
 // (k_plan_* chunk plan, vbatch.hip): k_ta_table builds every member's 15-entry subset table (the
 // first half of k_ta_straus), then one lane per chunk runs ONE 64-step ladder whose doublings the
@@ -336,6 +489,17 @@ void launch_ta_lambda(const int64_t* idx, const uint32_t* grp_off, uint32_t n_gr
 }
 
 size_t ta_table_bytes(uint32_t n_partials) { return (size_t)blocks_of(n_partials, 64) * 16 * sizeof(G2JEntry) * 64; }
+size_t ta_joint_table_bytes(uint32_t n_groups, uint32_t t, uint32_t c) {
+  const size_t lanes = (size_t)n_groups * ((t + c - 1) / c);
+  return (size_t)blocks_of(lanes, 64) * 16 * c * sizeof(G2JEntry) * 64;
+}
+void launch_ta_joint(const HmEntry* pts, const uint32_t* src, const TaDigits* dig, uint32_t n_groups, uint32_t t,
+                     uint32_t c, void* tab, G2JEntry* out, hipStream_t s) {
+  if (!n_groups || !t || !c || c > (uint32_t)TA_JOINT_MAX) return;
+  const size_t lanes = (size_t)n_groups * ((t + c - 1) / c);
+  hipLaunchKernelGGL(k_ta_joint, dim3(blocks_of(lanes, 64)), dim3(64), 0, s, pts, src, dig, n_groups, t, c,
+                     (uint4*)tab, out);
+}
 
 void launch_ta_table(const HmEntry* pts, const uint32_t* src, uint32_t n_partials, void* tab, hipStream_t s) {
   if (n_partials)

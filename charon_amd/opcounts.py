@@ -150,6 +150,39 @@ def ta_uniform(ids, b=BLOCKS):
     return tot / len(ids)
 
 
+def ta_joint(ids, chunk, b=BLOCKS):
+    """k_ta_joint (threshold.hip) per member: a lane per chunk of `chunk` members of a validator
+    aggregating the share indices `ids`; per member its odd-multiple table, per chunk ONE schedule
+    of top + 1 doublings (top over the chunk's members), one addition per nonzero NAF digit."""
+    lams = []
+    for i in ids:
+        lam = 1
+        for j in ids:
+            if j != i:
+                lam = lam * j % R_ORDER * pow(j - i, -1, R_ORDER) % R_ORDER
+        lams.append(lam)
+    table = b["jac_dbl_g2"] + b["jac_add_aff_g2"] + 2 * b["jac_add_g2"] + 4 * 24
+    tot = 0
+    for c0 in range(0, len(ids), chunk):
+        top, adds = 0, 0
+        for lam in lams[c0:c0 + chunk]:
+            for _ in range(4):
+                n = _naf4(lam % X_ABS)
+                lam //= X_ABS
+                adds += sum(1 for d in n if d)
+                top = max(top, len(n))
+            tot += table
+        tot += top * b["jac_dbl_g2"] + adds * b["jac_add_g2"]
+    return tot / len(ids)
+
+
+def ta_joint_chunk(t, n_partials, knob=0, lanes=98304):
+    """The library's choice of members per lane (hipbls.hip ta_tail): 0/1 = one ladder per member."""
+    c = knob if knob else n_partials // lanes
+    c = min(c, t, 8)
+    return c if c > 1 else 0
+
+
 def per_unit(b=BLOCKS, group_size=1, t=1):
     """{kernel: (alg, exec)} Fp products per unit (unit named in UNITS)."""
     p = pair3(b)

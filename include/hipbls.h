@@ -237,6 +237,10 @@ size_t hbls_slot_msm(size_t min_items);
  * calls of fewer than 2 lanes' worth keep one ladder per item).  0 restores the default 65536
  * (HBLS_RLC_LANES).  Returns the previous value.  Verdicts do not depend on it. */
 size_t hbls_rlc_lanes(size_t lanes);
+/* Tuning: ThresholdAggregate calls whose groups all have t members run joint ladders over chunks
+ * of `members` (<= 8) members of a validator, sharing the doublings; 0 = auto (HBLS_TA_JOINT), 1 =
+ * one ladder per member.  Returns the previous value.  Outputs do not depend on it. */
+size_t hbls_ta_joint(size_t members);
 /* Wait for all work the library queued on `stream`. */
 int hbls_sync(void* stream);
 

@@ -530,3 +530,35 @@ def test_pubkey_cache_same_verdicts(hipbls):
     hipbls.clear_pubkey_cache()
     assert cached == plain
     assert sorted(plain).count(0) == 36
+
+
+@pytest.mark.parametrize("members", [1, 2, 3, 4])
+def test_threshold_aggregate_joint_ladders(L, hipbls, members):
+    """ThresholdAggregate of 320 validators x 4 partials through the joint ladders (a lane per
+    chunk of `members` members; 1 = one ladder per member): the first 192 validators aggregate the
+    same share indices (wave-uniform Lagrange digits: the NAF schedule), the rest a random 4-subset
+    of 1..10 each (mixed digits in a wave: the general ladder), one group has an undecodable
+    partial.  Every aggregate equals the signature under the validator's secret."""
+    rng = random.Random(31 + members)
+    V, n, t = 320, 10, 4
+    msg = hashlib.sha256(b"joint ladders").digest()
+    secrets = [hipbls.generate_secret_key() for _ in range(V)]
+    roots = hipbls.sign_batch(secrets, [msg] * V)
+    groups, want = [], []
+    for v in range(V):
+        shares = hipbls.threshold_split(secrets[v], n, t)
+        ids = [1, 3, 4, 8] if v < 192 else sorted(rng.sample(range(1, n + 1), t))
+        sigs = hipbls.sign_batch([shares[i] for i in ids], [msg] * t)
+        groups.append(dict(zip(ids, sigs)))
+        want.append((OK, roots[v]))
+    groups[200][next(iter(groups[200]))] = b"\x00" * 96  # undecodable member
+    want[200] = (BAD_SIGNATURE, None)
+    prev = L.hbls_ta_joint(members)
+    try:
+        outs, sts = hipbls.threshold_aggregate_batch(groups)
+    finally:
+        L.hbls_ta_joint(prev)
+    for v in range(V):
+        assert sts[v] == want[v][0], v
+        if want[v][0] == OK:
+            assert outs[v] == want[v][1], v
