@@ -129,6 +129,28 @@ __device__ __forceinline__ void f2_select(Fp2& r, bool take_b, const Fp2& a, con
     r.c1.v[i] = take_b ? b.c1.v[i] : a.c1.v[i];
   }
 }
+// Fp2 values (6 quads) at quad offset q0 of entry e; affine points (x, y: 12 quads) at entry e
+__device__ __forceinline__ void f2_store_q(uint4* wt, int e, int q0, const Fp2& a) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(&a);
+  HB_UNROLL for (int q = 0; q < 6; q++)
+    wt[(e * TA_TAB_QUADS + q0 + q) * 64] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+}
+__device__ __forceinline__ Fp2 f2_load_q(const uint4* wt, int e, int q0) {
+  Fp2 a;
+  uint32_t* w = reinterpret_cast<uint32_t*>(&a);
+  HB_UNROLL for (int q = 0; q < 6; q++) {
+    const uint4 v = wt[(e * TA_TAB_QUADS + q0 + q) * 64];
+    w[4 * q] = v.x;
+    w[4 * q + 1] = v.y;
+    w[4 * q + 2] = v.z;
+    w[4 * q + 3] = v.w;
+  }
+  return a;
+}
+__device__ __forceinline__ void aff_store(uint4* wt, int e, const Fp2& x, const Fp2& y) {
+  f2_store_q(wt, e, 0, x);
+  f2_store_q(wt, e, 6, y);
+}
 #endif
 
 // One lane per partial: lambda sigma = sum_i [a_i] P_i with P_i = (-1)^i psi^i(sigma), as a
@@ -251,25 +273,58 @@ __global__ KB_OCC(HB_OCC_STRAUS) void k_ta_straus(const HmEntry* __restrict__ pt
 }
 
 #if defined(__HIP_DEVICE_COMPILE__)
-// The odd multiples {1, 3, 5, 7} of the four bases B_k = P0, -psi(P0), psi^2(P0), -psi^3(P0) of
-// one member: table entries e0 + 4 k + (|d| >> 1).
-__device__ __forceinline__ void odd_table(uint4* wt, int e0, const G2A& P0) {
-  const G2J J1 = jac_from_aff(P0);
-  const G2J J2 = jac_dbl(J1);
-  const G2J J3 = jac_add_aff(J2, P0);
-  const G2J J5 = jac_add(J3, J2);
-  const G2J J7 = jac_add(J5, J2);
+// Affine odd-multiple tables of the `cnt` members of a joint lane (k_ta_joint): member k's entries
+// 16 k + 4 b + (|d| >> 1) hold the affine odd multiples {1, 3, 5, 7} of the bases B_b = P0, -psi(P0),
+// psi^2(P0), -psi^3(P0), so the ladder adds them with mixed additions (7M + 4S instead of 11M + 5S
+// over Fp2).  3P0, 5P0, 7P0 of all members are made affine with ONE inversion (Montgomery's trick):
+// pass 1 keeps them Jacobian in entries 16 k + 1..3 and the running product of their Z before each
+// in entries 16 k + 5..7; pass 2 walks back, recovering every 1 / Z.  A member at infinity (an
+// undecodable partial: the validator's aggregate is discarded) multiplies Z = 1 into the product.
+__device__ __forceinline__ void odd_tables_affine(uint4* wt, const HmEntry* __restrict__ pts,
+                                                  const uint32_t* __restrict__ src, uint32_t m0, uint32_t cnt) {
+  Fp2 acc = f2_one();
+  HB_NOUNROLL for (uint32_t k = 0; k < cnt; k++) {
+    const HmEntry e = pts[src ? src[m0 + k] : m0 + k];
+    const G2A P0 = {e.x, e.y, e.inf != 0};
+    const G2J J1 = jac_from_aff(P0);
+    const G2J J2 = jac_dbl(J1);
+    const G2J J3 = jac_add_aff(J2, P0);
+    const G2J J5 = jac_add(J3, J2);
+    const G2J J7 = jac_add(J5, J2);
+    HB_NOUNROLL for (int j = 1; j < 4; j++) {
+      G2J J = j == 1 ? J3 : j == 2 ? J5 : J7;
+      if (f2_is_zero(J.Z)) J.Z = f2_one();
+      tab_store(wt, 16 * (int)k + j, J);
+      f2_store_q(wt, 16 * (int)k + 4 + j, 0, acc);
+      acc = f2_mul(acc, J.Z);
+    }
+    aff_store(wt, 16 * (int)k, P0.x, P0.y);
+  }
+  Fp2 inv = f2_inv(acc);
   const Fp2 cx = f2_from_const(PSI_CX), cy = f2_from_const(PSI_CY);
   const Fp2 c2x = f2_from_const(PSI2_CX), c2y = f2_from_const(PSI2_CY);
-  HB_NOUNROLL for (int j = 0; j < 4; j++) {
-    const G2J J = j == 0 ? J1 : j == 1 ? J3 : j == 2 ? J5 : J7;
-    tab_store(wt, e0 + j, J);
-    const G2J N1 = {f2_mul(f2_conj(J.X), cx), f2_neg(f2_mul(f2_conj(J.Y), cy)), f2_conj(J.Z)};
-    const G2J N2 = {f2_mul(J.X, c2x), f2_mul(J.Y, c2y), J.Z};
-    const G2J N3 = {f2_mul(f2_conj(N2.X), cx), f2_neg(f2_mul(f2_conj(N2.Y), cy)), f2_conj(N2.Z)};
-    tab_store(wt, e0 + 4 + j, N1);
-    tab_store(wt, e0 + 8 + j, N2);
-    tab_store(wt, e0 + 12 + j, N3);
+  HB_NOUNROLL for (int k = (int)cnt - 1; k >= 0; k--) {
+    HB_NOUNROLL for (int j = 3; j >= 0; j--) {
+      const int e = 16 * k + j;
+      Fp2 x, y;
+      if (j == 0) {
+        x = f2_load_q(wt, e, 0);
+        y = f2_load_q(wt, e, 6);
+      } else {
+        const G2J J = tab_load(wt, e);
+        const Fp2 zi = f2_mul(inv, f2_load_q(wt, 16 * k + 4 + j, 0));  // 1 / Z
+        inv = f2_mul(inv, J.Z);
+        const Fp2 zi2 = f2_sqr(zi);
+        x = f2_mul(J.X, zi2);
+        y = f2_mul(J.Y, f2_mul(zi2, zi));
+        aff_store(wt, e, x, y);
+      }
+      // -psi: (conj(x) cx, -conj(y) cy);  psi^2: (x c2x, y c2y);  -psi^3 = -psi(psi^2)
+      const Fp2 x2 = f2_mul(x, c2x), y2 = f2_mul(y, c2y);
+      aff_store(wt, e + 4, f2_mul(f2_conj(x), cx), f2_neg(f2_mul(f2_conj(y), cy)));
+      aff_store(wt, e + 8, x2, y2);
+      aff_store(wt, e + 12, f2_mul(f2_conj(x2), cx), f2_neg(f2_mul(f2_conj(y2), cy)));
+    }
   }
 }
 
@@ -371,10 +426,7 @@ __global__ KB_OCC(HB_OCC_STRAUS) void k_ta_joint(const HmEntry* __restrict__ pts
       naf_top = top;
     }
     __syncthreads();
-    HB_NOUNROLL for (uint32_t k = 0; k < cnt; k++) {
-      const HmEntry e = pts[src ? src[m0 + k] : m0 + k];
-      odd_table(wt, 16 * (int)k, G2A{e.x, e.y, e.inf != 0});
-    }
+    odd_tables_affine(wt, pts, src, m0, cnt);
     const int top = naf_top;
     HB_NOUNROLL for (int i = top; i >= 0; i--) {
       R = jac_dbl(R);
@@ -382,9 +434,10 @@ __global__ KB_OCC(HB_OCC_STRAUS) void k_ta_joint(const HmEntry* __restrict__ pts
         HB_NOUNROLL for (int b = 0; b < 4; b++) {
           const int dg = naf[k][b][i];
           if (dg != 0) {  // wave-uniform
-            G2J T = tab_load(wt, 16 * (int)k + 4 * b + ((dg < 0 ? -dg : dg) >> 1));
-            if (dg < 0) T.Y = f2_neg(T.Y);
-            R = jac_add(R, T);
+            const int e = 16 * (int)k + 4 * b + ((dg < 0 ? -dg : dg) >> 1);
+            G2A T = {f2_load_q(wt, e, 0), f2_load_q(wt, e, 6), false};
+            if (dg < 0) T.y = f2_neg(T.y);
+            R = jac_add_aff(R, T);
           }
         }
       }

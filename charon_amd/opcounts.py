@@ -74,9 +74,11 @@ TA_CHUNK = 8     # members per lane of k_ta_msm (layout.h)
 
 def rlc_msm(b=BLOCKS, chunk=1, sides=3):
     """k_rlc_msm per item of a chunk of `chunk` items: the ladder points (phi + one mixed addition
-    per side), 32 shared doublings per chunk, 32 additions per item.  sides: 1 the public-key side
+    per side; affine on the G1 side), 32 shared doublings per chunk, 32 additions per item.  sides: 1 the public-key side
     only (the slot-wide check takes the signature side as one MSM), 3 both."""
-    g1 = 1 + b["jac_add_aff_g1"] + 32 * b["jac_add_g1"] + 32 * b["jac_dbl_g1"] / chunk
+    # G1: P + phi(P) made affine with one inversion per chunk (3 products into and out of the
+    # running product, 1/Z^2, 1/Z^3, x, y), then 32 mixed additions
+    g1 = 1 + b["jac_add_aff_g1"] + 3 + 4 + b["fp_inv"] / chunk + 32 * b["jac_add_aff_g1"] + 32 * b["jac_dbl_g1"] / chunk
     g2 = 6 + b["jac_add_aff_g2"] + 32 * b["jac_add_g2"] + 32 * b["jac_dbl_g2"] / chunk
     return g1 + (g2 if sides & 2 else 0)
 
@@ -152,8 +154,9 @@ def ta_uniform(ids, b=BLOCKS):
 
 def ta_joint(ids, chunk, b=BLOCKS):
     """k_ta_joint (threshold.hip) per member: a lane per chunk of `chunk` members of a validator
-    aggregating the share indices `ids`; per member its odd-multiple table, per chunk ONE schedule
-    of top + 1 doublings (top over the chunk's members), one addition per nonzero NAF digit."""
+    aggregating the share indices `ids`; per member its affine odd-multiple table (one batched
+    inversion per chunk), per chunk ONE schedule of top + 1 doublings (top over the chunk's
+    members), one mixed addition per nonzero NAF digit."""
     lams = []
     for i in ids:
         lam = 1
@@ -161,7 +164,10 @@ def ta_joint(ids, chunk, b=BLOCKS):
             if j != i:
                 lam = lam * j % R_ORDER * pow(j - i, -1, R_ORDER) % R_ORDER
         lams.append(lam)
-    table = b["jac_dbl_g2"] + b["jac_add_aff_g2"] + 2 * b["jac_add_g2"] + 4 * 24
+    # per member: 2P, 3P, 5P, 7P; 3 products into the running product of Z; back: 2 products for
+    # 1/Z, then 1/Z^2, 1/Z^3 and x, y (Fp2: sqr 2, mul 3 Fp products) for 3 points; psi images of
+    # the 4 affine points (3 images x 2 Fp2 products); per chunk one Fp2 inversion
+    table = b["jac_dbl_g2"] + b["jac_add_aff_g2"] + 2 * b["jac_add_g2"] + 3 * 3 + 3 * (2 * 3 + 2 + 3 * 3) + 4 * 18
     tot = 0
     for c0 in range(0, len(ids), chunk):
         top, adds = 0, 0
@@ -172,7 +178,7 @@ def ta_joint(ids, chunk, b=BLOCKS):
                 adds += sum(1 for d in n if d)
                 top = max(top, len(n))
             tot += table
-        tot += top * b["jac_dbl_g2"] + adds * b["jac_add_g2"]
+        tot += b["fp_inv"] + 6 + top * b["jac_dbl_g2"] + adds * b["jac_add_aff_g2"]
     return tot / len(ids)
 
 
