@@ -643,12 +643,16 @@ def main(argv=None):
                  "k_ta_straus": (ta_units, (ta_w, ta_w)), "k_group_sum": (V, per_unit["k_group_sum"]),
                  "k_hash_to_g2": (M, per_unit["k_hash_to_g2"]), "k_lines_msg": (M, per_unit["k_lines_msg"])}
         if smsm:
-            nb1 = -(-V // opcounts.FE_BATCH)
-            nb2 = -(-nb1 // opcounts.FE_BATCH)
-            fin = opcounts.pair3_fin(batch=nb2)
+            # multi-Miller loops of MML_PAIRS groups, product tree of fan-in FE_BATCH to <= FE_BATCH
+            mmlk = int(os.environ.get("HBLS_MML_PAIRS", opcounts.MML_PAIRS))
+            n_prod, cur = 0, -(-V // mmlk)
+            while cur > opcounts.FE_BATCH:
+                n_prod += cur
+                cur = -(-cur // opcounts.FE_BATCH)
+            fin = opcounts.pair3_fin(batch=cur)
             units.update({"k_group_prep": (V, prep_units["k_group_prep_p"]),
-                          "k_pair3_ml": (V, per_unit["k_pair3_ml"]),
-                          "k_pair3_prod": (V + nb1, per_unit["k_pair3_prod"]),
+                          "k_pair3_mml": (V, opcounts.pair3_mml(pairs=mmlk)),
+                          "k_pair3_prod": (n_prod, per_unit["k_pair3_prod"]),
                           "k_pair3_fin": (1, fin), "k_slines": (1, per_unit["k_slines"]),
                           "k_msm_bucket": (opcounts.MSM_ENTRIES_PER_ITEM * n_rlc, per_unit["k_msm_bucket"]),
                           "k_msm_reduce": (opcounts.MSM_PARTS, per_unit["k_msm_reduce"]),

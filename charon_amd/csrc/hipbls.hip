@@ -247,6 +247,7 @@ std::atomic<size_t> g_fe_batch_min{2 * FE_BATCH};
 // multiplication (msm.hip), one final exponentiation for the call -- and fall back to the
 // per-batch check when that fails (0 = never)
 std::atomic<size_t> g_slot_msm_min{65536};
+size_t g_mml_pairs = MML_PAIRS;  // HBLS_MML_PAIRS: groups per multi-Miller loop of the slot-wide check
 
 struct DevBuf {
   void* p = nullptr;
@@ -448,6 +449,7 @@ int init_mask(uint32_t mask) {
   g_ta_joint = std::min<size_t>(8, env_size("HBLS_TA_JOINT", g_ta_joint.load()));
   g_fe_batch_min = env_size("HBLS_FE_BATCH", g_fe_batch_min.load());
   g_slot_msm_min = env_size("HBLS_SLOT_MSM", g_slot_msm_min.load());
+  g_mml_pairs = std::min<size_t>(64, std::max<size_t>(1, env_size("HBLS_MML_PAIRS", g_mml_pairs)));
   std::vector<Dev*> devs;
   for (int k = 0; k < 32; k++)
     if (mask & (1u << k)) {
@@ -641,7 +643,8 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
   // on the device flag sfail).  Needs all groups in one chunk.
   const size_t smin = g_slot_msm_min.load();
   const bool smsm = bfe && smin && n_groups <= gcap && n + n_agg >= smin;
-  const size_t nb1 = (gcap + FE_BATCH - 1) / FE_BATCH, nb2 = (nb1 + FE_BATCH - 1) / FE_BATCH;
+  const size_t mmlk = g_mml_pairs;
+  const size_t nb1 = (gcap + mmlk - 1) / mmlk, nb2 = (nb1 + FE_BATCH - 1) / FE_BATCH;
   G2MsmArgs ma{};
   Fp4Entry *pbuf1 = nullptr, *pbuf2 = nullptr;
   uint8_t* sfail = nullptr;
@@ -831,29 +834,40 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
         TIMED(d, "k_msm_sum", sm, launch_msm_sum(ma, sm));
         TIMED(d, "k_slines", sm, launch_slines(ma.total, nullptr, nullptr, 1, blines, 1, bbad, sm));
         HCHK(hipEventRecord(w.ev_side[0], sm));
-        TIMED(d, "k_pair3_ml", s, launch_pair3_ml(pm, s));
+        // multi-Miller loops over MML_PAIRS groups (shared squarings), then a product tree of
+        // fan-in FE_BATCH down to at most FE_BATCH values (ping-pong between pbuf1 and pbuf2)
         Pair3Args pp{};
-        pp.n = (uint32_t)((ng + FE_BATCH - 1) / FE_BATCH);
-        pp.f_in = fbuf;
-        pp.f_range = FE_BATCH;
+        pp.pk = gP;
+        pp.pk_st = gst;
+        pp.msg_idx = gmsg + g0;
+        pp.hm = hm;
+        pp.n = (uint32_t)((ng + mmlk - 1) / mmlk);
+        pp.f_range = (uint32_t)mmlk;
         pp.f_n = ng;
         pp.f_out = pbuf1;
-        TIMED(d, "k_pair3_prod", s, launch_pair3_prod(pp, s));
-        const uint32_t n1 = pp.n;
-        pp.n = (n1 + FE_BATCH - 1) / FE_BATCH;
-        pp.f_in = pbuf1;
-        pp.f_n = n1;
-        pp.f_out = pbuf2;
-        TIMED(d, "k_pair3_prod", s, launch_pair3_prod(pp, s));
+        TIMED(d, "k_pair3_mml", s, launch_pair3_mml(pp, s));
+        Fp4Entry* cur = pbuf1;
+        uint32_t cur_n = pp.n;
+        while (cur_n > FE_BATCH) {
+          Pair3Args pr{};
+          pr.n = (cur_n + FE_BATCH - 1) / FE_BATCH;
+          pr.f_in = cur;
+          pr.f_range = FE_BATCH;
+          pr.f_n = cur_n;
+          pr.f_out = cur == pbuf1 ? pbuf2 : pbuf1;
+          TIMED(d, "k_pair3_prod", s, launch_pair3_prod(pr, s));
+          cur = pr.f_out;
+          cur_n = pr.n;
+        }
         HCHK(hipStreamWaitEvent(s, w.ev_side[0], 0));
         Pair3Args pf{};
         pf.pk_st = bbad;
         pf.sig_lines = blines;
         pf.stride = 1;
         pf.n = 1;
-        pf.f_in = pbuf2;
-        pf.f_range = pp.n;
-        pf.f_n = pp.n;
+        pf.f_in = cur;
+        pf.f_range = cur_n;
+        pf.f_n = cur_n;
         pf.status = sfail;
         TIMED(d, "k_pair3_fin", s, launch_pair3_fin(pf, s));
         TIMED(d, "k_slot_verdict", s, launch_slot_verdict(gst, sfail, ng, gver + g0, s));
@@ -871,12 +885,13 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
                            apr, asr, s, const_cast<uint2*>(ma.coef) + n, 2, sfail));
         ga.p_only = 0;
         ga.guard = sfail;
+        pm.guard = sfail;
       }
       ga.gS = gS;
       ga.bS = bS;
       TIMED(d, "k_group_prep", s, launch_group_prep(ga, s));
       // the (P_g, H(m_g)) Miller loops, stored unexponentiated
-      if (!smsm) TIMED(d, "k_pair3_ml", s, launch_pair3_ml(pm, s));
+      TIMED(d, "k_pair3_ml", s, launch_pair3_ml(pm, s));
       // per batch: the lines of sum_g S_g, one Miller loop times the batch's stored loops, one
       // final exponentiation
       const uint8_t* guard = smsm ? sfail : nullptr;

@@ -156,6 +156,10 @@ void launch_pair3_ml(const Pair3Args& a, hipStream_t s);
 void launch_pair3_fin(const Pair3Args& a, hipStream_t s);
 // PROD: f_out[e] = product of the stored values f_in of entries [e f_range, min((e + 1) f_range, f_n))
 void launch_pair3_prod(const Pair3Args& a, hipStream_t s);
+// MML: f_out[e] = ONE Miller loop over the (pk[i], H(msg_idx[i])) pairs of entries i in
+// [e f_range, min((e + 1) f_range, f_n)) whose pk_st byte is zero (shared squarings)
+void launch_pair3_mml(const Pair3Args& a, hipStream_t s);
+constexpr uint32_t MML_PAIRS = 4;  // pairs per multi-Miller loop of the slot-wide check
 
 // Batched verification (vbatch.hip).
 void launch_item_group(const uint32_t* grp_off, uint32_t n_groups, uint32_t n, uint32_t* item_grp, hipStream_t s);

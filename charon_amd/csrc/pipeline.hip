@@ -25,7 +25,10 @@ __global__ KB_OCC(HB_OCC_LINES) void k_lines_msg(MsgEntry* __restrict__ hm, uint
 // final exponentiation of vgroup.hip).
 // P3_PROD: no lines, no exponentiation -- the product of a range of stored values (the
 // slot-wide check's product tree).
-enum { P3_FULL = 0, P3_ML = 1, P3_FIN = 2, P3_PROD = 3 };
+// P3_MML: one Miller loop over the (P, H(m)) pairs of f_range consecutive entries [e f_range, ...)
+// -- the squarings shared by the chunk, one sparse line product per pair and line -- stored
+// unexponentiated (entries with a nonzero pk_st byte contribute one).
+enum { P3_FULL = 0, P3_ML = 1, P3_FIN = 2, P3_PROD = 3, P3_MML = 4 };
 
 __device__ __forceinline__ Fp4 f4_load(const Fp4Entry& e) { return {e.x, e.y}; }
 
@@ -59,6 +62,33 @@ __global__ KB_OCC(HB_OCC_PAIR3) void k_pair3(Pair3Args a) {
       Fp4 t;
       f4_select(t, j >= cnt, f4_load(a.f_in[3ull * idx + g.k]), g_one(g));
       f = g_mul(g, f, t);
+    }
+    if (valid) a.f_out[3ull * e + g.k] = Fp4Entry{f.x, f.y};
+    return;
+  }
+  if (MODE == P3_MML) {  // wave-uniform trip counts; pairs past the end or not READY multiply by one
+    const uint32_t first = e * a.f_range;
+    const uint32_t cnt = first < a.f_n ? min(a.f_range, a.f_n - first) : 0u;
+    Fp4 f = g_one(g);
+    int bit = 62;
+    bool pending_add = false;
+    HB_NOUNROLL for (int j = 0; j < N_LINES; j++) {
+      const bool dbl = !pending_add;
+      if (dbl && j > 0) f = g_sqr(g, f);
+      HB_NOUNROLL for (uint32_t k = 0; k < a.f_range; k++) {
+        const uint32_t idx = k < cnt ? first + k : first;
+        const bool use = k < cnt && !(a.pk_st && a.pk_st[idx]);
+        const G1AEntry Pk = a.pk[idx];
+        const LineEntry L = a.hm[a.msg_idx[idx]].lines[j];
+        const Fp4 t = g_mul_line(g, f, L.a0, f2_mul_fp(L.a1, Pk.x), f2_mul_fp(L.b1, Pk.y));
+        f4_select(f, use, f, t);
+      }
+      if (dbl) {
+        pending_add = ((HB_X_ABS >> bit) & 1) != 0;
+        bit--;
+      } else {
+        pending_add = false;
+      }
     }
     if (valid) a.f_out[3ull * e + g.k] = Fp4Entry{f.x, f.y};
     return;
@@ -138,5 +168,6 @@ void launch_pair3(const Pair3Args& a, hipStream_t s) { pair3_launch<P3_FULL>(a, 
 void launch_pair3_ml(const Pair3Args& a, hipStream_t s) { pair3_launch<P3_ML>(a, s); }
 void launch_pair3_fin(const Pair3Args& a, hipStream_t s) { pair3_launch<P3_FIN>(a, s); }
 void launch_pair3_prod(const Pair3Args& a, hipStream_t s) { pair3_launch<P3_PROD>(a, s); }
+void launch_pair3_mml(const Pair3Args& a, hipStream_t s) { pair3_launch<P3_MML>(a, s); }
 
 }  // namespace hb

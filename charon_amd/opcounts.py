@@ -60,6 +60,17 @@ def pair3_ml(b=BLOCKS):
     return alg, exe
 
 
+MML_PAIRS = 4    # pairs per multi-Miller loop of the slot-wide check (layout.h)
+
+
+def pair3_mml(b=BLOCKS, pairs=MML_PAIRS):
+    """k_pair3_mml per verification group: its 68 line products (lines evaluated at P) in a
+    Miller loop whose 62 squarings `pairs` groups share."""
+    alg = N_LINES * (b["f12_mul_line"] + 4) + N_SQR * b["f12_sqr"] / pairs
+    exe = N_LINES * (45 + 12) + N_SQR * 36 / pairs
+    return alg, exe
+
+
 def pair3_fin(b=BLOCKS, batch=FE_BATCH):
     """k_pair3_fin, per batch of `batch` groups: the Miller loop of (-g1, sum S), times the stored
     loops, one final exponentiation."""
@@ -225,6 +236,7 @@ def per_unit(b=BLOCKS, group_size=1, t=1):
         # loops (one Fp12 product per stored value); the MSM kernels per entry / chunk / point
         "k_group_prep_p": ((k - 1) * b["jac_add_g1"] + b["to_aff_g1"],) * 2,
         "k_pair3_prod": (b["f12_mul"], 3 * 18),
+        "k_pair3_mml": pair3_mml(b),
         "k_msm_bucket": (msm_bucket(b),) * 2,
         "k_msm_reduce": (msm_reduce(b),) * 2,
         "k_msm_sum": (b["jac_add_g2"],) * 2,
@@ -239,7 +251,7 @@ UNITS = {"k_pair3": "pairing check", "k_pair3_fallback": "pairing check", "k_dec
          "k_va_point": "aggregation group", "k_sig_lines": "signature", "k_group_prep_b": "verification group",
          "k_pair3_ml": "verification group", "k_pair3_fin": "batch of 64 groups",
          "k_slines": "batch of 64 groups", "k_group_prep_p": "verification group",
-         "k_pair3_prod": "stored Miller loop", "k_msm_bucket": "bucket entry", "k_msm_reduce": "chunk of 16 buckets",
+         "k_pair3_prod": "stored Miller loop", "k_pair3_mml": "verification group", "k_msm_bucket": "bucket entry", "k_msm_reduce": "chunk of 16 buckets",
          "k_msm_sum": "point"}
 
 # SHA-256 compressions per attestation signing root (roots.hip: 8 two-block hashes)
