@@ -59,6 +59,11 @@ WORKLOADS = {
                desc="C2 (BASELINE configs[1]): 10k validators, 4-operator threshold-3 cluster, one attestation "
                     "slot with 64 committee signing roots: 40k partial Verify + 10k ThresholdAggregate "
                     "(+10k aggregate Verify)"),
+    "c5": dict(validators=125_000, n=7, t=5, distinct=False, n_msgs=64, adversarial=0.01,
+               desc="C5 (BASELINE configs[4]) per-GPU shard: the C4 shard with 1% of the partials corrupted in "
+                    "equal fifths (random bytes, off-subgroup points, wrong message, another share's partial, "
+                    "infinity), verdicts checked bit-exact against construction; sync-committee "
+                    "VerifyAggregate over 512 keys per message timed beside it"),
     "c4": dict(validators=125_000, n=7, t=5, distinct=False, n_msgs=64,
                desc="C4 (BASELINE configs[3]) per-GPU shard: 1M validators over 8 GPUs = 125k validators, "
                     "7-operator threshold-5 cluster, 64 committee signing roots: 875k partial Verify + 125k "
@@ -121,6 +126,74 @@ def ta_share_positions(n, t):
         if any(x.denominator != 1 for x in lam):
             return list(pos)
     return list(range(t))
+
+
+def corrupt(L, d, frac, seed):
+    """C5: corrupt `frac` of the partials in equal fifths (core/parsigex/parsigex_test.go:285-289,
+    core/sigagg/sigagg_test.go:46-67 classes) and derive every expected status by construction:
+      0 random 96 bytes without the compression flag   -> BAD_SIGNATURE (undecodable)
+      1 an on-curve point outside G2 (tests/golden/off_subgroup_g2.json) -> BAD_SIGNATURE
+      2 the partial signed over another message        -> NOT_VERIFIED
+      3 another share's valid partial of the validator -> NOT_VERIFIED
+      4 the infinity encoding                          -> NOT_VERIFIED
+    The aggregation sees the corrupted signatures of its members: an undecodable member makes the
+    validator's ThresholdAggregate BAD_SIGNATURE, any other corrupted member a wrong aggregate whose
+    post-aggregate verification fails (NOT_VERIFIED)."""
+    import hashlib
+    import json
+    import random
+    n, t, V, NP = d["n"], d["t"], d["V"], d["NP"]
+    rng = random.Random(seed)
+    bad = rng.sample(range(NP), int(NP * frac))
+    cls = {i: k % 5 for k, i in enumerate(bad)}
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests", "golden", "off_subgroup_g2.json")) as f:
+        offsub = [bytes.fromhex(x) for x in json.load(f)["points"]]
+    sigs = d["sigs"].reshape(NP, 96)
+    orig = sigs.copy()
+    exp_v = np.zeros(NP, dtype=np.uint8)
+    wm = [i for i, c in cls.items() if c == 2]
+    if wm:
+        other = hashlib.sha256(b"another signing root").digest()
+        msgs = np.frombuffer(other * len(wm), dtype=np.uint8).copy()
+        sks = np.concatenate([d["sks"][32 * i:32 * i + 32] for i in wm])
+        out = np.zeros(96 * len(wm), dtype=np.uint8)
+        st = np.zeros(len(wm), dtype=np.uint8)
+        off = np.arange(len(wm), dtype=np.uint64) * 32
+        ln = np.full(len(wm), 32, dtype=np.uint32)
+        _chk(L, L.hbls_sign_batch(_p(sks), _p(msgs), _p(off), _p(ln), len(wm), _p(out), _p(st)))
+        assert not st.any()
+        sigs[wm] = out.reshape(-1, 96)
+    for i, c in cls.items():
+        v, sh = divmod(i, n)
+        if c == 0:
+            b = bytearray(rng.randrange(256) for _ in range(96))
+            b[0] &= 0x7F
+            sigs[i] = np.frombuffer(bytes(b), dtype=np.uint8)
+            exp_v[i] = 2
+        elif c == 1:
+            sigs[i] = np.frombuffer(offsub[i % len(offsub)], dtype=np.uint8)
+            exp_v[i] = 2
+        elif c == 2:
+            exp_v[i] = 3
+        elif c == 3:
+            sigs[i] = orig[v * n + (sh + 1) % n]
+            exp_v[i] = 3
+        else:
+            sigs[i] = 0
+            sigs[i, 0] = 0xC0
+            exp_v[i] = 3
+    d["sigs"] = sigs.reshape(-1)
+    d["ta_sigs"] = sigs[d["ta_src"]].reshape(-1).copy()
+    members = np.asarray(d["ta_src"], dtype=np.int64).reshape(V, t)
+    exp_ta = np.zeros(V, dtype=np.uint8)
+    exp_agg = np.zeros(V, dtype=np.uint8)
+    for v in {i // n for i in cls}:
+        mem = [cls.get(int(i)) for i in members[v]]
+        if any(c in (0, 1) for c in mem):
+            exp_ta[v] = exp_agg[v] = 2
+        elif any(c is not None for c in mem):
+            exp_agg[v] = 3
+    d.update(exp_v=exp_v, exp_ta=exp_ta, exp_agg=exp_agg, n_corrupted=len(bad))
 
 
 def setup_inputs(L, wl, V, rank):
@@ -453,6 +526,8 @@ def main(argv=None):
     wl = WORKLOADS[args.workload]
     V = args.validators or wl["validators"]
     d = setup_inputs(L, wl, V, rank)
+    if wl.get("adversarial"):
+        corrupt(L, d, wl["adversarial"], seed=7 + rank)
     n, t, NP, M = d["n"], d["t"], d["NP"], d["M"]
     dev = torch.device("cuda", local)
 
@@ -579,17 +654,36 @@ def main(argv=None):
     # parity of the timed outputs: every partial verifies, every aggregate is byte-identical to the
     # root-key signature (tbls_test.go:72-97 property) and verifies under the DV key
     used = outs if not staged else outs[:1]
-    parity = {"verify_all_ok": all(bool((o["vst"] == 0).all().item()) for o in used),
-              "ta_all_ok": all(bool((o["tst"] == 0).all().item()) for o in used),
-              "ta_equals_root_signature": all(np.array_equal(o["tout"].cpu().numpy(), d["root_sigs"]) for o in used)}
-    if not staged:
-        parity["aggregate_verify_all_ok"] = all(bool((o["ast"] == 0).all().item()) for o in used)
-    if world > 1:
+    if "exp_v" in d:  # C5: every status bit-exact against construction
+        clean = d["exp_agg"] == 0
+        parity = {"verify_statuses_exact": all(np.array_equal(o["vst"].cpu().numpy(), d["exp_v"]) for o in used),
+                  "ta_statuses_exact": all(np.array_equal(o["tst"].cpu().numpy(), d["exp_ta"]) for o in used),
+                  "ta_equals_root_signature_where_clean": all(np.array_equal(
+                      o["tout"].cpu().numpy().reshape(V, 96)[clean], d["root_sigs"].reshape(V, 96)[clean])
+                      for o in used)}
+        if not staged:
+            parity["aggregate_verify_statuses_exact"] = all(
+                np.array_equal(o["ast"].cpu().numpy(), d["exp_agg"]) for o in used)
+    else:
+        parity = {"verify_all_ok": all(bool((o["vst"] == 0).all().item()) for o in used),
+                  "ta_all_ok": all(bool((o["tst"] == 0).all().item()) for o in used),
+                  "ta_equals_root_signature": all(np.array_equal(o["tout"].cpu().numpy(), d["root_sigs"])
+                                                  for o in used)}
+        if not staged:
+            parity["aggregate_verify_all_ok"] = all(bool((o["ast"] == 0).all().item()) for o in used)
+    if world > 1 and "exp_v" in d:  # every rank's block equals that rank's construction: check our own
+        parity["allgather_ok"] = bool(
+            np.array_equal(xchg["vst"][rank * NP:(rank + 1) * NP].cpu().numpy(), d["exp_v"]) and
+            np.array_equal(xchg["tst"][rank * V:(rank + 1) * V].cpu().numpy(), d["exp_ta"]) and
+            np.array_equal(xchg["ast"][rank * V:(rank + 1) * V].cpu().numpy(), d["exp_agg"]))
+    elif world > 1:
         parity["allgather_ok"] = bool((xchg["vst"] == 0).all().item() and (xchg["tst"] == 0).all().item() and
                                       (xchg["ast"] == 0).all().item())
         # rank r's block of the gathered aggregates is rank r's root signatures: check our own block
+        clean = d["exp_agg"] == 0 if "exp_v" in d else np.ones(V, dtype=bool)
         parity["allgather_own_block"] = bool(np.array_equal(
-            xchg["tout"][rank * V * 96:(rank + 1) * V * 96].cpu().numpy(), d["root_sigs"]))
+            xchg["tout"][rank * V * 96:(rank + 1) * V * 96].cpu().numpy().reshape(V, 96)[clean],
+            d["root_sigs"].reshape(V, 96)[clean]))
 
     items = world * (NP + V)
     ms_per_step = elapsed / args.steps * 1e3
@@ -622,7 +716,9 @@ def main(argv=None):
         s_min = L.hbls_slot_msm(0)
         L.hbls_slot_msm(s_min)
         n_rlc = NP + (0 if staged else V)
-        smsm = bool(bfe and s_min and n_rlc >= s_min)
+        # (C5: the slot-wide check fails on the corrupted partials and the per-batch check runs on
+        # top of it; the per-kernel table then counts the per-batch path's work)
+        smsm = bool(bfe and s_min and n_rlc >= s_min) and "exp_v" not in d
         sides = 1 if smsm else 3
         rlc_item = opcounts.BLOCKS["rlc_g1"] + (opcounts.BLOCKS["rlc_g2"] if sides & 2 else 0)
         cmax = min(opcounts.RLC_CHUNK, max(1, NP // int(os.environ.get("HBLS_RLC_LANES", "65536"))))
@@ -707,7 +803,8 @@ def main(argv=None):
                 "pubshares and signatures produced on device",
         "config": {"workload": wl["desc"], "validators_per_gpu": V, "operators": n, "threshold": t,
                    "aggregated_share_indices": [int(x) + 1 for x in ta_share_positions(n, t)],
-                   "distinct_messages": M, "partials_per_gpu": NP, "parallelism": f"validator-sharded x{world}"},
+                   "distinct_messages": M, "partials_per_gpu": NP, "parallelism": f"validator-sharded x{world}",
+                   **({"corrupted_partials_per_gpu": d["n_corrupted"]} if "exp_v" in d else {})},
         "verify_per_s": round(world * NP / (elapsed / args.steps), 1),
         "threshold_aggregate_per_s": round(world * V / (elapsed / args.steps), 1),
         "aggregate_verify_per_s": None if staged else round(world * V / (elapsed / args.steps), 1),

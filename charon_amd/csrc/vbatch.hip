@@ -64,12 +64,14 @@ __global__ KB_OCC(HB_OCC_DECPK) void k_dec_pk(const uint8_t* __restrict__ pks, u
 // One lane per signature: decompress + subgroup-check (herumi.go:295 / :257 Sign.Deserialize),
 // affine point + status (1 = undecodable or off the subgroup).  Serves the verification and,
 // through index arrays, the ThresholdAggregate of the same partials.
+// Two kernels: the square root (k_dec_sig_pt) and the subgroup check (k_g2_subgroup), so that
+// neither holds the other's working set (one kernel spilled 4 KB per lane to scratch).
 __global__ KB_OCC(HB_OCC_DECSIG) void k_dec_sig_pt(const uint8_t* __restrict__ sigs, uint32_t n, HmEntry* __restrict__ out,
                                 uint8_t* __restrict__ st) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   G2A q;
-  uint8_t bad = g2_decompress(q, sigs + 96ull * i);
+  uint8_t bad = g2_decompress(q, sigs + 96ull * i, false);
   if (bad) q = {f2_zero(), f2_zero(), true};
   HmEntry e;
   e.x = q.x;
@@ -78,6 +80,22 @@ __global__ KB_OCC(HB_OCC_DECSIG) void k_dec_sig_pt(const uint8_t* __restrict__ s
   e.pad[0] = e.pad[1] = e.pad[2] = 0;
   out[i] = e;
   st[i] = bad;
+}
+
+__global__ KB_OCC(HB_OCC_DECSIG) void k_g2_subgroup(uint32_t n, HmEntry* __restrict__ pts, uint8_t* __restrict__ st) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const HmEntry e = pts[i];
+  if (st[i] || e.inf) return;
+  if (!g2_in_subgroup(G2A{e.x, e.y, false})) {
+    HmEntry z;
+    z.x = f2_zero();
+    z.y = f2_zero();
+    z.inf = 1u;
+    z.pad[0] = z.pad[1] = z.pad[2] = 0;
+    pts[i] = z;
+    st[i] = 1;
+  }
 }
 
 // One lane per public key of a host-buffer call with a key cache (hbls_pubkey_cache_add): the
@@ -398,7 +416,9 @@ void launch_pk_gather(const uint8_t* pks, const uint32_t* idx, const G1AEntry* t
   if (n) hipLaunchKernelGGL(k_pk_gather, dim3(blocks_for(n)), dim3(BLOCK), 0, s, pks, idx, tab, tst, n, out, st);
 }
 void launch_dec_sig_pt(const uint8_t* sigs, uint32_t n, HmEntry* out, uint8_t* st, hipStream_t s) {
-  if (n) hipLaunchKernelGGL(k_dec_sig_pt, dim3(blocks_for(n)), dim3(BLOCK), 0, s, sigs, n, out, st);
+  if (!n) return;
+  hipLaunchKernelGGL(k_dec_sig_pt, dim3(blocks_for(n)), dim3(BLOCK), 0, s, sigs, n, out, st);
+  hipLaunchKernelGGL(k_g2_subgroup, dim3(blocks_for(n)), dim3(BLOCK), 0, s, n, out, st);
 }
 void launch_rlc(const G1AEntry* pk, const uint8_t* pk_st, const HmEntry* sig, const uint8_t* sig_st,
                 const uint32_t* item_grp, const uint32_t* grp_off, int always, uint32_t n, uint32_t key_base,

@@ -562,3 +562,27 @@ def test_threshold_aggregate_joint_ladders(L, hipbls, members):
         assert sts[v] == want[v][0], v
         if want[v][0] == OK:
             assert outs[v] == want[v][1], v
+
+
+def test_hash_paths_agree(L):
+    """hash_to_G2 of 65 536 messages takes the one-lane kernel (hash.hip k_hash_to_g2_1); the first
+    512 of them, hashed again alone, the two-lane kernel (k_hash_to_g2, KAT-pinned through Sign).
+    The points must agree."""
+    import torch
+    dev = torch.device("cuda", 0)
+    n, k = 65536, 512
+    msgs = np.frombuffer(b"".join(hashlib.sha256(b"m%d" % i).digest() for i in range(n)), dtype=np.uint8).copy()
+    E = L.hbls_hm_entry_bytes()
+    dm = torch.from_numpy(msgs).to(dev)
+    off = torch.from_numpy((np.arange(n, dtype=np.uint64) * 32).view(np.int64)).to(dev)
+    ln = torch.full((n,), 32, dtype=torch.int32, device=dev)
+    hm_a = torch.zeros(n * E, dtype=torch.uint8, device=dev)
+    hm_b = torch.zeros(k * E, dtype=torch.uint8, device=dev)
+    s = torch.cuda.Stream(device=dev)
+    sp = ctypes.c_void_p(s.cuda_stream)
+    _chk(L, L.hbls_hash_to_g2_device(_p(dm), _p(off), _p(ln), n, _p(hm_a), sp))
+    _chk(L, L.hbls_hash_to_g2_device(_p(dm), _p(off), _p(ln), k, _p(hm_b), sp))
+    s.synchronize()
+    a = hm_a.cpu().numpy().reshape(n, E)[:k, :208]
+    b = hm_b.cpu().numpy().reshape(k, E)[:, :208]
+    assert np.array_equal(a, b)

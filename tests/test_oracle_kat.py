@@ -72,3 +72,19 @@ def test_fixtures_consistent_with_oracle_fast_paths(fixtures):
             B.g2_decompress(sig)
         except B.DecodeError:
             assert c["status"] == B.ST_BAD_SIGNATURE, c["name"]
+
+
+def test_off_subgroup_fixture():
+    """tests/golden/off_subgroup_g2.json (bench.py's C5 class 1): every point decompresses onto the
+    curve but lies outside G2, so Verify reports an undecodable signature (oracle)."""
+    import json
+    import os
+    from oracle import bls12381 as B
+    path = os.path.join(os.path.dirname(__file__), "golden", "off_subgroup_g2.json")
+    pts = json.load(open(path))["points"]
+    assert len(pts) == 16
+    for h in pts[:4]:
+        b = bytes.fromhex(h)
+        x = (int.from_bytes(b[48:], "big"), int.from_bytes(bytes([b[0] & 0x1F]) + b[1:48], "big"))
+        y = B.f2_sqrt(B.f2_add(B.f2_mul(B.f2_sqr(x), x), B.B_G2))
+        assert y is not None and not B.g2_in_subgroup((x, y))

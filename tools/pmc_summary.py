@@ -39,7 +39,7 @@ def main():
         names[name] = 1
     # launches per slot of each kernel: the dispatches between the last two k_hash_to_g2 (slot start)
     order = list(sq.keys())
-    starts = [k for k, (i, n) in enumerate(order) if n == "k_hash_to_g2"]
+    starts = [k for k, (i, n) in enumerate(order) if n.startswith("k_hash_to_g2")]
     slot = order[starts[-1]:] if starts else order
     slot_names = collections.Counter(n for _, n in slot)
     for name, cnt in slot_names.items():
