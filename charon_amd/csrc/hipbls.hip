@@ -234,7 +234,7 @@ size_t g_kc_n = 0;
 // chunks of 2, 4 or 8 members.
 bool g_ta_msm = false;
 size_t g_ta_chunk = 4;   // HBLS_TA_CHUNK: members per lane of k_ta_msm (<= TA_CHUNK)
-// HBLS_TA_JOINT: members per lane of the joint aggregation ladders (k_ta_joint) when every group has
+// HBLS_TA_JOINT: members per lane of the joint aggregation ladders (k_ta_jtab, k_ta_jladder, k_ta_jgeneral) when every group has
 // the same size t; 0 = auto (about TA_JOINT_LANES lanes, at most t and 8), 1 = one ladder per member
 // (k_ta_straus)
 std::atomic<size_t> g_ta_joint{0};
@@ -549,7 +549,7 @@ int ta_tail(Dev& d, Ws& w, const HmEntry* pts, const uint32_t* src, const uint8_
   void* tab;
   G2JEntry* pj;
   if (wsbuf(w, W_TAMST, np, &mst) || wsbuf(w, W_TADIG, np, &dig) || wsbuf(w, W_TAJ, np, &pj)) return -1;
-  // joint ladders over chunks of a validator's members (k_ta_joint) when every group has t members
+  // joint ladders over chunks of a validator's members (k_ta_jtab, k_ta_jladder, k_ta_jgeneral) when every group has t members
   const size_t t_u = (n_groups && np % n_groups == 0) ? np / n_groups : 0;
   size_t jc = 0;
   if (mode == 0 && t_u > 1 && !g_ta_msm) {

@@ -103,7 +103,7 @@ size_t ta_table_bytes(uint32_t n_partials);
 void launch_ta_straus(const HmEntry* pts, const uint32_t* src, const TaDigits* dig, uint32_t n_partials,
                       uint32_t n_groups, void* tab, G2JEntry* out, hipStream_t s);
 // joint ladders over chunks of c (<= 8) members of a validator, every group of exactly t members
-// (threshold.hip k_ta_joint); table workspace of ta_joint_table_bytes
+// (threshold.hip k_ta_jtab, k_ta_jladder, k_ta_jgeneral); table workspace of ta_joint_table_bytes
 size_t ta_joint_table_bytes(uint32_t n_groups, uint32_t t, uint32_t c);
 void launch_ta_joint(const HmEntry* pts, const uint32_t* src, const TaDigits* dig, uint32_t n_groups, uint32_t t,
                      uint32_t c, void* tab, G2JEntry* out, hipStream_t s);

@@ -273,7 +273,7 @@ __global__ KB_OCC(HB_OCC_STRAUS) void k_ta_straus(const HmEntry* __restrict__ pt
 }
 
 #if defined(__HIP_DEVICE_COMPILE__)
-// Affine odd-multiple tables of the `cnt` members of a joint lane (k_ta_joint): member k's entries
+// Affine odd-multiple tables of the `cnt` members of a joint lane (k_ta_jtab): member k's entries
 // 16 k + 4 b + (|d| >> 1) hold the affine odd multiples {1, 3, 5, 7} of the bases B_b = P0, -psi(P0),
 // psi^2(P0), -psi^3(P0), so the ladder adds them with mixed additions (7M + 4S instead of 11M + 5S
 // over Fp2).  3P0, 5P0, 7P0 of all members are made affine with ONE inversion (Montgomery's trick):
@@ -391,68 +391,106 @@ __device__ __forceinline__ G2J member_general(uint4* wt, int e0, const HmEntry& 
 // takes the general 15-entry ladder.  The chunk's sum goes to its first member's slot of `out`,
 // infinity to the others (k_group_sum adds a group's t slots).
 constexpr int TA_JOINT_MAX = 8;
-__global__ KB_OCC(HB_OCC_STRAUS) void k_ta_joint(const HmEntry* __restrict__ pts, const uint32_t* __restrict__ src,
-                                                    const TaDigits* __restrict__ dig, uint32_t n_groups, uint32_t t,
-                                                    uint32_t c, uint4* __restrict__ tab, G2JEntry* __restrict__ out) {
+// Three kernels over the same lanes, so that each holds only its own working set (one kernel with
+// both ladders and the table build spilled 2.9 KB per lane): k_ta_jtab builds the affine tables,
+// k_ta_jladder runs the shared NAF schedule, k_ta_jgeneral the per-member ladders; the last two
+// return at once on the waves that are not theirs (the uniformity test is repeated in each).
 #if defined(__HIP_DEVICE_COMPILE__)
-  __shared__ int8_t naf[TA_JOINT_MAX][4][66];
-  __shared__ int naf_top;
+struct JointLane {
+  uint32_t L, cnt, m0;
+  bool valid, uniform;
+  uint4* wt;
+};
+__device__ __forceinline__ JointLane joint_lane(const TaDigits* __restrict__ dig, uint32_t n_groups, uint32_t t,
+                                                uint32_t c, uint4* __restrict__ tab) {
+  JointLane j;
   const int lane = (int)(threadIdx.x & 63u);
   const uint32_t n_chunks = (t + c - 1) / c, n_lanes = n_groups * n_chunks;
-  const uint32_t L = blockIdx.x * 64 + (uint32_t)lane;
-  const bool valid = L < n_lanes;
-  const uint32_t Lc = valid ? L : n_lanes - 1;
+  j.L = blockIdx.x * 64 + (uint32_t)lane;
+  j.valid = j.L < n_lanes;
+  const uint32_t Lc = j.valid ? j.L : n_lanes - 1;
   const uint32_t q = Lc / n_groups, v = Lc % n_groups;
-  const uint32_t j0 = q * c, cnt = min(c, t - j0);
-  const uint32_t m0 = v * t + j0;
-  uint4* wt = tab + (size_t)blockIdx.x * (16 * c) * TA_TAB_QUADS * 64 + lane;
-  bool same = cnt == (uint32_t)__builtin_amdgcn_readfirstlane((int)cnt);
+  const uint32_t j0 = q * c;
+  j.cnt = min(c, t - j0);
+  j.m0 = v * t + j0;
+  j.wt = tab + (size_t)blockIdx.x * (16 * c) * TA_TAB_QUADS * 64 + lane;
+  bool same = j.cnt == (uint32_t)__builtin_amdgcn_readfirstlane((int)j.cnt);
   HB_NOUNROLL for (uint32_t k = 0; k < c; k++) {
-    const TaDigits d = dig[m0 + (k < cnt ? k : 0)];
+    const TaDigits d = dig[j.m0 + (k < j.cnt ? k : 0)];
     HB_UNROLL for (int i = 0; i < 4; i++) {
       const uint32_t lo = (uint32_t)d.a[i], hi = (uint32_t)(d.a[i] >> 32);
       same = same && lo == (uint32_t)__builtin_amdgcn_readfirstlane((int)lo) &&
              hi == (uint32_t)__builtin_amdgcn_readfirstlane((int)hi);
     }
   }
-  G2J R = jac_infinity<Fp2>();
-  if (__all(same)) {
-    if (lane == 0) {
-      int top = 0;
-      for (uint32_t k = 0; k < cnt; k++) {
-        const TaDigits d = dig[m0 + k];
-        for (int i = 0; i < 4; i++) top = max(top, naf4_digits(d.a[i], naf[k][i]));
-      }
-      naf_top = top;
+  j.uniform = __all(same);
+  return j;
+}
+__device__ __forceinline__ void joint_store(G2JEntry* __restrict__ out, const JointLane& j, const G2J& R) {
+  if (!j.valid) return;
+  out[j.m0] = {R.X, R.Y, R.Z};
+  const G2J z = jac_infinity<Fp2>();
+  for (uint32_t k = 1; k < j.cnt; k++) out[j.m0 + k] = {z.X, z.Y, z.Z};
+}
+#endif
+
+__global__ KB_OCC(HB_OCC_STRAUS) void k_ta_jtab(const HmEntry* __restrict__ pts, const uint32_t* __restrict__ src,
+                                                   const TaDigits* __restrict__ dig, uint32_t n_groups, uint32_t t,
+                                                   uint32_t c, uint4* __restrict__ tab) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const JointLane j = joint_lane(dig, n_groups, t, c, tab);
+  if (j.uniform) odd_tables_affine(j.wt, pts, src, j.m0, j.cnt);
+#endif
+}
+
+__global__ KB_OCC(HB_OCC_STRAUS) void k_ta_jladder(const TaDigits* __restrict__ dig, uint32_t n_groups, uint32_t t,
+                                                      uint32_t c, uint4* __restrict__ tab, G2JEntry* __restrict__ out) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __shared__ int8_t naf[TA_JOINT_MAX][4][66];
+  __shared__ int naf_top;
+  const JointLane j = joint_lane(dig, n_groups, t, c, tab);
+  if (!j.uniform) return;  // wave-uniform
+  if ((threadIdx.x & 63u) == 0) {
+    int top = 0;
+    for (uint32_t k = 0; k < j.cnt; k++) {
+      const TaDigits d = dig[j.m0 + k];
+      for (int i = 0; i < 4; i++) top = max(top, naf4_digits(d.a[i], naf[k][i]));
     }
-    __syncthreads();
-    odd_tables_affine(wt, pts, src, m0, cnt);
-    const int top = naf_top;
-    HB_NOUNROLL for (int i = top; i >= 0; i--) {
-      R = jac_dbl(R);
-      HB_NOUNROLL for (uint32_t k = 0; k < cnt; k++) {
-        HB_NOUNROLL for (int b = 0; b < 4; b++) {
-          const int dg = naf[k][b][i];
-          if (dg != 0) {  // wave-uniform
-            const int e = 16 * (int)k + 4 * b + ((dg < 0 ? -dg : dg) >> 1);
-            G2A T = {f2_load_q(wt, e, 0), f2_load_q(wt, e, 6), false};
-            if (dg < 0) T.y = f2_neg(T.y);
-            R = jac_add_aff(R, T);
-          }
+    naf_top = top;
+  }
+  __syncthreads();
+  G2J R = jac_infinity<Fp2>();
+  const int top = naf_top;
+  HB_NOUNROLL for (int i = top; i >= 0; i--) {
+    R = jac_dbl(R);
+    HB_NOUNROLL for (uint32_t k = 0; k < j.cnt; k++) {
+      HB_NOUNROLL for (int b = 0; b < 4; b++) {
+        const int dg = naf[k][b][i];
+        if (dg != 0) {  // wave-uniform
+          const int e = 16 * (int)k + 4 * b + ((dg < 0 ? -dg : dg) >> 1);
+          G2A T = {f2_load_q(j.wt, e, 0), f2_load_q(j.wt, e, 6), false};
+          if (dg < 0) T.y = f2_neg(T.y);
+          R = jac_add_aff(R, T);
         }
       }
     }
-  } else {
-    HB_NOUNROLL for (uint32_t k = 0; k < cnt; k++) {
-      const HmEntry e = pts[src ? src[m0 + k] : m0 + k];
-      R = jac_add(R, member_general(wt, 0, e, dig[m0 + k]));
-    }
   }
-  if (valid) {
-    out[m0] = {R.X, R.Y, R.Z};
-    const G2J z = jac_infinity<Fp2>();
-    for (uint32_t k = 1; k < cnt; k++) out[m0 + k] = {z.X, z.Y, z.Z};
+  joint_store(out, j, R);
+#endif
+}
+
+__global__ KB_OCC(HB_OCC_STRAUS) void k_ta_jgeneral(const HmEntry* __restrict__ pts, const uint32_t* __restrict__ src,
+                                                       const TaDigits* __restrict__ dig, uint32_t n_groups, uint32_t t,
+                                                       uint32_t c, uint4* __restrict__ tab, G2JEntry* __restrict__ out) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const JointLane j = joint_lane(dig, n_groups, t, c, tab);
+  if (j.uniform) return;  // wave-uniform
+  G2J R = jac_infinity<Fp2>();
+  HB_NOUNROLL for (uint32_t k = 0; k < j.cnt; k++) {
+    const HmEntry e = pts[src ? src[j.m0 + k] : j.m0 + k];
+    R = jac_add(R, member_general(j.wt, 0, e, dig[j.m0 + k]));
   }
+  joint_store(out, j, R);
 #endif
 }
 
@@ -550,8 +588,10 @@ void launch_ta_joint(const HmEntry* pts, const uint32_t* src, const TaDigits* di
                      uint32_t c, void* tab, G2JEntry* out, hipStream_t s) {
   if (!n_groups || !t || !c || c > (uint32_t)TA_JOINT_MAX) return;
   const size_t lanes = (size_t)n_groups * ((t + c - 1) / c);
-  hipLaunchKernelGGL(k_ta_joint, dim3(blocks_of(lanes, 64)), dim3(64), 0, s, pts, src, dig, n_groups, t, c,
-                     (uint4*)tab, out);
+  const dim3 grid(blocks_of(lanes, 64));
+  hipLaunchKernelGGL(k_ta_jtab, grid, dim3(64), 0, s, pts, src, dig, n_groups, t, c, (uint4*)tab);
+  hipLaunchKernelGGL(k_ta_jladder, grid, dim3(64), 0, s, dig, n_groups, t, c, (uint4*)tab, out);
+  hipLaunchKernelGGL(k_ta_jgeneral, grid, dim3(64), 0, s, pts, src, dig, n_groups, t, c, (uint4*)tab, out);
 }
 
 void launch_ta_table(const HmEntry* pts, const uint32_t* src, uint32_t n_partials, void* tab, hipStream_t s) {
