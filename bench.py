@@ -500,7 +500,7 @@ def main(argv=None):
     ap.add_argument("--key-tables", type=int, default=1,
                     help="also time the slot with decompressed-key tables built once (steady state)")
     ap.add_argument("--host-api", action="store_true", help="also time the host-buffer (PCIe-inclusive) entry points")
-    ap.add_argument("--inflight", type=int, default=2,
+    ap.add_argument("--inflight", type=int, default=3,
                     help="slots in flight (each on its own stream and outputs); 1 = one slot at a time")
     ap.add_argument("--mode", default="slot", choices=["slot", "staged"],
                     help="slot: one hbls_slot_device call per step (stages overlap); staged: stage by stage")

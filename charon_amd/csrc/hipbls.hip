@@ -287,7 +287,7 @@ struct Ws {
 // host-call staging buffers (inputs and outputs of the host-buffer entry points)
 enum IoId { I_PK, I_SIG, I_MSG, I_OFF, I_LEN, I_MIDX, I_HM, I_STAT, I_IDX, I_GOFF, I_OUT, I_SK, I_VGOFF, I_KC, I_COUNT };
 
-constexpr int N_WS = 2;
+constexpr int N_WS = 3;
 
 struct Timed {
   const char* name;

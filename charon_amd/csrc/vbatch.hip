@@ -147,12 +147,12 @@ __device__ __forceinline__ bool item_usable(const G1AEntry& p, uint8_t pst, cons
 // items (undecodable, infinity) contribute the point at infinity, items of singleton groups keep
 // r = 1 unless `always` (the folded aggregates).  coef (nullable): the item's (a, b), (0, 0) when
 // unusable; sides 1 computes P' only and writes coef, sides 2 computes S' only from coef.
+template <int sides>
 __global__ KB_OCC(HB_OCC_RLC) void k_rlc(const G1AEntry* __restrict__ pk, const uint8_t* __restrict__ pk_st,
                          const HmEntry* __restrict__ sig, const uint8_t* __restrict__ sig_st,
                          const uint32_t* __restrict__ item_grp, const uint32_t* __restrict__ grp_off, int always,
                          uint32_t n, uint32_t key_base, RlcKey key, G1JEntry* __restrict__ pout,
-                         G2JEntry* __restrict__ sout, uint2* __restrict__ coef, int sides,
-                         const uint8_t* __restrict__ guard) {
+                         G2JEntry* __restrict__ sout, uint2* __restrict__ coef, const uint8_t* __restrict__ guard) {
 #if defined(__HIP_DEVICE_COMPILE__)
   if (guard && *guard == 0) return;
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -266,6 +266,9 @@ __device__ __forceinline__ Jac<F> msm_ladder(const Jac<F>* __restrict__ tab, con
   return R;
 }
 
+// SIDES as RlcMsmArgs::sides, a template argument so that the public-key-only launch of the
+// slot-wide check does not allocate registers for the G2 ladder
+template <int SIDES>
 __global__ KB_OCC(HB_OCC_RLC) void k_rlc_msm(RlcMsmArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
   if (a.guard && *a.guard == 0) return;
@@ -277,19 +280,19 @@ __global__ KB_OCC(HB_OCC_RLC) void k_rlc_msm(RlcMsmArgs a) {
     const uint32_t i = first;
     const bool usable = !a.pk_st[i] && !a.sig_st[i] && !a.pk[i].inf && !a.sig[i].inf;
     const G1AEntry pe = a.pk[i];
-    if (a.sides & 1) {
+    if (SIDES & 1) {
       const G1J rp = usable ? jac_from_aff(G1A{pe.x, pe.y, false}) : jac_infinity<Fp>();
       a.pout[i] = {rp.X, rp.Y, rp.Z};
       a.coef[i] = make_uint2(usable ? 1u : 0u, 0u);
     }
-    if (a.sides & 2) {
+    if (SIDES & 2) {
       const HmEntry se = a.sig[i];
       const G2J rs = usable ? jac_from_aff(G2A{se.x, se.y, false}) : jac_infinity<Fp2>();
       a.sout[i] = {rs.X, rs.Y, rs.Z};
     }
     return;
   }
-  if (a.sides & 1) {
+  if (SIDES & 1) {
     // coefficients and the G1 ladder points of the chunk's items
     Fp acc = fp_one();
     HB_NOUNROLL for (uint32_t k = 0; k < cnt; k++) {
@@ -328,7 +331,7 @@ __global__ KB_OCC(HB_OCC_RLC) void k_rlc_msm(RlcMsmArgs a) {
     const G1J zi = jac_infinity<Fp>();
     for (uint32_t k = 1; k < cnt; k++) a.pout[first + k] = {zi.X, zi.Y, zi.Z};
   }
-  if (!(a.sides & 2)) return;
+  if (!(SIDES & 2)) return;
   // the G2 ladder points, then the G2 ladder (coefficients from the workspace)
   HB_NOUNROLL for (uint32_t k = 0; k < cnt; k++) {
     const uint32_t i = first + k;
@@ -359,7 +362,11 @@ void launch_scan(const uint32_t* cnt, uint32_t n, uint32_t* off, hipStream_t s) 
   hipLaunchKernelGGL(k_plan_scan, dim3(1), dim3(1024), 0, s, cnt, n, off);
 }
 void launch_rlc_msm(const RlcMsmArgs& a, uint32_t max_chunks, hipStream_t s) {
-  if (max_chunks) hipLaunchKernelGGL(k_rlc_msm, dim3((max_chunks + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, a);
+  if (!max_chunks) return;
+  const dim3 grid((max_chunks + BLOCK - 1) / BLOCK);
+  if (a.sides == 1) hipLaunchKernelGGL(k_rlc_msm<1>, grid, dim3(BLOCK), 0, s, a);
+  else if (a.sides == 2) hipLaunchKernelGGL(k_rlc_msm<2>, grid, dim3(BLOCK), 0, s, a);
+  else hipLaunchKernelGGL(k_rlc_msm<3>, grid, dim3(BLOCK), 0, s, a);
 }
 
 // One lane per item (then per folded aggregate): final status, or a place in the fallback list.
@@ -424,9 +431,16 @@ void launch_rlc(const G1AEntry* pk, const uint8_t* pk_st, const HmEntry* sig, co
                 const uint32_t* item_grp, const uint32_t* grp_off, int always, uint32_t n, uint32_t key_base,
                 const RlcKey& key, G1JEntry* pout, G2JEntry* sout, hipStream_t s, uint2* coef, int sides,
                 const uint8_t* guard) {
-  if (n)
-    hipLaunchKernelGGL(k_rlc, dim3(blocks_for(n)), dim3(BLOCK), 0, s, pk, pk_st, sig, sig_st, item_grp, grp_off,
-                       always, n, key_base, key, pout, sout, coef, sides, guard);
+  if (!n) return;
+  if (sides == 1)
+    hipLaunchKernelGGL(k_rlc<1>, dim3(blocks_for(n)), dim3(BLOCK), 0, s, pk, pk_st, sig, sig_st, item_grp, grp_off,
+                       always, n, key_base, key, pout, sout, coef, guard);
+  else if (sides == 2)
+    hipLaunchKernelGGL(k_rlc<2>, dim3(blocks_for(n)), dim3(BLOCK), 0, s, pk, pk_st, sig, sig_st, item_grp, grp_off,
+                       always, n, key_base, key, pout, sout, coef, guard);
+  else
+    hipLaunchKernelGGL(k_rlc<3>, dim3(blocks_for(n)), dim3(BLOCK), 0, s, pk, pk_st, sig, sig_st, item_grp, grp_off,
+                       always, n, key_base, key, pout, sout, coef, guard);
 }
 void launch_scatter(const ScatterArgs& a, hipStream_t s) {
   const size_t tot = (size_t)a.n + a.n_agg;
