@@ -187,6 +187,81 @@ HDNI G2J iso3_map(const Fp2& x, const Fp2& y) {
   return r;
 }
 
+// A polynomial (coefficients c[0..n-1]) homogenised at x = X / Zh: sum c_i X^i Zh^(n-1-i), with
+// zp[k] = Zh^k.
+HDNI Fp2 f2_poly_eval_h(const uint32_t (*c)[2][12], int n, const Fp2& X, const Fp2* zp) {
+  Fp2 acc = f2_from_const(c[n - 1]);
+  for (int i = n - 2; i >= 0; i--) acc = f2_add(f2_mul(acc, X), f2_mul(f2_from_const(c[i]), zp[n - 1 - i]));
+  return acc;
+}
+
+// sswu_map followed by iso3_map without an inversion: two Fp exponentiations instead of three.
+//   x1 = xn / xd (xn = -B (tv1 + 1), xd = A tv1; B, Z A if tv1 = 0),  g(x1) = gn / xd^3 = a / n with
+//   a = gn conj(xd^3), n = N(xd^3) in Fp.  The norm method of f2_sqrt on a / n:
+//     S = N(a)^((p+1)/4)                      [sqrt(N(g(x1))) n, or sqrt(-N(g(x1))) n]
+//     c = cn / n,  cn = (a0 + S) / 2
+//     T = (cn n^3)^((p-3)/4),  so c^((p-3)/4) = T n^2,  y0 = c^((p+1)/4) = cn T n,  h = a1 T n / 2
+//   (g(x2) = (Z u^2)^3 g(x1) shares the denominator n).  The isogeny is evaluated homogeneously at
+//   x = X / Zh; with D1 = XD Zh, D2 = YD: x' = XN / D1, y' = y YN / D2, Jacobian (XN D1 D2^2,
+//   y YN D1^3 D2^2, D1 D2).  Same point as iso3_map(sswu_map(u)).
+HDNI G2J sswu_iso_map(const Fp2& u) {
+  const Fp2 A = f2_from_const(SSWU_A), B = f2_from_const(SSWU_B), Z = f2_from_const(SSWU_Z);
+  const Fp2 zu2 = f2_mul(Z, f2_sqr(u));
+  const Fp2 tv1 = f2_add(f2_sqr(zu2), zu2);
+  const bool tv1_zero = f2_is_zero(tv1);
+  Fp2 xn = f2_neg(f2_mul(B, f2_add(tv1, f2_one())));
+  Fp2 xd = f2_mul(A, tv1);
+  if (tv1_zero) {
+    xn = B;
+    xd = f2_mul(Z, A);
+  }
+  const Fp2 xd2 = f2_sqr(xd);
+  const Fp2 gd = f2_mul(xd2, xd);
+  const Fp2 gn = f2_add(f2_mul(f2_add(f2_sqr(xn), f2_mul(A, xd2)), xn), f2_mul(B, gd));
+  const Fp2 a = f2_mul(gn, f2_conj(gd));
+  const Fp n = fp_add(fp_sqr(gd.c0), fp_sqr(gd.c1));
+  const Fp na = fp_add(fp_sqr(a.c0), fp_sqr(a.c1));
+  const Fp s1 = fp_pow_win(na, WIN_SQRT, WIN_SQRT_N);
+  const bool sq1 = fp_eq(fp_sqr(s1), na);
+  const Fp nu = fp_add(fp_sqr(u.c0), fp_sqr(u.c1));
+  const Fp s2 = fp_mul(fp_mul(s1, fp_mul(fp_sqr(nu), nu)), fp_from_const(SSWU_SQRT_MNZ3));
+  const Fp2 zu2_3 = f2_mul(f2_sqr(zu2), zu2);
+  const Fp2 as = sq1 ? a : f2_mul(zu2_3, a);
+  const Fp S = sq1 ? s1 : s2;
+  const Fp2 X = sq1 ? xn : f2_mul(zu2, xn);
+  const Fp inv2 = fp_from_const(FP_INV2);
+  Fp cn = fp_mul(fp_add(as.c0, S), inv2);
+  if (fp_is_zero(cn)) cn = fp_mul(fp_sub(as.c0, S), inv2);
+  const Fp T = fp_pow_win(fp_mul(cn, fp_mul(fp_sqr(n), n)), WIN_P_M3_4, WIN_P_M3_4_N);
+  const Fp Tn = fp_mul(T, n);
+  const Fp y0 = fp_mul(cn, Tn);
+  const Fp h = fp_mul(fp_mul(as.c1, Tn), inv2);
+  Fp2 y;
+  if (fp_eq(fp_mul(fp_sqr(y0), n), cn)) {
+    y = {y0, h};
+  } else {
+    y = {fp_neg(h), y0};
+  }
+  if (f2_sgn0(u) != f2_sgn0(y)) y = f2_neg(y);
+  Fp2 zp[4];
+  zp[0] = f2_one();
+  zp[1] = xd;
+  zp[2] = xd2;
+  zp[3] = gd;
+  const Fp2 XN = f2_poly_eval_h(ISO_XNUM, 4, X, zp);
+  const Fp2 XD = f2_poly_eval_h(ISO_XDEN, 3, X, zp);
+  const Fp2 YN = f2_poly_eval_h(ISO_YNUM, 4, X, zp);
+  const Fp2 YD = f2_poly_eval_h(ISO_YDEN, 4, X, zp);
+  const Fp2 D1 = f2_mul(XD, xd), D2 = YD;
+  const Fp2 D22 = f2_sqr(D2);
+  const Fp2 D1D22 = f2_mul(D1, D22);
+  G2J r;
+  r.Z = f2_mul(D1, D2);
+  r.X = f2_mul(XN, D1D22);
+  r.Y = f2_mul(f2_mul(y, YN), f2_mul(D1D22, f2_sqr(D1)));
+  return r;
+}
+
 // h_eff * P via  [x^2 - x - 1]P + [x - 1]psi(P) + psi^2(2P)  (RFC 9380 G.3), x < 0.
 HDNI G2J g2_clear_cofactor(const G2J& P) {
   G2J t1 = jac_neg(jac_mul_by_xabs(P));  // [x]P
@@ -203,11 +278,8 @@ HDNI G2J g2_clear_cofactor(const G2J& P) {
 HDNI G2J hash_to_g2(const uint8_t* msg, uint32_t len) {
   Fp2 u0, u1;
   hash_to_field_fp2(u0, u1, msg, len);
-  Fp2 x, y;
-  sswu_map(x, y, u0);
-  G2J q0 = iso3_map(x, y);
-  sswu_map(x, y, u1);
-  G2J q1 = iso3_map(x, y);
+  const G2J q0 = sswu_iso_map(u0);
+  const G2J q1 = sswu_iso_map(u1);
   return g2_clear_cofactor(jac_add(q0, q1));
 }
 

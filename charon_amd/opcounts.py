@@ -30,8 +30,9 @@ N_LINES = 68      # Miller-loop lines (63 doublings + 5 additions)
 N_SQR = 62        # Fp12 squarings of the Miller loop
 LINE_PRODUCTS = 2 * N_LINES  # two pairs per check
 
-# expand_message_xmd -> 2 SSWU (straight-line, 3 exponentiations each) -> 3-isogeny -> cofactor -> affine
-HASH_TO_G2 = 6188
+# expand_message_xmd -> 2 inversion-free SSWU + 3-isogeny maps (2 exponentiations each; 6188 with
+# the inversion, 3 exponentiations) -> cofactor -> affine
+HASH_TO_G2 = 5374
 
 
 def _pair3_exec_per_lane(b=BLOCKS):
