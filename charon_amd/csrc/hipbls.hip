@@ -242,6 +242,11 @@ constexpr size_t TA_JOINT_LANES = 98304;
 // HBLS_FE_BATCH: verifications of at least this many groups check FE_BATCH groups per final
 // exponentiation (vgroup.hip; 0 = one final exponentiation per group)
 std::atomic<size_t> g_fe_batch_min{2 * FE_BATCH};
+// HBLS_FALLBACK_BATCH: groups per final exponentiation of the per-batch check behind a FAILED
+// slot-wide check (a power of two <= FE_BATCH).  A failed slot has at least one bad item and often
+// many (an attack): smaller batches pass more often (group testing; C5, 1 % corrupted partials:
+// 64-group batches nearly all fail and every group then pays its own exponentiation).
+size_t g_fb_batch = 8;
 // HBLS_SLOT_MSM: batched verifications of at least this many items (partials + folded aggregates,
 // one chunk of groups) check every group at once -- the signature side as one multi-scalar
 // multiplication (msm.hip), one final exponentiation for the call -- and fall back to the
@@ -449,6 +454,11 @@ int init_mask(uint32_t mask) {
   g_ta_joint = std::min<size_t>(8, env_size("HBLS_TA_JOINT", g_ta_joint.load()));
   g_fe_batch_min = env_size("HBLS_FE_BATCH", g_fe_batch_min.load());
   g_slot_msm_min = env_size("HBLS_SLOT_MSM", g_slot_msm_min.load());
+  {
+    size_t fb = std::min<size_t>(FE_BATCH, std::max<size_t>(2, env_size("HBLS_FALLBACK_BATCH", g_fb_batch)));
+    while (fb & (fb - 1)) fb &= fb - 1;  // a power of two
+    g_fb_batch = fb;
+  }
   g_mml_pairs = std::min<size_t>(64, std::max<size_t>(1, env_size("HBLS_MML_PAIRS", g_mml_pairs)));
   std::vector<Dev*> devs;
   for (int k = 0; k < 32; k++)
@@ -628,7 +638,7 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
   // fixed coefficients in one combination, errors of two items could cancel.
   const size_t fe_min = g_fe_batch_min.load();
   const bool bfe = fe_min && n_groups >= fe_min;
-  const size_t nbcap = (gcap + FE_BATCH - 1) / FE_BATCH;
+  const size_t nbcap = (gcap + 1) / 2;  // batches of >= 2 groups (FE_BATCH, or g_fb_batch behind the slot-wide check)
   Fp4Entry* fbuf = nullptr;
   G2JEntry *gS = nullptr, *bS = nullptr;
   LineEntry* blines = nullptr;
@@ -799,7 +809,9 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
     ga.gst = gst;
     ga.glines = glines;
     if (bfe) {
-      const uint32_t nb = (ng + FE_BATCH - 1) / FE_BATCH;
+      const uint32_t fb = smsm ? (uint32_t)g_fb_batch : FE_BATCH;
+      const uint32_t nb = (ng + fb - 1) / fb;
+      ga.fe_batch = fb;
       Pair3Args pm{};
       pm.pk = gP;
       pm.pk_st = gst;
@@ -902,14 +914,14 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
       pf.stride = nb;
       pf.n = nb;
       pf.f_in = fbuf;
-      pf.f_range = FE_BATCH;
+      pf.f_range = fb;
       pf.f_n = ng;
       pf.status = bver;
       pf.guard = guard;
       TIMED(d, "k_pair3_fin", s, launch_pair3_fin(pf, s));
       // groups of a failing batch: checked one by one (their stored loop, their own S lines)
       HCHK(hipMemsetAsync(gcount, 0, sizeof(uint32_t), s));
-      TIMED(d, "k_batch_verdict", s, launch_batch_verdict(gst, bver, ng, gver + g0, glist, gcount, s, guard));
+      TIMED(d, "k_batch_verdict", s, launch_batch_verdict(gst, bver, ng, gver + g0, glist, gcount, s, guard, fb));
       TIMED(d, "k_slines", s, launch_slines(gS, glist, gcount, ng, glines, ng, nullptr, s));
       Pair3Args pg{};
       pg.sig_lines = glines;

@@ -221,9 +221,10 @@ struct GroupPrepArgs {
   uint8_t* gst;      // [ng]
   LineEntry* glines; // [N_LINES][ng]
   // batched final exponentiation (non-null): no lines; the group's S (Jacobian, infinity unless
-  // READY) and the sum over each batch of FE_BATCH consecutive groups
+  // READY) and the sum over each batch of fe_batch consecutive groups
   G2JEntry* gS;      // [ng]
-  G2JEntry* bS;      // [ceil(ng / FE_BATCH)]
+  G2JEntry* bS;      // [ceil(ng / fe_batch)]
+  uint32_t fe_batch; // groups per batch (a power of two <= FE_BATCH; 0 = FE_BATCH)
   int p_only;        // slot-wide check (msm.hip): the public-key side and the state only, no S
   const uint8_t* guard;  // nullable: nothing unless *guard != 0
 };
@@ -236,7 +237,7 @@ void launch_slines(const G2JEntry* pts, const uint32_t* list, const uint32_t* co
 // group verdicts from the batch verdicts: not READY -> 1, READY in a passing batch -> 0, else the
 // group joins list (its verdict comes from the per-group check)
 void launch_batch_verdict(const uint8_t* gst, const uint8_t* bver, uint32_t ng, uint8_t* gver, uint32_t* list,
-                          uint32_t* count, hipStream_t s, const uint8_t* guard = nullptr);
+                          uint32_t* count, hipStream_t s, const uint8_t* guard = nullptr, uint32_t fe_batch = FE_BATCH);
 // slot-wide check passed (*sfail == 0): gver[g] = (gst[g] != READY); else nothing (the per-group
 // path decides)
 void launch_slot_verdict(const uint8_t* gst, const uint8_t* sfail, uint32_t ng, uint8_t* gver, hipStream_t s);

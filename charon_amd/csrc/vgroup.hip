@@ -109,7 +109,8 @@ __global__ KB_OCC(HB_OCC_PREP) void k_group_prep(GroupPrepArgs a) {
 }
 
 // Batched final exponentiation: one lane per group as above but no lines; the group's S is kept
-// (gS) and the 64 groups of the wave -- one batch -- sum their S into bS (butterfly over the wave).
+// (gS) and each batch of fe_batch consecutive groups of the wave sums its S into bS (butterfly
+// over the batch's lanes).
 __global__ KB_OCC(HB_OCC_PREP) void k_group_prep_b(GroupPrepArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
   if (a.guard && *a.guard == 0) return;
@@ -128,12 +129,13 @@ __global__ KB_OCC(HB_OCC_PREP) void k_group_prep_b(GroupPrepArgs a) {
     a.gS[lg] = {S.X, S.Y, S.Z};
   }
   const int lane = (int)(threadIdx.x & 63u);
-  HB_NOUNROLL for (int off = 32; off; off >>= 1) {
+  const int fb = a.fe_batch ? (int)a.fe_batch : (int)FE_BATCH;
+  HB_NOUNROLL for (int off = fb >> 1; off; off >>= 1) {
     const int addr = (lane ^ off) << 2;
     const G2J T = {xch(S.X, addr), xch(S.Y, addr), xch(S.Z, addr)};
     S = jac_add(S, T);
   }
-  if (lane == 0) a.bS[blockIdx.x] = {S.X, S.Y, S.Z};
+  if ((lane & (fb - 1)) == 0 && lg < a.ng) a.bS[lg / (uint32_t)fb] = {S.X, S.Y, S.Z};
 #endif
 }
 
@@ -172,12 +174,12 @@ __global__ KB_OCC(HB_OCC_LINES) void k_slines(const G2JEntry* __restrict__ pts, 
 
 __global__ __launch_bounds__(64) void k_batch_verdict(const uint8_t* __restrict__ gst, const uint8_t* __restrict__ bver, uint32_t ng,
                                    uint8_t* __restrict__ gver, uint32_t* __restrict__ list,
-                                   uint32_t* __restrict__ count, const uint8_t* __restrict__ guard) {
+                                   uint32_t* __restrict__ count, const uint8_t* __restrict__ guard, uint32_t fb) {
   if (guard && *guard == 0) return;
   const uint32_t lg = blockIdx.x * blockDim.x + threadIdx.x;
   if (lg >= ng) return;
   if (gst[lg] != G_READY) gver[lg] = 1;
-  else if (bver[lg / FE_BATCH] == 0) gver[lg] = 0;
+  else if (bver[lg / fb] == 0) gver[lg] = 0;
   else list[atomicAdd(count, 1u)] = lg;
 }
 
@@ -191,7 +193,7 @@ __global__ __launch_bounds__(64) void k_slot_verdict(const uint8_t* __restrict__
 void launch_group_prep(const GroupPrepArgs& a, hipStream_t s) {
   if (!a.ng) return;
   if (a.p_only) hipLaunchKernelGGL(k_group_prep_p, dim3((a.ng + 63) / 64), dim3(64), 0, s, a);
-  else if (a.gS) hipLaunchKernelGGL(k_group_prep_b, dim3((a.ng + FE_BATCH - 1) / FE_BATCH), dim3(FE_BATCH), 0, s, a);
+  else if (a.gS) hipLaunchKernelGGL(k_group_prep_b, dim3((a.ng + 63) / 64), dim3(64), 0, s, a);
   else hipLaunchKernelGGL(k_group_prep, dim3((a.ng + 63) / 64), dim3(64), 0, s, a);
 }
 void launch_slines(const G2JEntry* pts, const uint32_t* list, const uint32_t* count, uint32_t n, LineEntry* lines,
@@ -200,9 +202,10 @@ void launch_slines(const G2JEntry* pts, const uint32_t* list, const uint32_t* co
     hipLaunchKernelGGL(k_slines, dim3((n + 63) / 64), dim3(64), 0, s, pts, list, count, n, lines, stride, bad, guard);
 }
 void launch_batch_verdict(const uint8_t* gst, const uint8_t* bver, uint32_t ng, uint8_t* gver, uint32_t* list,
-                          uint32_t* count, hipStream_t s, const uint8_t* guard) {
+                          uint32_t* count, hipStream_t s, const uint8_t* guard, uint32_t fe_batch) {
   if (ng)
-    hipLaunchKernelGGL(k_batch_verdict, dim3((ng + 63) / 64), dim3(64), 0, s, gst, bver, ng, gver, list, count, guard);
+    hipLaunchKernelGGL(k_batch_verdict, dim3((ng + 63) / 64), dim3(64), 0, s, gst, bver, ng, gver, list, count, guard,
+                       fe_batch ? fe_batch : FE_BATCH);
 }
 void launch_slot_verdict(const uint8_t* gst, const uint8_t* sfail, uint32_t ng, uint8_t* gver, hipStream_t s) {
   if (ng) hipLaunchKernelGGL(k_slot_verdict, dim3((ng + 63) / 64), dim3(64), 0, s, gst, sfail, ng, gver);
