@@ -182,6 +182,17 @@ HDNI Jac<F> jac_mul_by_xabs(const Jac<F>& p) {
   return r;
 }
 
+// [|x|] q for q affine (not infinity): the five additions are mixed ones
+template <class F>
+HDNI Jac<F> jac_mul_by_xabs_aff(const Aff<F>& q) {
+  Jac<F> r = jac_from_aff(q);
+  HB_NOUNROLL for (int i = 62; i >= 0; i--) {
+    r = jac_dbl(r);
+    if ((HB_X_ABS >> i) & 1) r = jac_add_aff(r, q);
+  }
+  return r;
+}
+
 // [k] q for q affine, k given as little-endian 32-bit words (nbits significant bits)
 template <class F>
 HDNI Jac<F> jac_mul_aff(const Aff<F>& q, const uint32_t* k, int nbits) {
@@ -212,15 +223,14 @@ HDNI G2J g2_psi2(const G2J& p) {
 HDNI bool g2_in_subgroup(const G2A& q) {
   if (q.inf) return true;
   G2J Q = jac_from_aff(q);
-  G2J xq = jac_neg(jac_mul_by_xabs(Q));
+  G2J xq = jac_neg(jac_mul_by_xabs_aff(q));
   return jac_eq(g2_psi(Q), xq);
 }
 
 // P in G1  <=>  phi(P) == [-x^2] P with phi(x, y) = (beta x, y).
 HDNI bool g1_in_subgroup(const G1A& p) {
   if (p.inf) return true;
-  G1J P = jac_from_aff(p);
-  G1J t = jac_mul_by_xabs(jac_mul_by_xabs(P));  // [x^2] P
+  G1J t = jac_mul_by_xabs(jac_mul_by_xabs_aff(p));  // [x^2] P
   G1J phi = jac_from_aff(G1A{fp_mul(p.x, fp_from_const(G1_BETA)), p.y, false});
   return jac_eq(phi, jac_neg(t));
 }

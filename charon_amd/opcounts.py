@@ -23,7 +23,7 @@ PEAK_MAD_TOPS_NOMINAL = 39.3
 BLOCK_NAMES = ("f12_sqr", "f12_mul_line", "final_exp", "fp_inv", "g1_dec", "g2_dec", "rlc_g1", "rlc_g2",
                "jac_add_g1", "jac_add_g2", "to_aff_g1", "to_aff_g2", "lines_eval", "lines_uneval", "jac_dbl_g2",
                "jac_add_aff_g2", "cyclo_sqr", "f12_mul", "g2_compress", "jac_add_aff_g1", "jac_dbl_g1")
-BLOCKS = dict(zip(BLOCK_NAMES, (36, 39, 8141, 463, 1517, 2192, 732, 1880, 16, 43, 467, 478, 1843, 1571, 16, 29, 18,
+BLOCKS = dict(zip(BLOCK_NAMES, (36, 39, 8141, 463, 1492, 2122, 732, 1880, 16, 43, 467, 478, 1843, 1571, 16, 29, 18,
                                 54, 4, 11, 7)))
 
 N_LINES = 68      # Miller-loop lines (63 doublings + 5 additions)
