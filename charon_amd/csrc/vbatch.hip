@@ -332,18 +332,35 @@ __global__ KB_OCC(HB_OCC_RLC) void k_rlc_msm(RlcMsmArgs a) {
     for (uint32_t k = 1; k < cnt; k++) a.pout[first + k] = {zi.X, zi.Y, zi.Z};
   }
   if (!(SIDES & 2)) return;
-  // the G2 ladder points, then the G2 ladder (coefficients from the workspace)
+  // the G2 ladder points (S + (-psi^2 S) affine like the G1 side: one Fp2 inversion per chunk),
+  // then the G2 ladder (coefficients from the workspace)
+  Fp2 acc2 = f2_one();
   HB_NOUNROLL for (uint32_t k = 0; k < cnt; k++) {
     const uint32_t i = first + k;
     const HmEntry se = a.sig[i];
     const G2A S = {se.x, se.y, false};
     const G2A S2 = {f2_mul(S.x, f2_from_const(PSI2_CX)), f2_neg(f2_mul(S.y, f2_from_const(PSI2_CY))), false};
-    const G2J J1 = jac_from_aff(S), J2 = jac_from_aff(S2), J3 = jac_add_aff(J1, S2);
-    a.t2[3ull * i] = J1;
+    const G2J J1 = jac_from_aff(S), J2 = jac_from_aff(S2);
+    G2J J3 = jac_add_aff(J1, S2);
+    if (f2_is_zero(J3.Z)) J3.Z = f2_one();  // an unusable item's placeholder: keeps the product invertible
+    a.t2[3ull * i] = {J1.X, J1.Y, acc2};     // the running product of the Z before this item
     a.t2[3ull * i + 1] = J2;
     a.t2[3ull * i + 2] = J3;
+    acc2 = f2_mul(acc2, J3.Z);
   }
-  const G2J rs = msm_ladder<Fp2>(a.t2, a.coef, first, cnt);
+  Fp2 inv2 = f2_inv(acc2);
+  HB_NOUNROLL for (int k = (int)cnt - 1; k >= 0; k--) {
+    const uint32_t i = first + (uint32_t)k;
+    const G2J J3 = a.t2[3ull * i + 2];
+    G2J J1 = a.t2[3ull * i];
+    const Fp2 zi = f2_mul(inv2, J1.Z);
+    inv2 = f2_mul(inv2, J3.Z);
+    const Fp2 zi2 = f2_sqr(zi);
+    J1.Z = f2_one();
+    a.t2[3ull * i] = J1;
+    a.t2[3ull * i + 2] = {f2_mul(J3.X, zi2), f2_mul(J3.Y, f2_mul(zi2, zi)), f2_one()};
+  }
+  const G2J rs = msm_ladder<Fp2, true>(a.t2, a.coef, first, cnt);
   a.sout[first] = {rs.X, rs.Y, rs.Z};
   const G2J zs = jac_infinity<Fp2>();
   for (uint32_t k = 1; k < cnt; k++) a.sout[first + k] = {zs.X, zs.Y, zs.Z};

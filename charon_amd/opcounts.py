@@ -91,7 +91,10 @@ def rlc_msm(b=BLOCKS, chunk=1, sides=3):
     # G1: P + phi(P) made affine with one inversion per chunk (3 products into and out of the
     # running product, 1/Z^2, 1/Z^3, x, y), then 32 mixed additions
     g1 = 1 + b["jac_add_aff_g1"] + 3 + 4 + b["fp_inv"] / chunk + 32 * b["jac_add_aff_g1"] + 32 * b["jac_dbl_g1"] / chunk
-    g2 = 6 + b["jac_add_aff_g2"] + 32 * b["jac_add_g2"] + 32 * b["jac_dbl_g2"] / chunk
+    # G2 likewise: S + (-psi^2 S) affine with one Fp2 inversion per chunk (products into and out of
+    # the running product 3 x 3, then 1/Z^2, 1/Z^3, x, y: 2 + 3 x 3), 32 mixed additions
+    g2 = 6 + b["jac_add_aff_g2"] + 9 + 11 + (b["fp_inv"] + 6) / chunk + 32 * b["jac_add_aff_g2"] + \
+        32 * b["jac_dbl_g2"] / chunk
     return g1 + (g2 if sides & 2 else 0)
 
 
