@@ -13,6 +13,7 @@
   racing a host-buffer call on another stream (the workspaces are ordered by events).
 """
 import ctypes
+import os
 import hashlib
 import random
 import threading
@@ -586,3 +587,56 @@ def test_hash_paths_agree(L):
     a = hm_a.cpu().numpy().reshape(n, E)[:k, :208]
     b = hm_b.cpu().numpy().reshape(k, E)[:, :208]
     assert np.array_equal(a, b)
+
+
+def test_slot_c3_full_size(L):
+    """BASELINE configs[2] at full size through the benchmarked entry point: 100 000 validators of
+    a 10-operator threshold-7 cluster over distinct messages (1 M partials, the slot-wide check,
+    the joint aggregation ladders).  Every partial and every aggregate verifies, every aggregate
+    is byte-identical to the root-key signature, and the oracle agrees on a sample: three partial
+    verdicts and one aggregate recomputed from its seven members."""
+    import sys
+    import torch
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from oracle import bls12381 as B
+    wl = bench.WORKLOADS["c3"]
+    V = wl["validators"]
+    d = bench.setup_inputs(L, wl, V, 0)
+    n, t, NP, M = d["n"], d["t"], d["NP"], d["M"]
+    dev = torch.device("cuda", 0)
+
+    def up(a):
+        return torch.from_numpy(a).to(dev)
+
+    g = {k: up(a) for k, a in dict(msgs=d["msgs"], moff=d["moff"].view(np.int64), mlen=d["mlen"].view(np.int32),
+                                   pks=d["pks"], sigs=d["sigs"], midx=d["midx"].view(np.int32),
+                                   vgoff=d["vgrp_off"].view(np.int32), tsrc=d["ta_src"].view(np.int32),
+                                   tidx=d["ta_idx"], goff=d["grp_off"].view(np.int32), dvpk=d["dv_pks"]).items()}
+    hm = torch.zeros(M * L.hbls_hm_entry_bytes(), dtype=torch.uint8, device=dev)
+    vst = torch.full((NP,), 255, dtype=torch.uint8, device=dev)
+    tout = torch.zeros(V * 96, dtype=torch.uint8, device=dev)
+    tst = torch.full((V,), 255, dtype=torch.uint8, device=dev)
+    ast = torch.full((V,), 255, dtype=torch.uint8, device=dev)
+    slot = _lib.HblsSlot(msgs=_p(g["msgs"]).value, msg_off=_p(g["moff"]).value, msg_len=_p(g["mlen"]).value,
+                         n_msgs=M, hm=_p(hm).value, pks=_p(g["pks"]).value, sigs=_p(g["sigs"]).value,
+                         msg_idx=_p(g["midx"]).value, n=NP, vgrp_off=_p(g["vgoff"]).value, n_vgroups=V,
+                         vstatus=_p(vst).value, ta_sigs=None, ta_src=_p(g["tsrc"]).value,
+                         ta_idx=_p(g["tidx"]).value, grp_off=_p(g["goff"]).value, n_groups=V, n_ta_partials=V * t,
+                         ta_out=_p(tout).value, ta_status=_p(tst).value, dv_pks=_p(g["dvpk"]).value,
+                         agg_vstatus=_p(ast).value)
+    s = torch.cuda.Stream(device=dev)
+    _chk(L, L.hbls_slot_device(ctypes.byref(slot), ctypes.c_void_p(s.cuda_stream)))
+    s.synchronize()
+    assert int((vst != 0).sum().item()) == 0
+    assert int((tst != 0).sum().item()) == 0 and int((ast != 0).sum().item()) == 0
+    assert np.array_equal(tout.cpu().numpy(), d["root_sigs"])
+    rng = random.Random(3)
+    for i in rng.sample(range(NP), 3):
+        st = B.verify(bytes(d["pks"][48 * i:48 * i + 48]), bytes(d["item_msgs"][32 * i:32 * i + 32]),
+                      bytes(d["sigs"][96 * i:96 * i + 96]))
+        assert st == 0, i
+    v = rng.randrange(V)
+    members = {int(d["ta_idx"][v * t + k]): bytes(d["ta_sigs"][96 * (v * t + k):96 * (v * t + k + 1)])
+               for k in range(t)}
+    assert B.threshold_aggregate(members)[1] == bytes(tout[96 * v:96 * v + 96].cpu().numpy())
