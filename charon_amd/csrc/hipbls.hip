@@ -269,7 +269,7 @@ enum WsId {
   W_PCNT, W_PCOFF, W_PCFIRST, W_PCCOUNT, W_COEF, W_RT1, W_RT2,  // chunk plan + multi-scalar RLC
   W_TPCNT, W_TPCOFF, W_TPCFIRST, W_TPCCOUNT,                    // chunk plan of the aggregation
   W_FBUF, W_GS, W_BS, W_BLINES, W_BBAD, W_BVER, W_GLIST, W_GCOUNT,  // batched final exponentiation
-  W_MCNT, W_MOFF, W_MCUR, W_MENT, W_MBUCKET, W_MPART, W_MPART2, W_MTOT, W_PBUF1, W_PBUF2, W_SFAIL,  // slot-wide check
+  W_MCNT, W_MOFF, W_MCUR, W_MORDER, W_MENT, W_MBUCKET, W_MPART, W_MPART2, W_MTOT, W_PBUF1, W_PBUF2, W_SFAIL,  // slot-wide check
   W_COUNT_
 };
 
@@ -662,7 +662,7 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
   Fp4Entry *pbuf1 = nullptr, *pbuf2 = nullptr;
   uint8_t* sfail = nullptr;
   if (smsm && (wsbuf(w, W_MCNT, MSM_KEYS, &ma.cnt) || wsbuf(w, W_MOFF, MSM_KEYS + 1, &ma.off) ||
-               wsbuf(w, W_MCUR, MSM_KEYS, &ma.cur) || wsbuf(w, W_MENT, 2 * MSM_WINDOWS * (n + n_agg), &ma.ent) ||
+               wsbuf(w, W_MCUR, MSM_KEYS, &ma.cur) || wsbuf(w, W_MORDER, MSM_KEYS, &ma.order) || wsbuf(w, W_MENT, 2 * MSM_WINDOWS * (n + n_agg), &ma.ent) ||
                wsbuf(w, W_MBUCKET, MSM_KEYS, &ma.bucket) || wsbuf(w, W_MPART, MSM_PARTS, &ma.part) ||
                wsbuf(w, W_MPART2, MSM_PARTS / 128, &ma.part2) || wsbuf(w, W_MTOT, 1, &ma.total) ||
                wsbuf(w, W_PBUF1, 3 * nb1, &pbuf1) || wsbuf(w, W_PBUF2, 3 * nb2, &pbuf2) ||

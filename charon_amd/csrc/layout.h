@@ -260,6 +260,7 @@ struct G2MsmArgs {
   uint32_t* off;           // [MSM_KEYS + 1]
   uint32_t* cur;           // [MSM_KEYS] zeroed
   uint32_t* ent;           // [2 MSM_WINDOWS (n + n_agg)]
+  uint32_t* order;         // [MSM_KEYS] buckets by decreasing size
   G2JEntry* bucket;        // [MSM_KEYS]
   G2JEntry* part;          // [MSM_PARTS]
   G2JEntry* part2;         // [MSM_PARTS / 128]

@@ -62,11 +62,35 @@ __global__ __launch_bounds__(64) void k_msm_fill(G2MsmArgs a) {
   }
 }
 
-// one lane per bucket: the sum of its points (half 1: -psi^2 of the signature)
+// one workgroup: the buckets in decreasing order of size (counting sort on the sizes, capped at
+// 255), so that the lanes of a wave of k_msm_bucket sum buckets of nearly equal size (lane per
+// bucket in key order: Poisson sizes, a wave waits for its largest)
+__global__ __launch_bounds__(1024) void k_msm_order(const uint32_t* __restrict__ cnt, uint32_t* __restrict__ order) {
+  __shared__ uint32_t hist[256];
+  const uint32_t t = threadIdx.x;
+  if (t < 256) hist[t] = 0;
+  __syncthreads();
+  for (uint32_t k = t; k < MSM_KEYS; k += 1024) atomicAdd(&hist[255u - min(cnt[k], 255u)], 1u);
+  __syncthreads();
+  if (t == 0) {  // exclusive scan, largest sizes first
+    uint32_t run = 0;
+    for (int b = 0; b < 256; b++) {
+      const uint32_t c = hist[b];
+      hist[b] = run;
+      run += c;
+    }
+  }
+  __syncthreads();
+  for (uint32_t k = t; k < MSM_KEYS; k += 1024) order[atomicAdd(&hist[255u - min(cnt[k], 255u)], 1u)] = k;
+}
+
+// one lane per bucket (in the order of k_msm_order): the sum of its points (half 1: -psi^2 of the
+// signature)
 __global__ KB_OCC(HB_OCC_RLC) void k_msm_bucket(G2MsmArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= MSM_KEYS) return;
+  const uint32_t L = blockIdx.x * blockDim.x + threadIdx.x;
+  if (L >= MSM_KEYS) return;
+  const uint32_t k = a.order[L];
   const uint32_t b = a.off[k], e = a.off[k + 1];
   G2J acc = jac_infinity<Fp2>();
   HB_NOUNROLL for (uint32_t j = b; j < e; j++) {
@@ -148,6 +172,7 @@ void launch_msm_fill(const G2MsmArgs& a, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_msm_fill, dim3(blocks_for(n)), dim3(BLOCK), 0, s, a);
 }
 void launch_msm_bucket(const G2MsmArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_msm_order, dim3(1), dim3(1024), 0, s, (const uint32_t*)a.cnt, a.order);
   hipLaunchKernelGGL(k_msm_bucket, dim3(blocks_for(MSM_KEYS)), dim3(BLOCK), 0, s, a);
 }
 void launch_msm_reduce(const G2MsmArgs& a, hipStream_t s) {
