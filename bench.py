@@ -695,7 +695,7 @@ def main(argv=None):
     def kernel_roofline():
         # per-kernel roofline: the same slot once more with every kernel ALONE on the device
         # (timing mode 2 serialises the launches), after every other measurement -- overlapped
-        # launches of two slots in flight share the chip and their durations say nothing about one
+        # launches of the slots in flight share the chip and their durations say nothing about one
         # kernel; as the last slot of the run it is also the last one in a rocprofv3 trace
         torch.cuda.synchronize()
         _chk(L, L.hbls_timing(2))
@@ -788,7 +788,7 @@ def main(argv=None):
                                   "slot after the timed region, library timing mode 2)",
                         "slot": {"fpmul_alg_per_step": slot_fpmul, "achieved": round(slot_tops, 3),
                                  "frac": round(slot_tops / opcounts.PEAK_MAD_TOPS, 4),
-                                 "note": "all kernels' algorithmic work over ms_per_step (two slots in flight)"},
+                                 "note": "all kernels' algorithmic work over ms_per_step (slots in flight overlap)"},
                         "k_pair3": pair}
         return per, roofline
 

@@ -635,7 +635,8 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
     return -1;
   RlcKey key;
   if (rlc_key(key)) return -1;
-  // Batched final exponentiation: FE_BATCH groups share one final exponentiation and one Miller
+  // Batched final exponentiation: a batch of groups (FE_BATCH; g_fb_batch behind a failed slot-wide
+  // check) shares one final exponentiation and one Miller
   // loop of the signature side, checking prod_g e(P_g, H(m_g)) * e(-g1, sum_g S_g) == 1.  Every
   // item (singletons and folded aggregates included) then takes a random coefficient: with two
   // fixed coefficients in one combination, errors of two items could cancel.
@@ -662,7 +663,8 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
   Fp4Entry *pbuf1 = nullptr, *pbuf2 = nullptr;
   uint8_t* sfail = nullptr;
   if (smsm && (wsbuf(w, W_MCNT, MSM_KEYS, &ma.cnt) || wsbuf(w, W_MOFF, MSM_KEYS + 1, &ma.off) ||
-               wsbuf(w, W_MCUR, MSM_KEYS, &ma.cur) || wsbuf(w, W_MORDER, MSM_KEYS, &ma.order) || wsbuf(w, W_MENT, 2 * MSM_WINDOWS * (n + n_agg), &ma.ent) ||
+               wsbuf(w, W_MCUR, MSM_KEYS, &ma.cur) || wsbuf(w, W_MORDER, MSM_KEYS, &ma.order) ||
+               wsbuf(w, W_MENT, 2 * MSM_WINDOWS * (n + n_agg), &ma.ent) ||
                wsbuf(w, W_MBUCKET, MSM_KEYS, &ma.bucket) || wsbuf(w, W_MPART, MSM_PARTS, &ma.part) ||
                wsbuf(w, W_MPART2, MSM_PARTS / 128, &ma.part2) || wsbuf(w, W_MTOT, 1, &ma.total) ||
                wsbuf(w, W_PBUF1, 3 * nb1, &pbuf1) || wsbuf(w, W_PBUF2, 3 * nb2, &pbuf2) ||
