@@ -247,6 +247,10 @@ std::atomic<size_t> g_fe_batch_min{2 * FE_BATCH};
 // many (an attack): smaller batches pass more often (group testing; C5, 1 % corrupted partials:
 // 64-group batches nearly all fail and every group then pays its own exponentiation).
 size_t g_fb_batch = 8;
+// HBLS_STAGGER=1: a verification's decompression starts after the previous verification's (slots in
+// flight staggered instead of in lockstep).  Off: with three slots in flight overlapping
+// decompressions measured 131.0-131.5 vs 132.7-133.1 ms per C3 slot (C2 19.9-20.1 vs 20.0-20.4)
+bool g_stagger = false;
 // HBLS_SLOT_MSM: batched verifications of at least this many items (partials + folded aggregates,
 // one chunk of groups) check every group at once -- the signature side as one multi-scalar
 // multiplication (msm.hip), one final exponentiation for the call -- and fall back to the
@@ -306,8 +310,8 @@ struct Dev {
   unsigned next_ws = 0;
   DevBuf io[I_COUNT];
   std::mutex mu;  // one call at a time enqueues on this device
-  // end of the last verification's decompression stage: the next verification starts its own
-  // decompression after it, so consecutive slots in flight run staggered (one slot's
+  // end of the last verification's decompression stage: with HBLS_STAGGER=1 the next verification
+  // starts its own decompression after it, so consecutive slots in flight run staggered (one slot's
   // decompression beside the previous slot's combinations and pairings) instead of in lockstep
   hipEvent_t ev_dec = nullptr;
   bool dec_valid = false;
@@ -457,6 +461,7 @@ int init_mask(uint32_t mask) {
   g_ta_joint = std::min<size_t>(8, env_size("HBLS_TA_JOINT", g_ta_joint.load()));
   g_fe_batch_min = env_size("HBLS_FE_BATCH", g_fe_batch_min.load());
   g_slot_msm_min = env_size("HBLS_SLOT_MSM", g_slot_msm_min.load());
+  g_stagger = env_size("HBLS_STAGGER", 0) != 0;
   {
     size_t fb = std::min<size_t>(FE_BATCH, std::max<size_t>(2, env_size("HBLS_FALLBACK_BATCH", g_fb_batch)));
     while (fb & (fb - 1)) fb &= fb - 1;  // a power of two
@@ -673,7 +678,7 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
   const int sides1 = smsm ? 1 : 3;  // first pass: the public-key side only when the MSM takes the other
 
   // fork: decompression on the side streams (after the previous verification's decompression)
-  if (d.dec_valid) HCHK(hipStreamWaitEvent(s, d.ev_dec, 0));
+  if (d.dec_valid && g_stagger) HCHK(hipStreamWaitEvent(s, d.ev_dec, 0));
   HCHK(hipEventRecord(w.ev_fork, s));
   for (int k = 0; k < 2; k++) HCHK(hipStreamWaitEvent(w.side[k], w.ev_fork, 0));
   // public keys: from the caller's decompressed-key tables when given (static per cluster lock:
@@ -1782,7 +1787,7 @@ int hbls_slot_device(const hbls_slot* a, void* stream) {
                    "aggregation group");
   std::lock_guard<std::mutex> lk(d->mu);
   Ws& w = ws_acquire(*d, s);
-  if (d->dec_valid) HCHK(hipStreamWaitEvent(s, d->ev_dec, 0));  // staggered slots (Dev::ev_dec)
+  if (d->dec_valid && g_stagger) HCHK(hipStreamWaitEvent(s, d->ev_dec, 0));  // staggered slots (Dev::ev_dec)
   HCHK(hipEventRecord(w.ev_fork, s));
   // messages: hash + Miller lines (side 2)
   hipStream_t sh = w.side[2];
