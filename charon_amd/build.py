@@ -69,6 +69,23 @@ def build_hostcheck(force: bool = False, verbose: bool = True) -> str:
     return out
 
 
+def build_hostcheck_sanitized(force: bool = False, verbose: bool = True) -> str:
+    """The test harness under AddressSanitizer + UndefinedBehaviorSanitizer (host code only; the
+    GPU build has no sanitizer here).  tests/test_sanitizers.py runs the host tests against it."""
+    src = os.path.join(ROOT, "tests", "native", "hostcheck.cpp")
+    out = os.path.join(ROOT, "tests", "native", "libhbls_hostcheck_asan.so")
+    deps = [src] + [os.path.join(CSRC, f) for f in HEADERS]
+    if not force and _newer(out, deps):
+        return out
+    cmd = ["g++", "-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
+           "-fno-sanitize-recover=undefined", "-std=c++17", "-pthread", "-shared", "-fPIC", "-o", out + ".tmp", src]
+    subprocess.run(cmd, check=True, timeout=900)
+    os.replace(out + ".tmp", out)
+    if verbose:
+        print(f"built {out}")
+    return out
+
+
 def main(argv=None):
     force = "--force" in (argv or sys.argv[1:])
     build_library(force)

@@ -16,8 +16,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 
 @pytest.fixture(scope="module")
 def hc():
+    import os
     from charon_amd.build import build_hostcheck
-    return ctypes.CDLL(build_hostcheck(verbose=False))
+    # HBLS_HOSTCHECK_LIB: another build of the harness (tests/test_sanitizers.py: ASan + UBSan)
+    return ctypes.CDLL(os.environ.get("HBLS_HOSTCHECK_LIB") or build_hostcheck(verbose=False))
 
 
 def _b(n):
