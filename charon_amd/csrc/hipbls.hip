@@ -1047,25 +1047,47 @@ struct MsgTable {
   std::vector<uint32_t> idx;  // per item
 };
 
+// 64-bit FNV-1a over the message bytes, finished with a multiply-xorshift (messages are usually
+// 32-byte signing roots, already uniform)
+inline uint64_t msg_hash(const uint8_t* p, uint32_t n) {
+  uint64_t h = 0xcbf29ce484222325ull ^ n;
+  for (uint32_t k = 0; k < n; k++) h = (h ^ p[k]) * 0x100000001b3ull;
+  h ^= h >> 29;
+  h *= 0xbf58476d1ce4e5b9ull;
+  return h ^ (h >> 32);
+}
+
+// distinct messages of the items (open addressing on item indices: no per-message allocation;
+// a slot's million host-buffer partials dedup in a few milliseconds)
 void dedup_messages(const uint8_t* msgs, const uint64_t* off, const uint32_t* len, size_t n, const size_t* items,
                     MsgTable& t) {
-  std::unordered_map<std::string, uint32_t> seen;
-  seen.reserve(n * 2 + 1);
+  size_t cap = 16;
+  while (cap < 2 * n + 2) cap <<= 1;
+  std::vector<uint32_t> slot(cap, 0xffffffffu);  // distinct-message id, or empty
+  std::vector<uint64_t> src;                      // first item of each distinct message
   t.idx.resize(n);
   for (size_t k = 0; k < n; k++) {
     const size_t i = items ? items[k] : k;
-    std::string key((const char*)msgs + off[i], len[i]);
-    auto it = seen.find(key);
-    if (it == seen.end()) {
-      uint32_t id = (uint32_t)t.len.size();
-      seen.emplace(std::move(key), id);
-      t.off.push_back(t.bytes.size());
-      t.len.push_back(len[i]);
-      t.bytes.insert(t.bytes.end(), msgs + off[i], msgs + off[i] + len[i]);
-      t.idx[k] = id;
-    } else {
-      t.idx[k] = it->second;
+    const uint8_t* m = msgs + off[i];
+    const uint32_t l = len[i];
+    size_t h = (size_t)msg_hash(m, l) & (cap - 1);
+    uint32_t id;
+    for (;;) {
+      id = slot[h];
+      if (id == 0xffffffffu) break;
+      const uint64_t j = src[id];
+      if (len[j] == l && memcmp(msgs + off[j], m, l) == 0) break;
+      h = (h + 1) & (cap - 1);
     }
+    if (id == 0xffffffffu) {
+      id = (uint32_t)t.len.size();
+      slot[h] = id;
+      src.push_back(i);
+      t.off.push_back(t.bytes.size());
+      t.len.push_back(l);
+      t.bytes.insert(t.bytes.end(), m, m + l);
+    }
+    t.idx[k] = id;
   }
 }
 
@@ -1142,9 +1164,11 @@ int verify_host(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msgs, co
   // global message ids, order items by (message, position), groups of <= g_gmax
   MsgTable all;
   dedup_messages(msgs, msg_off, msg_len, n, nullptr, all);
-  std::vector<size_t> order(n);
-  std::iota(order.begin(), order.end(), 0);
-  std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) { return all.idx[a] < all.idx[b]; });
+  // items ordered by message id, stable (a counting sort: one pass, no comparisons)
+  std::vector<size_t> order(n), mstart(all.len.size() + 1, 0);
+  for (size_t k = 0; k < n; k++) mstart[all.idx[k] + 1]++;
+  for (size_t j = 0; j < all.len.size(); j++) mstart[j + 1] += mstart[j];
+  for (size_t k = 0; k < n; k++) order[mstart[all.idx[k]]++] = k;
   std::vector<size_t> gstart;  // group starts in `order`
   for (size_t k = 0; k < n; k++)
     if (k == 0 || all.idx[order[k]] != all.idx[order[k - 1]] || k - gstart.back() >= g_gmax) gstart.push_back(k);
