@@ -26,7 +26,7 @@
 #define HB_OCC_PREP 2
 #endif
 #ifndef HB_OCC_PAIR3
-#define HB_OCC_PAIR3 2
+#define HB_OCC_PAIR3 1
 #endif
 #ifndef HB_OCC_STRAUS
 #define HB_OCC_STRAUS 2
