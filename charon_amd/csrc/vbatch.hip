@@ -42,6 +42,9 @@ __global__ KB void k_item_group(const uint32_t* __restrict__ grp_off, uint32_t n
   item_grp[i] = grp_off ? find_group_vb(grp_off, n_groups, i) : i;
 }
 
+#ifndef HB_DECPK_FUSED
+#define HB_DECPK_FUSED 0  // 1: the subgroup check inside k_dec_pk (A/B variant)
+#endif
 // One lane per partial: decompress + subgroup-check the public key (herumi.go:290
 // PublicKey.Deserialize).  A rejected key is replaced by g1 so later stages run the same
 // arithmetic on well-formed values; its status byte decides the verdict.
@@ -50,7 +53,7 @@ __global__ KB_OCC(HB_OCC_DECPK) void k_dec_pk(const uint8_t* __restrict__ pks, u
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   G1A p;
-  uint8_t bad = g1_decompress(p, pks + 48ull * i);
+  uint8_t bad = g1_decompress(p, pks + 48ull * i, HB_DECPK_FUSED != 0);
   if (bad) p = g1_generator();
   G1AEntry e;
   e.x = p.x;
@@ -59,6 +62,25 @@ __global__ KB_OCC(HB_OCC_DECPK) void k_dec_pk(const uint8_t* __restrict__ pks, u
   e.pad[0] = e.pad[1] = e.pad[2] = 0;
   out[i] = e;
   st[i] = bad;
+}
+
+// The subgroup check of k_dec_pk's points, a kernel of its own like k_g2_subgroup (the fused
+// kernel spilled the square root's window table beside the ladder).
+__global__ KB_OCC(HB_OCC_DECPK) void k_g1_subgroup(uint32_t n, G1AEntry* __restrict__ pts, uint8_t* __restrict__ st) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const G1AEntry e = pts[i];
+  if (st[i] || e.inf) return;
+  if (!g1_in_subgroup(G1A{e.x, e.y, false})) {
+    const G1A g = g1_generator();
+    G1AEntry z;
+    z.x = g.x;
+    z.y = g.y;
+    z.inf = 0u;
+    z.pad[0] = z.pad[1] = z.pad[2] = 0;
+    pts[i] = z;
+    st[i] = 1;
+  }
 }
 
 // One lane per signature: decompress + subgroup-check (herumi.go:295 / :257 Sign.Deserialize),
@@ -433,7 +455,9 @@ void launch_item_group(const uint32_t* grp_off, uint32_t n_groups, uint32_t n, u
   if (n) hipLaunchKernelGGL(k_item_group, dim3(blocks_for(n)), dim3(BLOCK), 0, s, grp_off, n_groups, n, item_grp);
 }
 void launch_dec_pk(const uint8_t* pks, uint32_t n, G1AEntry* out, uint8_t* st, hipStream_t s) {
-  if (n) hipLaunchKernelGGL(k_dec_pk, dim3(blocks_for(n)), dim3(BLOCK), 0, s, pks, n, out, st);
+  if (!n) return;
+  hipLaunchKernelGGL(k_dec_pk, dim3(blocks_for(n)), dim3(BLOCK), 0, s, pks, n, out, st);
+  if (!HB_DECPK_FUSED) hipLaunchKernelGGL(k_g1_subgroup, dim3(blocks_for(n)), dim3(BLOCK), 0, s, n, out, st);
 }
 void launch_pk_gather(const uint8_t* pks, const uint32_t* idx, const G1AEntry* tab, const uint8_t* tst, uint32_t n,
                       G1AEntry* out, uint8_t* st, hipStream_t s) {
