@@ -19,6 +19,9 @@
 #ifndef HB_OCC_DECSIG
 #define HB_OCC_DECSIG 2
 #endif
+#ifndef HB_OCC_SUBG
+#define HB_OCC_SUBG 2  // k_g1_subgroup, k_g2_subgroup
+#endif
 #ifndef HB_OCC_RLC
 #define HB_OCC_RLC 2
 #endif

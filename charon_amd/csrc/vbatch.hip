@@ -66,7 +66,7 @@ __global__ KB_OCC(HB_OCC_DECPK) void k_dec_pk(const uint8_t* __restrict__ pks, u
 
 // The subgroup check of k_dec_pk's points, a kernel of its own like k_g2_subgroup (the fused
 // kernel spilled the square root's window table beside the ladder).
-__global__ KB_OCC(HB_OCC_DECPK) void k_g1_subgroup(uint32_t n, G1AEntry* __restrict__ pts, uint8_t* __restrict__ st) {
+__global__ KB_OCC(HB_OCC_SUBG) void k_g1_subgroup(uint32_t n, G1AEntry* __restrict__ pts, uint8_t* __restrict__ st) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const G1AEntry e = pts[i];
@@ -104,7 +104,7 @@ __global__ KB_OCC(HB_OCC_DECSIG) void k_dec_sig_pt(const uint8_t* __restrict__ s
   st[i] = bad;
 }
 
-__global__ KB_OCC(HB_OCC_DECSIG) void k_g2_subgroup(uint32_t n, HmEntry* __restrict__ pts, uint8_t* __restrict__ st) {
+__global__ KB_OCC(HB_OCC_SUBG) void k_g2_subgroup(uint32_t n, HmEntry* __restrict__ pts, uint8_t* __restrict__ st) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const HmEntry e = pts[i];
