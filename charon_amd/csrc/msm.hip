@@ -22,6 +22,15 @@ namespace hb {
 
 constexpr int BLOCK = 64;
 
+// The reduction and the butterflies run 128 and at most 64 waves: far fewer than the SIMDs, so
+// they are latency-bound and take one wave per SIMD's full register file (no scratch spills).
+#ifndef HB_OCC_MSMBUCKET
+#define HB_OCC_MSMBUCKET HB_OCC_RLC
+#endif
+#ifndef HB_OCC_MSMTAIL
+#define HB_OCC_MSMTAIL 1
+#endif
+
 __device__ __forceinline__ bool msm_take(const G2MsmArgs& a, uint32_t i, uint2& ab) {
   ab = a.coef[i];
   if ((ab.x | ab.y) == 0) return false;
@@ -86,7 +95,7 @@ __global__ __launch_bounds__(1024) void k_msm_order(const uint32_t* __restrict__
 
 // one lane per bucket (in the order of k_msm_order): the sum of its points (half 1: -psi^2 of the
 // signature)
-__global__ KB_OCC(HB_OCC_RLC) void k_msm_bucket(G2MsmArgs a) {
+__global__ KB_OCC(HB_OCC_MSMBUCKET) void k_msm_bucket(G2MsmArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
   const uint32_t L = blockIdx.x * blockDim.x + threadIdx.x;
   if (L >= MSM_KEYS) return;
@@ -118,7 +127,7 @@ __device__ __forceinline__ G2J mul16(const G2J& p, uint32_t m) {
 
 // one lane per chunk of MSM_CHUNK buckets of one window: sum_d d * 2^(16 w) B_d over the chunk,
 // as running sums T = sum_j (j + 1) B_(lo + j), R = sum_j B_(lo + j), then T + (lo - 1) R
-__global__ KB_OCC(HB_OCC_RLC) void k_msm_reduce(G2MsmArgs a) {
+__global__ KB_OCC(HB_OCC_MSMTAIL) void k_msm_reduce(G2MsmArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= MSM_PARTS) return;
@@ -140,7 +149,7 @@ __global__ KB_OCC(HB_OCC_RLC) void k_msm_reduce(G2MsmArgs a) {
 }
 
 // sum of m Jacobian points: workgroup b (one wave) sums in[b * 64 q, (b + 1) * 64 q) into out[b]
-__global__ KB_OCC(HB_OCC_RLC) void k_msm_sum(const G2JEntry* __restrict__ in, uint32_t m, uint32_t q,
+__global__ KB_OCC(HB_OCC_MSMTAIL) void k_msm_sum(const G2JEntry* __restrict__ in, uint32_t m, uint32_t q,
                                              G2JEntry* __restrict__ out) {
 #if defined(__HIP_DEVICE_COMPILE__)
   const uint32_t lane = threadIdx.x & 63u, base = blockIdx.x * 64u * q;
