@@ -47,7 +47,8 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 from charon_amd import opcounts  # noqa: E402
-from charon_amd.shard import max_over_ranks, owned_validators  # noqa: E402
+from charon_amd.shard import (SlotExchange, init_library_comm, library_allgather, max_over_ranks,  # noqa: E402
+                               owned_validators)
 
 METRIC = "verified partial sigs/sec + ThresholdAggregate/sec per node, 1-8 MI355X"
 
@@ -552,20 +553,16 @@ def main(argv=None):
     d_hm, d_vst, d_tout, d_tst, d_ast = (outs[0][k] for k in ("hm", "vst", "tout", "tst", "ast"))
 
     xchg = None
+    exch = None
     if world > 1:
-        # RCCL communicator of the library: rank 0's id travels over the gloo control plane
-        idb = np.zeros(L.hbls_comm_id_bytes(), dtype=np.uint8)
-        if rank == 0:
-            _chk(L, L.hbls_comm_unique_id(_p(idb)))
-        obj = [idb.tobytes()]
-        dist.broadcast_object_list(obj, src=0)
-        idb = np.frombuffer(obj[0], dtype=np.uint8).copy()
-        _chk(L, L.hbls_comm_init(world, rank, _p(idb)))
+        # the library's RCCL communicator (rank 0's id over the gloo control plane), then ONE
+        # exchange stream for the all-gathers of every in-flight slot (charon_amd/shard.py
+        # SlotExchange: the same ordering code tests/test_shard.py runs over gloo)
+        init_library_comm(L, world, rank)
+        exch = SlotExchange(world, rank, {"vst": NP, "tout": V * 96, "tst": V, "ast": V}, dev,
+                            library_allgather(L), stream=torch.cuda.Stream(device=dev))
         for o in outs:
-            o["xchg"] = {"vst": torch.empty(world * NP, dtype=torch.uint8, device=dev),
-                         "tout": torch.empty(world * V * 96, dtype=torch.uint8, device=dev),
-                         "tst": torch.empty(world * V, dtype=torch.uint8, device=dev),
-                         "ast": torch.empty(world * V, dtype=torch.uint8, device=dev)}
+            o["xchg"] = exch.gather_buffers()
         xchg = outs[0]["xchg"]
 
     stream = outs[0]["stream"]
@@ -579,20 +576,8 @@ def main(argv=None):
             grp_off=_p(d_goff).value, n_groups=V, n_ta_partials=V * t, ta_out=_p(o["tout"]).value,
             ta_status=_p(o["tst"]).value, dv_pks=_p(d_dvpk).value, agg_vstatus=_p(o["ast"]).value)
 
-    # the collectives of all in-flight slots go through ONE stream, so every rank issues them to
-    # the communicator in the same order and they never run concurrently
-    xs = torch.cuda.Stream(device=dev)
-    xsp = ctypes.c_void_p(xs.cuda_stream)
-
     def exchange(o):  # all-gather verdicts + compressed aggregates to every rank (RCCL)
-        done = torch.cuda.Event()
-        done.record(o["stream"])
-        xs.wait_event(done)
-        for src, dst in ((o["vst"], "vst"), (o["tout"], "tout"), (o["tst"], "tst"), (o["ast"], "ast")):
-            _chk(L, L.hbls_allgather_device(_p(src), _p(o["xchg"][dst]), src.numel(), xsp))
-        back = torch.cuda.Event()
-        back.record(xs)
-        o["stream"].wait_event(back)  # the set's next slot overwrites the outputs only after the exchange
+        exch.exchange({f: o[f] for f in ("vst", "tout", "tst", "ast")}, o["xchg"], producer=o["stream"])
 
     step_no = [0]
 

@@ -33,6 +33,7 @@ EXPORTS = (
     "hbls_allgather_device", "hbls_comm_destroy", "hbls_stats", "hbls_fe_batch", "hbls_slot_msm", "hbls_rlc_lanes", "hbls_ta_joint", "hbls_attestation_signing_roots",
     "hbls_signing_roots", "hbls_attestation_signing_roots_device", "hbls_pk_entry_bytes",
     "hbls_decompress_pubkeys_device", "hbls_pubkey_cache_add", "hbls_pubkey_cache_clear", "hbls_pubkey_cache_size",
+    "hbls_debug_split",
 )
 
 ALL_DEVICES = 0xFFFFFFFF
@@ -89,6 +90,7 @@ def _declare(lib):
         "hbls_pubkey_cache_add": ([P, SZ], ctypes.c_int),
         "hbls_pubkey_cache_clear": ([], ctypes.c_int),
         "hbls_pubkey_cache_size": ([], SZ),
+        "hbls_debug_split": ([U32], ctypes.c_int),
         "hbls_slot_device": ([ctypes.POINTER(HblsSlot), P], ctypes.c_int),
         "hbls_hm_entry_bytes": ([], SZ),
         "hbls_sync": ([P], ctypes.c_int),

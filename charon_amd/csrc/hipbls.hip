@@ -224,10 +224,16 @@ size_t g_gcap = 131072, g_fbcap = 65536, g_gmax = 16;
 // HBLS_RLC_MSM=0: one ladder per item (k_rlc) instead of shared-doubling chunks (k_rlc_msm)
 bool g_rlc_msm = true;
 std::atomic<size_t> g_rlc_lanes{65536};   // HBLS_RLC_LANES: lanes the chunk size aims to keep busy
-// public-key cache: compressed key -> entry index (the same on every device)
+// public-key cache: compressed key -> entry index (the same on every device).  Lock order: an
+// adder (or clear) takes g_kc_add_mu, then one Dev::mu at a time to fill that device's table, then
+// g_kc_mu to publish; verifications hold their Dev::mu and take g_kc_mu for the lookup.  g_kc_mu is
+// always the innermost lock, so adds and verifications never wait on each other in a cycle; a
+// lookup made under a Dev::mu stays valid while it is held (entries are only written under it).
+std::mutex g_kc_add_mu;
 std::mutex g_kc_mu;
 std::unordered_map<std::string, uint32_t> g_kc_map;
-size_t g_kc_n = 0;
+size_t g_kc_n = 0;             // published entries (g_kc_mu; written under g_kc_add_mu too)
+std::vector<uint8_t> g_kc_keys;  // their compressed bytes, 48 B each (g_kc_add_mu): fills new devices
 // HBLS_TA_MSM=1: the aggregation as shared-doubling chunks (k_ta_msm) instead of one Straus ladder
 // per member (k_ta_straus).  Off: measured slower at C3 (per-member tables read across lanes
 // uncoalesced; fewer, longer lanes) -- 222.8 ms/slot with per-member ladders vs 224.2-227.8 with
@@ -326,7 +332,9 @@ struct Dev {
 };
 
 std::mutex g_init_mu;
-std::vector<Dev*> g_devs;  // in device-mask order
+std::vector<Dev*> g_devs;  // in device-mask order (hbls_debug_split: each ordinal repeated)
+std::vector<Dev*> g_base_devs;   // one per device of the mask
+std::vector<std::vector<Dev*>> g_split_pool;  // per base device: extra contexts of hbls_debug_split (reused)
 uint32_t g_mask = 0;
 std::atomic<bool> g_ready{false};
 
@@ -436,7 +444,7 @@ int dev_create(int ord, Dev** out) {
 // visible device.  Idempotent for the same mask; a different mask afterwards is an error.
 int init_mask(uint32_t mask) {
   if (g_ready.load()) {
-    if (mask != 0 && mask != g_mask && !(mask == 0xffffffffu && g_mask == ((1u << g_devs.size()) - 1)))
+    if (mask != 0 && mask != g_mask && !(mask == 0xffffffffu && g_mask == ((1u << g_base_devs.size()) - 1)))
       return set_err("hipbls already initialised with device mask " + std::to_string(g_mask));
     return 0;
   }
@@ -476,6 +484,7 @@ int init_mask(uint32_t mask) {
       devs.push_back(d);
     }
   g_devs = devs;
+  g_base_devs = devs;
   g_mask = mask;
   g_ready.store(true);
   return 0;
@@ -640,6 +649,10 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
     return -1;
   RlcKey key;
   if (rlc_key(key)) return -1;
+  // Coefficients: at most ONE fixed (r = 1) coefficient per combined check.  Items of a singleton
+  // group keep r = 1 only when nothing else joins their group's check; with a folded aggregate
+  // (which keeps r = 1 without the batched final exponentiation) every item takes a random one --
+  // otherwise an error +D on a group's single partial and -D on its aggregate would cancel.
   // Batched final exponentiation: a batch of groups (FE_BATCH; g_fb_batch behind a failed slot-wide
   // check) shares one final exponentiation and one Miller
   // loop of the signature side, checking prod_g e(P_g, H(m_g)) * e(-g1, sum_g S_g) == 1.  Every
@@ -647,6 +660,7 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
   // fixed coefficients in one combination, errors of two items could cancel.
   const size_t fe_min = g_fe_batch_min.load();
   const bool bfe = fe_min && n_groups >= fe_min;
+  const int item_always = (bfe || n_agg) ? 1 : 0;  // see the coefficient rule above
   const size_t nbcap = (gcap + 1) / 2;  // batches of >= 2 groups (FE_BATCH, or g_fb_batch behind the slot-wide check)
   Fp4Entry* fbuf = nullptr;
   G2JEntry *gS = nullptr, *bS = nullptr;
@@ -765,7 +779,7 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
     ra.t2 = t2;
     ra.pout = pr;
     ra.sout = sr;
-    ra.always = bfe ? 1 : 0;
+    ra.always = item_always;
     ra.sides = sides1;
     TIMED(d, "k_rlc", s, launch_rlc_msm(ra, (uint32_t)max_chunks, s));
     if (smsm) {  // the per-item signature side, only if the slot-wide check fails
@@ -777,14 +791,14 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
   } else {
     if (smsm && wsbuf(w, W_COEF, n + n_agg, &coef_pi)) return -1;
     TIMED(d, "k_rlc", s,
-          launch_rlc(vpk, vpkst, vsig, vsigst, igrp, dgoff, bfe ? 1 : 0, (uint32_t)n, 0, key, pr, sr, s, coef_pi,
+          launch_rlc(vpk, vpkst, vsig, vsigst, igrp, dgoff, item_always, (uint32_t)n, 0, key, pr, sr, s, coef_pi,
                      sides1));
   }
   if (n_agg) {
     // without the batched final exponentiation the folded aggregate keeps r = 1: one coefficient
     // per combination may be fixed without losing soundness (an invalid aggregate alone fails the
     // combined check exactly; with an invalid partial j beside it the check passes for one value
-    // of the random r_j only)
+    // of the random r_j only) -- the group's items all take random coefficients (item_always)
     HCHK(hipStreamWaitEvent(s, w.ev_ta, 0));
     uint2* acoef = smsm ? (coef_pi ? coef_pi : rlc_fallback.coef) + n : nullptr;
     TIMED(d, "k_rlc", s,
@@ -1143,6 +1157,33 @@ int for_each_device(size_t n_units, const std::function<int(Dev&, size_t, size_t
 // (at most g_gmax per group), the groups sharded over the devices, statuses scattered back.
 // Cache indices of m packed compressed keys (0xffffffff: not cached).  false when the cache is
 // empty or holds none of them (the call then decompresses every key).
+// Decompress m compressed keys into entries first .. first+m-1 of d's key table (grown, keeping
+// the entries before `first`).  Caller holds d.mu.
+int kc_fill(Dev& d, const uint8_t* keys, size_t first, size_t m) {
+  HCHK(hipSetDevice(d.ord));
+  const size_t tot = first + m;
+  if (d.kc_tab.cap < tot * sizeof(G1AEntry) || d.kc_st.cap < tot) {  // grow, keeping the old entries
+    DevBuf nt, ns;
+    void* p;
+    if (ensure_buf(nt, tot * sizeof(G1AEntry), &p) || ensure_buf(ns, tot, &p)) return -1;
+    if (first) {
+      HCHK(hipMemcpyAsync(nt.p, d.kc_tab.p, first * sizeof(G1AEntry), hipMemcpyDeviceToDevice, d.stream));
+      HCHK(hipMemcpyAsync(ns.p, d.kc_st.p, first, hipMemcpyDeviceToDevice, d.stream));
+      HCHK(hipStreamSynchronize(d.stream));
+    }
+    if (d.kc_tab.p) HCHK(hipFree(d.kc_tab.p));
+    if (d.kc_st.p) HCHK(hipFree(d.kc_st.p));
+    d.kc_tab = nt;
+    d.kc_st = ns;
+  }
+  uint8_t* dpk;
+  if (upload(d, I_PK, keys, 48 * m, &dpk)) return -1;
+  TIMED(d, "k_dec_pk", d.stream,
+        launch_dec_pk(dpk, (uint32_t)m, (G1AEntry*)d.kc_tab.p + first, (uint8_t*)d.kc_st.p + first, d.stream));
+  HCHK(hipStreamSynchronize(d.stream));
+  return 0;
+}
+
 bool kc_lookup(const uint8_t* pks, size_t m, std::vector<uint32_t>& idx) {
   std::lock_guard<std::mutex> lk(g_kc_mu);
   if (g_kc_map.empty()) return false;
@@ -1689,58 +1730,77 @@ size_t hbls_pk_entry_bytes(void) { return sizeof(G1AEntry); }
 
 int hbls_pubkey_cache_add(const uint8_t* pks, size_t n) {
   if (ensure_init()) return -1;
-  std::lock_guard<std::mutex> lk(g_kc_mu);
+  std::lock_guard<std::mutex> al(g_kc_add_mu);
   std::vector<uint8_t> fresh;
   std::unordered_map<std::string, uint32_t> add;
-  for (size_t k = 0; k < n; k++) {
-    std::string key((const char*)pks + 48 * k, 48);
-    if (g_kc_map.count(key) || add.count(key)) continue;
-    add.emplace(key, (uint32_t)(g_kc_n + add.size()));
-    fresh.insert(fresh.end(), pks + 48 * k, pks + 48 * k + 48);
+  {
+    std::lock_guard<std::mutex> lk(g_kc_mu);
+    for (size_t k = 0; k < n; k++) {
+      std::string key((const char*)pks + 48 * k, 48);
+      if (g_kc_map.count(key) || add.count(key)) continue;
+      add.emplace(key, (uint32_t)(g_kc_n + add.size()));
+      fresh.insert(fresh.end(), pks + 48 * k, pks + 48 * k + 48);
+    }
   }
   const size_t m = add.size();
   if (m == 0) return 0;
   if (g_kc_n + m > 0xffffffffull) return set_err("pubkey cache full");
-  for (Dev* dp : g_devs) {
-    Dev& d = *dp;
-    std::lock_guard<std::mutex> dl(d.mu);
-    HCHK(hipSetDevice(d.ord));
-    const size_t tot = g_kc_n + m;
-    if (d.kc_tab.cap < tot * sizeof(G1AEntry) || d.kc_st.cap < tot) {  // grow, keeping the old entries
-      DevBuf nt, ns;
-      void* p;
-      if (ensure_buf(nt, tot * sizeof(G1AEntry), &p) || ensure_buf(ns, tot, &p)) return -1;
-      if (g_kc_n) {
-        HCHK(hipMemcpyAsync(nt.p, d.kc_tab.p, g_kc_n * sizeof(G1AEntry), hipMemcpyDeviceToDevice, d.stream));
-        HCHK(hipMemcpyAsync(ns.p, d.kc_st.p, g_kc_n, hipMemcpyDeviceToDevice, d.stream));
-        HCHK(hipStreamSynchronize(d.stream));
-      }
-      if (d.kc_tab.p) HCHK(hipFree(d.kc_tab.p));
-      if (d.kc_st.p) HCHK(hipFree(d.kc_st.p));
-      d.kc_tab = nt;
-      d.kc_st = ns;
-    }
-    uint8_t* dpk;
-    if (upload(d, I_PK, fresh.data(), fresh.size(), &dpk)) return -1;
-    TIMED(d, "k_dec_pk", d.stream,
-          launch_dec_pk(dpk, (uint32_t)m, (G1AEntry*)d.kc_tab.p + g_kc_n, (uint8_t*)d.kc_st.p + g_kc_n, d.stream));
-    HCHK(hipStreamSynchronize(d.stream));
+  for (Dev* dp : g_devs) {  // the device work under each Dev::mu in turn, g_kc_mu not held
+    std::lock_guard<std::mutex> dl(dp->mu);
+    if (kc_fill(*dp, fresh.data(), g_kc_n, m)) return -1;
   }
+  g_kc_keys.insert(g_kc_keys.end(), fresh.begin(), fresh.end());
+  std::lock_guard<std::mutex> lk(g_kc_mu);  // publish: lookups see the entries only now
   for (auto& kv : add) g_kc_map.emplace(kv.first, kv.second);
   g_kc_n += m;
   return 0;
 }
 
 int hbls_pubkey_cache_clear(void) {
+  std::lock_guard<std::mutex> al(g_kc_add_mu);
   std::lock_guard<std::mutex> lk(g_kc_mu);
   g_kc_map.clear();
   g_kc_n = 0;
+  g_kc_keys.clear();
   return 0;
 }
 
 size_t hbls_pubkey_cache_size(void) {
   std::lock_guard<std::mutex> lk(g_kc_mu);
   return g_kc_n;
+}
+
+// Test switch of the in-process multi-device split: every device of the mask is driven through
+// `copies` contexts (streams, workspaces, host thread), so host-buffer calls shard over them as
+// over several GPUs (for_each_device) on a one-GPU box.  Call while no other call is in flight.
+int hbls_debug_split(uint32_t copies) {
+  if (ensure_init()) return -1;
+  if (copies == 0 || copies > 16) return set_err("hbls_debug_split: copies must be in 1..16");
+  std::lock_guard<std::mutex> il(g_init_mu);
+  std::lock_guard<std::mutex> al(g_kc_add_mu);
+  std::vector<Dev*> devs;
+  g_split_pool.resize(g_base_devs.size());
+  for (size_t bi = 0; bi < g_base_devs.size(); bi++) {
+    Dev* b = g_base_devs[bi];
+    std::vector<Dev*>& pool = g_split_pool[bi];
+    devs.push_back(b);
+    for (uint32_t c = 1; c < copies; c++) {
+      if (pool.size() < c) {
+        Dev* d;
+        if (dev_create(b->ord, &d)) return -1;
+        pool.push_back(d);
+      }
+      Dev* d = pool[c - 1];
+      d->timing = b->timing;
+      d->serial = b->serial;
+      std::lock_guard<std::mutex> dl(d->mu);
+      if (hipSetDevice(d->ord) != hipSuccess) return set_err("hipSetDevice failed");
+      if (g_kc_n && kc_fill(*d, g_kc_keys.data(), 0, g_kc_n)) return -1;  // the same key cache
+      devs.push_back(d);
+    }
+  }
+  g_devs = devs;
+  return 0;
 }
 
 int hbls_decompress_pubkeys_device(const uint8_t* pks, size_t n, void* table, uint8_t* status, void* stream) {

@@ -90,9 +90,10 @@ __global__ __launch_bounds__(64) void k_attestation_roots(const uint8_t* __restr
   const Chunk n45 = h2(tgt, z);
   const Chunk n67 = h2(z, z);
   const Chunk root = h2(h2(n01, n23), h2(n45, n67));
-  uint32_t d = dom_idx ? dom_idx[i] : 0u;
-  if (d >= n_domains) d = 0;  // validated on the host for host-buffer calls
-  chunk_store(roots + 32ull * i, h2(root, chunk_load(domains + 32ull * d)));
+  const uint32_t d = dom_idx ? dom_idx[i] : 0u;
+  // an out-of-range domain index (validated on the host for host-buffer calls) yields the all-zero
+  // root, never a root under another domain: no signature over a real signing root verifies on it
+  chunk_store(roots + 32ull * i, d < n_domains ? h2(root, chunk_load(domains + 32ull * d)) : chunk_zero());
 }
 
 // One lane per object root: roots[i] = SigningData{object_roots[i], domains[dom_idx[i]]}.HTR
@@ -102,9 +103,9 @@ __global__ __launch_bounds__(64) void k_signing_roots(const uint8_t* __restrict_
                                                      uint8_t* __restrict__ roots) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  uint32_t d = dom_idx ? dom_idx[i] : 0u;
-  if (d >= n_domains) d = 0;
-  chunk_store(roots + 32ull * i, h2(chunk_load(obj + 32ull * i), chunk_load(domains + 32ull * d)));
+  const uint32_t d = dom_idx ? dom_idx[i] : 0u;
+  chunk_store(roots + 32ull * i,
+              d < n_domains ? h2(chunk_load(obj + 32ull * i), chunk_load(domains + 32ull * d)) : chunk_zero());
 }
 
 void launch_attestation_roots(const uint8_t* data, uint32_t n, const uint8_t* domains, uint32_t n_domains,

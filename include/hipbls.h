@@ -108,6 +108,13 @@ int hbls_pubkey_cache_add(const uint8_t* pks, size_t n);
 int hbls_pubkey_cache_clear(void);
 size_t hbls_pubkey_cache_size(void);
 
+/* Test switch of the in-process multi-device split (charon is one process over every GPU of the
+ * node, app/app.go:131): every device of the mask is driven through `copies` contexts (own streams,
+ * workspaces and host thread), so the host-buffer entry points shard their items over them exactly
+ * as over several GPUs, on a one-GPU machine.  1 restores one context per device.  Call while no
+ * other call is in flight.  Results never depend on it. */
+int hbls_debug_split(uint32_t copies);
+
 /* Sign (herumi.go:306-316) and SecretToPublicKey (herumi.go:66-79), batched.
  * Sign status in {OK, BAD_SECRET}; SecretToPublicKey additionally rejects the zero key. */
 int hbls_sign_batch(const uint8_t* sks, const uint8_t* msgs, const uint64_t* msg_off,
@@ -143,8 +150,10 @@ int hbls_threshold_aggregate_device(const uint8_t* sigs, const int64_t* idx, con
                                     void* stream);
 
 /* Attestation signing roots on device buffers (see hbls_attestation_signing_roots); dom_idx
- * entries must be < n_domains (out-of-range entries use domain 0).  Writes the messages a slot
- * then hashes (hbls_hash_to_g2_device / hbls_slot_device msgs). */
+ * entries must be < n_domains: the device path cannot return a per-call error without a host
+ * synchronisation, so an out-of-range entry yields the all-zero root (never a root under another
+ * domain; no signature over a real signing root verifies against it -- the item fails closed).
+ * Writes the messages a slot then hashes (hbls_hash_to_g2_device / hbls_slot_device msgs). */
 int hbls_attestation_signing_roots_device(const uint8_t* data, size_t n, const uint8_t* domains, size_t n_domains,
                                           const uint32_t* dom_idx, uint8_t* roots, void* stream);
 

@@ -3,8 +3,11 @@
 
 The sharded cluster must be the unsharded one split in rank order (weak scaling: rank r owns
 validators [r*V, (r+1)*V)), and after the exchange every rank must hold every rank's verdicts,
-aggregates and statuses in global validator order.  The per-rank slot results are stand-ins
-(deterministic bytes derived from each validator's shares); the GPU computes the real ones.
+aggregates and statuses in global validator order.  The exchange is bench.py's own code
+(shard.SlotExchange, with gloo in place of the library's RCCL all-gather): several slots in flight
+over two output sets, every rank issuing its collectives in the same (slot, field) order.  The
+per-rank slot results are stand-ins (deterministic bytes derived from each validator's shares and
+the slot number); the GPU computes the real ones.
 """
 
 import os
@@ -16,17 +19,19 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from charon_amd import synth
-from charon_amd.shard import SlotExchange, max_over_ranks, owned_validators
+from charon_amd.shard import FIELDS, SlotExchange, gloo_allgather, max_over_ranks, owned_validators
 
 V, N, T, WORLD = 3, 4, 3, 2
 
 
-def _slot_results(cl):
-    """Stand-in slot outputs of one shard: verdict byte per partial, 96 B and a status per validator."""
-    vst = torch.tensor([sk[0] % 5 for sk in cl.share_sks], dtype=torch.uint8)
-    tout = torch.tensor(list(b"".join(r * 3 for r in cl.root_sks)), dtype=torch.uint8)
-    tst = torch.tensor([r[-1] % 3 for r in cl.root_sks], dtype=torch.uint8)
-    return vst, tout, tst
+def _slot_results(cl, slot=0):
+    """Stand-in slot outputs of one shard: verdict byte per partial, 96 B, an aggregation status and
+    a post-aggregate verification status per validator."""
+    vst = torch.tensor([(sk[0] + slot) % 5 for sk in cl.share_sks], dtype=torch.uint8)
+    tout = torch.tensor([(b + slot) % 256 for b in b"".join(r * 3 for r in cl.root_sks)], dtype=torch.uint8)
+    tst = torch.tensor([(r[-1] + slot) % 3 for r in cl.root_sks], dtype=torch.uint8)
+    ast = torch.tensor([(r[-2] + slot) % 4 for r in cl.root_sks], dtype=torch.uint8)
+    return {"vst": vst, "tout": tout, "tst": tst, "ast": ast}
 
 
 def _worker(rank, port, errq):
@@ -41,18 +46,29 @@ def _worker(rank, port, errq):
         assert cl.root_sks == full.root_sks[first:first + V]
         assert cl.share_sks == full.share_sks[first * N:(first + V) * N]
         assert [cl.msgs[m] for m in cl.msg_of_validator] == [full.msgs[m] for m in full.msg_of_validator][first:first + V]
-        xchg = SlotExchange(WORLD, V, N, "cpu")
-        xchg.exchange(*_slot_results(cl))
-        want = [torch.cat(x) for x in zip(*[_slot_results(synth.make_cluster(V, N, T, first_validator=owned_validators(r, V).start))
-                                             for r in range(WORLD)])]
-        assert torch.equal(xchg.vst_all, want[0])
-        assert torch.equal(xchg.tout_all, want[1])
-        assert torch.equal(xchg.tst_all, want[2])
-        assert torch.equal(xchg.tout_all, _slot_results(full)[1])  # global validator order
-        assert xchg.all_ok() == bool((want[0] == 0).all() and (want[2] == 0).all())
+        shards = [synth.make_cluster(V, N, T, first_validator=owned_validators(r, V).start) for r in range(WORLD)]
+        exch = SlotExchange(WORLD, rank, {"vst": V * N, "tout": V * 96, "tst": V, "ast": V}, "cpu", gloo_allgather)
+        sets = [exch.gather_buffers() for _ in range(2)]  # two slots in flight, as bench.py --inflight 2
+        for slot in range(5):
+            recv = sets[slot % 2]
+            assert exch.exchange(_slot_results(cl, slot), recv) == slot
+            want = {f: torch.cat([_slot_results(sh, slot)[f] for sh in shards]) for f in FIELDS}
+            for f in FIELDS:
+                assert torch.equal(recv[f], want[f]), (slot, f)
+                for r in range(WORLD):
+                    assert torch.equal(exch.block(recv, f, r), _slot_results(shards[r], slot)[f])
+            # global validator order: the unsharded cluster's aggregates
+            assert torch.equal(recv["tout"], _slot_results(full, slot)["tout"])
+        # every rank issued the same collectives in the same order
+        logs = [None] * WORLD
+        dist.all_gather_object(logs, exch.issued)
+        assert logs[0] == logs[1] == [(k, f) for k in range(5) for f in FIELDS], logs
         with pytest.raises(ValueError):
-            xchg.exchange(torch.zeros(1, dtype=torch.uint8), torch.zeros(1, dtype=torch.uint8),
-                          torch.zeros(1, dtype=torch.uint8))
+            bad = dict(_slot_results(cl))
+            bad["vst"] = torch.zeros(1, dtype=torch.uint8)
+            exch.exchange(bad, sets[0])
+        with pytest.raises(ValueError):
+            SlotExchange(WORLD, rank, {"votes": 1}, "cpu", gloo_allgather)
         # bench.py reports throughput against the slowest rank
         assert max_over_ranks(1.5 + rank, "cpu") == 1.5 + (WORLD - 1)
         dist.barrier()
