@@ -14,6 +14,7 @@ calls.  INTEGRATION.md §3 gives the same changes as Go patches.
   dkg_agg_lock_hash_sig           dkg/dkg.go:659-703 (Verify of every partial + plain Aggregate)
   dkg_verify_lock_multisig        dkg/dkg.go:595-598 (VerifyAggregate of that aggregate)
   exit_aggregate                  app/obolapi/exit.go:165-194 (ThresholdAggregate of the exit partials)
+  exit_aggregate_batch            cmd/exit_fetch.go:120-137 --all: every validator's exit partials in one batch
 
 First-error semantics.  The reference loops check item by item and return at the first failure.
 A batch call verifies everything at once, so each mirror (i) runs the cheap per-item pre-checks
@@ -283,3 +284,27 @@ def exit_aggregate(impl, partial_sigs: Sequence[Optional[bytes]]) -> bytes:
     if sts[0] != OK:
         raise _wrap("partial signatures threshold aggregate", _TA_ERR.get(sts[0], "cannot combine signatures"))
     return outs[0]
+
+
+def exit_aggregate_batch(impl, validators: Sequence[Tuple[str, Sequence[Optional[bytes]]]]) -> List[bytes]:
+    """`charon exit fetch --all` (cmd/exit_fetch.go:120-137) with INTEGRATION.md's
+    AggregateFullExits: every validator's fetched exit partials (entry i = share i+1's signature or
+    None) threshold-aggregated in ONE batch; the first validator (in lock order) whose aggregation
+    fails aborts with "load full exit data from Obol API: partial signatures threshold aggregate:
+    <error>"."""
+    groups = []
+    for _, partial_sigs in validators:
+        group = {}
+        for i, s in enumerate(partial_sigs):
+            if not s:
+                continue
+            if len(s) != 96:
+                raise _wrap("load full exit data from Obol API", _wrap("invalid partial signature", _LEN_ERR).args[0])
+            group[i + 1] = s
+        groups.append(group)
+    outs, sts = impl.threshold_aggregate_batch(groups) if groups else ([], [])
+    for st in sts:
+        if st != OK:
+            raise _wrap("load full exit data from Obol API",
+                        "partial signatures threshold aggregate: " + _TA_ERR.get(st, "cannot combine signatures"))
+    return outs

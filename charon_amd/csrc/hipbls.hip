@@ -244,6 +244,8 @@ size_t g_ta_chunk = 4;   // HBLS_TA_CHUNK: members per lane of k_ta_msm (<= TA_C
 // the same size t; 0 = auto (about TA_JOINT_LANES lanes, at most t and 8), 1 = one ladder per member
 // (k_ta_straus)
 std::atomic<size_t> g_ta_joint{0};
+// HBLS_TA_SMALL=0: no small-scalar aggregation (threshold.hip k_ta_small; ta_small.h)
+bool g_ta_small = true;
 constexpr size_t TA_JOINT_LANES = 98304;
 // HBLS_FE_BATCH: verifications of at least this many groups check FE_BATCH groups per final
 // exponentiation (vgroup.hip; 0 = one final exponentiation per group)
@@ -275,6 +277,7 @@ enum WsId {
   W_FBLINES,
   W_APK, W_APKST, W_ASIG, W_APR, W_ASR,          // folded aggregates (post-aggregate verification)
   W_TAPTS, W_TADST, W_TAMST, W_TADIG, W_TATAB, W_TAJ,  // ThresholdAggregate / Aggregate
+  W_TACSM, W_TASDIG, W_TASOK, W_TASDONE, W_TASTAB, W_TANONUNI,  // its small-scalar path
   W_SEGA, W_SEGB, W_SEGSTA, W_SEGSTB, W_VAPT, W_VAPV, W_PLAN,  // VerifyAggregate key reduction
   W_PCNT, W_PCOFF, W_PCFIRST, W_PCCOUNT, W_COEF, W_RT1, W_RT2,  // chunk plan + multi-scalar RLC
   W_TPCNT, W_TPCOFF, W_TPCFIRST, W_TPCCOUNT,                    // chunk plan of the aggregation
@@ -467,6 +470,7 @@ int init_mask(uint32_t mask) {
   g_ta_msm = env_size("HBLS_TA_MSM", 0) != 0;
   g_ta_chunk = std::min<size_t>(TA_CHUNK, std::max<size_t>(1, env_size("HBLS_TA_CHUNK", g_ta_chunk)));
   g_ta_joint = std::min<size_t>(8, env_size("HBLS_TA_JOINT", g_ta_joint.load()));
+  g_ta_small = env_size("HBLS_TA_SMALL", 1) != 0;
   g_fe_batch_min = env_size("HBLS_FE_BATCH", g_fe_batch_min.load());
   g_slot_msm_min = env_size("HBLS_SLOT_MSM", g_slot_msm_min.load());
   g_stagger = env_size("HBLS_STAGGER", 0) != 0;
@@ -585,14 +589,38 @@ int ta_tail(Dev& d, Ws& w, const HmEntry* pts, const uint32_t* src, const uint8_
     jc = std::min<size_t>(std::min<size_t>(jc, t_u), 8);
     if (jc <= 1) jc = 0;
   }
-  const size_t tab_bytes = jc ? ta_joint_table_bytes((uint32_t)n_groups, (uint32_t)t_u, (uint32_t)jc)
+  // (the joint path's guarded per-member fallback reads the same buffer: the larger of the two)
+  const size_t tab_bytes = jc ? std::max(ta_joint_table_bytes((uint32_t)n_groups, (uint32_t)t_u, (uint32_t)jc),
+                                         ta_table_bytes((uint32_t)np))
                               : ta_table_bytes((uint32_t)np);
   if (wsbuf(w, W_TATAB, tab_bytes, (uint8_t**)&tab)) return -1;
   if (np) {
     if (src) launch_ta_member_status(mst_in, src, (uint32_t)np, mst, s);
     else HCHK(hipMemcpyAsync(mst, mst_in, np, hipMemcpyDeviceToDevice, s));
     HCHK(hipGetLastError());
-    TIMED(d, "k_ta_lambda", s, launch_ta_lambda(didx, dgoff, (uint32_t)n_groups, (uint32_t)np, mode, dig, mst, s));
+    // t_u > 1: the joint and small-scalar paths assume groups of exactly t_u members; k_ta_lambda
+    // flags any other layout in nonuni (the per-member ladders then run instead)
+    uint8_t* nonuni = nullptr;
+    if (mode == 0 && t_u > 1) {
+      if (wsbuf(w, W_TANONUNI, 1, &nonuni)) return -1;
+      HCHK(hipMemsetAsync(nonuni, 0, 1, s));
+    }
+    TIMED(d, "k_ta_lambda", s,
+          launch_ta_lambda(didx, dgoff, (uint32_t)n_groups, (uint32_t)np, mode, dig, mst, s, (uint32_t)t_u, nonuni));
+    // small-scalar path first (groups of exactly t members, wave-uniform index sets); the
+    // per-member ladders below skip the groups it aggregated
+    uint8_t* sdone = nullptr;
+    if (mode == 0 && !g_ta_msm && g_ta_small && t_u >= 2 && t_u <= (size_t)TA_SMALL_MAX) {
+      int64_t* csm;
+      TaDigits* sdig;
+      uint8_t *sok, *stab;
+      if (wsbuf(w, W_TACSM, np, &csm) || wsbuf(w, W_TASDIG, n_groups, &sdig) || wsbuf(w, W_TASOK, n_groups, &sok) ||
+          wsbuf(w, W_TASDONE, n_groups, &sdone) || wsbuf(w, W_TASTAB, ta_small_table_bytes((uint32_t)n_groups), &stab))
+        return -1;
+      TIMED(d, "k_ta_small", s,
+            launch_ta_small(pts, src, didx, (uint32_t)n_groups, (uint32_t)t_u, csm, sdig, sok, stab, sdone, pj, s,
+                            nonuni));
+    }
     if (g_ta_msm && n_groups) {
       // chunks of at most TA_CHUNK members share their ladder's doublings (k_ta_msm)
       const size_t max_chunks = np / g_ta_chunk + n_groups;
@@ -606,9 +634,12 @@ int ta_tail(Dev& d, Ws& w, const HmEntry* pts, const uint32_t* src, const uint8_
             launch_ta_msm(pts, src, dig, tab, pcf, pcc, pcoff + n_groups, (uint32_t)max_chunks, mode, pj, s));
     } else if (jc) {
       TIMED(d, "k_ta_straus", s,
-            launch_ta_joint(pts, src, dig, (uint32_t)n_groups, (uint32_t)t_u, (uint32_t)jc, tab, pj, s));
+            launch_ta_joint(pts, src, dig, (uint32_t)n_groups, (uint32_t)t_u, (uint32_t)jc, tab, pj, s, sdone, nonuni));
+      // groups not all of t_u members: the per-member ladders instead (nothing unless nonuni)
+      TIMED(d, "k_ta_straus", s,
+            launch_ta_straus(pts, src, dig, (uint32_t)np, (uint32_t)n_groups, tab, pj, s, nullptr, nonuni));
     } else {
-      TIMED(d, "k_ta_straus", s, launch_ta_straus(pts, src, dig, (uint32_t)np, (uint32_t)n_groups, tab, pj, s));
+      TIMED(d, "k_ta_straus", s, launch_ta_straus(pts, src, dig, (uint32_t)np, (uint32_t)n_groups, tab, pj, s, sdone));
     }
   }
   TIMED(d, "k_group_sum", s,

@@ -3,6 +3,7 @@
 // pairing kernel; vbatch.hip: batched verification; threshold.hip: ThresholdAggregate).
 #pragma once
 #include "ops.h"
+#include "ta_small.h"
 
 // Occupancy targets (waves per SIMD) of the heavy kernels: 1 lets the compiler use all 512
 // registers of a lane, 2 gives each wave 256, 3 gives 168 (spilling the rest to scratch).  Chosen
@@ -95,21 +96,35 @@ struct RlcKey {
 };
 
 // Staged ThresholdAggregate (threshold.hip).  src (nullable): member j's point is pts[src[j]].
+// nonuni (nullable, zeroed by the caller): set when t_u != 0 and some group does not hold exactly
+// t_u members at offset g t_u -- the joint and small-scalar paths then stand down (nonuni below)
+// and the per-member ladders run instead
 void launch_ta_lambda(const int64_t* idx, const uint32_t* grp_off, uint32_t n_groups, uint32_t n_partials, int mode,
-                      TaDigits* dig, uint8_t* mstat, hipStream_t s);
+                      TaDigits* dig, uint8_t* mstat, hipStream_t s, uint32_t t_u = 0, uint8_t* nonuni = nullptr);
 constexpr uint32_t TA_CHUNK = 8;  // members per lane of k_ta_msm
 void launch_ta_table(const HmEntry* pts, const uint32_t* src, uint32_t n_partials, void* tab, hipStream_t s);
 void launch_ta_msm(const HmEntry* pts, const uint32_t* src, const TaDigits* dig, void* tab, const uint32_t* cfirst,
                    const uint32_t* ccount, const uint32_t* total, uint32_t max_chunks, int mode, G2JEntry* out,
                    hipStream_t s);
 size_t ta_table_bytes(uint32_t n_partials);
+// guard (nullable): nothing unless *guard != 0 (then one lane per member in plain order, skip unused)
 void launch_ta_straus(const HmEntry* pts, const uint32_t* src, const TaDigits* dig, uint32_t n_partials,
-                      uint32_t n_groups, void* tab, G2JEntry* out, hipStream_t s);
+                      uint32_t n_groups, void* tab, G2JEntry* out, hipStream_t s, const uint8_t* skip = nullptr,
+                      const uint8_t* guard = nullptr);
 // joint ladders over chunks of c (<= 8) members of a validator, every group of exactly t members
 // (threshold.hip k_ta_jtab, k_ta_jladder, k_ta_jgeneral); table workspace of ta_joint_table_bytes
 size_t ta_joint_table_bytes(uint32_t n_groups, uint32_t t, uint32_t c);
 void launch_ta_joint(const HmEntry* pts, const uint32_t* src, const TaDigits* dig, uint32_t n_groups, uint32_t t,
-                     uint32_t c, void* tab, G2JEntry* out, hipStream_t s);
+                     uint32_t c, void* tab, G2JEntry* out, hipStream_t s, const uint8_t* skip = nullptr,
+                     const uint8_t* nonuni = nullptr);
+// small-scalar aggregation (threshold.hip k_ta_sprep / k_ta_small / k_ta_sladder, ta_small.h): groups
+// of exactly t members (idx: their share indices); done[g] != 0 for the groups it aggregated (their
+// sums at out[g t], infinity at the other members), the rest left to the per-member ladders
+// (skip = done).  Workspace: csm [n_groups t], sdig / sok / done [n_groups], tab ta_small_table_bytes.
+size_t ta_small_table_bytes(uint32_t n_groups);
+void launch_ta_small(const HmEntry* pts, const uint32_t* src, const int64_t* idx, uint32_t n_groups, uint32_t t,
+                     int64_t* csm, TaDigits* sdig, uint8_t* sok, void* tab, uint8_t* done, G2JEntry* out,
+                     hipStream_t s, const uint8_t* nonuni);
 void launch_ta_member_status(const uint8_t* sig_st, const uint32_t* src, uint32_t n_partials, uint8_t* mstat,
                              hipStream_t s);
 

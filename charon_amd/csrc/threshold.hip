@@ -19,8 +19,11 @@
 // same group element, so the 96-byte output is byte-identical to herumi's Sign.Recover.
 #define HB_FAST_FPMUL 1
 #include "layout.h"
+#include "ta_small.h"
 
 namespace hb {
+
+static inline unsigned blocks_of(size_t n, unsigned per) { return (unsigned)((n + per - 1) / per); }
 
 // u (8 little-endian limbs, < 2^256) <- u / z, returns u mod z   (z = |x|, bit-serial: the three
 // divisions per partial cost a few Fp products)
@@ -54,7 +57,8 @@ __device__ __forceinline__ uint32_t find_group_ta(const uint32_t* grp_off, uint3
 // index 0 mod r, or duplicated) is flagged unless the partial is already undecodable.
 __global__ __launch_bounds__(64) void k_ta_lambda(const int64_t* __restrict__ idx, const uint32_t* __restrict__ grp_off,
                                                   uint32_t n_groups, uint32_t n_partials, int mode,
-                                                  TaDigits* __restrict__ dig, uint8_t* __restrict__ mstat) {
+                                                  TaDigits* __restrict__ dig, uint8_t* __restrict__ mstat,
+                                                  uint32_t t_u, uint8_t* __restrict__ nonuni) {
   uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n_partials) return;
   TaDigits d;
@@ -62,6 +66,7 @@ __global__ __launch_bounds__(64) void k_ta_lambda(const int64_t* __restrict__ id
   d.a[1] = d.a[2] = d.a[3] = 0;
   uint32_t g = find_group_ta(grp_off, n_groups, j);
   uint32_t b = grp_off[g], en = grp_off[g + 1];
+  if (nonuni && t_u && (en - b != t_u || b != g * t_u)) *nonuni = 1;
   if (mode == 0 && en - b > 1) {  // k = 1: the single partial is returned as is
     // lambda_j = prod_m x_m / prod_m (x_m - x_j).  Share indices are small integers, so each
     // denominator factor normally comes from the 1/d table (no Fr inversion); anything else
@@ -161,18 +166,22 @@ __device__ __forceinline__ void aff_store(uint4* wt, int e, const Fp2& x, const 
 __global__ KB_OCC(HB_OCC_STRAUS) void k_ta_straus(const HmEntry* __restrict__ pts, const uint32_t* __restrict__ src,
                                                      const TaDigits* __restrict__ dig,
                                                      uint32_t n_partials, uint32_t n_groups, uint32_t t_uniform,
-                                                     uint4* __restrict__ tab, G2JEntry* __restrict__ out) {
+                                                     uint4* __restrict__ tab, G2JEntry* __restrict__ out,
+                                                     const uint8_t* __restrict__ skip, const uint8_t* __restrict__ guard) {
 #if defined(__HIP_DEVICE_COMPILE__)
   __shared__ int8_t naf[4][66];
   __shared__ int naf_top;
+  if (guard && *guard == 0) return;
   const int lane = (int)(threadIdx.x & 63u);
   const uint32_t item = blockIdx.x * 64 + (uint32_t)lane;
-  const bool valid = item < n_partials;
-  const uint32_t it = valid ? item : n_partials - 1;
+  const uint32_t it = item < n_partials ? item : n_partials - 1;
   // member of this lane: with t members in every group, lane L takes member j = L / n_groups of
   // validator v = L % n_groups, so a wave holds the same share position of 64 validators -- whose
   // Lagrange digits agree whenever the validators' index sets do (the common slot)
   const uint32_t m = t_uniform ? (it % n_groups) * t_uniform + it / n_groups : it;
+  // skip (nullable, t_uniform only): groups the small-scalar path aggregated
+  const bool valid = item < n_partials && !(skip && t_uniform && skip[m / t_uniform]);
+  if (!__any(valid)) return;
   uint4* wt = tab + (size_t)blockIdx.x * 16 * TA_TAB_QUADS * 64 + lane;
   const TaDigits d = dig[m];
   bool same = true;
@@ -398,16 +407,26 @@ constexpr int TA_JOINT_MAX = 8;
 #if defined(__HIP_DEVICE_COMPILE__)
 struct JointLane {
   uint32_t L, cnt, m0;
-  bool valid, uniform;
+  bool valid, uniform, any;
   uint4* wt;
 };
+// skip (nullable): groups already aggregated by the small-scalar path (k_ta_small); their lanes
+// neither compute for the uniformity test's sake nor store.  nonuni (nullable): the groups are not
+// all of t members (k_ta_lambda): no lane is valid (the per-member ladders run instead)
 __device__ __forceinline__ JointLane joint_lane(const TaDigits* __restrict__ dig, uint32_t n_groups, uint32_t t,
-                                                uint32_t c, uint4* __restrict__ tab) {
+                                                uint32_t c, uint4* __restrict__ tab, const uint8_t* __restrict__ skip,
+                                                const uint8_t* __restrict__ nonuni) {
   JointLane j;
+  if (nonuni && *nonuni) {
+    j.valid = j.uniform = j.any = false;
+    j.L = j.cnt = j.m0 = 0;
+    j.wt = tab;
+    return j;
+  }
   const int lane = (int)(threadIdx.x & 63u);
   const uint32_t n_chunks = (t + c - 1) / c, n_lanes = n_groups * n_chunks;
   j.L = blockIdx.x * 64 + (uint32_t)lane;
-  j.valid = j.L < n_lanes;
+  j.valid = j.L < n_lanes && !(skip && skip[j.L % n_groups]);
   const uint32_t Lc = j.valid ? j.L : n_lanes - 1;
   const uint32_t q = Lc / n_groups, v = Lc % n_groups;
   const uint32_t j0 = q * c;
@@ -424,6 +443,7 @@ __device__ __forceinline__ JointLane joint_lane(const TaDigits* __restrict__ dig
     }
   }
   j.uniform = __all(same);
+  j.any = __any(j.valid);
   return j;
 }
 __device__ __forceinline__ void joint_store(G2JEntry* __restrict__ out, const JointLane& j, const G2J& R) {
@@ -436,20 +456,22 @@ __device__ __forceinline__ void joint_store(G2JEntry* __restrict__ out, const Jo
 
 __global__ KB_OCC(HB_OCC_STRAUS) void k_ta_jtab(const HmEntry* __restrict__ pts, const uint32_t* __restrict__ src,
                                                    const TaDigits* __restrict__ dig, uint32_t n_groups, uint32_t t,
-                                                   uint32_t c, uint4* __restrict__ tab) {
+                                                   uint32_t c, uint4* __restrict__ tab, const uint8_t* __restrict__ skip,
+                                                   const uint8_t* __restrict__ nonuni) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  const JointLane j = joint_lane(dig, n_groups, t, c, tab);
-  if (j.uniform) odd_tables_affine(j.wt, pts, src, j.m0, j.cnt);
+  const JointLane j = joint_lane(dig, n_groups, t, c, tab, skip, nonuni);
+  if (j.any && j.uniform) odd_tables_affine(j.wt, pts, src, j.m0, j.cnt);
 #endif
 }
 
 __global__ KB_OCC(HB_OCC_STRAUS) void k_ta_jladder(const TaDigits* __restrict__ dig, uint32_t n_groups, uint32_t t,
-                                                      uint32_t c, uint4* __restrict__ tab, G2JEntry* __restrict__ out) {
+                                                      uint32_t c, uint4* __restrict__ tab, G2JEntry* __restrict__ out,
+                                                      const uint8_t* __restrict__ skip, const uint8_t* __restrict__ nonuni) {
 #if defined(__HIP_DEVICE_COMPILE__)
   __shared__ int8_t naf[TA_JOINT_MAX][4][66];
   __shared__ int naf_top;
-  const JointLane j = joint_lane(dig, n_groups, t, c, tab);
-  if (!j.uniform) return;  // wave-uniform
+  const JointLane j = joint_lane(dig, n_groups, t, c, tab, skip, nonuni);
+  if (!j.any || !j.uniform) return;  // wave-uniform
   if ((threadIdx.x & 63u) == 0) {
     int top = 0;
     for (uint32_t k = 0; k < j.cnt; k++) {
@@ -481,10 +503,11 @@ __global__ KB_OCC(HB_OCC_STRAUS) void k_ta_jladder(const TaDigits* __restrict__ 
 
 __global__ KB_OCC(HB_OCC_STRAUS) void k_ta_jgeneral(const HmEntry* __restrict__ pts, const uint32_t* __restrict__ src,
                                                        const TaDigits* __restrict__ dig, uint32_t n_groups, uint32_t t,
-                                                       uint32_t c, uint4* __restrict__ tab, G2JEntry* __restrict__ out) {
+                                                       uint32_t c, uint4* __restrict__ tab, G2JEntry* __restrict__ out,
+                                                       const uint8_t* __restrict__ skip, const uint8_t* __restrict__ nonuni) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  const JointLane j = joint_lane(dig, n_groups, t, c, tab);
-  if (j.uniform) return;  // wave-uniform
+  const JointLane j = joint_lane(dig, n_groups, t, c, tab, skip, nonuni);
+  if (!j.any || j.uniform) return;  // wave-uniform
   G2J R = jac_infinity<Fp2>();
   HB_NOUNROLL for (uint32_t k = 0; k < j.cnt; k++) {
     const HmEntry e = pts[src ? src[j.m0 + k] : j.m0 + k];
@@ -492,6 +515,239 @@ __global__ KB_OCC(HB_OCC_STRAUS) void k_ta_jgeneral(const HmEntry* __restrict__ 
   }
   joint_store(out, j, R);
 #endif
+}
+
+// ---------------------------------------------------------------------------------------
+// Small-scalar aggregation (ta_small.h): sigma_v = [s] (sum_j [c_j] sigma_{v,j}) with small
+// integers c_j and one scalar s per index set.  One lane per validator; a wave whose validators
+// share the index set (the common slot: parsigdb fires with the partials of the same t operators,
+// parsigex exchanges whole sets per peer) runs
+//   k_ta_small    the joint NAF ladder of the c_j (~22 bits for any index set of a cluster of up to
+//                 10 operators, shared doublings, mixed additions of +-sigma_j), then the affine
+//                 odd-multiple tables of Q = sum_j [c_j] sigma_j (one inversion), and
+//   k_ta_sladder  [s] Q: the signed width-4 NAF schedule over the four base-|x| digits of s,
+// about 5.4k Fp products per validator against 1 856 per MEMBER on the per-member ladders (13k at
+// t = 7).  Waves with mixed index sets (or splits refused by ta_small_split) leave `done` at 0 and
+// take the per-member ladders (k_ta_jtab / k_ta_jladder / k_ta_jgeneral, or k_ta_straus), which
+// skip the done groups.
+// ---------------------------------------------------------------------------------------
+
+// One lane per group of exactly t members: the split of the group's index set.
+__global__ __launch_bounds__(64) void k_ta_sprep(const int64_t* __restrict__ idx, uint32_t n_groups, uint32_t t,
+                                                 int64_t* __restrict__ csm, TaDigits* __restrict__ sdig,
+                                                 uint8_t* __restrict__ sok, const uint8_t* __restrict__ nonuni) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n_groups) return;
+  int64_t x[TA_SMALL_MAX], c[TA_SMALL_MAX];
+  const uint32_t tt = (t <= (uint32_t)TA_SMALL_MAX && !(nonuni && *nonuni)) ? t : 0u;
+  for (uint32_t k = 0; k < tt; k++) x[k] = idx[(size_t)g * t + k];
+  Fr s = fr_zero();
+  const bool ok = tt && ta_small_split(x, (int)tt, c, s);
+  for (uint32_t k = 0; k < tt; k++) csm[(size_t)g * t + k] = ok ? c[k] : 0;
+  TaDigits d;
+  d.a[0] = d.a[1] = d.a[2] = d.a[3] = 0;
+  if (ok) {
+    const Fr sc = fr_from_mont(s);
+    uint32_t u[NLR];
+    HB_UNROLL for (int i = 0; i < NLR; i++) u[i] = sc.v[i];
+    d.a[0] = divmod_xabs(u);
+    d.a[1] = divmod_xabs(u);
+    d.a[2] = divmod_xabs(u);
+    d.a[3] = ((uint64_t)u[1] << 32) | u[0];
+  }
+  sdig[g] = d;
+  sok[g] = ok ? 1 : 0;
+}
+
+#if defined(__HIP_DEVICE_COMPILE__)
+// The affine odd multiples {1, 3, 5, 7} of the four bases B_b = Q, -psi(Q), psi^2(Q), -psi^3(Q) of a
+// Jacobian Q into entries 4 b + (|d| >> 1) (the layout k_ta_jladder reads, one member), with ONE
+// inversion over the four Z (Montgomery's trick; entries 4..7 hold the running products until the
+// psi images overwrite them).  Returns false if Q is the point at infinity (the table is then
+// garbage and [s] Q = infinity).
+__device__ __forceinline__ bool odd_tables_affine_jac(uint4* wt, const G2J& Q) {
+  const bool qinf = jac_is_inf(Q);
+  Fp2 acc = f2_one();
+  {
+    const G2J J2 = jac_dbl(Q);
+    const G2J J3 = jac_add(Q, J2);
+    const G2J J5 = jac_add(J3, J2);
+    const G2J J7 = jac_add(J5, J2);
+    HB_NOUNROLL for (int j = 0; j < 4; j++) {
+      G2J J = j == 0 ? Q : j == 1 ? J3 : j == 2 ? J5 : J7;
+      if (f2_is_zero(J.Z)) J.Z = f2_one();
+      tab_store(wt, j, J);
+      f2_store_q(wt, 4 + j, 0, acc);
+      acc = f2_mul(acc, J.Z);
+    }
+  }
+  Fp2 inv = f2_inv(acc);
+  const Fp2 cx = f2_from_const(PSI_CX), cy = f2_from_const(PSI_CY);
+  const Fp2 c2x = f2_from_const(PSI2_CX), c2y = f2_from_const(PSI2_CY);
+  HB_NOUNROLL for (int j = 3; j >= 0; j--) {
+    const G2J J = tab_load(wt, j);
+    const Fp2 zi = f2_mul(inv, f2_load_q(wt, 4 + j, 0));  // 1 / Z
+    inv = f2_mul(inv, J.Z);
+    const Fp2 zi2 = f2_sqr(zi);
+    const Fp2 x = f2_mul(J.X, zi2), y = f2_mul(J.Y, f2_mul(zi2, zi));
+    aff_store(wt, j, x, y);
+    const Fp2 x2 = f2_mul(x, c2x), y2 = f2_mul(y, c2y);
+    aff_store(wt, j + 4, f2_mul(f2_conj(x), cx), f2_neg(f2_mul(f2_conj(y), cy)));
+    aff_store(wt, j + 8, x2, y2);
+    aff_store(wt, j + 12, f2_mul(f2_conj(x2), cx), f2_neg(f2_mul(f2_conj(y2), cy)));
+  }
+  return !qinf;
+}
+
+// wave-uniform small path?  ok flag, the t scalars and the digits of s agree across the wave
+__device__ __forceinline__ bool ta_small_uniform(const int64_t* __restrict__ csm, const TaDigits* __restrict__ sdig,
+                                                 const uint8_t* __restrict__ sok, uint32_t v, uint32_t t) {
+  bool same = sok[v] != 0;
+  for (uint32_t k = 0; k < t; k++) {
+    const uint64_t c = (uint64_t)csm[(size_t)v * t + k];
+    same = same && (uint32_t)c == (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)c) &&
+           (uint32_t)(c >> 32) == (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(c >> 32));
+  }
+  const TaDigits d = sdig[v];
+  HB_UNROLL for (int i = 0; i < 4; i++) {
+    const uint32_t lo = (uint32_t)d.a[i], hi = (uint32_t)(d.a[i] >> 32);
+    same = same && lo == (uint32_t)__builtin_amdgcn_readfirstlane((int)lo) &&
+           hi == (uint32_t)__builtin_amdgcn_readfirstlane((int)hi);
+  }
+  return __all(same);
+}
+#endif
+
+// One lane per validator: Q = sum_j [c_j] sigma_j (joint signed-binary NAF, the doublings shared by
+// the t members) into out[v t]; done[v] = 1, or 0 when the wave is not uniform.
+__global__ KB_OCC(HB_OCC_STRAUS) void k_ta_small(const HmEntry* __restrict__ pts, const uint32_t* __restrict__ src,
+                                                    const int64_t* __restrict__ csm, const TaDigits* __restrict__ sdig,
+                                                    const uint8_t* __restrict__ sok, uint32_t n_groups, uint32_t t,
+                                                    G2JEntry* __restrict__ out, uint8_t* __restrict__ done) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __shared__ int8_t naf[TA_SMALL_MAX][64];
+  __shared__ int naf_top;
+  const int lane = (int)(threadIdx.x & 63u);
+  const uint32_t v = blockIdx.x * 64 + (uint32_t)lane;
+  const bool valid = v < n_groups;
+  const uint32_t vc = valid ? v : n_groups - 1;
+  if (t < 2 || t > (uint32_t)TA_SMALL_MAX || !ta_small_uniform(csm, sdig, sok, vc, t)) {
+    if (valid) done[v] = 0;
+    return;  // wave-uniform
+  }
+  if (lane == 0) {  // NAF (digits +-1) of |c_k|, the sign folded in
+    int top = 0;
+    for (uint32_t k = 0; k < t; k++) {
+      const int64_t c = csm[(size_t)vc * t + k];
+      uint64_t m = (uint64_t)(c < 0 ? -c : c);  // < 2^63
+      const int sg = c < 0 ? -1 : 1;
+      for (int i = 0; i < 64; i++) {
+        int dg = 0;
+        if (m & 1u) {
+          dg = (m & 2u) ? -1 : 1;
+          m = dg > 0 ? m - 1 : m + 1;
+        }
+        naf[k][i] = (int8_t)(dg * sg);
+        if (dg && i > top) top = i;
+        m >>= 1;
+      }
+    }
+    naf_top = top;
+  }
+  __syncthreads();
+  const uint32_t m0 = vc * t;
+  G2J R = jac_infinity<Fp2>();
+  const int top = naf_top;
+  HB_NOUNROLL for (int i = top; i >= 0; i--) {
+    R = jac_dbl(R);
+    HB_NOUNROLL for (uint32_t k = 0; k < t; k++) {
+      const int dg = naf[k][i];
+      if (dg != 0) {  // wave-uniform
+        const HmEntry e = pts[src ? src[m0 + k] : m0 + k];
+        const G2A P = {e.x, dg < 0 ? f2_neg(e.y) : e.y, e.inf != 0};
+        R = jac_add_aff(R, P);
+      }
+    }
+  }
+  if (valid) {
+    out[(size_t)v * t] = {R.X, R.Y, R.Z};
+    done[v] = 1;
+  }
+#endif
+}
+
+// One lane per validator of a wave k_ta_small took: Q's affine odd-multiple tables; done[v] = 2 when
+// Q is the point at infinity ([s] Q is then infinity).
+__global__ KB_OCC(HB_OCC_STRAUS) void k_ta_stab(const G2JEntry* __restrict__ q, uint32_t n_groups, uint32_t t,
+                                                   uint4* __restrict__ tab, uint8_t* __restrict__ done) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const int lane = (int)(threadIdx.x & 63u);
+  const uint32_t v = blockIdx.x * 64 + (uint32_t)lane;
+  const bool valid = v < n_groups;
+  const uint32_t vc = valid ? v : n_groups - 1;
+  if (done[vc] == 0) return;  // wave-uniform
+  const G2JEntry e = q[(size_t)vc * t];
+  uint4* wt = tab + (size_t)blockIdx.x * 16 * TA_TAB_QUADS * 64 + lane;
+  const bool finite = odd_tables_affine_jac(wt, G2J{e.X, e.Y, e.Z});
+  if (valid && !finite) done[v] = 2;
+#endif
+}
+
+// One lane per validator of a wave k_ta_small took: [s] Q over Q's tables (k_ta_jladder's schedule
+// for one member), into the validator's first member slot of `out`, infinity into the others.
+__global__ KB_OCC(HB_OCC_STRAUS) void k_ta_sladder(const TaDigits* __restrict__ sdig, const uint8_t* __restrict__ done,
+                                                      uint32_t n_groups, uint32_t t, uint4* __restrict__ tab,
+                                                      G2JEntry* __restrict__ out) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __shared__ int8_t naf[4][66];
+  __shared__ int naf_top;
+  const int lane = (int)(threadIdx.x & 63u);
+  const uint32_t v = blockIdx.x * 64 + (uint32_t)lane;
+  const bool valid = v < n_groups;
+  const uint32_t vc = valid ? v : n_groups - 1;
+  const uint8_t dn = done[vc];
+  if (dn == 0) return;  // wave-uniform (k_ta_small decides per wave)
+  if (lane == 0) {
+    const TaDigits d = sdig[vc];
+    int top = 0;
+    for (int i = 0; i < 4; i++) top = max(top, naf4_digits(d.a[i], naf[i]));
+    naf_top = top;
+  }
+  __syncthreads();
+  const uint4* wt = tab + (size_t)blockIdx.x * 16 * TA_TAB_QUADS * 64 + lane;
+  G2J R = jac_infinity<Fp2>();
+  const int top = naf_top;
+  HB_NOUNROLL for (int i = top; i >= 0; i--) {
+    R = jac_dbl(R);
+    HB_NOUNROLL for (int b = 0; b < 4; b++) {
+      const int dg = naf[b][i];
+      if (dg != 0) {  // wave-uniform
+        const int e = 4 * b + ((dg < 0 ? -dg : dg) >> 1);
+        G2A T = {f2_load_q(wt, e, 0), f2_load_q(wt, e, 6), false};
+        if (dg < 0) T.y = f2_neg(T.y);
+        R = jac_add_aff(R, T);
+      }
+    }
+  }
+  if (!valid) return;
+  if (dn == 2) R = jac_infinity<Fp2>();
+  out[(size_t)v * t] = {R.X, R.Y, R.Z};
+  const G2J z = jac_infinity<Fp2>();
+  for (uint32_t k = 1; k < t; k++) out[(size_t)v * t + k] = {z.X, z.Y, z.Z};
+#endif
+}
+
+size_t ta_small_table_bytes(uint32_t n_groups) { return (size_t)blocks_of(n_groups, 64) * 16 * sizeof(G2JEntry) * 64; }
+
+void launch_ta_small(const HmEntry* pts, const uint32_t* src, const int64_t* idx, uint32_t n_groups, uint32_t t,
+                     int64_t* csm, TaDigits* sdig, uint8_t* sok, void* tab, uint8_t* done, G2JEntry* out,
+                     hipStream_t s, const uint8_t* nonuni) {
+  if (!n_groups) return;
+  const dim3 grid(blocks_of(n_groups, 64));
+  hipLaunchKernelGGL(k_ta_sprep, grid, dim3(64), 0, s, idx, n_groups, t, csm, sdig, sok, nonuni);
+  hipLaunchKernelGGL(k_ta_small, grid, dim3(64), 0, s, pts, src, csm, sdig, sok, n_groups, t, out, done);
+  hipLaunchKernelGGL(k_ta_stab, grid, dim3(64), 0, s, (const G2JEntry*)out, n_groups, t, (uint4*)tab, done);
+  hipLaunchKernelGGL(k_ta_sladder, grid, dim3(64), 0, s, sdig, done, n_groups, t, (uint4*)tab, out);
 }
 
 // The same aggregation as multi-scalar ladders over chunks of up to TA_CHUNK members of a group
@@ -570,13 +826,12 @@ __global__ KB_OCC(HB_OCC_STRAUS) void k_ta_msm(const HmEntry* __restrict__ pts, 
 #endif
 }
 
-static inline unsigned blocks_of(size_t n, unsigned per) { return (unsigned)((n + per - 1) / per); }
-
 void launch_ta_lambda(const int64_t* idx, const uint32_t* grp_off, uint32_t n_groups,
-                      uint32_t n_partials, int mode, TaDigits* dig, uint8_t* mstat, hipStream_t s) {
+                      uint32_t n_partials, int mode, TaDigits* dig, uint8_t* mstat, hipStream_t s, uint32_t t_u,
+                      uint8_t* nonuni) {
   if (!n_partials) return;
   hipLaunchKernelGGL(k_ta_lambda, dim3(blocks_of(n_partials, 64)), dim3(64), 0, s, idx, grp_off, n_groups,
-                     n_partials, mode, dig, mstat);
+                     n_partials, mode, dig, mstat, t_u, nonuni);
 }
 
 size_t ta_table_bytes(uint32_t n_partials) { return (size_t)blocks_of(n_partials, 64) * 16 * sizeof(G2JEntry) * 64; }
@@ -585,13 +840,15 @@ size_t ta_joint_table_bytes(uint32_t n_groups, uint32_t t, uint32_t c) {
   return (size_t)blocks_of(lanes, 64) * 16 * c * sizeof(G2JEntry) * 64;
 }
 void launch_ta_joint(const HmEntry* pts, const uint32_t* src, const TaDigits* dig, uint32_t n_groups, uint32_t t,
-                     uint32_t c, void* tab, G2JEntry* out, hipStream_t s) {
+                     uint32_t c, void* tab, G2JEntry* out, hipStream_t s, const uint8_t* skip,
+                     const uint8_t* nonuni) {
   if (!n_groups || !t || !c || c > (uint32_t)TA_JOINT_MAX) return;
   const size_t lanes = (size_t)n_groups * ((t + c - 1) / c);
   const dim3 grid(blocks_of(lanes, 64));
-  hipLaunchKernelGGL(k_ta_jtab, grid, dim3(64), 0, s, pts, src, dig, n_groups, t, c, (uint4*)tab);
-  hipLaunchKernelGGL(k_ta_jladder, grid, dim3(64), 0, s, dig, n_groups, t, c, (uint4*)tab, out);
-  hipLaunchKernelGGL(k_ta_jgeneral, grid, dim3(64), 0, s, pts, src, dig, n_groups, t, c, (uint4*)tab, out);
+  hipLaunchKernelGGL(k_ta_jtab, grid, dim3(64), 0, s, pts, src, dig, n_groups, t, c, (uint4*)tab, skip, nonuni);
+  hipLaunchKernelGGL(k_ta_jladder, grid, dim3(64), 0, s, dig, n_groups, t, c, (uint4*)tab, out, skip, nonuni);
+  hipLaunchKernelGGL(k_ta_jgeneral, grid, dim3(64), 0, s, pts, src, dig, n_groups, t, c, (uint4*)tab, out, skip,
+                     nonuni);
 }
 
 void launch_ta_table(const HmEntry* pts, const uint32_t* src, uint32_t n_partials, void* tab, hipStream_t s) {
@@ -607,12 +864,15 @@ void launch_ta_msm(const HmEntry* pts, const uint32_t* src, const TaDigits* dig,
 }
 
 void launch_ta_straus(const HmEntry* pts, const uint32_t* src, const TaDigits* dig, uint32_t n_partials,
-                      uint32_t n_groups, void* tab, G2JEntry* out, hipStream_t s) {
+                      uint32_t n_groups, void* tab, G2JEntry* out, hipStream_t s, const uint8_t* skip,
+                      const uint8_t* guard) {
   if (!n_partials) return;
-  // members laid out share-position-major when every group has the same size t
-  const uint32_t t = (n_groups && n_partials % n_groups == 0) ? n_partials / n_groups : 0;
+  // members laid out share-position-major when every group has the same size t (a permutation of
+  // the members: right for any group structure); the guarded launch behind the joint path takes
+  // them in plain order
+  const uint32_t t = (!guard && n_groups && n_partials % n_groups == 0) ? n_partials / n_groups : 0;
   hipLaunchKernelGGL(k_ta_straus, dim3(blocks_of(n_partials, 64)), dim3(64), 0, s, pts, src, dig, n_partials,
-                     n_groups, t, (uint4*)tab, out);
+                     n_groups, t, (uint4*)tab, out, guard ? nullptr : skip, guard);
 }
 
 // Member statuses of a ThresholdAggregate whose partials were decompressed by the verification

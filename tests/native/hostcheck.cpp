@@ -6,6 +6,7 @@
 #define HB_COUNT_OPS 1
 #include "../../charon_amd/csrc/ops.h"
 #include "../../charon_amd/csrc/rlc.h"
+#include "../../charon_amd/csrc/ta_small.h"
 #include <string.h>
 
 namespace hb {
@@ -444,5 +445,37 @@ extern "C" int hc_sum_raw(const uint8_t* pr_raw, uint32_t n, uint8_t* out48) {
     acc = jac_add(acc, p);
   }
   g1_compress(out48, jac_to_aff(acc));
+  return 0;
+}
+
+// The small-scalar split of a ThresholdAggregate's Lagrange coefficients (ta_small.h): c[0..t)
+// and s (32 B big-endian, canonical); returns 1 if the split applies.
+extern "C" int hc_ta_small(const int64_t* idx, int t, int64_t* c, uint8_t* s32) {
+  Fr s;
+  if (!ta_small_split(idx, t, c, s)) return 0;
+  fr_to_be(s32, fr_from_mont(s));
+  return 1;
+}
+
+// ThresholdAggregate through the small-scalar split: [s] (sum_j [c_j] sigma_j), compressed
+// (the GPU's k_ta_small / k_ta_sladder restated one lane at a time); 2 = undecodable member,
+// 7 = split refused.
+extern "C" int hc_lagrange_g2_small(const uint8_t* sigs, const int64_t* idx, int k, uint8_t* out96) {
+  int64_t c[TA_SMALL_MAX];
+  Fr s;
+  if (!ta_small_split(idx, k, c, s)) return 7;
+  G2J q = jac_infinity<Fp2>();
+  for (int i = 0; i < k; i++) {
+    G2A a;
+    if (g2_decompress(a, sigs + 96 * i)) return ST_BAD_SIGNATURE;
+    const uint64_t m = c[i] < 0 ? (uint64_t)(-c[i]) : (uint64_t)c[i];
+    const uint32_t mw[2] = {(uint32_t)m, (uint32_t)(m >> 32)};
+    G2J t = jac_mul_aff(a, mw, 64);
+    if (c[i] < 0) t = jac_neg(t);
+    q = jac_add(q, t);
+  }
+  const Fr sc = fr_from_mont(s);
+  const G2A qa = jac_to_aff(q);
+  g2_compress(out96, jac_to_aff(qa.inf ? jac_infinity<Fp2>() : jac_mul_aff(qa, sc.v, 256)));
   return 0;
 }

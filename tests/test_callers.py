@@ -113,6 +113,13 @@ def _flows(impl, sign, pub):
     assert callers.exit_aggregate(impl, [parts[1], None, parts[3], parts[4]]) == sign(secret, root)
     with pytest.raises(CallerError, match="^partial signatures threshold aggregate: cannot combine signatures$"):
         callers.exit_aggregate(impl, [None, None, None, None])
+    full = callers.exit_aggregate_batch(impl, [("0xa", [parts[1], parts[2], None, parts[4]]),
+                                               ("0xb", [None, parts[2], parts[3], parts[4]])])
+    assert full == [sign(secret, root)] * 2
+    with pytest.raises(CallerError, match="^load full exit data from Obol API: partial signatures threshold "
+                                          "aggregate: cannot unmarshal signature into Herumi signature$"):
+        callers.exit_aggregate_batch(impl, [("0xa", [parts[1], parts[2], None, parts[4]]),
+                                            ("0xb", [b"\x11" * 96, parts[2], parts[3], None])])
 
     # --- DKG deposit data / registrations: verify + aggregate + verify per DV (dkg.go:820-984)
     roots = {dv: root}

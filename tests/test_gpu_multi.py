@@ -47,6 +47,7 @@ def test_rccl_world_of_one_slot_exchange(L):
     from charon_amd.shard import SlotExchange, init_library_comm, library_allgather
     dev = torch.device("cuda", 0)
     V, n = 1000, 7
+    torch.zeros(1, device=dev)  # torch's HIP context first, as bench.py does (torch.cuda.set_device)
     init_library_comm(L, 1, 0)
     try:
         exch = SlotExchange(1, 0, {"vst": V * n, "tout": V * 96, "tst": V, "ast": V}, dev, library_allgather(L),

@@ -565,6 +565,31 @@ def test_threshold_aggregate_joint_ladders(L, hipbls, members):
             assert outs[v] == want[v][1], v
 
 
+@pytest.mark.parametrize("members", [0, 2])
+def test_threshold_aggregate_uneven_groups(L, hipbls, members):
+    """Groups of 2 and 4 members alternating: the member count divides evenly (3 per group on
+    average), yet no group has 3 -- the joint and small-scalar paths (which assume exactly t per
+    group) must stand down for the per-member ladders, and every aggregate stays right.  members:
+    the joint-ladder knob (0 = auto, 2 = forced joint path)."""
+    V, n = 128, 10
+    msg = hashlib.sha256(b"uneven groups").digest()
+    secrets = [hipbls.generate_secret_key() for _ in range(V)]
+    roots = hipbls.sign_batch(secrets, [msg] * V)
+    groups = []
+    for v in range(V):
+        t = 2 if v % 2 == 0 else 4
+        shares = hipbls.threshold_split(secrets[v], n, t)
+        ids = [1, 3] if t == 2 else [2, 5, 7, 9]
+        groups.append(dict(zip(ids, hipbls.sign_batch([shares[i] for i in ids], [msg] * t))))
+    prev = L.hbls_ta_joint(members)
+    try:
+        outs, sts = hipbls.threshold_aggregate_batch(groups)
+    finally:
+        L.hbls_ta_joint(prev)
+    assert sts == [OK] * V
+    assert outs == roots
+
+
 def test_hash_paths_agree(L):
     """hash_to_G2 of 65 536 messages takes the one-lane kernel (hash.hip k_hash_to_g2_1); the first
     512 of them, hashed again alone, the two-lane kernel (k_hash_to_g2, KAT-pinned through Sign).

@@ -108,6 +108,74 @@ def test_threshold_aggregate_fixtures(hc, fixtures):
             assert o.raw.hex() == c["out"], c["name"]
 
 
+def _lagrange(ids):
+    lam = []
+    for j in ids:
+        num, den = 1, 1
+        for m in ids:
+            if m != j:
+                num, den = num * m % B.R, den * (m - j) % B.R
+        lam.append(num * pow(den, -1, B.R) % B.R)
+    return lam
+
+
+def test_ta_small_split(hc):
+    """ta_small.h: lambda_j(0) = s c_j (mod r) with small integers c_j for every index set a
+    cluster of up to 10 operators can aggregate (and random larger ones); refused for index 0,
+    duplicates and sizes outside 2..16 (the general path runs there)."""
+    import itertools
+    rng = random.Random(8)
+    sets = [list(c) for t in range(2, 11) for c in itertools.combinations(range(1, 11), t)]
+    sets = rng.sample(sets, 300) + [[1, 2, 3, 4, 8, 9, 10], [1, 3, 4, 8], [-3, 5, 7], [1, 64, 2 ** 20]]
+    sets += [rng.sample(range(1, 65), rng.randrange(2, 17)) for _ in range(40)]
+    c = (ctypes.c_int64 * 16)()
+    s = _b(32)
+    worst = 0
+    for ids in sets:
+        arr = (ctypes.c_int64 * len(ids))(*ids)
+        if not hc.hc_ta_small(arr, len(ids), c, s):
+            assert max(map(abs, ids)) > 10, ids  # only large index sets may overflow 63 bits
+            continue
+        sv = int.from_bytes(s.raw, "big")
+        for j, lam in enumerate(_lagrange(ids)):
+            assert lam == sv * c[j] % B.R, (ids, j)
+        if max(map(abs, ids)) <= 10:
+            worst = max(worst, max(abs(c[j]) for j in range(len(ids))))
+    assert 0 < worst < 2 ** 22
+    for bad in ([0, 1, 2], [1, 1, 2], [5], list(range(1, 18))):
+        arr = (ctypes.c_int64 * len(bad))(*bad)
+        assert hc.hc_ta_small(arr, len(bad), c, s) == 0, bad
+
+
+def test_ta_small_aggregate_matches_lagrange(hc, fixtures):
+    """[s](sum_j [c_j] sigma_j) == sum_j [lambda_j] sigma_j, byte for byte, on the golden
+    ThresholdAggregate fixtures and a 7-of-10 non-prefix set."""
+    checked = 0
+    for case in fixtures["threshold_aggregate"]:
+        items = list(case["partials"].items())
+        if case["status"] != 0 or len(items) < 2:
+            continue
+        sigs = b"".join(bytes.fromhex(v) for _, v in items)
+        idx = (ctypes.c_int64 * len(items))(*[int(k) for k, _ in items])
+        o = _b(96)
+        st = hc.hc_lagrange_g2_small(sigs, idx, len(items), o)
+        if st == 7:
+            continue
+        assert st == 0 and o.raw.hex() == case["out"], case["name"]
+        checked += 1
+    assert checked >= 1
+    secret = 0x1234567890ABCDEF % B.R
+    coeffs = [0x1111 * k + 7 for k in range(1, 7)]
+    msg = hashlib.sha256(b"ta small").digest()
+    ids = [1, 2, 3, 4, 8, 9, 10]
+    shares = {i: (secret + sum(a * i ** (k + 1) for k, a in enumerate(coeffs))) % B.R for i in ids}
+    sigs = b"".join(B.sign(shares[i].to_bytes(32, "big"), msg) for i in ids)
+    idx = (ctypes.c_int64 * 7)(*ids)
+    o = _b(96)
+    assert hc.hc_lagrange_g2_small(sigs, idx, 7, o) == 0
+    assert o.raw == B.sign(secret.to_bytes(32, "big"), msg)
+
+
 def test_pairing_matches_oracle(hc):
     rng = random.Random(3)
     a, b = rng.randrange(1, B.R), rng.randrange(1, B.R)
