@@ -719,16 +719,22 @@ def main(argv=None):
         ta_ids = [x + 1 for x in ta_share_positions(n, t)]
         jc = opcounts.ta_joint_chunk(t, ta_units, jc_knob)
         ta_w = opcounts.ta_joint(ta_ids, jc) if jc else opcounts.ta_uniform(ta_ids)
+        # the small-scalar aggregation (threshold.hip k_ta_small, one lane per validator) takes every
+        # group whose index set it can split; the per-member ladders then have nothing to do
+        ta_small_w = opcounts.ta_small(ta_ids) if os.environ.get("HBLS_TA_SMALL", "1") != "0" else None
         prep_units = opcounts.per_unit(group_size=n + (0 if staged else 1), t=t)
         units = {"k_rlc": (n_rlc, (rlc_avg, rlc_avg)),
                  "k_dec_pk": (NP + (0 if staged else V), per_unit["k_dec_pk"]),
                  "k_dec_sig_pt": (NP + (ta_units if staged else 0), per_unit["k_dec_sig_pt"]),
                  # the aggregation ladders: the uniform-digit schedule of the aggregated index set
-                 "k_ta_straus": (ta_units, (ta_w, ta_w)), "k_group_sum": (V, per_unit["k_group_sum"]),
+                 "k_ta_straus": (0 if ta_small_w else ta_units, (ta_w, ta_w)),
+                 "k_ta_small": (V if ta_small_w else 0, (ta_small_w or 0, ta_small_w or 0)),
+                 "k_group_sum": (V, per_unit["k_group_sum"]),
                  "k_hash_to_g2": (M, per_unit["k_hash_to_g2"]), "k_lines_msg": (M, per_unit["k_lines_msg"])}
         if smsm:
             # multi-Miller loops of MML_PAIRS groups, product tree of fan-in FE_BATCH to <= FE_BATCH
-            mmlk = int(os.environ.get("HBLS_MML_PAIRS", opcounts.MML_PAIRS))
+            n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
+            mmlk = int(os.environ.get("HBLS_MML_PAIRS", "0")) or opcounts.mml_pairs(V, n_cu)
             n_prod, cur = 0, -(-V // mmlk)
             while cur > opcounts.FE_BATCH:
                 n_prod += cur
@@ -736,6 +742,7 @@ def main(argv=None):
             fin = opcounts.pair3_fin(batch=cur)
             units.update({"k_group_prep": (V, prep_units["k_group_prep_p"]),
                           "k_pair3_mml": (V, opcounts.pair3_mml(pairs=mmlk)),
+                          "k_mml_eval": (V, per_unit["k_mml_eval"]),
                           "k_pair3_prod": (n_prod, per_unit["k_pair3_prod"]),
                           "k_pair3_fin": (1, fin), "k_slines": (1, per_unit["k_slines"]),
                           "k_msm_bucket": (opcounts.MSM_ENTRIES_PER_ITEM * n_rlc, per_unit["k_msm_bucket"]),

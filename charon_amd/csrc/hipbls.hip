@@ -264,7 +264,7 @@ bool g_stagger = false;
 // multiplication (msm.hip), one final exponentiation for the call -- and fall back to the
 // per-batch check when that fails (0 = never)
 std::atomic<size_t> g_slot_msm_min{65536};
-size_t g_mml_pairs = MML_PAIRS;  // HBLS_MML_PAIRS: groups per multi-Miller loop of the slot-wide check
+size_t g_mml_pairs = 0;  // HBLS_MML_PAIRS: groups per multi-Miller loop of the slot-wide check (0: sized to the chip)
 
 struct DevBuf {
   void* p = nullptr;
@@ -283,6 +283,7 @@ enum WsId {
   W_TPCNT, W_TPCOFF, W_TPCFIRST, W_TPCCOUNT,                    // chunk plan of the aggregation
   W_FBUF, W_GS, W_BS, W_BLINES, W_BBAD, W_BVER, W_GLIST, W_GCOUNT,  // batched final exponentiation
   W_MCNT, W_MOFF, W_MCUR, W_MORDER, W_MENT, W_MBUCKET, W_MPART, W_MPART2, W_MTOT, W_PBUF1, W_PBUF2, W_SFAIL,  // slot-wide check
+  W_MLEV,                                                                          // its evaluated Miller lines
   W_COUNT_
 };
 
@@ -314,6 +315,7 @@ struct Timed {
 
 struct Dev {
   int ord = -1;
+  int n_cu = 256;  // compute units (4 SIMDs each)
   hipStream_t stream = nullptr;  // the library stream of host-buffer calls
   Ws ws[N_WS];
   unsigned next_ws = 0;
@@ -420,6 +422,7 @@ int dev_create(int ord, Dev** out) {
                    prop.gcnArchName);
   Dev* d = new Dev();
   d->ord = ord;
+  d->n_cu = std::max(1, prop.multiProcessorCount);
   // the verification's side streams (decompression, hashing) get the highest priority: they
   // gate the pairing kernel; the library stream is the lowest
   int prio_lo = 0, prio_hi = 0;
@@ -479,7 +482,7 @@ int init_mask(uint32_t mask) {
     while (fb & (fb - 1)) fb &= fb - 1;  // a power of two
     g_fb_batch = fb;
   }
-  g_mml_pairs = std::min<size_t>(64, std::max<size_t>(1, env_size("HBLS_MML_PAIRS", g_mml_pairs)));
+  g_mml_pairs = std::min<size_t>(64, env_size("HBLS_MML_PAIRS", g_mml_pairs));
   std::vector<Dev*> devs;
   for (int k = 0; k < 32; k++)
     if (mask & (1u << k)) {
@@ -707,18 +710,25 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
   // on the device flag sfail).  Needs all groups in one chunk.
   const size_t smin = g_slot_msm_min.load();
   const bool smsm = bfe && smin && n_groups <= gcap && n + n_agg >= smin;
-  const size_t mmlk = g_mml_pairs;
+  // pairs per multi-Miller loop: enough that the loops fill at most one round of waves (21 groups
+  // per wave, one wave per SIMD) -- a second, partial round would double the kernel's span
+  // (HBLS_MML_PAIRS fixes it)
+  const size_t mmlk = g_mml_pairs ? g_mml_pairs
+                                  : std::min<size_t>(16, std::max<size_t>(1, (std::min(gcap, n_groups) +
+                                                                              GROUPS_PER_WAVE * 4 * d.n_cu - 1) /
+                                                                             (GROUPS_PER_WAVE * 4 * d.n_cu)));
   const size_t nb1 = (gcap + mmlk - 1) / mmlk, nb2 = (nb1 + FE_BATCH - 1) / FE_BATCH;
   G2MsmArgs ma{};
   Fp4Entry *pbuf1 = nullptr, *pbuf2 = nullptr;
   uint8_t* sfail = nullptr;
+  LineEntry* mlev = nullptr;
   if (smsm && (wsbuf(w, W_MCNT, MSM_KEYS, &ma.cnt) || wsbuf(w, W_MOFF, MSM_KEYS + 1, &ma.off) ||
                wsbuf(w, W_MCUR, MSM_KEYS, &ma.cur) || wsbuf(w, W_MORDER, MSM_KEYS, &ma.order) ||
                wsbuf(w, W_MENT, 2 * MSM_WINDOWS * (n + n_agg), &ma.ent) ||
                wsbuf(w, W_MBUCKET, MSM_KEYS, &ma.bucket) || wsbuf(w, W_MPART, MSM_PARTS, &ma.part) ||
                wsbuf(w, W_MPART2, MSM_PARTS / 128, &ma.part2) || wsbuf(w, W_MTOT, 1, &ma.total) ||
                wsbuf(w, W_PBUF1, 3 * nb1, &pbuf1) || wsbuf(w, W_PBUF2, 3 * nb2, &pbuf2) ||
-               wsbuf(w, W_SFAIL, 1, &sfail)))
+               wsbuf(w, W_SFAIL, 1, &sfail) || wsbuf(w, W_MLEV, N_LINES * gcap, &mlev)))
     return -1;
   const int sides1 = smsm ? 1 : 3;  // first pass: the public-key side only when the MSM takes the other
 
@@ -912,6 +922,8 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
         pp.f_range = (uint32_t)mmlk;
         pp.f_n = ng;
         pp.f_out = pbuf1;
+        pp.sig_lines = mlev;
+        TIMED(d, "k_mml_eval", s, launch_mml_eval(pp, mlev, s));
         TIMED(d, "k_pair3_mml", s, launch_pair3_mml(pp, s));
         Fp4Entry* cur = pbuf1;
         uint32_t cur_n = pp.n;

@@ -174,9 +174,11 @@ void launch_pair3_ml(const Pair3Args& a, hipStream_t s);
 void launch_pair3_fin(const Pair3Args& a, hipStream_t s);
 // PROD: f_out[e] = product of the stored values f_in of entries [e f_range, min((e + 1) f_range, f_n))
 void launch_pair3_prod(const Pair3Args& a, hipStream_t s);
-// MML: f_out[e] = ONE Miller loop over the (pk[i], H(msg_idx[i])) pairs of entries i in
-// [e f_range, min((e + 1) f_range, f_n)) whose pk_st byte is zero (shared squarings)
+// MML: f_out[e] = ONE Miller loop over the pairs i in [e f_range, min((e + 1) f_range, f_n)) with
+// the shared squarings; the lines come from sig_lines as evaluated by launch_mml_eval (pk, pk_st,
+// msg_idx, hm, f_n of the same arguments), line j of pair i at sig_lines[j f_n + i]
 void launch_pair3_mml(const Pair3Args& a, hipStream_t s);
+void launch_mml_eval(const Pair3Args& a, LineEntry* ev, hipStream_t s);
 constexpr uint32_t MML_PAIRS = 4;  // pairs per multi-Miller loop of the slot-wide check
 
 // Batched verification (vbatch.hip).

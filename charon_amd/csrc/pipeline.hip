@@ -66,22 +66,30 @@ __global__ KB_OCC(HB_OCC_PAIR3) void k_pair3(Pair3Args a) {
     if (valid) a.f_out[3ull * e + g.k] = Fp4Entry{f.x, f.y};
     return;
   }
-  if (MODE == P3_MML) {  // wave-uniform trip counts; pairs past the end or not READY multiply by one
+  if (MODE == P3_MML) {  // wave-uniform trip counts; pairs past the end multiply by one
+    // the lines come evaluated at each pair's P (k_mml_eval: sig_lines[j * f_n + pair], a unit line
+    // for pairs that are not READY), so the three lanes of a group do not each repeat the
+    // evaluation; the next (line, pair)'s load is issued before the current product (one wave per
+    // SIMD: nothing else would hide its latency)
     const uint32_t first = e * a.f_range;
     const uint32_t cnt = first < a.f_n ? min(a.f_range, a.f_n - first) : 0u;
+    const LineEntry* ev = a.sig_lines;
+    const size_t fn = a.f_n;
     Fp4 f = g_one(g);
     int bit = 62;
     bool pending_add = false;
+    LineEntry Ln = ev[first];
     HB_NOUNROLL for (int j = 0; j < N_LINES; j++) {
       const bool dbl = !pending_add;
       if (dbl && j > 0) f = g_sqr(g, f);
       HB_NOUNROLL for (uint32_t k = 0; k < a.f_range; k++) {
-        const uint32_t idx = k < cnt ? first + k : first;
-        const bool use = k < cnt && !(a.pk_st && a.pk_st[idx]);
-        const G1AEntry Pk = a.pk[idx];
-        const LineEntry L = a.hm[a.msg_idx[idx]].lines[j];
-        const Fp4 t = g_mul_line(g, f, L.a0, f2_mul_fp(L.a1, Pk.x), f2_mul_fp(L.b1, Pk.y));
-        f4_select(f, use, f, t);
+        const LineEntry L = Ln;
+        // prefetch: the next pair of this line, else the first pair of the next line
+        const uint32_t k1 = k + 1 < a.f_range ? k + 1 : 0u;
+        const int j1 = k + 1 < a.f_range ? j : (j + 1 < N_LINES ? j + 1 : j);
+        Ln = ev[(size_t)j1 * fn + (k1 < cnt ? first + k1 : first)];
+        const Fp4 t = g_mul_line(g, f, L.a0, L.a1, L.b1);
+        f4_select(f, k < cnt, f, t);
       }
       if (dbl) {
         pending_add = ((HB_X_ABS >> bit) & 1) != 0;
@@ -153,7 +161,38 @@ __global__ KB_OCC(HB_OCC_PAIR3) void k_pair3(Pair3Args a) {
 #endif
 }
 
+// The Miller lines of every verification group's (P_g, H(m_g)) evaluated at P_g, for the
+// multi-Miller loops: one lane per (line j, group g), ev[j * n + g] = (a0, a1 x_P, b1 y_P) -- a unit
+// line (1, 0, 0) for groups that are not READY (pk_st nonzero), which the loop then multiplies in
+// as one.  Four Fp products per line and group, once, where the three lanes of a k_pair3<MML> group
+// each repeated them.
+__global__ __launch_bounds__(64) void k_mml_eval(const G1AEntry* __restrict__ pk, const uint8_t* __restrict__ pk_st,
+                                                 const uint32_t* __restrict__ msg_idx, const MsgEntry* __restrict__ hm,
+                                                 uint32_t n, LineEntry* __restrict__ ev) {
+  const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid >= (size_t)N_LINES * n) return;
+  const uint32_t j = (uint32_t)(tid / n), g = (uint32_t)(tid % n);
+  LineEntry o;
+  if (pk_st && pk_st[g]) {
+    o.a0 = f2_one();
+    o.a1 = f2_zero();
+    o.b1 = f2_zero();
+  } else {
+    const G1AEntry P = pk[g];
+    const LineEntry L = hm[msg_idx[g]].lines[j];
+    o.a0 = L.a0;
+    o.a1 = f2_mul_fp(L.a1, P.x);
+    o.b1 = f2_mul_fp(L.b1, P.y);
+  }
+  ev[tid] = o;
+}
+
 static inline unsigned blocks_for(size_t n) { return (unsigned)((n + BLOCK - 1) / BLOCK); }
+
+void launch_mml_eval(const Pair3Args& a, LineEntry* ev, hipStream_t s) {
+  const size_t n = (size_t)N_LINES * a.f_n;
+  if (n) hipLaunchKernelGGL(k_mml_eval, dim3(blocks_for(n)), dim3(BLOCK), 0, s, a.pk, a.pk_st, a.msg_idx, a.hm, a.f_n, ev);
+}
 
 void launch_lines_msg(MsgEntry* hm, uint32_t n, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_lines_msg, dim3(blocks_for(n)), dim3(BLOCK), 0, s, hm, n);

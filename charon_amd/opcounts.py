@@ -65,11 +65,23 @@ MML_PAIRS = 4    # pairs per multi-Miller loop of the slot-wide check (layout.h)
 
 
 def pair3_mml(b=BLOCKS, pairs=MML_PAIRS):
-    """k_pair3_mml per verification group: its 68 line products (lines evaluated at P) in a
-    Miller loop whose 62 squarings `pairs` groups share."""
-    alg = N_LINES * (b["f12_mul_line"] + 4) + N_SQR * b["f12_sqr"] / pairs
-    exe = N_LINES * (45 + 12) + N_SQR * 36 / pairs
+    """k_pair3_mml per verification group: its 68 line products (the lines come evaluated at P,
+    k_mml_eval) in a Miller loop whose 62 squarings `pairs` groups share."""
+    alg = N_LINES * b["f12_mul_line"] + N_SQR * b["f12_sqr"] / pairs
+    exe = N_LINES * 45 + N_SQR * 36 / pairs
     return alg, exe
+
+
+def mml_eval(b=BLOCKS):
+    """k_mml_eval per verification group: its 68 lines evaluated at P once (two Fp2 x Fp products
+    each), where the three lanes of a multi-Miller loop group each repeated them."""
+    return (N_LINES * 4,) * 2
+
+
+def mml_pairs(groups, n_cu=256, groups_per_wave=21):
+    """The library's pairs per multi-Miller loop (hipbls.hip verify_pipeline): enough that the loops
+    fit one round of waves, one wave per SIMD (4 per CU)."""
+    return min(16, max(1, -(-groups // (groups_per_wave * 4 * n_cu))))
 
 
 def pair3_fin(b=BLOCKS, batch=FE_BATCH):
@@ -197,6 +209,69 @@ def ta_joint(ids, chunk, b=BLOCKS):
     return tot / len(ids)
 
 
+def ta_small_split(ids):
+    """ta_small.h restated: (c_j, s) with lambda_j(0) = s c_j mod r and small integers c_j, or None
+    where the library refuses the split (the per-member ladders run)."""
+    from math import gcd
+    t = len(ids)
+    if t < 2 or t > 16 or any(x == 0 or abs(x) >= 2 ** 31 for x in ids) or len(set(ids)) != t:
+        return None
+    E = []
+    for j in ids:
+        e = j
+        for m in ids:
+            if m != j:
+                e *= m - j
+        E.append(e)
+    L = 1
+    for e in E:
+        L = L // gcd(L, abs(e)) * abs(e)
+    if L >= 2 ** 63 or any(abs(e) >= 2 ** 63 for e in E):
+        return None
+    P = 1
+    for x in ids:
+        P = P * x % R_ORDER
+    return [L // e for e in E], P * pow(L, -1, R_ORDER) % R_ORDER
+
+
+def _naf2(v):
+    out = []
+    while v:
+        d = 0
+        if v & 1:
+            d = -1 if v & 2 else 1
+            v -= d
+        out.append(d)
+        v >>= 1
+    return out
+
+
+def ta_small(ids, b=BLOCKS):
+    """k_ta_small + k_ta_stab + k_ta_sladder (threshold.hip) per VALIDATOR aggregating the share
+    indices `ids` through the small-scalar split: the joint signed-binary ladder over the c_j
+    (shared doublings, one mixed addition per nonzero digit), the affine odd-multiple tables of Q
+    (a doubling, three additions, one Fp2 inversion: 4 x 3 products into the running product, 17
+    per point back out, the psi images 3 x 6 per point), then [s] Q by the width-4 NAF schedule of
+    the four base-|x| digits of s.  None if the split is refused."""
+    sp = ta_small_split(ids)
+    if sp is None:
+        return None
+    c, s = sp
+    nafs = [_naf2(abs(x)) for x in c]
+    top = max(len(n) for n in nafs)
+    adds = sum(1 for n in nafs for d in n if d)
+    small = top * b["jac_dbl_g2"] + adds * b["jac_add_aff_g2"]
+    table = b["jac_dbl_g2"] + 3 * b["jac_add_g2"] + b["fp_inv"] + 6 + 4 * 3 + 4 * 17 + 4 * 18
+    digits = []
+    for _ in range(4):
+        digits.append(s % X_ABS)
+        s //= X_ABS
+    nafs = [_naf4(a) for a in digits]
+    top4 = max((len(n) for n in nafs), default=1)
+    adds4 = sum(1 for n in nafs for d in n if d)
+    return small + table + top4 * b["jac_dbl_g2"] + adds4 * b["jac_add_aff_g2"]
+
+
 def ta_joint_chunk(t, n_partials, knob=0, lanes=98304):
     """The library's choice of members per lane (hipbls.hip ta_tail): 0/1 = one ladder per member."""
     c = knob if knob else n_partials // lanes
@@ -241,6 +316,7 @@ def per_unit(b=BLOCKS, group_size=1, t=1):
         "k_group_prep_p": ((k - 1) * b["jac_add_g1"] + b["to_aff_g1"],) * 2,
         "k_pair3_prod": (b["f12_mul"], 3 * 18),
         "k_pair3_mml": pair3_mml(b),
+        "k_mml_eval": mml_eval(b),
         "k_msm_bucket": (msm_bucket(b),) * 2,
         "k_msm_reduce": (msm_reduce(b),) * 2,
         "k_msm_sum": (b["jac_add_g2"],) * 2,
@@ -256,7 +332,7 @@ UNITS = {"k_pair3": "pairing check", "k_pair3_fallback": "pairing check", "k_dec
          "k_pair3_ml": "verification group", "k_pair3_fin": "batch of 64 groups",
          "k_slines": "batch of 64 groups", "k_group_prep_p": "verification group",
          "k_pair3_prod": "stored Miller loop", "k_pair3_mml": "verification group", "k_msm_bucket": "bucket entry", "k_msm_reduce": "chunk of 16 buckets",
-         "k_msm_sum": "point"}
+         "k_msm_sum": "point", "k_mml_eval": "verification group", "k_ta_small": "aggregation group (validator)"}
 
 # SHA-256 compressions per attestation signing root (roots.hip: 8 two-block hashes)
 SHA256_PER_ATTESTATION_ROOT = 16
