@@ -17,8 +17,9 @@ CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "lib", "libhipbls.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
-SOURCES = ["hipbls.hip", "pipeline.hip", "threshold.hip", "vbatch.hip", "vgroup.hip", "roots.hip", "hash.hip", "msm.hip"]
-HEADERS = ["hd.h", "consts.h", "fp.h", "fr.h", "tower.h", "ec.h", "sha256.h", "h2c.h", "pairing.h", "ops.h", "pair3.h", "layout.h", "lines.h", "rlc.h"]
+SOURCES = ["hipbls.hip", "pipeline.hip", "threshold.hip", "vbatch.hip", "vgroup.hip", "roots.hip", "hash.hip", "msm.hip",
+           "hashsplit.hip"]
+HEADERS = ["hd.h", "consts.h", "fp.h", "fr.h", "tower.h", "ec.h", "sha256.h", "h2c.h", "pairing.h", "ops.h", "pair3.h", "layout.h", "lines.h", "rlc.h", "ta_small.h"]
 
 
 def _newer(target, deps):

@@ -83,6 +83,13 @@ static size_t hash_one_lane_min() {
 void launch_hash_to_g2(const uint8_t* msgs, const uint64_t* off, const uint32_t* len, uint32_t n, MsgEntry* hm,
                        hipStream_t s) {
   if (!n) return;
+  // default: the staged fast-unit kernels (hashsplit.hip); HBLS_HASH_SPLIT=0 (read per call) takes
+  // the kernels of this file -- kept as the cross-check of tests/test_gpu_scale.py
+  const char* sp = getenv("HBLS_HASH_SPLIT");
+  if (!(sp && sp[0] == '0')) {
+    launch_hash_to_g2_split(msgs, off, len, n, hm, s);
+    return;
+  }
   if (n >= hash_one_lane_min())
     hipLaunchKernelGGL(k_hash_to_g2_1, dim3((unsigned)((n + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s, msgs, off, len,
                        n, hm);

@@ -132,6 +132,9 @@ void launch_ta_member_status(const uint8_t* sig_st, const uint32_t* src, uint32_
 constexpr int GROUPS_PER_WAVE = 21;  // k_pair3: 3 lanes per pairing, 21 pairings per wave
 void launch_hash_to_g2(const uint8_t* msgs, const uint64_t* off, const uint32_t* len, uint32_t n, MsgEntry* hm,
                        hipStream_t s);
+// the staged form (hashsplit.hip): uses hm[i].lines[0..3] as hand-over space (k_lines_msg overwrites it)
+void launch_hash_to_g2_split(const uint8_t* msgs, const uint64_t* off, const uint32_t* len, uint32_t n, MsgEntry* hm,
+                             hipStream_t s);
 void launch_lines_msg(MsgEntry* hm, uint32_t n, hipStream_t s);
 
 // k_pair3 arguments.  Unit u of a launch pairs (P, H(m)) and (-g1, S) where S's lines evaluated at

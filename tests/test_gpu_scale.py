@@ -590,10 +590,11 @@ def test_threshold_aggregate_uneven_groups(L, hipbls, members):
     assert outs == roots
 
 
-def test_hash_paths_agree(L):
-    """hash_to_G2 of 65 536 messages takes the one-lane kernel (hash.hip k_hash_to_g2_1); the first
-    512 of them, hashed again alone, the two-lane kernel (k_hash_to_g2, KAT-pinned through Sign).
-    The points must agree."""
+def test_hash_paths_agree(L, monkeypatch):
+    """hash_to_G2 of 65 536 messages through the staged fast kernels (hashsplit.hip, the default),
+    then the first 512 of them again through each kernel of hash.hip (HBLS_HASH_SPLIT=0: the
+    one-lane kernel for 65 536 messages, the two-lane one for 512; the latter KAT-pinned through
+    Sign).  The points must agree."""
     import torch
     dev = torch.device("cuda", 0)
     n, k = 65536, 512
@@ -602,16 +603,23 @@ def test_hash_paths_agree(L):
     dm = torch.from_numpy(msgs).to(dev)
     off = torch.from_numpy((np.arange(n, dtype=np.uint64) * 32).view(np.int64)).to(dev)
     ln = torch.full((n,), 32, dtype=torch.int32, device=dev)
+    hm_s = torch.zeros(n * E, dtype=torch.uint8, device=dev)
     hm_a = torch.zeros(n * E, dtype=torch.uint8, device=dev)
     hm_b = torch.zeros(k * E, dtype=torch.uint8, device=dev)
     s = torch.cuda.Stream(device=dev)
     sp = ctypes.c_void_p(s.cuda_stream)
+    _chk(L, L.hbls_hash_to_g2_device(_p(dm), _p(off), _p(ln), n, _p(hm_s), sp))
+    s.synchronize()
+    monkeypatch.setenv("HBLS_HASH_SPLIT", "0")
     _chk(L, L.hbls_hash_to_g2_device(_p(dm), _p(off), _p(ln), n, _p(hm_a), sp))
     _chk(L, L.hbls_hash_to_g2_device(_p(dm), _p(off), _p(ln), k, _p(hm_b), sp))
     s.synchronize()
-    a = hm_a.cpu().numpy().reshape(n, E)[:k, :208]
+    monkeypatch.delenv("HBLS_HASH_SPLIT")
+    hs = hm_s.cpu().numpy().reshape(n, E)[:, :208]
+    a = hm_a.cpu().numpy().reshape(n, E)[:, :208]
     b = hm_b.cpu().numpy().reshape(k, E)[:, :208]
-    assert np.array_equal(a, b)
+    assert np.array_equal(hs, a)
+    assert np.array_equal(a[:k], b)
 
 
 def test_slot_c3_full_size(L):
