@@ -735,12 +735,10 @@ def main(argv=None):
             # multi-Miller loops of MML_PAIRS groups, product tree of fan-in FE_BATCH to <= FE_BATCH
             n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
             mmlk = int(os.environ.get("HBLS_MML_PAIRS", "0")) or opcounts.mml_pairs(V, n_cu)
-            n_prod, cur = 0, -(-V // mmlk)
-            while cur > opcounts.FE_BATCH:
-                n_prod += cur
-                cur = -(-cur // opcounts.FE_BATCH)
-            fin = opcounts.pair3_fin(batch=cur)
+            n_prod = opcounts.prod_tree_inputs(-(-V // mmlk))
+            fin = opcounts.pair3_fin(batch=2, lines=False)
             units.update({"k_group_prep": (V, prep_units["k_group_prep_p"]),
+                          "k_pair3_mls": (1, per_unit["k_pair3_mls"]),
                           "k_pair3_mml": (V, opcounts.pair3_mml(pairs=mmlk)),
                           "k_mml_eval": (V, per_unit["k_mml_eval"]),
                           "k_pair3_prod": (n_prod, per_unit["k_pair3_prod"]),
@@ -752,6 +750,8 @@ def main(argv=None):
             nb = -(-V // opcounts.FE_BATCH)
             units.update({"k_group_prep": (V, prep_units["k_group_prep_b"]),
                           "k_pair3_ml": (V, per_unit["k_pair3_ml"]), "k_pair3_fin": (nb, per_unit["k_pair3_fin"]),
+                          "k_pair3_mls": (nb, per_unit["k_pair3_mls"]),
+                          "k_pair3_prod": (V + -(-V // opcounts.PROD_FAN), per_unit["k_pair3_prod"]),
                           "k_slines": (nb, per_unit["k_slines"])})
         else:
             units.update({"k_group_prep": (V, prep_units["k_group_prep"]), "k_pair3": (V, per_unit["k_pair3"])})

@@ -284,6 +284,7 @@ enum WsId {
   W_FBUF, W_GS, W_BS, W_BLINES, W_BBAD, W_BVER, W_GLIST, W_GCOUNT,  // batched final exponentiation
   W_MCNT, W_MOFF, W_MCUR, W_MORDER, W_MENT, W_MBUCKET, W_MPART, W_MPART2, W_MTOT, W_PBUF1, W_PBUF2, W_SFAIL,  // slot-wide check
   W_MLEV,                                                                          // its evaluated Miller lines
+  W_PFIN, W_TBUF,                                                                  // final exponentiations' factors
   W_COUNT_
 };
 
@@ -701,9 +702,13 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
   LineEntry* blines = nullptr;
   uint8_t *bbad = nullptr, *bver = nullptr;
   uint32_t *glist = nullptr, *gcount = nullptr;
+  // the two factors of each final exponentiation side by side (product tree root, signature-side
+  // loop), and the product tree's intermediate level
+  Fp4Entry *pfin = nullptr, *tbuf = nullptr;
   if (bfe && (wsbuf(w, W_FBUF, 3 * gcap, &fbuf) || wsbuf(w, W_GS, gcap, &gS) || wsbuf(w, W_BS, nbcap, &bS) ||
               wsbuf(w, W_BLINES, nbcap * N_LINES, &blines) || wsbuf(w, W_BBAD, nbcap, &bbad) ||
-              wsbuf(w, W_BVER, nbcap, &bver) || wsbuf(w, W_GLIST, gcap, &glist) || wsbuf(w, W_GCOUNT, 1, &gcount)))
+              wsbuf(w, W_BVER, nbcap, &bver) || wsbuf(w, W_GLIST, gcap, &glist) || wsbuf(w, W_GCOUNT, 1, &gcount) ||
+              wsbuf(w, W_PFIN, 3 * 2 * std::max<size_t>(nbcap, 1), &pfin) || wsbuf(w, W_TBUF, 3 * nbcap, &tbuf)))
     return -1;
   // Slot-wide check (msm.hip): every group of the call at once, the signature side as one
   // multi-scalar multiplication; the per-batch path below runs only if it fails (its kernels wait
@@ -717,7 +722,7 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
                                   : std::min<size_t>(16, std::max<size_t>(1, (std::min(gcap, n_groups) +
                                                                               GROUPS_PER_WAVE * 4 * d.n_cu - 1) /
                                                                              (GROUPS_PER_WAVE * 4 * d.n_cu)));
-  const size_t nb1 = (gcap + mmlk - 1) / mmlk, nb2 = (nb1 + FE_BATCH - 1) / FE_BATCH;
+  const size_t nb1 = (gcap + mmlk - 1) / mmlk, nb2 = (nb1 + PROD_FAN - 1) / PROD_FAN;
   G2MsmArgs ma{};
   Fp4Entry *pbuf1 = nullptr, *pbuf2 = nullptr;
   uint8_t* sfail = nullptr;
@@ -910,9 +915,21 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
         TIMED(d, "k_msm_reduce", sm, launch_msm_reduce(ma, sm));
         TIMED(d, "k_msm_sum", sm, launch_msm_sum(ma, sm));
         TIMED(d, "k_slines", sm, launch_slines(ma.total, nullptr, nullptr, 1, blines, 1, bbad, sm));
+        // the signature side's Miller loop, beside the multi-Miller loops and their product tree:
+        // the final exponentiation's second factor, pfin[1]
+        {
+          Pair3Args ps{};
+          ps.sig_lines = blines;
+          ps.stride = 1;
+          ps.n = 1;
+          ps.f_out = pfin;
+          ps.f_out_off = 1;
+          TIMED(d, "k_pair3_mls", sm, launch_pair3_mls(ps, sm));
+        }
         HCHK(hipEventRecord(w.ev_side[0], sm));
-        // multi-Miller loops over MML_PAIRS groups (shared squarings), then a product tree of
-        // fan-in FE_BATCH down to at most FE_BATCH values (ping-pong between pbuf1 and pbuf2)
+        // multi-Miller loops over mmlk groups (shared squarings), then a product tree of fan-in
+        // PROD_FAN down to ONE value, pfin[0] (ping-pong between pbuf1 and pbuf2): eight products
+        // per level in each lane group instead of a chain of 64
         Pair3Args pp{};
         pp.pk = gP;
         pp.pk_st = gst;
@@ -927,26 +944,24 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
         TIMED(d, "k_pair3_mml", s, launch_pair3_mml(pp, s));
         Fp4Entry* cur = pbuf1;
         uint32_t cur_n = pp.n;
-        while (cur_n > FE_BATCH) {
+        do {
           Pair3Args pr{};
-          pr.n = (cur_n + FE_BATCH - 1) / FE_BATCH;
+          pr.n = (cur_n + PROD_FAN - 1) / PROD_FAN;
           pr.f_in = cur;
-          pr.f_range = FE_BATCH;
+          pr.f_range = PROD_FAN;
           pr.f_n = cur_n;
-          pr.f_out = cur == pbuf1 ? pbuf2 : pbuf1;
+          pr.f_out = pr.n == 1 ? pfin : (cur == pbuf1 ? pbuf2 : pbuf1);
           TIMED(d, "k_pair3_prod", s, launch_pair3_prod(pr, s));
           cur = pr.f_out;
           cur_n = pr.n;
-        }
+        } while (cur_n > 1);
         HCHK(hipStreamWaitEvent(s, w.ev_side[0], 0));
         Pair3Args pf{};
         pf.pk_st = bbad;
-        pf.sig_lines = blines;
-        pf.stride = 1;
         pf.n = 1;
-        pf.f_in = cur;
-        pf.f_range = cur_n;
-        pf.f_n = cur_n;
+        pf.f_in = pfin;
+        pf.f_range = 2;
+        pf.f_n = 2;
         pf.status = sfail;
         TIMED(d, "k_pair3_fin", s, launch_pair3_fin(pf, s));
         TIMED(d, "k_slot_verdict", s, launch_slot_verdict(gst, sfail, ng, gver + g0, s));
@@ -975,14 +990,53 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
       // final exponentiation
       const uint8_t* guard = smsm ? sfail : nullptr;
       TIMED(d, "k_slines", s, launch_slines(bS, nullptr, nullptr, nb, blines, nb, bbad, s, guard));
+      // the batches' signature-side loops on side 0 (pfin[2b + 1]) beside the product trees of their
+      // stored loops on s (fan-in PROD_FAN, the last level into pfin[2b]); then each batch's final
+      // exponentiation multiplies just the two
+      HCHK(hipEventRecord(w.ev_msm, s));
+      HCHK(hipStreamWaitEvent(w.side[0], w.ev_msm, 0));
+      {
+        Pair3Args ps{};
+        ps.sig_lines = blines;
+        ps.stride = nb;
+        ps.n = nb;
+        ps.f_out = pfin;
+        ps.f_out_stride = 2;
+        ps.f_out_off = 1;
+        ps.guard = guard;
+        TIMED(d, "k_pair3_mls", w.side[0], launch_pair3_mls(ps, w.side[0]));
+        HCHK(hipEventRecord(w.ev_side[0], w.side[0]));
+      }
+      {
+        const Fp4Entry* cur = fbuf;
+        uint32_t cur_n = ng, span = 1;
+        while (span < fb) {
+          const uint32_t fan = std::min<uint32_t>(PROD_FAN, fb / span);
+          Pair3Args pr{};
+          pr.n = (cur_n + fan - 1) / fan;
+          pr.f_in = cur;
+          pr.f_range = fan;
+          pr.f_n = cur_n;
+          pr.guard = guard;
+          span *= fan;
+          if (span == fb) {
+            pr.f_out = pfin;
+            pr.f_out_stride = 2;
+          } else {
+            pr.f_out = tbuf;
+          }
+          TIMED(d, "k_pair3_prod", s, launch_pair3_prod(pr, s));
+          cur = pr.f_out;
+          cur_n = pr.n;
+        }
+      }
+      HCHK(hipStreamWaitEvent(s, w.ev_side[0], 0));
       Pair3Args pf{};
       pf.pk_st = bbad;
-      pf.sig_lines = blines;
-      pf.stride = nb;
       pf.n = nb;
-      pf.f_in = fbuf;
-      pf.f_range = fb;
-      pf.f_n = ng;
+      pf.f_in = pfin;
+      pf.f_range = 2;
+      pf.f_n = 2 * nb;
       pf.status = bver;
       pf.guard = guard;
       TIMED(d, "k_pair3_fin", s, launch_pair3_fin(pf, s));

@@ -171,6 +171,10 @@ struct Pair3Args {
   const Fp4Entry* f_in;
   uint32_t f_range, f_n;
   const uint8_t* guard;  // nullable: the launch does nothing unless *guard != 0 (slot-wide check failed)
+  // PROD / MLS / ML / MML outputs: entry e goes to f_out[e * f_out_stride + f_out_off] (stride 0 = 1),
+  // so that a final exponentiation's two factors (product tree root, signature-side loop) sit side
+  // by side
+  uint32_t f_out_stride, f_out_off;
 };
 void launch_pair3(const Pair3Args& a, hipStream_t s);
 void launch_pair3_ml(const Pair3Args& a, hipStream_t s);
@@ -182,6 +186,11 @@ void launch_pair3_prod(const Pair3Args& a, hipStream_t s);
 // msg_idx, hm, f_n of the same arguments), line j of pair i at sig_lines[j f_n + i]
 void launch_pair3_mml(const Pair3Args& a, hipStream_t s);
 void launch_mml_eval(const Pair3Args& a, LineEntry* ev, hipStream_t s);
+// MLS: f_out[e] = the Miller loop of (-g1, S) alone from sig_lines (unit e at sig_lines[j stride + e]),
+// stored unexponentiated; the final exponentiation then runs with sig_lines == nullptr (FIN: no loop
+// of its own, the product of its f_range stored values, exponentiated)
+void launch_pair3_mls(const Pair3Args& a, hipStream_t s);
+constexpr uint32_t PROD_FAN = 8;  // fan-in of the product trees in front of a final exponentiation
 constexpr uint32_t MML_PAIRS = 4;  // pairs per multi-Miller loop of the slot-wide check
 
 // Batched verification (vbatch.hip).

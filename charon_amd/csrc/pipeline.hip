@@ -28,7 +28,13 @@ __global__ KB_OCC(HB_OCC_LINES) void k_lines_msg(MsgEntry* __restrict__ hm, uint
 // P3_MML: one Miller loop over the (P, H(m)) pairs of f_range consecutive entries [e f_range, ...)
 // -- the squarings shared by the chunk, one sparse line product per pair and line -- stored
 // unexponentiated (entries with a nonzero pk_st byte contribute one).
-enum { P3_FULL = 0, P3_ML = 1, P3_FIN = 2, P3_PROD = 3, P3_MML = 4 };
+// P3_MLS: the (-g1, S) loop alone, stored (the final exponentiation's second factor, computed beside
+// the product tree instead of in front of the exponentiation).
+enum { P3_FULL = 0, P3_ML = 1, P3_FIN = 2, P3_PROD = 3, P3_MML = 4, P3_MLS = 5 };
+
+__device__ __forceinline__ size_t f_out_index(const Pair3Args& a, uint32_t e) {
+  return (size_t)e * (a.f_out_stride ? a.f_out_stride : 1u) + a.f_out_off;
+}
 
 __device__ __forceinline__ Fp4 f4_load(const Fp4Entry& e) { return {e.x, e.y}; }
 
@@ -63,7 +69,7 @@ __global__ KB_OCC(HB_OCC_PAIR3) void k_pair3(Pair3Args a) {
       f4_select(t, j >= cnt, f4_load(a.f_in[3ull * idx + g.k]), g_one(g));
       f = g_mul(g, f, t);
     }
-    if (valid) a.f_out[3ull * e + g.k] = Fp4Entry{f.x, f.y};
+    if (valid) a.f_out[3 * f_out_index(a, e) + g.k] = Fp4Entry{f.x, f.y};
     return;
   }
   if (MODE == P3_MML) {  // wave-uniform trip counts; pairs past the end multiply by one
@@ -98,24 +104,26 @@ __global__ KB_OCC(HB_OCC_PAIR3) void k_pair3(Pair3Args a) {
         pending_add = false;
       }
     }
-    if (valid) a.f_out[3ull * e + g.k] = Fp4Entry{f.x, f.y};
+    if (valid) a.f_out[3 * f_out_index(a, e) + g.k] = Fp4Entry{f.x, f.y};
     return;
   }
-  if (MODE != P3_FIN) {
+  if (MODE != P3_FIN && MODE != P3_MLS) {
     P = agg ? a.agg_pk[e - a.n_items] : a.pk[e];
     m = agg ? a.agg_msg[e - a.n_items] : a.msg_idx[e];
     ml = a.hm[m].lines;
   }
   const LineEntry* sl = a.sig_lines + u;
   // Lines in loop order: for each bit i = 62..0 of |x| a doubling line (preceded by f^2 except
-  // at the top) and, if bit i is set, an addition line.  One copy of the line products.
+  // at the top) and, if bit i is set, an addition line.  One copy of the line products.  FIN without
+  // sig_lines: no loop (its factors come stored, the signature side's from MLS).
   Fp4 f = g_one(g);
   int bit = 62;
   bool pending_add = false;
-  HB_NOUNROLL for (int j = 0; j < N_LINES; j++) {
+  const int n_lines = (MODE == P3_FIN && !a.sig_lines) ? 0 : N_LINES;
+  HB_NOUNROLL for (int j = 0; j < n_lines; j++) {
     const bool dbl = !pending_add;
     if (dbl && j > 0) f = g_sqr(g, f);
-    if (MODE != P3_FIN) {
+    if (MODE != P3_FIN && MODE != P3_MLS) {
       LineEntry L = ml[j];
       f = g_mul_line(g, f, L.a0, f2_mul_fp(L.a1, P.x), f2_mul_fp(L.b1, P.y));
     }
@@ -133,7 +141,11 @@ __global__ KB_OCC(HB_OCC_PAIR3) void k_pair3(Pair3Args a) {
   if (MODE == P3_ML) {
     Fp4 r;
     f4_select(r, a.pk_st && a.pk_st[e], f, g_one(g));
-    if (valid) a.f_out[3ull * e + g.k] = Fp4Entry{r.x, r.y};
+    if (valid) a.f_out[3 * f_out_index(a, e) + g.k] = Fp4Entry{r.x, r.y};
+    return;
+  }
+  if (MODE == P3_MLS) {
+    if (valid) a.f_out[3 * f_out_index(a, e) + g.k] = Fp4Entry{f.x, f.y};
     return;
   }
   if (MODE == P3_FIN) {  // times the stored Miller loops of entries [e f_range, ...) (wave-uniform trip count)
@@ -208,5 +220,6 @@ void launch_pair3_ml(const Pair3Args& a, hipStream_t s) { pair3_launch<P3_ML>(a,
 void launch_pair3_fin(const Pair3Args& a, hipStream_t s) { pair3_launch<P3_FIN>(a, s); }
 void launch_pair3_prod(const Pair3Args& a, hipStream_t s) { pair3_launch<P3_PROD>(a, s); }
 void launch_pair3_mml(const Pair3Args& a, hipStream_t s) { pair3_launch<P3_MML>(a, s); }
+void launch_pair3_mls(const Pair3Args& a, hipStream_t s) { pair3_launch<P3_MLS>(a, s); }
 
 }  // namespace hb

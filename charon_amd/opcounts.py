@@ -84,12 +84,31 @@ def mml_pairs(groups, n_cu=256, groups_per_wave=21):
     return min(16, max(1, -(-groups // (groups_per_wave * 4 * n_cu))))
 
 
-def pair3_fin(b=BLOCKS, batch=FE_BATCH):
-    """k_pair3_fin, per batch of `batch` groups: the Miller loop of (-g1, sum S), times the stored
-    loops, one final exponentiation."""
-    alg = N_SQR * b["f12_sqr"] + N_LINES * b["f12_mul_line"] + batch * b["f12_mul"] + b["final_exp"]
-    exe = N_SQR * 36 + N_LINES * 45 + batch * 54 + 3 * _pair3_exec_per_lane(b)
+def pair3_fin(b=BLOCKS, batch=FE_BATCH, lines=True):
+    """k_pair3_fin, per final exponentiation: the Miller loop of (-g1, sum S) (unless lines=False:
+    k_pair3_mls computed it beside the product tree), times `batch` stored values, exponentiated."""
+    ml = (N_SQR * b["f12_sqr"] + N_LINES * b["f12_mul_line"], N_SQR * 36 + N_LINES * 45) if lines else (0, 0)
+    alg = ml[0] + batch * b["f12_mul"] + b["final_exp"]
+    exe = ml[1] + batch * 54 + 3 * _pair3_exec_per_lane(b)
     return alg, exe
+
+
+def pair3_mls(b=BLOCKS):
+    """k_pair3_mls, per final exponentiation: the Miller loop of (-g1, S) alone, stored."""
+    return N_SQR * b["f12_sqr"] + N_LINES * b["f12_mul_line"], N_SQR * 36 + N_LINES * 45
+
+
+PROD_FAN = 8     # fan-in of the product trees in front of a final exponentiation (layout.h)
+
+
+def prod_tree_inputs(n, fan=PROD_FAN):
+    """Stored values multiplied by a product tree of fan-in `fan` down to one value."""
+    tot = 0
+    while True:
+        tot += n
+        n = -(-n // fan)
+        if n <= 1:
+            return tot
 
 
 RLC_CHUNK = 16   # items per lane of k_rlc_msm (layout.h)
@@ -309,7 +328,8 @@ def per_unit(b=BLOCKS, group_size=1, t=1):
         "k_group_prep_b": ((k - 1) * (b["jac_add_g1"] + b["jac_add_g2"]) + b["to_aff_g1"] + b["jac_add_g2"],
                            (k - 1) * (b["jac_add_g1"] + b["jac_add_g2"]) + b["to_aff_g1"] + 6 * b["jac_add_g2"]),
         "k_pair3_ml": pair3_ml(b),
-        "k_pair3_fin": pair3_fin(b),
+        "k_pair3_fin": pair3_fin(b, batch=2, lines=False),
+        "k_pair3_mls": pair3_mls(b),
         "k_slines": (b["to_aff_g2"] + b["lines_eval"],) * 2,
         # slot-wide check (msm.hip): per group the key sum alone; the product tree of the stored
         # loops (one Fp12 product per stored value); the MSM kernels per entry / chunk / point
@@ -329,10 +349,10 @@ UNITS = {"k_pair3": "pairing check", "k_pair3_fallback": "pairing check", "k_dec
          "k_fb_lines": "partial", "k_ta_straus": "aggregation member", "k_group_sum": "aggregation group",
          "k_hash_to_g2": "message", "k_lines_msg": "message", "k_seg_sum": "public key (pass 1)",
          "k_va_point": "aggregation group", "k_sig_lines": "signature", "k_group_prep_b": "verification group",
-         "k_pair3_ml": "verification group", "k_pair3_fin": "batch of 64 groups",
+         "k_pair3_ml": "verification group", "k_pair3_fin": "final exponentiation",
          "k_slines": "batch of 64 groups", "k_group_prep_p": "verification group",
          "k_pair3_prod": "stored Miller loop", "k_pair3_mml": "verification group", "k_msm_bucket": "bucket entry", "k_msm_reduce": "chunk of 16 buckets",
-         "k_msm_sum": "point", "k_mml_eval": "verification group", "k_ta_small": "aggregation group (validator)"}
+         "k_msm_sum": "point", "k_mml_eval": "verification group", "k_pair3_mls": "final exponentiation", "k_ta_small": "aggregation group (validator)"}
 
 # SHA-256 compressions per attestation signing root (roots.hip: 8 two-block hashes)
 SHA256_PER_ATTESTATION_ROOT = 16
