@@ -122,6 +122,14 @@ def load_library(path: str = ""):
         if _lib is None:
             if not os.path.exists(path):
                 raise HipBlsUnavailable(f"{path} not built; run `python -m charon_amd.build`")
+            # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64.so.  Loaded after
+            # ours, it would bind to the runtime this library pulled in from /opt/rocm and find no
+            # device ("No HIP GPUs are available"); loaded first, the library binds to torch's (same
+            # soname) and both see the GPU.  Importing torch does not touch the GPU.
+            try:
+                import torch  # noqa: F401
+            except ImportError:
+                pass
             lib = ctypes.CDLL(path)
             _declare(lib)
             _lib = lib

@@ -4,6 +4,9 @@ import sys
 
 import pytest
 
+# PyTorch's HIP runtime first (charon_amd/_lib.py load_library explains why); no GPU is touched
+import torch  # noqa: F401,E402
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
