@@ -615,11 +615,20 @@ def test_hash_paths_agree(L, monkeypatch):
     _chk(L, L.hbls_hash_to_g2_device(_p(dm), _p(off), _p(ln), k, _p(hm_b), sp))
     s.synchronize()
     monkeypatch.delenv("HBLS_HASH_SPLIT")
-    hs = hm_s.cpu().numpy().reshape(n, E)[:, :208]
     a = hm_a.cpu().numpy().reshape(n, E)[:, :208]
     b = hm_b.cpu().numpy().reshape(k, E)[:, :208]
-    assert np.array_equal(hs, a)
-    assert np.array_equal(a[:k], b)
+    assert np.array_equal(a[:k], b)  # the same operations: the same (lazily reduced) words
+
+    # the staged kernels compute the same points by other operation orders: compare mod p (the
+    # stored coordinates are Montgomery forms in [0, 2p))
+    from oracle import bls12381 as B
+
+    def canon(rows):
+        w = rows[:, :192].reshape(len(rows), 4, 48)
+        return [tuple(int.from_bytes(bytes(c), "little") % B.P for c in r) for r in w], rows[:, 192].tolist()
+
+    hs = hm_s.cpu().numpy().reshape(n, E)[:, :208]
+    assert canon(hs) == canon(a)
 
 
 def test_slot_c3_full_size(L):

@@ -11,7 +11,7 @@ rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 starts = [i for i, r in enumerate(rows) if "k_attestation_roots" in r["Kernel_Name"]]
 last = rows[starts[-1]:] if starts else rows
 # the serialised slot ends where bench.py's later measurements begin (their first message hashing)
-hashes = [i for i, r in enumerate(last) if "k_hash_to_g2" in r["Kernel_Name"]]
+hashes = [i for i, r in enumerate(last) if "k_hash_to_g2" in r["Kernel_Name"] or "k_h2c_field" in r["Kernel_Name"]]
 last = last[:hashes[1]] if len(hashes) > 1 else last
 tot = collections.OrderedDict()
 for r in last:
