@@ -264,6 +264,9 @@ bool g_stagger = false;
 // multiplication (msm.hip), one final exponentiation for the call -- and fall back to the
 // per-batch check when that fails (0 = never)
 std::atomic<size_t> g_slot_msm_min{65536};
+// HBLS_FE6=0: the final exponentiations without lines in three lanes (k_pair3<FIN>) instead of six
+// (k_pair6_fin, pair6.h)
+bool g_fe6 = true;
 size_t g_mml_pairs = 0;  // HBLS_MML_PAIRS: groups per multi-Miller loop of the slot-wide check (0: sized to the chip)
 
 struct DevBuf {
@@ -475,6 +478,7 @@ int init_mask(uint32_t mask) {
   g_ta_chunk = std::min<size_t>(TA_CHUNK, std::max<size_t>(1, env_size("HBLS_TA_CHUNK", g_ta_chunk)));
   g_ta_joint = std::min<size_t>(8, env_size("HBLS_TA_JOINT", g_ta_joint.load()));
   g_ta_small = env_size("HBLS_TA_SMALL", 1) != 0;
+  g_fe6 = env_size("HBLS_FE6", 1) != 0;
   g_fe_batch_min = env_size("HBLS_FE_BATCH", g_fe_batch_min.load());
   g_slot_msm_min = env_size("HBLS_SLOT_MSM", g_slot_msm_min.load());
   g_stagger = env_size("HBLS_STAGGER", 0) != 0;
@@ -963,7 +967,7 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
         pf.f_range = 2;
         pf.f_n = 2;
         pf.status = sfail;
-        TIMED(d, "k_pair3_fin", s, launch_pair3_fin(pf, s));
+        TIMED(d, "k_pair3_fin", s, g_fe6 ? launch_pair6_fin(pf, s) : launch_pair3_fin(pf, s));
         TIMED(d, "k_slot_verdict", s, launch_slot_verdict(gst, sfail, ng, gver + g0, s));
         // the slot-wide check failed: the per-batch check (signature sides per item and group)
         if (rlc_fallback_chunks) {
@@ -1039,7 +1043,7 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
       pf.f_n = 2 * nb;
       pf.status = bver;
       pf.guard = guard;
-      TIMED(d, "k_pair3_fin", s, launch_pair3_fin(pf, s));
+      TIMED(d, "k_pair3_fin", s, g_fe6 ? launch_pair6_fin(pf, s) : launch_pair3_fin(pf, s));
       // groups of a failing batch: checked one by one (their stored loop, their own S lines)
       HCHK(hipMemsetAsync(gcount, 0, sizeof(uint32_t), s));
       TIMED(d, "k_batch_verdict", s, launch_batch_verdict(gst, bver, ng, gver + g0, glist, gcount, s, guard, fb));
@@ -1202,7 +1206,11 @@ void dedup_messages(const uint8_t* msgs, const uint64_t* off, const uint32_t* le
   }
 }
 
-int hash_table(Dev& d, const MsgTable& t, MsgEntry** hm_out, bool lines) {
+// Upload the distinct messages (library stream) and hash them; with a workspace set, the hashing
+// runs on its side stream 2 (beside the decompression the verification forks next) and *ready is
+// the event the verification waits on before it needs H(m).
+int hash_table(Dev& d, const MsgTable& t, MsgEntry** hm_out, bool lines, Ws* w = nullptr,
+               hipEvent_t* ready = nullptr) {
   uint8_t* dmsg;
   uint64_t* doff;
   uint32_t* dlen;
@@ -1211,9 +1219,18 @@ int hash_table(Dev& d, const MsgTable& t, MsgEntry** hm_out, bool lines) {
   if (upload(d, I_OFF, t.off.data(), t.off.size(), &doff)) return -1;
   if (upload(d, I_LEN, t.len.data(), t.len.size(), &dlen)) return -1;
   if (ensure_buf(d.io[I_HM], t.len.size() * sizeof(MsgEntry), &hm)) return -1;
-  TIMED(d, "k_hash_to_g2", d.stream,
-        launch_hash_to_g2(dmsg, doff, dlen, (uint32_t)t.len.size(), (MsgEntry*)hm, d.stream));
-  if (lines) TIMED(d, "k_lines_msg", d.stream, launch_lines_msg((MsgEntry*)hm, (uint32_t)t.len.size(), d.stream));
+  hipStream_t hs = d.stream;
+  if (w) {
+    HCHK(hipEventRecord(w->ev_ta, d.stream));  // the uploads (ev_ta is free until the verification)
+    hs = w->side[2];
+    HCHK(hipStreamWaitEvent(hs, w->ev_ta, 0));
+  }
+  TIMED(d, "k_hash_to_g2", hs, launch_hash_to_g2(dmsg, doff, dlen, (uint32_t)t.len.size(), (MsgEntry*)hm, hs));
+  if (lines) TIMED(d, "k_lines_msg", hs, launch_lines_msg((MsgEntry*)hm, (uint32_t)t.len.size(), hs));
+  if (w) {
+    HCHK(hipEventRecord(w->ev_side[2], hs));
+    *ready = w->ev_side[2];
+  }
   *hm_out = (MsgEntry*)hm;
   return 0;
 }
@@ -1324,8 +1341,12 @@ int verify_host(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msgs, co
     }
     std::vector<uint32_t> goff(ge - gb + 1);
     for (size_t g = gb; g <= ge; g++) goff[g - gb] = (uint32_t)(gstart[g] - ib);
+    // the messages hash on a side stream while the keys and signatures decompress (latency of
+    // one call: the two chains run side by side)
+    Ws& w = ws_acquire(d, d.stream);
     MsgEntry* hm;
-    if (hash_table(d, t, &hm, true)) return -1;
+    hipEvent_t hm_ready = nullptr;
+    if (hash_table(d, t, &hm, true, &w, &hm_ready)) return -1;
     uint8_t *dpk, *dsig, *dst;
     uint32_t *didx, *dgoff, *dkc = nullptr;
     if (upload(d, I_PK, hpk.data(), hpk.size(), &dpk) || upload(d, I_SIG, hsig.data(), hsig.size(), &dsig) ||
@@ -1336,8 +1357,7 @@ int verify_host(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msgs, co
     void* p;
     if (ensure_buf(d.io[I_STAT], m, &p)) return -1;
     dst = (uint8_t*)p;
-    Ws& w = ws_acquire(d, d.stream);
-    if (verify_pipeline(d, w, dpk, dsig, didx, hm, m, dgoff, ge - gb, dst, d.stream, nullptr, nullptr, dkc))
+    if (verify_pipeline(d, w, dpk, dsig, didx, hm, m, dgoff, ge - gb, dst, d.stream, hm_ready, nullptr, dkc))
       return -1;
     if (ws_release(w, d.stream)) return -1;
     std::vector<uint8_t> hst(m);

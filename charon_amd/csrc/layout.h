@@ -191,6 +191,9 @@ void launch_mml_eval(const Pair3Args& a, LineEntry* ev, hipStream_t s);
 // of its own, the product of its f_range stored values, exponentiated)
 void launch_pair3_mls(const Pair3Args& a, hipStream_t s);
 constexpr uint32_t PROD_FAN = 8;  // fan-in of the product trees in front of a final exponentiation
+// FIN without sig_lines over six lanes per unit (pair6.h: Fp2 products split across lane pairs):
+// the same statuses at about half the latency
+void launch_pair6_fin(const Pair3Args& a, hipStream_t s);
 constexpr uint32_t MML_PAIRS = 4;  // pairs per multi-Miller loop of the slot-wide check
 
 // Batched verification (vbatch.hip).

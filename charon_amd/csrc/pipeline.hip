@@ -6,6 +6,7 @@
 #define HB_FAST_FPMUL 1
 #include "lines.h"
 #include "pair3.h"
+#include "pair6.h"
 
 namespace hb {
 
@@ -171,6 +172,40 @@ __global__ KB_OCC(HB_OCC_PAIR3) void k_pair3(Pair3Args a) {
     else a.status[e] = s;
   }
 #endif
+}
+
+// A final exponentiation over SIX lanes per unit (pair6.h: every Fp2 product split between two
+// lanes): the product of the unit's f_range stored values, exponentiated, its verdict -- k_pair3<FIN>
+// with sig_lines == nullptr at about half the latency.  Ten units per wavefront.
+constexpr int FE6_PER_WAVE = 10;
+__global__ KB_OCC(HB_OCC_PAIR3) void k_pair6_fin(Pair3Args a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (a.guard && *a.guard == 0) return;
+  const Grp6 g = grp6_make();
+  const int grp = (int)(threadIdx.x & 63u) / 6;
+  if (blockIdx.x * FE6_PER_WAVE >= a.n) return;  // wave-uniform
+  const uint32_t unit = blockIdx.x * FE6_PER_WAVE + (uint32_t)grp;
+  const bool valid = grp < FE6_PER_WAVE && unit < a.n;
+  const uint32_t e = valid ? unit : a.n - 1;
+  const uint32_t first = e * a.f_range;
+  const uint32_t cnt = first < a.f_n ? min(a.f_range, a.f_n - first) : 0u;
+  Fp4 f = g6_one(g);
+  HB_NOUNROLL for (uint32_t j = 0; j < a.f_range; j++) {
+    const uint32_t idx = j < cnt ? first + j : 0u;
+    Fp4 t;
+    f4_select(t, j >= cnt, f4_load(a.f_in[3ull * idx + g.k]), g6_one(g));
+    f = j == 0 ? t : g6_mul(g, f, t);
+  }
+  f = g6_final_exp(g, f);
+  const bool one = g6_is_one(g, f);
+  if (valid && g.k == 0 && g.h == 0)
+    a.status[e] = (a.pk_st && a.pk_st[e]) ? (uint8_t)1 : (one ? ST_OK : ST_NOT_VERIFIED);
+#endif
+}
+
+void launch_pair6_fin(const Pair3Args& a, hipStream_t s) {
+  if (!a.n) return;
+  hipLaunchKernelGGL(k_pair6_fin, dim3((a.n + FE6_PER_WAVE - 1) / FE6_PER_WAVE), dim3(64), 0, s, a);
 }
 
 // The Miller lines of every verification group's (P_g, H(m_g)) evaluated at P_g, for the
