@@ -994,11 +994,10 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
       // final exponentiation
       const uint8_t* guard = smsm ? sfail : nullptr;
       TIMED(d, "k_slines", s, launch_slines(bS, nullptr, nullptr, nb, blines, nb, bbad, s, guard));
-      // the batches' signature-side loops on side 0 (pfin[2b + 1]) beside the product trees of their
-      // stored loops on s (fan-in PROD_FAN, the last level into pfin[2b]); then each batch's final
-      // exponentiation multiplies just the two
-      HCHK(hipEventRecord(w.ev_msm, s));
-      HCHK(hipStreamWaitEvent(w.side[0], w.ev_msm, 0));
+      // the batches' signature-side loops (pfin[2b + 1]), the product trees of their stored loops
+      // (fan-in PROD_FAN, the last level into pfin[2b]), then each batch's final exponentiation
+      // multiplies just the two.  All on s: with several slots in flight a side stream here would
+      // share a hardware queue with another slot's long kernels (C2 24.4 vs 19.1 ms per slot)
       {
         Pair3Args ps{};
         ps.sig_lines = blines;
@@ -1008,8 +1007,7 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
         ps.f_out_stride = 2;
         ps.f_out_off = 1;
         ps.guard = guard;
-        TIMED(d, "k_pair3_mls", w.side[0], launch_pair3_mls(ps, w.side[0]));
-        HCHK(hipEventRecord(w.ev_side[0], w.side[0]));
+        TIMED(d, "k_pair3_mls", s, launch_pair3_mls(ps, s));
       }
       {
         const Fp4Entry* cur = fbuf;
@@ -1034,7 +1032,6 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
           cur_n = pr.n;
         }
       }
-      HCHK(hipStreamWaitEvent(s, w.ev_side[0], 0));
       Pair3Args pf{};
       pf.pk_st = bbad;
       pf.n = nb;
