@@ -14,7 +14,7 @@ own AttestationData,
   4. verify every aggregate under the validator's DV public key (core/sigagg/sigagg.go:117).
 Steps 1-4 are one hbls_slot_device call (include/hipbls.h).  Inputs (compressed pubshares, partial
 signatures, DV public keys, AttestationData, share indices) are resident in HBM before the timed
-region; outputs are per-item status bytes and 96-byte aggregates in HBM.  Two consecutive slots
+region; outputs are per-item status bytes and 96-byte aggregates in HBM.  Three consecutive slots
 are in flight (--inflight), each on its own stream with its own outputs.
 
 value = (verified partials + threshold aggregates) per second summed over all ranks; the
@@ -41,6 +41,14 @@ import threading
 import time
 
 import numpy as np
+
+# One hardware queue per stream: three slots in flight x (the slot's stream + its workspace set's
+# four side streams) + the library stream.  With HIP's default of four, streams share queues and a
+# latency-bound kernel (one final exponentiation, a hashing stage of 64 messages) holds up
+# whatever else sits in its queue: C3 106.4 -> 101.3 ms, C2 16.7 -> 16.0 ms per slot on one box
+# (profiles/r03j_*).  Set before anything initialises the HIP runtime; a value from the
+# environment wins.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 if ROOT not in sys.path:
@@ -800,6 +808,7 @@ def main(argv=None):
         "config": {"workload": wl["desc"], "validators_per_gpu": V, "operators": n, "threshold": t,
                    "aggregated_share_indices": [int(x) + 1 for x in ta_share_positions(n, t)],
                    "distinct_messages": M, "partials_per_gpu": NP, "parallelism": f"validator-sharded x{world}",
+                   "slots_in_flight": n_sets, "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
                    **({"corrupted_partials_per_gpu": d["n_corrupted"]} if "exp_v" in d else {})},
         "verify_per_s": round(world * NP / (elapsed / args.steps), 1),
         "threshold_aggregate_per_s": round(world * V / (elapsed / args.steps), 1),

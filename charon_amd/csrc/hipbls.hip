@@ -310,7 +310,8 @@ struct Ws {
 // host-call staging buffers (inputs and outputs of the host-buffer entry points)
 enum IoId { I_PK, I_SIG, I_MSG, I_OFF, I_LEN, I_MIDX, I_HM, I_STAT, I_IDX, I_GOFF, I_OUT, I_SK, I_VGOFF, I_KC, I_COUNT };
 
-constexpr int N_WS = 3;
+constexpr int N_WS_MAX = 8;  // workspace sets per device: HBLS_WS_SETS (default 3)
+int g_ws_sets = 3;
 
 struct Timed {
   const char* name;
@@ -321,7 +322,7 @@ struct Dev {
   int ord = -1;
   int n_cu = 256;  // compute units (4 SIMDs each)
   hipStream_t stream = nullptr;  // the library stream of host-buffer calls
-  Ws ws[N_WS];
+  Ws ws[N_WS_MAX];
   unsigned next_ws = 0;
   DevBuf io[I_COUNT];
   std::mutex mu;  // one call at a time enqueues on this device
@@ -372,7 +373,7 @@ int wsbuf(Ws& w, WsId id, size_t count, T** out) {
 
 // Acquire a workspace set for a call whose kernels run on `s` and the set's side streams.
 Ws& ws_acquire(Dev& d, hipStream_t s) {
-  Ws& w = d.ws[d.next_ws++ % N_WS];
+  Ws& w = d.ws[d.next_ws++ % (unsigned)g_ws_sets];
   if (w.used) {
     (void)hipStreamWaitEvent(s, w.free_ev, 0);
     for (hipStream_t x : w.side) (void)hipStreamWaitEvent(x, w.free_ev, 0);
@@ -433,7 +434,8 @@ int dev_create(int ord, Dev** out) {
   HCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
   HCHK(hipStreamCreateWithPriority(&d->stream, hipStreamNonBlocking, prio_lo));
   HCHK(hipEventCreateWithFlags(&d->ev_dec, hipEventDisableTiming));
-  for (auto& w : d->ws) {
+  for (int k_ws = 0; k_ws < g_ws_sets; k_ws++) {
+    Ws& w = d->ws[k_ws];
     HCHK(hipEventCreateWithFlags(&w.free_ev, hipEventDisableTiming));
     for (int k = 0; k < N_SIDE; k++) {
       // side 3 (the slot's ThresholdAggregate): high priority like the others (HBLS_TA_PRIO=0: the
@@ -482,6 +484,7 @@ int init_mask(uint32_t mask) {
   g_fe_batch_min = env_size("HBLS_FE_BATCH", g_fe_batch_min.load());
   g_slot_msm_min = env_size("HBLS_SLOT_MSM", g_slot_msm_min.load());
   g_stagger = env_size("HBLS_STAGGER", 0) != 0;
+  g_ws_sets = (int)std::min<size_t>(N_WS_MAX, std::max<size_t>(1, env_size("HBLS_WS_SETS", 3)));
   {
     size_t fb = std::min<size_t>(FE_BATCH, std::max<size_t>(2, env_size("HBLS_FALLBACK_BATCH", g_fb_batch)));
     while (fb & (fb - 1)) fb &= fb - 1;  // a power of two

@@ -1,5 +1,5 @@
 # GPU box (round 3): GPU tests (pytest -k $2, "all" = every test), then C2 / C3 bench lines under
-# environment variants.  $1 = tag; then "WORKLOAD:NAME=VAL ..." strings ("-" = no variables)
+# environment variants.  $1 = tag; then "WORKLOAD:NAME=VAL ...|bench args" strings ("-" = no variables)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
@@ -15,8 +15,11 @@ k=0
 for v in "$@"; do
   k=$((k+1))
   wl=${v%%:*}
-  vars=${v#*:}
+  rest=${v#*:}
+  vars=${rest%%|*}
+  extra=""
+  [ "$rest" != "$vars" ] && extra=${rest#*|}
   [ "$vars" = "-" ] && vars=""
-  env $vars timeout -k 10 300 python -u bench.py --workload $wl --steps 5 --warmup 2 --cpu-seconds 0 --callers 0 --aggregate-verify 0 --key-tables 0 --host-api 0 > gpurun_out/ab_${TAG}_$k.json 2> gpurun_out/ab_${TAG}_$k.err || exit 1
+  env $vars timeout -k 10 300 python -u bench.py --workload $wl $extra --steps 5 --warmup 2 --cpu-seconds 0 --callers 0 --aggregate-verify 0 --key-tables 0 --host-api 0 > gpurun_out/ab_${TAG}_$k.json 2> gpurun_out/ab_${TAG}_$k.err || exit 1
   echo "$v" > gpurun_out/ab_${TAG}_$k.env
 done
