@@ -229,6 +229,52 @@ HD void fp2_fix_neg(uint32_t* out, const uint32_t* r, bool neg) {  // r (mod 2^3
   HB_UNROLL for (int i = 0; i < 12; i++) out[i] = neg ? s[i] : w[i];
 }
 
+#if !defined(HB_FP2_SCHOOL)
+// Karatsuba over the columns: per column k the three sums
+//   t00 = sum a0_j b0_{k-j},   t11 = sum a1_j b1_{k-j},   t01 = sum (a0 + a1)_j (b0 + b1)_{k-j}
+// give the real column t00 - t11 and the imaginary column t01 - t00 - t11 (= sum a0 b1 + a1 b0):
+// three multiply-add chains per column instead of four (3 x 196 + 2 x 196 = 980 multiply-adds per
+// Fp2 product against 1 176), for five 64-bit additions per column.  The limb sums are < 2^29, so a
+// column of t01 stays < 14 * 2^58; t11 is accumulated negated (signed multiply-adds against -a1),
+// and the imaginary accumulator is exact modulo 2^64 with a true value in [0, 2^63).
+HD void fp2_mul_core(uint32_t* o0, uint32_t* o1, const uint32_t* a0w, const uint32_t* a1w, const uint32_t* b0w,
+                     const uint32_t* b1w) {
+  uint32_t a0[14], a1[14], b0[14], b1[14], sa[14], sb[14], m0[14], m1[14], r0[14], r1[14];
+  int32_t na1[14];
+  fp_split28(a0, a0w);
+  fp_split28(a1, a1w);
+  fp_split28(b0, b0w);
+  fp_split28(b1, b1w);
+  HB_UNROLL for (int j = 0; j < 14; j++) {
+    na1[j] = -(int32_t)a1[j];
+    sa[j] = a0[j] + a1[j];
+    sb[j] = b0[j] + b1[j];
+  }
+  uint64_t ar = 0, ai = 0;
+  HB_UNROLL for (int k = 0; k < 27; k++) {
+    const int lo = k < 14 ? 0 : k - 13, hi = k < 14 ? k : 13;
+    uint64_t t00 = 0, t11n = 0;
+    HB_UNROLL for (int j = lo; j <= hi; j++) {
+      t00 += (uint64_t)a0[j] * b0[k - j];
+      t11n += (uint64_t)((int64_t)na1[j] * (int64_t)(int32_t)b1[k - j]);
+      ai += (uint64_t)sa[j] * sb[k - j];
+    }
+    ar += t00 + t11n;
+    ai += t11n - t00;
+    HB_UNROLL for (int j = lo; j <= hi; j++)
+      if (j < k || k >= 14) {
+        ar += (uint64_t)m0[j] * P28[k - j];
+        ai += (uint64_t)m1[j] * P28[k - j];
+      }
+    HB_MONT28_TAIL_S(ar, m0, k, r0)
+    HB_MONT28_TAIL(ai, m1, k, r1)
+  }
+  r0[13] = (uint32_t)ar;
+  r1[13] = (uint32_t)ai;
+  fp2_fix_neg(o0, r0, (int64_t)ar < 0);
+  fp_join28(o1, r1);
+}
+#else
 HD void fp2_mul_core(uint32_t* o0, uint32_t* o1, const uint32_t* a0w, const uint32_t* a1w, const uint32_t* b0w,
                      const uint32_t* b1w) {
   uint32_t a0[14], a1[14], b0[14], b1[14], m0[14], m1[14], r0[14], r1[14];
@@ -260,6 +306,7 @@ HD void fp2_mul_core(uint32_t* o0, uint32_t* o1, const uint32_t* a0w, const uint
   fp2_fix_neg(o0, r0, (int64_t)ar < 0);
   fp_join28(o1, r1);
 }
+#endif
 
 // (a0 + a1 u)^2 = (a0^2 - a1^2) + 2 a0 a1 u, squares with the doubled-limb cross products
 HD void fp2_sqr_core(uint32_t* o0, uint32_t* o1, const uint32_t* a0w, const uint32_t* a1w) {

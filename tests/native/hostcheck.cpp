@@ -159,6 +159,24 @@ int hc_fp_mul(const uint8_t* a48, const uint8_t* b48, uint8_t* out48) {
   return 0;
 }
 
+// Fp2 product and square of raw Montgomery-domain values (lazily reduced: anything below 2p), as the
+// kernels hold them: a = (a0, a1), b = (b0, b1) as 48-byte big-endian numbers; out = a b / R and
+// a^2 / R (R = 2^392), raw
+int hc_fp2_mul_raw(const uint8_t* a96, const uint8_t* b96, uint8_t* out96, uint8_t* sq96) {
+  Fp a0, a1, b0, b1, r0, r1;
+  fp_from_be_raw(a0, a96);
+  fp_from_be_raw(a1, a96 + 48);
+  fp_from_be_raw(b0, b96);
+  fp_from_be_raw(b1, b96 + 48);
+  fp2_mul_core(r0.v, r1.v, a0.v, a1.v, b0.v, b1.v);
+  fp_to_be_raw(out96, r0);
+  fp_to_be_raw(out96 + 48, r1);
+  fp2_sqr_core(r0.v, r1.v, a0.v, a1.v);
+  fp_to_be_raw(sq96, r0);
+  fp_to_be_raw(sq96 + 48, r1);
+  return 0;
+}
+
 int hc_fp2_sqrt(const uint8_t* a96, uint8_t* out96) {
   Fp a0, a1;
   fp_from_be_raw(a0, a96);

@@ -43,6 +43,27 @@ def test_fp_mul_edges(hc):
             assert int.from_bytes(o.raw, "big") == a * b % B.P
 
 
+def test_fp2_mul_lazy_bounds(hc):
+    """The Fp2 product and square on lazily reduced operands (any value below 2p, the kernels'
+    invariant), extremes included: result = a b / 2^392 mod p and below 2p."""
+    P, R_INV = B.P, pow(2, -392, B.P)
+    top = 2 * P - 1
+    vals = [0, 1, 2, P - 1, P, P + 1, top, top - 1, (1 << 381) - 1, (1 << 380), 2 * P - (1 << 200)]
+    rng = random.Random(7)
+    pairs = [((x, y), (u, v)) for x in vals[::2] for y in vals[1::2] for u in (top, 0, P) for v in (top, 1, P - 1)]
+    pairs += [((rng.randrange(2 * P), rng.randrange(2 * P)), (rng.randrange(2 * P), rng.randrange(2 * P)))
+              for _ in range(300)]
+    for (a0, a1), (b0, b1) in pairs:
+        o, q = _b(96), _b(96)
+        hc.hc_fp2_mul_raw(a0.to_bytes(48, "big") + a1.to_bytes(48, "big"),
+                          b0.to_bytes(48, "big") + b1.to_bytes(48, "big"), o, q)
+        r = (int.from_bytes(o.raw[:48], "big"), int.from_bytes(o.raw[48:], "big"))
+        s = (int.from_bytes(q.raw[:48], "big"), int.from_bytes(q.raw[48:], "big"))
+        assert r[0] % P == (a0 * b0 - a1 * b1) * R_INV % P and r[1] % P == (a0 * b1 + a1 * b0) * R_INV % P
+        assert s[0] % P == (a0 * a0 - a1 * a1) * R_INV % P and s[1] % P == 2 * a0 * a1 * R_INV % P
+        assert max(r + s) < 2 * P
+
+
 def test_fp2_sqrt(hc):
     rng = random.Random(2)
     for _ in range(30):
