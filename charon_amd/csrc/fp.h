@@ -229,7 +229,10 @@ HD void fp2_fix_neg(uint32_t* out, const uint32_t* r, bool neg) {  // r (mod 2^3
   HB_UNROLL for (int i = 0; i < 12; i++) out[i] = neg ? s[i] : w[i];
 }
 
-#if !defined(HB_FP2_SCHOOL)
+#if defined(HB_FP2_KARA)
+// (Opt-in, measured slower: the leaf needs 248 VGPRs + 14 AGPRs against 145, which drops the G2
+// kernels that call it to one wave per SIMD and adds caller spills -- k_dec_sig_pt + k_g2_subgroup
+// 33.5 -> 40.9 ms, the C3 slot 104.3 -> 109.0 ms, profiles/r03k_*.)
 // Karatsuba over the columns: per column k the three sums
 //   t00 = sum a0_j b0_{k-j},   t11 = sum a1_j b1_{k-j},   t01 = sum (a0 + a1)_j (b0 + b1)_{k-j}
 // give the real column t00 - t11 and the imaginary column t01 - t00 - t11 (= sum a0 b1 + a1 b0):
