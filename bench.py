@@ -317,6 +317,15 @@ def concurrent_callers(L, d, threads: int, seconds: float):
                                     _p(st)))
         lat.append(time.perf_counter() - t0)
         assert st[0] == 0
+    # where one call's time goes: the same call with every launch timed (library timing mode 2:
+    # HIP events around each launch, launches serialised)
+    _chk(L, L.hbls_timing(2))
+    st = np.zeros(1, dtype=np.uint8)
+    _chk(L, L.hbls_verify_batch(_p(pks), _p(sigs), _p(msgs), _p(off0), _p(len32), 1, _p(st)))
+    single_kern = {}
+    for k, ms in _lib_timing(L):
+        single_kern[k] = round(single_kern.get(k, 0.0) + ms, 3)
+    _chk(L, L.hbls_timing(0))
     stop = time.perf_counter() + seconds
     counts = [0] * threads
     lats = [[] for _ in range(threads)]
@@ -347,6 +356,7 @@ def concurrent_callers(L, d, threads: int, seconds: float):
     return {"threads": threads, "calls_per_s": round(sum(counts) / wall, 1),
             "mean_latency_ms": round(1e3 * statistics.mean(all_l), 2) if all_l else None,
             "single_call_latency_ms": round(1e3 * statistics.median(lat), 2), "all_ok": bad[0] == 0,
+            "single_call_kernels_ms": single_kern,
             "coalesce_us": int(os.environ.get("HBLS_COALESCE_US", "200"))}
 
 

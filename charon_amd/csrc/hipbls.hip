@@ -609,17 +609,16 @@ int ta_tail(Dev& d, Ws& w, const HmEntry* pts, const uint32_t* src, const uint8_
     if (src) launch_ta_member_status(mst_in, src, (uint32_t)np, mst, s);
     else HCHK(hipMemcpyAsync(mst, mst_in, np, hipMemcpyDeviceToDevice, s));
     HCHK(hipGetLastError());
-    // t_u > 1: the joint and small-scalar paths assume groups of exactly t_u members; k_ta_lambda
+    // t_u > 1: the joint and small-scalar paths assume groups of exactly t_u members; k_ta_layout
     // flags any other layout in nonuni (the per-member ladders then run instead)
     uint8_t* nonuni = nullptr;
     if (mode == 0 && t_u > 1) {
       if (wsbuf(w, W_TANONUNI, 1, &nonuni)) return -1;
       HCHK(hipMemsetAsync(nonuni, 0, 1, s));
+      TIMED(d, "k_ta_lambda", s, launch_ta_layout(dgoff, (uint32_t)n_groups, (uint32_t)t_u, nonuni, s));
     }
-    TIMED(d, "k_ta_lambda", s,
-          launch_ta_lambda(didx, dgoff, (uint32_t)n_groups, (uint32_t)np, mode, dig, mst, s, (uint32_t)t_u, nonuni));
-    // small-scalar path first (groups of exactly t members, wave-uniform index sets); the
-    // per-member ladders below skip the groups it aggregated
+    // small-scalar path first (groups of exactly t members, wave-uniform index sets); the Lagrange
+    // digits and the per-member ladders below skip the groups it aggregated
     uint8_t* sdone = nullptr;
     if (mode == 0 && !g_ta_msm && g_ta_small && t_u >= 2 && t_u <= (size_t)TA_SMALL_MAX) {
       int64_t* csm;
@@ -632,6 +631,9 @@ int ta_tail(Dev& d, Ws& w, const HmEntry* pts, const uint32_t* src, const uint8_
             launch_ta_small(pts, src, didx, (uint32_t)n_groups, (uint32_t)t_u, csm, sdig, sok, stab, sdone, pj, s,
                             nonuni));
     }
+    TIMED(d, "k_ta_lambda", s,
+          launch_ta_lambda(didx, dgoff, (uint32_t)n_groups, (uint32_t)np, mode, dig, mst, s, (uint32_t)t_u, nonuni,
+                           sdone));
     if (g_ta_msm && n_groups) {
       // chunks of at most TA_CHUNK members share their ladder's doublings (k_ta_msm)
       const size_t max_chunks = np / g_ta_chunk + n_groups;

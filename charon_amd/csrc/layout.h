@@ -98,9 +98,13 @@ struct RlcKey {
 // Staged ThresholdAggregate (threshold.hip).  src (nullable): member j's point is pts[src[j]].
 // nonuni (nullable, zeroed by the caller): set when t_u != 0 and some group does not hold exactly
 // t_u members at offset g t_u -- the joint and small-scalar paths then stand down (nonuni below)
-// and the per-member ladders run instead
+// and the per-member ladders run instead.  launch_ta_layout sets it alone (one lane per group);
+// k_ta_lambda sets it too.  skip (nullable, per group): groups the small-scalar path aggregated --
+// their lambda digits are not needed and not computed.
+void launch_ta_layout(const uint32_t* grp_off, uint32_t n_groups, uint32_t t_u, uint8_t* nonuni, hipStream_t s);
 void launch_ta_lambda(const int64_t* idx, const uint32_t* grp_off, uint32_t n_groups, uint32_t n_partials, int mode,
-                      TaDigits* dig, uint8_t* mstat, hipStream_t s, uint32_t t_u = 0, uint8_t* nonuni = nullptr);
+                      TaDigits* dig, uint8_t* mstat, hipStream_t s, uint32_t t_u = 0, uint8_t* nonuni = nullptr,
+                      const uint8_t* skip = nullptr);
 constexpr uint32_t TA_CHUNK = 8;  // members per lane of k_ta_msm
 void launch_ta_table(const HmEntry* pts, const uint32_t* src, uint32_t n_partials, void* tab, hipStream_t s);
 void launch_ta_msm(const HmEntry* pts, const uint32_t* src, const TaDigits* dig, void* tab, const uint32_t* cfirst,

@@ -58,7 +58,8 @@ __device__ __forceinline__ uint32_t find_group_ta(const uint32_t* grp_off, uint3
 __global__ __launch_bounds__(64) void k_ta_lambda(const int64_t* __restrict__ idx, const uint32_t* __restrict__ grp_off,
                                                   uint32_t n_groups, uint32_t n_partials, int mode,
                                                   TaDigits* __restrict__ dig, uint8_t* __restrict__ mstat,
-                                                  uint32_t t_u, uint8_t* __restrict__ nonuni) {
+                                                  uint32_t t_u, uint8_t* __restrict__ nonuni,
+                                                  const uint8_t* __restrict__ skip) {
   uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n_partials) return;
   TaDigits d;
@@ -67,6 +68,7 @@ __global__ __launch_bounds__(64) void k_ta_lambda(const int64_t* __restrict__ id
   uint32_t g = find_group_ta(grp_off, n_groups, j);
   uint32_t b = grp_off[g], en = grp_off[g + 1];
   if (nonuni && t_u && (en - b != t_u || b != g * t_u)) *nonuni = 1;
+  if (skip && skip[g]) return;  // aggregated by the small-scalar path: no digits needed
   if (mode == 0 && en - b > 1) {  // k = 1: the single partial is returned as is
     // lambda_j = prod_m x_m / prod_m (x_m - x_j).  Share indices are small integers, so each
     // denominator factor normally comes from the 1/d table (no Fr inversion); anything else
@@ -183,12 +185,22 @@ __global__ KB_OCC(HB_OCC_STRAUS) void k_ta_straus(const HmEntry* __restrict__ pt
   const bool valid = item < n_partials && !(skip && t_uniform && skip[m / t_uniform]);
   if (!__any(valid)) return;
   uint4* wt = tab + (size_t)blockIdx.x * 16 * TA_TAB_QUADS * 64 + lane;
-  const TaDigits d = dig[m];
+  // skipped lanes' digits are never computed (k_ta_lambda skips their groups): they read a
+  // neutral value and stay out of the uniformity test, which runs over the valid lanes only
+  TaDigits d;
+  if (valid) {
+    d = dig[m];
+  } else {
+    d.a[0] = 1;
+    d.a[1] = d.a[2] = d.a[3] = 0;
+  }
   bool same = true;
-  HB_UNROLL for (int k = 0; k < 4; k++) {
-    const uint32_t lo = (uint32_t)d.a[k], hi = (uint32_t)(d.a[k] >> 32);
-    same = same && lo == (uint32_t)__builtin_amdgcn_readfirstlane((int)lo) &&
-           hi == (uint32_t)__builtin_amdgcn_readfirstlane((int)hi);
+  if (valid) {
+    HB_UNROLL for (int k = 0; k < 4; k++) {
+      const uint32_t lo = (uint32_t)d.a[k], hi = (uint32_t)(d.a[k] >> 32);
+      same = same && lo == (uint32_t)__builtin_amdgcn_readfirstlane((int)lo) &&
+             hi == (uint32_t)__builtin_amdgcn_readfirstlane((int)hi);
+    }
   }
   const HmEntry e = pts[src ? src[m] : m];
   const G2A P0 = {e.x, e.y, e.inf != 0};
@@ -196,11 +208,19 @@ __global__ KB_OCC(HB_OCC_STRAUS) void k_ta_straus(const HmEntry* __restrict__ pt
   if (__all(same)) {
     // wave-uniform digits: signed width-4 NAF of each digit (one shared schedule, uniform
     // branches) over the odd multiples {1, 3, 5, 7} of the four bases B_k = P0, -psi(P0),
-    // psi^2(P0), -psi^3(P0): ~13 additions per 64-bit digit instead of one per ladder step
+    // psi^2(P0), -psi^3(P0): ~13 additions per 64-bit digit instead of one per ladder step.
+    // The schedule comes from the first valid lane.
+    const int fl = __ffsll((unsigned long long)__ballot(valid)) - 1;
+    uint64_t da[4];
+    HB_UNROLL for (int k = 0; k < 4; k++) {
+      const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)d.a[k], fl);
+      const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(d.a[k] >> 32), fl);
+      da[k] = ((uint64_t)hi << 32) | lo;
+    }
     if (lane == 0) {
       int top = 0;
       HB_UNROLL for (int k = 0; k < 4; k++) {
-        uint64_t v = d.a[k];  // < |x| < 2^64 - 7: v + 7 cannot overflow
+        uint64_t v = da[k];  // < |x| < 2^64 - 7: v + 7 cannot overflow
         for (int i = 0; i < 66; i++) {
           int dg = 0;
           if (v & 1u) {
@@ -433,18 +453,27 @@ __device__ __forceinline__ JointLane joint_lane(const TaDigits* __restrict__ dig
   j.cnt = min(c, t - j0);
   j.m0 = v * t + j0;
   j.wt = tab + (size_t)blockIdx.x * (16 * c) * TA_TAB_QUADS * 64 + lane;
-  bool same = j.cnt == (uint32_t)__builtin_amdgcn_readfirstlane((int)j.cnt);
-  HB_NOUNROLL for (uint32_t k = 0; k < c; k++) {
-    const TaDigits d = dig[j.m0 + (k < j.cnt ? k : 0)];
-    HB_UNROLL for (int i = 0; i < 4; i++) {
-      const uint32_t lo = (uint32_t)d.a[i], hi = (uint32_t)(d.a[i] >> 32);
-      same = same && lo == (uint32_t)__builtin_amdgcn_readfirstlane((int)lo) &&
-             hi == (uint32_t)__builtin_amdgcn_readfirstlane((int)hi);
+  // the uniformity test runs over the valid lanes only (readfirstlane inside the branch reads the
+  // first valid lane): skipped groups' digits are never computed (k_ta_lambda skips them)
+  bool same = true;
+  if (j.valid) {
+    same = j.cnt == (uint32_t)__builtin_amdgcn_readfirstlane((int)j.cnt);
+    HB_NOUNROLL for (uint32_t k = 0; k < c; k++) {
+      const TaDigits d = dig[j.m0 + (k < j.cnt ? k : 0)];
+      HB_UNROLL for (int i = 0; i < 4; i++) {
+        const uint32_t lo = (uint32_t)d.a[i], hi = (uint32_t)(d.a[i] >> 32);
+        same = same && lo == (uint32_t)__builtin_amdgcn_readfirstlane((int)lo) &&
+               hi == (uint32_t)__builtin_amdgcn_readfirstlane((int)hi);
+      }
     }
   }
   j.uniform = __all(same);
   j.any = __any(j.valid);
   return j;
+}
+// the first valid lane of the wave (j.any): its members' digits are the wave's schedule
+__device__ __forceinline__ int joint_first_lane(const JointLane& j) {
+  return __ffsll((unsigned long long)__ballot(j.valid)) - 1;
 }
 __device__ __forceinline__ void joint_store(G2JEntry* __restrict__ out, const JointLane& j, const G2J& R) {
   if (!j.valid) return;
@@ -472,10 +501,12 @@ __global__ KB_OCC(HB_OCC_STRAUS) void k_ta_jladder(const TaDigits* __restrict__ 
   __shared__ int naf_top;
   const JointLane j = joint_lane(dig, n_groups, t, c, tab, skip, nonuni);
   if (!j.any || !j.uniform) return;  // wave-uniform
+  const int fl = joint_first_lane(j);
+  const uint32_t m0f = (uint32_t)__shfl((int)j.m0, fl), cntf = (uint32_t)__shfl((int)j.cnt, fl);
   if ((threadIdx.x & 63u) == 0) {
     int top = 0;
-    for (uint32_t k = 0; k < j.cnt; k++) {
-      const TaDigits d = dig[j.m0 + k];
+    for (uint32_t k = 0; k < cntf; k++) {
+      const TaDigits d = dig[m0f + k];
       for (int i = 0; i < 4; i++) top = max(top, naf4_digits(d.a[i], naf[k][i]));
     }
     naf_top = top;
@@ -485,7 +516,7 @@ __global__ KB_OCC(HB_OCC_STRAUS) void k_ta_jladder(const TaDigits* __restrict__ 
   const int top = naf_top;
   HB_NOUNROLL for (int i = top; i >= 0; i--) {
     R = jac_dbl(R);
-    HB_NOUNROLL for (uint32_t k = 0; k < j.cnt; k++) {
+    HB_NOUNROLL for (uint32_t k = 0; k < cntf; k++) {
       HB_NOUNROLL for (int b = 0; b < 4; b++) {
         const int dg = naf[k][b][i];
         if (dg != 0) {  // wave-uniform
@@ -828,10 +859,24 @@ __global__ KB_OCC(HB_OCC_STRAUS) void k_ta_msm(const HmEntry* __restrict__ pts, 
 
 void launch_ta_lambda(const int64_t* idx, const uint32_t* grp_off, uint32_t n_groups,
                       uint32_t n_partials, int mode, TaDigits* dig, uint8_t* mstat, hipStream_t s, uint32_t t_u,
-                      uint8_t* nonuni) {
+                      uint8_t* nonuni, const uint8_t* skip) {
   if (!n_partials) return;
   hipLaunchKernelGGL(k_ta_lambda, dim3(blocks_of(n_partials, 64)), dim3(64), 0, s, idx, grp_off, n_groups,
-                     n_partials, mode, dig, mstat, t_u, nonuni);
+                     n_partials, mode, dig, mstat, t_u, nonuni, skip);
+}
+
+// one lane per group: does group g hold exactly t_u members at offset g t_u?  (vector stores only)
+__global__ __launch_bounds__(64) void k_ta_layout(const uint32_t* __restrict__ grp_off, uint32_t n_groups, uint32_t t_u,
+                                                  uint8_t* __restrict__ nonuni) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n_groups) return;
+  const uint32_t b = grp_off[g], en = grp_off[g + 1];
+  if (en - b != t_u || b != g * t_u) *nonuni = 1;
+}
+
+void launch_ta_layout(const uint32_t* grp_off, uint32_t n_groups, uint32_t t_u, uint8_t* nonuni, hipStream_t s) {
+  if (!n_groups) return;
+  hipLaunchKernelGGL(k_ta_layout, dim3(blocks_of(n_groups, 64)), dim3(64), 0, s, grp_off, n_groups, t_u, nonuni);
 }
 
 size_t ta_table_bytes(uint32_t n_partials) { return (size_t)blocks_of(n_partials, 64) * 16 * sizeof(G2JEntry) * 64; }
