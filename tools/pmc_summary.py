@@ -37,10 +37,13 @@ def main():
     names = collections.OrderedDict()
     for (_, name) in sq:
         names[name] = 1
-    # launches per slot of each kernel: the dispatches between the last two k_hash_to_g2 (slot start)
+    # launches per slot of each kernel: the dispatches of the last slot (from its k_attestation_roots
+    # to the next message hashing after it, as tools/last_slot.py)
     order = list(sq.keys())
-    starts = [k for k, (i, n) in enumerate(order) if n.startswith("k_hash_to_g2")]
+    starts = [k for k, (i, n) in enumerate(order) if n.startswith("k_attestation_roots")]
     slot = order[starts[-1]:] if starts else order
+    hashes = [k for k, (i, n) in enumerate(slot) if n.startswith("k_hash_to_g2") or n.startswith("k_h2c_field")]
+    slot = slot[:hashes[1]] if len(hashes) > 1 else slot
     slot_names = collections.Counter(n for _, n in slot)
     for name, cnt in slot_names.items():
         S = [sq[k] for k in slot if k[1] == name]
