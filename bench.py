@@ -723,10 +723,12 @@ def main(argv=None):
         s_min = L.hbls_slot_msm(0)
         L.hbls_slot_msm(s_min)
         n_rlc = NP + (0 if staged else V)
-        # (C5: the slot-wide check fails on the corrupted partials and the per-batch check runs on
-        # top of it; the per-kernel table then counts the per-batch path's work)
-        smsm = bool(bfe and s_min and n_rlc >= s_min) and "exp_v" not in d
-        sides = 1 if smsm else 3
+        # (C5: the slot-wide check fails on the corrupted partials and the per-batch, per-group and
+        # per-item checks run behind it -- data-dependent work: the kernels that only they launch, or
+        # share with the slot-wide check, are listed with zero units; k_rlc counts both sides)
+        smsm = bool(bfe and s_min and n_rlc >= s_min)
+        fallback = "exp_v" in d
+        sides = 1 if smsm and not fallback else 3
         rlc_item = opcounts.BLOCKS["rlc_g1"] + (opcounts.BLOCKS["rlc_g2"] if sides & 2 else 0)
         cmax = min(opcounts.RLC_CHUNK, max(1, NP // int(os.environ.get("HBLS_RLC_LANES", "65536"))))
         if cmax > 1:  # the library's chunking (hipbls.hip verify_pipeline): balanced chunks of a group
@@ -765,6 +767,9 @@ def main(argv=None):
                           "k_msm_bucket": (opcounts.MSM_ENTRIES_PER_ITEM * n_rlc, per_unit["k_msm_bucket"]),
                           "k_msm_reduce": (opcounts.MSM_PARTS, per_unit["k_msm_reduce"]),
                           "k_msm_sum": (opcounts.MSM_PARTS + opcounts.MSM_PARTS // 128, per_unit["k_msm_sum"])})
+            if fallback:
+                for kname in ("k_group_prep", "k_pair3_fin", "k_slines", "k_pair3_ml", "k_pair3_fallback", "k_fb_lines"):
+                    units[kname] = (0, units.get(kname, (0, (0, 0)))[1])
         elif bfe:
             nb = -(-V // opcounts.FE_BATCH)
             units.update({"k_group_prep": (V, prep_units["k_group_prep_b"]),

@@ -19,7 +19,8 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 SOURCES = ["hipbls.hip", "pipeline.hip", "threshold.hip", "vbatch.hip", "vgroup.hip", "roots.hip", "hash.hip", "msm.hip",
            "hashsplit.hip"]
-HEADERS = ["hd.h", "consts.h", "fp.h", "fr.h", "tower.h", "ec.h", "sha256.h", "h2c.h", "pairing.h", "ops.h", "pair3.h", "layout.h", "lines.h", "rlc.h", "ta_small.h"]
+HEADERS = ["hd.h", "consts.h", "fp.h", "fr.h", "tower.h", "ec.h", "sha256.h", "h2c.h", "pairing.h", "ops.h", "pair3.h",
+           "pair6.h", "layout.h", "lines.h", "rlc.h", "ta_small.h"]
 
 
 def _newer(target, deps):
@@ -56,13 +57,16 @@ def build_library(force: bool = False, verbose: bool = True, defines=(), out: st
     return LIB
 
 
-def build_hostcheck(force: bool = False, verbose: bool = True) -> str:
+def build_hostcheck(force: bool = False, verbose: bool = True, defines=(), out: str = "") -> str:
+    """defines / out: another build of the harness (e.g. ("HB_FP_ILP",): the two-accumulator
+    products, tests/test_sanitizers.py)."""
     src = os.path.join(ROOT, "tests", "native", "hostcheck.cpp")
-    out = os.path.join(ROOT, "tests", "native", "libhbls_hostcheck.so")
+    out = out or os.path.join(ROOT, "tests", "native", "libhbls_hostcheck.so")
     deps = [src] + [os.path.join(CSRC, f) for f in HEADERS]
     if not force and _newer(out, deps):
         return out
     cmd = ["g++", "-O3", "-march=x86-64-v3", "-std=c++17", "-pthread", "-shared", "-fPIC", "-o", out + ".tmp", src]
+    cmd[1:1] = ["-D" + d for d in defines]
     subprocess.run(cmd, check=True, timeout=900)
     os.replace(out + ".tmp", out)
     if verbose:

@@ -285,9 +285,9 @@ enum WsId {
   W_PCNT, W_PCOFF, W_PCFIRST, W_PCCOUNT, W_COEF, W_RT1, W_RT2,  // chunk plan + multi-scalar RLC
   W_TPCNT, W_TPCOFF, W_TPCFIRST, W_TPCCOUNT,                    // chunk plan of the aggregation
   W_FBUF, W_GS, W_BS, W_BLINES, W_BBAD, W_BVER, W_GLIST, W_GCOUNT,  // batched final exponentiation
-  W_MCNT, W_MOFF, W_MCUR, W_MORDER, W_MENT, W_MBUCKET, W_MPART, W_MPART2, W_MTOT, W_PBUF1, W_PBUF2, W_SFAIL,  // slot-wide check
+  W_MCNT, W_MOFF, W_MCUR, W_MORDER, W_MENT, W_MBUCKET, W_MPART, W_MPART2, W_MTOT, W_PBUF1, W_PBUF2, W_PBUF3, W_SFAIL,  // slot-wide check
   W_MLEV,                                                                          // its evaluated Miller lines
-  W_PFIN, W_TBUF,                                                                  // final exponentiations' factors
+  W_PFIN, W_TBUF, W_F1, W_F1BAD,                                                                  // final exponentiations' factors
   W_COUNT_
 };
 
@@ -705,7 +705,16 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
   const size_t fe_min = g_fe_batch_min.load();
   const bool bfe = fe_min && n_groups >= fe_min;
   const int item_always = (bfe || n_agg) ? 1 : 0;  // see the coefficient rule above
-  const size_t nbcap = (gcap + 1) / 2;  // batches of >= 2 groups (FE_BATCH, or g_fb_batch behind the slot-wide check)
+  // pairs per multi-Miller loop of the slot-wide check: enough that the loops fill at most one
+  // round of waves (21 groups per wave, one wave per SIMD) -- a second, partial round would double
+  // the kernel's span (HBLS_MML_PAIRS fixes it)
+  const size_t mmlk = g_mml_pairs ? g_mml_pairs
+                                  : std::min<size_t>(16, std::max<size_t>(1, (std::min(gcap, n_groups) +
+                                                                              GROUPS_PER_WAVE * 4 * d.n_cu - 1) /
+                                                                             (GROUPS_PER_WAVE * 4 * d.n_cu)));
+  const size_t nb1 = (gcap + mmlk - 1) / mmlk, nb2 = (nb1 + PROD_FAN - 1) / PROD_FAN;
+  // batches of >= 2 groups (FE_BATCH), or behind a failed slot-wide check its multi-Miller loops' chunks
+  const size_t nbcap = std::max((gcap + 1) / 2, nb1);
   Fp4Entry* fbuf = nullptr;
   G2JEntry *gS = nullptr, *bS = nullptr;
   LineEntry* blines = nullptr;
@@ -724,16 +733,10 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
   // on the device flag sfail).  Needs all groups in one chunk.
   const size_t smin = g_slot_msm_min.load();
   const bool smsm = bfe && smin && n_groups <= gcap && n + n_agg >= smin;
-  // pairs per multi-Miller loop: enough that the loops fill at most one round of waves (21 groups
-  // per wave, one wave per SIMD) -- a second, partial round would double the kernel's span
-  // (HBLS_MML_PAIRS fixes it)
-  const size_t mmlk = g_mml_pairs ? g_mml_pairs
-                                  : std::min<size_t>(16, std::max<size_t>(1, (std::min(gcap, n_groups) +
-                                                                              GROUPS_PER_WAVE * 4 * d.n_cu - 1) /
-                                                                             (GROUPS_PER_WAVE * 4 * d.n_cu)));
-  const size_t nb1 = (gcap + mmlk - 1) / mmlk, nb2 = (nb1 + PROD_FAN - 1) / PROD_FAN;
   G2MsmArgs ma{};
-  Fp4Entry *pbuf1 = nullptr, *pbuf2 = nullptr;
+  // pbuf1: the multi-Miller loops (kept: behind a failed slot-wide check they are the per-batch
+  // check's public-key sides); pbuf2 / pbuf3: the product tree's levels
+  Fp4Entry *pbuf1 = nullptr, *pbuf2 = nullptr, *pbuf3 = nullptr;
   uint8_t* sfail = nullptr;
   LineEntry* mlev = nullptr;
   if (smsm && (wsbuf(w, W_MCNT, MSM_KEYS, &ma.cnt) || wsbuf(w, W_MOFF, MSM_KEYS + 1, &ma.off) ||
@@ -742,6 +745,7 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
                wsbuf(w, W_MBUCKET, MSM_KEYS, &ma.bucket) || wsbuf(w, W_MPART, MSM_PARTS, &ma.part) ||
                wsbuf(w, W_MPART2, MSM_PARTS / 128, &ma.part2) || wsbuf(w, W_MTOT, 1, &ma.total) ||
                wsbuf(w, W_PBUF1, 3 * nb1, &pbuf1) || wsbuf(w, W_PBUF2, 3 * nb2, &pbuf2) ||
+               wsbuf(w, W_PBUF3, 3 * nb2, &pbuf3) ||
                wsbuf(w, W_SFAIL, 1, &sfail) || wsbuf(w, W_MLEV, N_LINES * gcap, &mlev)))
     return -1;
   const int sides1 = smsm ? 1 : 3;  // first pass: the public-key side only when the MSM takes the other
@@ -860,7 +864,12 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
           launch_rlc(apk, apkst, asig, fold->ta_status, nullptr, nullptr, bfe ? 1 : 0, (uint32_t)n_agg, (uint32_t)n,
                      key, apr, asr, s, acoef, sides1));
   }
-  if (hm_ready) HCHK(hipStreamWaitEvent(s, hm_ready, 0));
+  // small calls (no batched final exponentiation): the groups' sums and signature lines do not
+  // need the hashed messages, so they overlap the hashing; the wait comes before the pairing
+  if (hm_ready && bfe) HCHK(hipStreamWaitEvent(s, hm_ready, 0));
+  Fp4Entry* f1 = nullptr;
+  uint8_t* f1bad = nullptr;
+  if (!bfe && (wsbuf(w, W_F1, 3 * gcap, &f1) || wsbuf(w, W_F1BAD, gcap, &f1bad))) return -1;
   for (size_t g0 = 0; g0 < n_groups; g0 += gcap) {
     const uint32_t ng = (uint32_t)std::min(gcap, n_groups - g0);
     GroupPrepArgs ga{};
@@ -959,7 +968,7 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
           pr.f_in = cur;
           pr.f_range = PROD_FAN;
           pr.f_n = cur_n;
-          pr.f_out = pr.n == 1 ? pfin : (cur == pbuf1 ? pbuf2 : pbuf1);
+          pr.f_out = pr.n == 1 ? pfin : (cur == pbuf2 ? pbuf3 : pbuf2);
           TIMED(d, "k_pair3_prod", s, launch_pair3_prod(pr, s));
           cur = pr.f_out;
           cur_n = pr.n;
@@ -989,66 +998,98 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
         ga.p_only = 0;
         ga.guard = sfail;
         pm.guard = sfail;
+        // the per-batch check over the multi-Miller loops' chunks (mmlk consecutive groups): their
+        // stored loops (pbuf1) are the batches' public-key sides, so no group's (P_g, H(m_g)) loop
+        // is recomputed unless its batch fails.  Per batch: the signature sides S_g summed, the
+        // lines of the sum, its loop times the stored one, one final exponentiation (3 lanes: one
+        // round of waves for the chip-sized batch count, where six lanes would take two)
+        const uint32_t nbm = (uint32_t)((ng + mmlk - 1) / mmlk);
+        ga.gS = gS;
+        ga.bS = nullptr;
+        ga.fe_batch = 1;
+        TIMED(d, "k_group_prep", s, launch_group_prep(ga, s));
+        TIMED(d, "k_group_prep", s, launch_batch_sum(gS, ng, (uint32_t)mmlk, bS, s, sfail));
+        TIMED(d, "k_slines", s, launch_slines(bS, nullptr, nullptr, nbm, blines, nbm, bbad, s, sfail));
+        Pair3Args pb{};
+        pb.sig_lines = blines;
+        pb.stride = nbm;
+        pb.n = nbm;
+        pb.f_in = pbuf1;
+        pb.f_range = 1;
+        pb.f_n = nbm;
+        pb.pk_st = bbad;
+        pb.status = bver;
+        pb.guard = sfail;
+        TIMED(d, "k_pair3_fin", s, launch_pair3_fin(pb, s));
+        HCHK(hipMemsetAsync(gcount, 0, sizeof(uint32_t), s));
+        TIMED(d, "k_batch_verdict", s,
+              launch_batch_verdict(gst, bver, ng, gver + g0, glist, gcount, s, sfail, (uint32_t)mmlk));
+        // groups of a failing batch: their own (P_g, H(m_g)) loops, then each group alone below
+        pm.list = glist;
+        pm.count = gcount;
+        TIMED(d, "k_pair3_ml", s, launch_pair3_ml(pm, s));
       }
-      ga.gS = gS;
-      ga.bS = bS;
-      TIMED(d, "k_group_prep", s, launch_group_prep(ga, s));
-      // the (P_g, H(m_g)) Miller loops, stored unexponentiated
-      TIMED(d, "k_pair3_ml", s, launch_pair3_ml(pm, s));
-      // per batch: the lines of sum_g S_g, one Miller loop times the batch's stored loops, one
-      // final exponentiation
-      const uint8_t* guard = smsm ? sfail : nullptr;
-      TIMED(d, "k_slines", s, launch_slines(bS, nullptr, nullptr, nb, blines, nb, bbad, s, guard));
-      // the batches' signature-side loops (pfin[2b + 1]), the product trees of their stored loops
-      // (fan-in PROD_FAN, the last level into pfin[2b]), then each batch's final exponentiation
-      // multiplies just the two.  All on s: with several slots in flight a side stream here would
-      // share a hardware queue with another slot's long kernels (C2 24.4 vs 19.1 ms per slot)
-      {
-        Pair3Args ps{};
-        ps.sig_lines = blines;
-        ps.stride = nb;
-        ps.n = nb;
-        ps.f_out = pfin;
-        ps.f_out_stride = 2;
-        ps.f_out_off = 1;
-        ps.guard = guard;
-        TIMED(d, "k_pair3_mls", s, launch_pair3_mls(ps, s));
-      }
-      {
-        const Fp4Entry* cur = fbuf;
-        uint32_t cur_n = ng, span = 1;
-        while (span < fb) {
-          const uint32_t fan = std::min<uint32_t>(PROD_FAN, fb / span);
-          Pair3Args pr{};
-          pr.n = (cur_n + fan - 1) / fan;
-          pr.f_in = cur;
-          pr.f_range = fan;
-          pr.f_n = cur_n;
-          pr.guard = guard;
-          span *= fan;
-          if (span == fb) {
-            pr.f_out = pfin;
-            pr.f_out_stride = 2;
-          } else {
-            pr.f_out = tbuf;
-          }
-          TIMED(d, "k_pair3_prod", s, launch_pair3_prod(pr, s));
-          cur = pr.f_out;
-          cur_n = pr.n;
+      if (!smsm) {  // the per-batch check of FE_BATCH groups (below the slot-wide check's size)
+        ga.gS = gS;
+        ga.bS = bS;
+        TIMED(d, "k_group_prep", s, launch_group_prep(ga, s));
+        // the (P_g, H(m_g)) Miller loops, stored unexponentiated
+        TIMED(d, "k_pair3_ml", s, launch_pair3_ml(pm, s));
+        // per batch: the lines of sum_g S_g, one Miller loop times the batch's stored loops, one
+        // final exponentiation
+        const uint8_t* guard = nullptr;
+        TIMED(d, "k_slines", s, launch_slines(bS, nullptr, nullptr, nb, blines, nb, bbad, s, guard));
+        // the batches' signature-side loops (pfin[2b + 1]), the product trees of their stored loops
+        // (fan-in PROD_FAN, the last level into pfin[2b]), then each batch's final exponentiation
+        // multiplies just the two.  All on s: with several slots in flight a side stream here would
+        // share a hardware queue with another slot's long kernels (C2 24.4 vs 19.1 ms per slot)
+        {
+          Pair3Args ps{};
+          ps.sig_lines = blines;
+          ps.stride = nb;
+          ps.n = nb;
+          ps.f_out = pfin;
+          ps.f_out_stride = 2;
+          ps.f_out_off = 1;
+          ps.guard = guard;
+          TIMED(d, "k_pair3_mls", s, launch_pair3_mls(ps, s));
         }
+        {
+          const Fp4Entry* cur = fbuf;
+          uint32_t cur_n = ng, span = 1;
+          while (span < fb) {
+            const uint32_t fan = std::min<uint32_t>(PROD_FAN, fb / span);
+            Pair3Args pr{};
+            pr.n = (cur_n + fan - 1) / fan;
+            pr.f_in = cur;
+            pr.f_range = fan;
+            pr.f_n = cur_n;
+            pr.guard = guard;
+            span *= fan;
+            if (span == fb) {
+              pr.f_out = pfin;
+              pr.f_out_stride = 2;
+            } else {
+              pr.f_out = tbuf;
+            }
+            TIMED(d, "k_pair3_prod", s, launch_pair3_prod(pr, s));
+            cur = pr.f_out;
+            cur_n = pr.n;
+          }
+        }
+        Pair3Args pf{};
+        pf.pk_st = bbad;
+        pf.n = nb;
+        pf.f_in = pfin;
+        pf.f_range = 2;
+        pf.f_n = 2 * nb;
+        pf.status = bver;
+        pf.guard = guard;
+        TIMED(d, "k_pair3_fin", s, g_fe6 ? launch_pair6_fin(pf, s) : launch_pair3_fin(pf, s));
+        // groups of a failing batch: checked one by one (their stored loop, their own S lines)
+        HCHK(hipMemsetAsync(gcount, 0, sizeof(uint32_t), s));
+        TIMED(d, "k_batch_verdict", s, launch_batch_verdict(gst, bver, ng, gver + g0, glist, gcount, s, guard, fb));
       }
-      Pair3Args pf{};
-      pf.pk_st = bbad;
-      pf.n = nb;
-      pf.f_in = pfin;
-      pf.f_range = 2;
-      pf.f_n = 2 * nb;
-      pf.status = bver;
-      pf.guard = guard;
-      TIMED(d, "k_pair3_fin", s, g_fe6 ? launch_pair6_fin(pf, s) : launch_pair3_fin(pf, s));
-      // groups of a failing batch: checked one by one (their stored loop, their own S lines)
-      HCHK(hipMemsetAsync(gcount, 0, sizeof(uint32_t), s));
-      TIMED(d, "k_batch_verdict", s, launch_batch_verdict(gst, bver, ng, gver + g0, glist, gcount, s, guard, fb));
       TIMED(d, "k_slines", s, launch_slines(gS, glist, gcount, ng, glines, ng, nullptr, s));
       Pair3Args pg{};
       pg.sig_lines = glines;
@@ -1063,7 +1104,12 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
       TIMED(d, "k_pair3_fin", s, launch_pair3_fin(pg, s));
       continue;
     }
+    ga.skip_hm = 1;
     TIMED(d, "k_group_prep", s, launch_group_prep(ga, s));
+    if (hm_ready && g0 == 0) HCHK(hipStreamWaitEvent(s, hm_ready, 0));
+    // each group's two-pair Miller loop (3 lanes), then its final exponentiation in six lanes:
+    // about half the latency of one three-lane k_pair3 -- these calls are single Verifies and
+    // small batches, latency-bound
     Pair3Args pa{};
     pa.pk = gP;
     pa.pk_st = gst;
@@ -1073,8 +1119,17 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
     pa.stride = ng;
     pa.n = ng;
     pa.n_items = 0xffffffffu;
-    pa.status = gver + g0;
-    TIMED(d, "k_pair3", s, launch_pair3(pa, s));
+    pa.f_out = f1;
+    pa.f_bad = f1bad;
+    TIMED(d, "k_pair3", s, launch_pair3_fml(pa, s));
+    Pair3Args pf{};
+    pf.pk_st = f1bad;
+    pf.n = ng;
+    pf.f_in = f1;
+    pf.f_range = 1;
+    pf.f_n = ng;
+    pf.status = gver + g0;
+    TIMED(d, "k_pair3", s, launch_pair6_fin(pf, s));
   }
   HCHK(hipMemsetAsync(count, 0, sizeof(uint32_t), s));
   ScatterArgs sa{};

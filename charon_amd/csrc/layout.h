@@ -179,8 +179,14 @@ struct Pair3Args {
   // so that a final exponentiation's two factors (product tree root, signature-side loop) sit side
   // by side
   uint32_t f_out_stride, f_out_off;
+  // FML: one byte per unit, nonzero when the unit fails without its pairing (state, P or H(m) at
+  // infinity); the six-lane final exponentiation takes it as pk_st
+  uint8_t* f_bad;
 };
 void launch_pair3(const Pair3Args& a, hipStream_t s);
+// FML: the loop of launch_pair3 (both pairs), stored unexponentiated at f_out[e] with f_bad[e];
+// launch_pair6_fin over it (f_range 1, pk_st = f_bad) gives the same verdicts at half the latency
+void launch_pair3_fml(const Pair3Args& a, hipStream_t s);
 void launch_pair3_ml(const Pair3Args& a, hipStream_t s);
 void launch_pair3_fin(const Pair3Args& a, hipStream_t s);
 // PROD: f_out[e] = product of the stored values f_in of entries [e f_range, min((e + 1) f_range, f_n))
@@ -266,9 +272,14 @@ struct GroupPrepArgs {
   uint32_t fe_batch; // groups per batch (a power of two <= FE_BATCH; 0 = FE_BATCH)
   int p_only;        // slot-wide check (msm.hip): the public-key side and the state only, no S
   const uint8_t* guard;  // nullable: nothing unless *guard != 0
+  // small calls: do not read hm (the launch need not wait for the hashing); a message hashing to
+  // infinity is then caught by the group's pairing check (its status, k_pair3<FML>) instead of
+  // G_EMPTY -- either way the group fails and its items are checked alone
+  int skip_hm;
 };
 constexpr uint32_t FE_BATCH = 64;  // groups per batched final exponentiation (one wave of k_group_prep)
 void launch_group_prep(const GroupPrepArgs& a, hipStream_t s);
+void launch_batch_sum(const G2JEntry* gS, uint32_t ng, uint32_t k, G2JEntry* bS, hipStream_t s, const uint8_t* guard);
 // lines at -g1 of the affine images of pts[e], e = list ? list[u] (u < *count) : u, into
 // lines[j * stride + u]; bad[u] (nullable) = the point is infinity
 void launch_slines(const G2JEntry* pts, const uint32_t* list, const uint32_t* count, uint32_t n, LineEntry* lines,

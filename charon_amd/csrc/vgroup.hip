@@ -41,7 +41,7 @@ __device__ __forceinline__ uint8_t group_scan(const GroupPrepArgs& a, uint32_t l
                         cnt > 0;  // the aggregate takes its message from the group's partials
   if (cnt == 0 && e > b) m = a.msg_idx[b];  // the folded aggregate's message (a fallback may need it)
   a.gmsg[g] = m;
-  if (cnt == 0 || a.hm[m].h.inf) return G_EMPTY;
+  if (cnt == 0 || (!a.skip_hm && a.hm[m].h.inf)) return G_EMPTY;
   if (!consistent) return G_FALLBACK;
   if (!BATCH && cnt == 1 && !with_agg) {
     P = g1a_load(a.pk[first]);
@@ -135,7 +135,26 @@ __global__ KB_OCC(HB_OCC_PREP) void k_group_prep_b(GroupPrepArgs a) {
     const G2J T = {xch(S.X, addr), xch(S.Y, addr), xch(S.Z, addr)};
     S = jac_add(S, T);
   }
-  if ((lane & (fb - 1)) == 0 && lg < a.ng) a.bS[lg / (uint32_t)fb] = {S.X, S.Y, S.Z};
+  if (a.bS && (lane & (fb - 1)) == 0 && lg < a.ng) a.bS[lg / (uint32_t)fb] = {S.X, S.Y, S.Z};
+#endif
+}
+
+// Behind a failed slot-wide check: one lane per batch of k consecutive groups (a multi-Miller
+// loop's chunk), the sum of their signature sides S_g (infinity for groups that are not READY).
+__global__ KB_OCC(HB_OCC_PREP) void k_batch_sum(const G2JEntry* __restrict__ gS, uint32_t ng, uint32_t k,
+                                              G2JEntry* __restrict__ bS, const uint8_t* __restrict__ guard) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (guard && *guard == 0) return;
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t first = b * k;
+  if (first >= ng) return;
+  const uint32_t last = min(first + k, ng);
+  G2J S = jac_infinity<Fp2>();
+  for (uint32_t i = first; i < last; i++) {
+    const G2JEntry e = gS[i];
+    S = jac_add(S, G2J{e.X, e.Y, e.Z});
+  }
+  bS[b] = {S.X, S.Y, S.Z};
 #endif
 }
 
@@ -195,6 +214,10 @@ void launch_group_prep(const GroupPrepArgs& a, hipStream_t s) {
   if (a.p_only) hipLaunchKernelGGL(k_group_prep_p, dim3((a.ng + 63) / 64), dim3(64), 0, s, a);
   else if (a.gS) hipLaunchKernelGGL(k_group_prep_b, dim3((a.ng + 63) / 64), dim3(64), 0, s, a);
   else hipLaunchKernelGGL(k_group_prep, dim3((a.ng + 63) / 64), dim3(64), 0, s, a);
+}
+void launch_batch_sum(const G2JEntry* gS, uint32_t ng, uint32_t k, G2JEntry* bS, hipStream_t s, const uint8_t* guard) {
+  const uint32_t nb = (ng + k - 1) / k;
+  if (nb) hipLaunchKernelGGL(k_batch_sum, dim3((nb + 63) / 64), dim3(64), 0, s, gS, ng, k, bS, guard);
 }
 void launch_slines(const G2JEntry* pts, const uint32_t* list, const uint32_t* count, uint32_t n, LineEntry* lines,
                    uint32_t stride, uint8_t* bad, hipStream_t s, const uint8_t* guard) {

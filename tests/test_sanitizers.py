@@ -26,3 +26,4 @@ def test_host_harness_under_asan_ubsan():
     tail = (r.stdout + r.stderr)[-3000:]
     assert r.returncode == 0, tail
     assert "ERROR: AddressSanitizer" not in tail and "runtime error" not in tail, tail
+

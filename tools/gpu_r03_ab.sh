@@ -20,6 +20,6 @@ for v in "$@"; do
   extra=""
   [ "$rest" != "$vars" ] && extra=${rest#*|}
   [ "$vars" = "-" ] && vars=""
-  env $vars timeout -k 10 300 python -u bench.py --workload $wl $extra --steps 5 --warmup 2 --cpu-seconds 0 --callers 0 --aggregate-verify 0 --key-tables 0 --host-api 0 > gpurun_out/ab_${TAG}_$k.json 2> gpurun_out/ab_${TAG}_$k.err || exit 1
+  env $vars timeout -k 10 300 python -u bench.py --workload $wl --steps 5 --warmup 2 --cpu-seconds 0 --callers 0 --aggregate-verify 0 --key-tables 0 --host-api 0 $extra > gpurun_out/ab_${TAG}_$k.json 2> gpurun_out/ab_${TAG}_$k.err || exit 1
   echo "$v" > gpurun_out/ab_${TAG}_$k.env
 done
