@@ -46,9 +46,10 @@ import numpy as np
 # four side streams) + the library stream.  With HIP's default of four, streams share queues and a
 # latency-bound kernel (one final exponentiation, a hashing stage of 64 messages) holds up
 # whatever else sits in its queue: C3 106.4 -> 101.3 ms, C2 16.7 -> 16.0 ms per slot on one box
-# (profiles/r03j_*).  Set before anything initialises the HIP runtime; a value from the
-# environment wins.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+# (profiles/r03j_*).  Set before anything initialises the HIP runtime, over the environment's
+# value (the GPU pool exports HIP's default of four); HBLS_HW_QUEUES chooses another count (at most
+# 32).  A charon process sets it the same way in its environment.
+os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, max(1, int(os.environ.get("HBLS_HW_QUEUES", "16")))))
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 if ROOT not in sys.path:
@@ -521,6 +522,8 @@ def main(argv=None):
                     help="also time the slot with decompressed-key tables built once (steady state)")
     ap.add_argument("--host-api", type=int, default=1,
                     help="also time the host-buffer (PCIe-inclusive) entry points on the same inputs (0: skip)")
+    ap.add_argument("--host-threads", type=int, default=3,
+                    help="threads calling the host-buffer entry points at once (with --host-api; 1: skip)")
     ap.add_argument("--inflight", type=int, default=3,
                     help="slots in flight (each on its own stream and outputs); 1 = one slot at a time")
     ap.add_argument("--mode", default="slot", choices=["slot", "staged"],
@@ -858,6 +861,38 @@ def main(argv=None):
         # the rate the Go shim sees (host buffers, PCIe both ways, partial Verify then
         # ThresholdAggregate as two calls); never the headline
         out["pcie_inclusive_items_per_s"] = out["host_buffer_items_per_s"]
+        # the same pair of calls from several threads at once (charon's goroutines: parsigex and
+        # sigagg of different duties); each call owns a host-call context, so their transfers and
+        # kernels overlap on the device (hipbls.hip Hc)
+        if args.host_threads > 1:
+            rounds = 2
+            res = [None] * args.host_threads
+
+            def worker(k):
+                st_k = np.zeros(NP, dtype=np.uint8)
+                to_k = np.zeros(V * 96, dtype=np.uint8)
+                ts_k = np.zeros(V, dtype=np.uint8)
+                ok = True
+                for _ in range(rounds):
+                    rc1 = L.hbls_verify_batch(_p(d["pks"]), _p(d["sigs"]), _p(d["item_msgs"]), _p(d["item_off"]),
+                                              _p(d["item_len"]), NP, _p(st_k))
+                    rc2 = L.hbls_threshold_aggregate_batch(_p(d["ta_sigs"]), _p(d["ta_idx"]), _p(d["grp_off"]), V,
+                                                           _p(to_k), _p(ts_k))
+                    ok = ok and rc1 == 0 and rc2 == 0 and np.array_equal(st_k, st) and np.array_equal(ts_k, tst_h) \
+                        and np.array_equal(to_k, tout_h)
+                res[k] = ok
+
+            ths = [threading.Thread(target=worker, args=(k,)) for k in range(args.host_threads)]
+            t0 = time.perf_counter()
+            for th in ths:
+                th.start()
+            for th in ths:
+                th.join()
+            dt = time.perf_counter() - t0
+            out["host_buffer_concurrent"] = {
+                "threads": args.host_threads, "calls_per_thread": 2 * rounds,
+                "items_per_s": round(args.host_threads * rounds * (NP + V) / dt, 1),
+                "same_results_as_sequential": all(res)}
 
     if rank == 0 and world == 1 and args.key_tables and not staged:
         out["with_key_tables"] = key_table_slots(L, d_pk, d_dvpk, outs, NP, V, args.steps, step_slot, mk, items)

@@ -318,6 +318,18 @@ struct Timed {
   hipEvent_t a, b;
 };
 
+// Host-call contexts: a blocking host-buffer call (Verify / ThresholdAggregate / VerifyAggregate
+// batches: what the Go shim calls from its goroutines) owns one from its first upload to its last
+// download -- its own stream and staging buffers -- and holds the device lock only while it
+// enqueues.  Several calls from different threads therefore overlap on the device (one workspace
+// set each), as consecutive slots do on the device-buffer path.  g_ws_sets contexts per device; a
+// caller beyond them waits for one to finish.
+struct Hc {
+  hipStream_t s = nullptr;
+  DevBuf io[I_COUNT];
+  bool busy = false;
+};
+
 struct Dev {
   int ord = -1;
   int n_cu = 256;  // compute units (4 SIMDs each)
@@ -326,6 +338,9 @@ struct Dev {
   unsigned next_ws = 0;
   DevBuf io[I_COUNT];
   std::mutex mu;  // one call at a time enqueues on this device
+  Hc hc[N_WS_MAX];
+  std::mutex hc_mu;  // hc[].busy
+  std::condition_variable hc_cv;
   // end of the last verification's decompression stage: with HBLS_STAGGER=1 the next verification
   // starts its own decompression after it, so consecutive slots in flight run staggered (one slot's
   // decompression beside the previous slot's combinations and pairings) instead of in lockstep
@@ -447,6 +462,7 @@ int dev_create(int ord, Dev** out) {
     HCHK(hipEventCreateWithFlags(&w.ev_fork, hipEventDisableTiming));
     HCHK(hipEventCreateWithFlags(&w.ev_ta, hipEventDisableTiming));
     HCHK(hipEventCreateWithFlags(&w.ev_msm, hipEventDisableTiming));
+    HCHK(hipStreamCreateWithPriority(&d->hc[k_ws].s, hipStreamNonBlocking, prio_lo));
   }
   *out = d;
   return 0;
@@ -525,13 +541,37 @@ int dev_of_stream(hipStream_t s, Dev** out) {
   return set_err("stream belongs to device " + std::to_string(ord) + ", outside the library's device mask");
 }
 
+// a host call's stream and staging buffers: its context's, or the device's own (h == nullptr: the
+// small entry points, which hold the device lock throughout)
+inline hipStream_t call_stream(Dev& d, Hc* h) { return h ? h->s : d.stream; }
+inline DevBuf* call_io(Dev& d, Hc* h) { return h ? h->io : d.io; }
+
 template <class T>
-int upload(Dev& d, IoId id, const T* src, size_t count, T** dst) {
+int upload(Dev& d, IoId id, const T* src, size_t count, T** dst, Hc* h = nullptr) {
   void* p;
-  if (ensure_buf(d.io[id], count * sizeof(T), &p)) return -1;
-  if (count) HCHK(hipMemcpyAsync(p, src, count * sizeof(T), hipMemcpyHostToDevice, d.stream));
+  if (ensure_buf(call_io(d, h)[id], count * sizeof(T), &p)) return -1;
+  if (count) HCHK(hipMemcpyAsync(p, src, count * sizeof(T), hipMemcpyHostToDevice, call_stream(d, h)));
   *dst = (T*)p;
   return 0;
+}
+
+Hc& hc_acquire(Dev& d) {
+  std::unique_lock<std::mutex> lk(d.hc_mu);
+  for (;;) {
+    for (int k = 0; k < g_ws_sets; k++)
+      if (!d.hc[k].busy) {
+        d.hc[k].busy = true;
+        return d.hc[k];
+      }
+    d.hc_cv.wait(lk);
+  }
+}
+void hc_release(Dev& d, Hc& h) {
+  {
+    std::lock_guard<std::mutex> lk(d.hc_mu);
+    h.busy = false;
+  }
+  d.hc_cv.notify_one();
 }
 
 // per-call random linear combination key (OS CSPRNG)
@@ -1267,18 +1307,18 @@ void dedup_messages(const uint8_t* msgs, const uint64_t* off, const uint32_t* le
 // runs on its side stream 2 (beside the decompression the verification forks next) and *ready is
 // the event the verification waits on before it needs H(m).
 int hash_table(Dev& d, const MsgTable& t, MsgEntry** hm_out, bool lines, Ws* w = nullptr,
-               hipEvent_t* ready = nullptr) {
+               hipEvent_t* ready = nullptr, Hc* h = nullptr) {
   uint8_t* dmsg;
   uint64_t* doff;
   uint32_t* dlen;
   void* hm;
-  if (upload(d, I_MSG, t.bytes.data(), t.bytes.size(), &dmsg)) return -1;
-  if (upload(d, I_OFF, t.off.data(), t.off.size(), &doff)) return -1;
-  if (upload(d, I_LEN, t.len.data(), t.len.size(), &dlen)) return -1;
-  if (ensure_buf(d.io[I_HM], t.len.size() * sizeof(MsgEntry), &hm)) return -1;
-  hipStream_t hs = d.stream;
+  if (upload(d, I_MSG, t.bytes.data(), t.bytes.size(), &dmsg, h)) return -1;
+  if (upload(d, I_OFF, t.off.data(), t.off.size(), &doff, h)) return -1;
+  if (upload(d, I_LEN, t.len.data(), t.len.size(), &dlen, h)) return -1;
+  if (ensure_buf(call_io(d, h)[I_HM], t.len.size() * sizeof(MsgEntry), &hm)) return -1;
+  hipStream_t hs = call_stream(d, h);
   if (w) {
-    HCHK(hipEventRecord(w->ev_ta, d.stream));  // the uploads (ev_ta is free until the verification)
+    HCHK(hipEventRecord(w->ev_ta, hs));  // the uploads (ev_ta is free until the verification)
     hs = w->side[2];
     HCHK(hipStreamWaitEvent(hs, w->ev_ta, 0));
   }
@@ -1315,6 +1355,40 @@ int for_each_device(size_t n_units, const std::function<int(Dev&, size_t, size_t
         return;
       }
       rc[k] = fn(d, b, e);
+      if (rc[k]) errs[k] = g_err;
+    });
+  }
+  for (auto& t : th) t.join();
+  for (size_t k = 0; k < nd; k++)
+    if (rc[k]) return set_err("device " + std::to_string(g_devs[k]->ord) + ": " + errs[k]);
+  return 0;
+}
+
+// for_each_device for the heavy host-buffer calls: each device's share runs in a host-call context
+// (acquired before the device lock); fn may release the lock once everything is enqueued and then
+// wait for its own stream only
+using HcFn = std::function<int(Dev&, Hc&, size_t, size_t, std::unique_lock<std::mutex>&)>;
+int for_each_device_hc(size_t n_units, const HcFn& fn) {
+  auto run = [&fn](Dev& d, size_t b, size_t e) -> int {
+    Hc& h = hc_acquire(d);
+    struct Rel {
+      Dev& d;
+      Hc& h;
+      ~Rel() { hc_release(d, h); }
+    } rel{d, h};
+    std::unique_lock<std::mutex> lk(d.mu);
+    if (hipSetDevice(d.ord) != hipSuccess) return set_err("hipSetDevice failed");
+    return fn(d, h, b, e, lk);
+  };
+  const size_t nd = std::min(g_devs.size(), std::max<size_t>(n_units, 1));
+  if (nd <= 1) return run(*g_devs[0], 0, n_units);
+  std::vector<int> rc(nd, 0);
+  std::vector<std::string> errs(nd);
+  std::vector<std::thread> th;
+  for (size_t k = 0; k < nd; k++) {
+    const size_t b = n_units * k / nd, e = n_units * (k + 1) / nd;
+    th.emplace_back([&, k, b, e]() {
+      rc[k] = run(*g_devs[k], b, e);
       if (rc[k]) errs[k] = g_err;
     });
   }
@@ -1386,7 +1460,7 @@ int verify_host(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msgs, co
     if (k == 0 || all.idx[order[k]] != all.idx[order[k - 1]] || k - gstart.back() >= g_gmax) gstart.push_back(k);
   const size_t n_groups = gstart.size();
   gstart.push_back(n);
-  return for_each_device(n_groups, [&](Dev& d, size_t gb, size_t ge) -> int {
+  return for_each_device_hc(n_groups, [&](Dev& d, Hc& h, size_t gb, size_t ge, std::unique_lock<std::mutex>& lk) -> int {
     const size_t ib = gstart[gb], ie = gstart[ge], m = ie - ib;
     if (m == 0) return 0;
     MsgTable t;
@@ -1400,26 +1474,27 @@ int verify_host(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msgs, co
     for (size_t g = gb; g <= ge; g++) goff[g - gb] = (uint32_t)(gstart[g] - ib);
     // the messages hash on a side stream while the keys and signatures decompress (latency of
     // one call: the two chains run side by side)
-    Ws& w = ws_acquire(d, d.stream);
+    Ws& w = ws_acquire(d, h.s);
     MsgEntry* hm;
     hipEvent_t hm_ready = nullptr;
-    if (hash_table(d, t, &hm, true, &w, &hm_ready)) return -1;
+    if (hash_table(d, t, &hm, true, &w, &hm_ready, &h)) return -1;
     uint8_t *dpk, *dsig, *dst;
     uint32_t *didx, *dgoff, *dkc = nullptr;
-    if (upload(d, I_PK, hpk.data(), hpk.size(), &dpk) || upload(d, I_SIG, hsig.data(), hsig.size(), &dsig) ||
-        upload(d, I_MIDX, t.idx.data(), m, &didx) || upload(d, I_VGOFF, goff.data(), goff.size(), &dgoff))
+    if (upload(d, I_PK, hpk.data(), hpk.size(), &dpk, &h) || upload(d, I_SIG, hsig.data(), hsig.size(), &dsig, &h) ||
+        upload(d, I_MIDX, t.idx.data(), m, &didx, &h) || upload(d, I_VGOFF, goff.data(), goff.size(), &dgoff, &h))
       return -1;
     std::vector<uint32_t> kc;
-    if (kc_lookup(hpk.data(), m, kc) && upload(d, I_KC, kc.data(), m, &dkc)) return -1;
+    if (kc_lookup(hpk.data(), m, kc) && upload(d, I_KC, kc.data(), m, &dkc, &h)) return -1;
     void* p;
-    if (ensure_buf(d.io[I_STAT], m, &p)) return -1;
+    if (ensure_buf(h.io[I_STAT], m, &p)) return -1;
     dst = (uint8_t*)p;
-    if (verify_pipeline(d, w, dpk, dsig, didx, hm, m, dgoff, ge - gb, dst, d.stream, hm_ready, nullptr, dkc))
+    if (verify_pipeline(d, w, dpk, dsig, didx, hm, m, dgoff, ge - gb, dst, h.s, hm_ready, nullptr, dkc))
       return -1;
-    if (ws_release(w, d.stream)) return -1;
+    if (ws_release(w, h.s)) return -1;
+    lk.unlock();  // enqueued: other callers may enqueue while this one waits for its stream
     std::vector<uint8_t> hst(m);
-    HCHK(hipMemcpyAsync(hst.data(), dst, m, hipMemcpyDeviceToHost, d.stream));
-    HCHK(hipStreamSynchronize(d.stream));
+    HCHK(hipMemcpyAsync(hst.data(), dst, m, hipMemcpyDeviceToHost, h.s));
+    HCHK(hipStreamSynchronize(h.s));
     for (size_t k = 0; k < m; k++) status[order[ib + k]] = hst[k];
     return 0;
   });
@@ -1436,7 +1511,7 @@ int check_offsets(const uint32_t* grp_off, size_t n_groups) {
 int group_op_host(const uint8_t* sigs, const int64_t* idx, const uint32_t* grp_off, size_t n_groups, int mode,
                   uint8_t* out, uint8_t* status) {
   if (check_offsets(grp_off, n_groups)) return -1;
-  return for_each_device(n_groups, [&](Dev& d, size_t gb, size_t ge) -> int {
+  return for_each_device_hc(n_groups, [&](Dev& d, Hc& h, size_t gb, size_t ge, std::unique_lock<std::mutex>& lk) -> int {
     const size_t ng = ge - gb, pb = grp_off[gb], np = grp_off[ge] - pb;
     if (ng == 0) return 0;
     std::vector<uint32_t> goff(ng + 1);
@@ -1444,23 +1519,23 @@ int group_op_host(const uint8_t* sigs, const int64_t* idx, const uint32_t* grp_o
     uint8_t* dsig;
     int64_t* didx = nullptr;
     uint32_t* dgoff;
-    if (upload(d, I_SIG, sigs + 96 * pb, np * 96, &dsig)) return -1;
-    if (mode == 0 && upload(d, I_IDX, idx + pb, np, &didx)) return -1;
-    if (upload(d, I_GOFF, goff.data(), ng + 1, &dgoff)) return -1;
+    if (upload(d, I_SIG, sigs + 96 * pb, np * 96, &dsig, &h)) return -1;
+    if (mode == 0 && upload(d, I_IDX, idx + pb, np, &didx, &h)) return -1;
+    if (upload(d, I_GOFF, goff.data(), ng + 1, &dgoff, &h)) return -1;
     void *dout, *dst;
-    if (ensure_buf(d.io[I_OUT], ng * 96, &dout) || ensure_buf(d.io[I_STAT], ng, &dst)) return -1;
-    Ws& w = ws_acquire(d, d.stream);
+    if (ensure_buf(h.io[I_OUT], ng * 96, &dout) || ensure_buf(h.io[I_STAT], ng, &dst)) return -1;
+    Ws& w = ws_acquire(d, h.s);
     HmEntry* pts;
     uint8_t* mst0;
     if (wsbuf(w, W_TAPTS, np, &pts) || wsbuf(w, W_TADST, np, &mst0)) return -1;
-    if (np) TIMED(d, "k_dec_sig_pt", d.stream, launch_dec_sig_pt(dsig, (uint32_t)np, pts, mst0, d.stream));
-    if (ta_tail(d, w, pts, nullptr, mst0, didx, dgoff, ng, np, mode, (uint8_t*)dout, (uint8_t*)dst, nullptr,
-                d.stream))
+    if (np) TIMED(d, "k_dec_sig_pt", h.s, launch_dec_sig_pt(dsig, (uint32_t)np, pts, mst0, h.s));
+    if (ta_tail(d, w, pts, nullptr, mst0, didx, dgoff, ng, np, mode, (uint8_t*)dout, (uint8_t*)dst, nullptr, h.s))
       return -1;
-    if (ws_release(w, d.stream)) return -1;
-    HCHK(hipMemcpyAsync(out + 96 * gb, dout, ng * 96, hipMemcpyDeviceToHost, d.stream));
-    HCHK(hipMemcpyAsync(status + gb, dst, ng, hipMemcpyDeviceToHost, d.stream));
-    HCHK(hipStreamSynchronize(d.stream));
+    if (ws_release(w, h.s)) return -1;
+    lk.unlock();  // enqueued: other callers may enqueue while this one waits for its stream
+    HCHK(hipMemcpyAsync(out + 96 * gb, dout, ng * 96, hipMemcpyDeviceToHost, h.s));
+    HCHK(hipMemcpyAsync(status + gb, dst, ng, hipMemcpyDeviceToHost, h.s));
+    HCHK(hipStreamSynchronize(h.s));
     return 0;
   });
 }
@@ -1718,7 +1793,7 @@ int hbls_verify_aggregate_batch(const uint8_t* pks, const uint32_t* grp_off, con
   if (ensure_init()) return -1;
   if (n_groups == 0) return 0;
   if (check_offsets(grp_off, n_groups)) return -1;
-  return for_each_device(n_groups, [&](Dev& d, size_t gb, size_t ge) -> int {
+  return for_each_device_hc(n_groups, [&](Dev& d, Hc& h, size_t gb, size_t ge, std::unique_lock<std::mutex>& lk) -> int {
     const size_t ng = ge - gb, pb = grp_off[gb], np = grp_off[ge] - pb;
     if (ng == 0) return 0;
     MsgTable t;  // one hash per group (messages need not be distinct)
@@ -1731,20 +1806,22 @@ int hbls_verify_aggregate_batch(const uint8_t* pks, const uint32_t* grp_off, con
     std::vector<uint32_t> goff(ng + 1);
     for (size_t g = 0; g <= ng; g++) goff[g] = grp_off[gb + g] - (uint32_t)pb;
     uint8_t *dpk, *dsig;
-    if (upload(d, I_PK, pks + 48 * pb, np * 48, &dpk) || upload(d, I_SIG, sigs + 96 * gb, ng * 96, &dsig)) return -1;
-    void* p;
-    if (ensure_buf(d.io[I_STAT], ng, &p)) return -1;
-    Ws& w = ws_acquire(d, d.stream);
-    uint8_t* dst = (uint8_t*)p;
-    void* hmp;  // the message table's buffer (hash_table fills the same one on the library stream)
-    if (ensure_buf(d.io[I_HM], ng * sizeof(MsgEntry), &hmp)) return -1;
-    MsgEntry* hm = (MsgEntry*)hmp;
-    if (va_pipeline(d, w, dpk, np, goff.data(), ng, dsig, hm, dst, d.stream,
-                    [&]() -> int { MsgEntry* h; return hash_table(d, t, &h, true); }))
+    if (upload(d, I_PK, pks + 48 * pb, np * 48, &dpk, &h) || upload(d, I_SIG, sigs + 96 * gb, ng * 96, &dsig, &h))
       return -1;
-    if (ws_release(w, d.stream)) return -1;
-    HCHK(hipMemcpyAsync(status + gb, dst, ng, hipMemcpyDeviceToHost, d.stream));
-    HCHK(hipStreamSynchronize(d.stream));
+    void* p;
+    if (ensure_buf(h.io[I_STAT], ng, &p)) return -1;
+    Ws& w = ws_acquire(d, h.s);
+    uint8_t* dst = (uint8_t*)p;
+    void* hmp;  // the message table's buffer (hash_table fills the same one on the call's stream)
+    if (ensure_buf(h.io[I_HM], ng * sizeof(MsgEntry), &hmp)) return -1;
+    MsgEntry* hm = (MsgEntry*)hmp;
+    if (va_pipeline(d, w, dpk, np, goff.data(), ng, dsig, hm, dst, h.s,
+                    [&]() -> int { MsgEntry* hx; return hash_table(d, t, &hx, true, nullptr, nullptr, &h); }))
+      return -1;
+    if (ws_release(w, h.s)) return -1;
+    lk.unlock();  // enqueued: other callers may enqueue while this one waits for its stream
+    HCHK(hipMemcpyAsync(status + gb, dst, ng, hipMemcpyDeviceToHost, h.s));
+    HCHK(hipStreamSynchronize(h.s));
     return 0;
   });
 }

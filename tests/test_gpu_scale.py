@@ -333,6 +333,55 @@ def test_device_call_and_host_call_do_not_race(L, hipbls):
     assert list(vst.cpu().numpy()) == [NOT_VERIFIED if i % 3 == 0 else OK for i in range(96)]
 
 
+def test_concurrent_host_batches_overlap_exactly(hipbls):
+    """Five threads (more than the library's three host-call contexts, so some wait for one) each
+    call VerifyBatch, ThresholdAggregateBatch and VerifyAggregateBatch on their own inputs at once:
+    every result equals the same call made alone (hipbls.hip Hc: each call owns a context, the
+    device lock covers only the enqueueing)."""
+    rng = random.Random(17)
+    n_keys = 48
+    keys = [hipbls.generate_secret_key() for _ in range(n_keys)]
+    pks = [hipbls.secret_to_public_key(k) for k in keys]
+    jobs = []
+    for t in range(5):
+        msgs = [hashlib.sha256(b"host call %d %d" % (t, i % 9)).digest() for i in range(600)]
+        ks = [rng.randrange(n_keys) for _ in range(600)]
+        sigs = hipbls.sign_batch([keys[k] for k in ks], msgs)
+        sigs = [sigs[(i + 1) % 600] if i % 11 == t else sigs[i] for i in range(600)]  # some wrong
+        split = hipbls.threshold_split(keys[t], 5, 3)
+        m = hashlib.sha256(b"ta %d" % t).digest()
+        parts = sorted((i, hipbls.sign(sk, m)) for i, sk in split.items())
+        groups = [dict(parts[j:j + 3]) for j in range(3)] * 20
+        va_m = [hashlib.sha256(b"va %d %d" % (t, g)).digest() for g in range(40)]
+        va_pk = [[pks[(g + j) % n_keys] for j in range(8)] for g in range(40)]
+        va_sig = [hipbls.aggregate(hipbls.sign_batch([keys[(g + j) % n_keys] for j in range(8)], [va_m[g]] * 8))
+                  for g in range(40)]
+        va_sig[t] = va_sig[t + 1]
+        jobs.append(([pks[k] for k in ks], msgs, sigs, groups, va_pk, va_sig, va_m))
+
+    def run(j):
+        pk, m, sg, groups, va_pk, va_sig, va_m = j
+        v = hipbls.verify_batch(pk, m, sg)
+        ta = hipbls.threshold_aggregate_batch(groups)
+        va = hipbls.verify_aggregate_batch(va_pk, va_sig, va_m)
+        return v, ta, va
+
+    alone = [run(j) for j in jobs]
+    got = [None] * len(jobs)
+
+    def worker(k):
+        got[k] = run(jobs[k])
+
+    th = [threading.Thread(target=worker, args=(k,)) for k in range(len(jobs))]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert got == alone
+    assert all(any(st != OK for st in a[0]) for a in alone)  # the wrong signatures were caught
+    assert all(a[2][k] != OK for k, a in enumerate(alone))  # and the wrong aggregates
+
+
 def _stats(L):
     out = (ctypes.c_uint64 * 6)()
     assert L.hbls_stats(out, 6) == 0
