@@ -262,8 +262,10 @@ bool g_stagger = false;
 // HBLS_SLOT_MSM: batched verifications of at least this many items (partials + folded aggregates,
 // one chunk of groups) check every group at once -- the signature side as one multi-scalar
 // multiplication (msm.hip), one final exponentiation for the call -- and fall back to the
-// per-batch check when that fails (0 = never)
-std::atomic<size_t> g_slot_msm_min{65536};
+// per-batch check when that fails (0 = never).  32 768: at C2 (40 k partials + 10 k folded
+// aggregates) the slot-wide check beats the per-batch one since the multi-Miller loops and the
+// six-lane final exponentiation (14.4 vs 15.3 ms per slot, profiles/r03s_ab_summary.txt)
+std::atomic<size_t> g_slot_msm_min{32768};
 // HBLS_FE6=0: the final exponentiations without lines in three lanes (k_pair3<FIN>) instead of six
 // (k_pair6_fin, pair6.h)
 bool g_fe6 = true;
@@ -909,7 +911,7 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
   if (hm_ready && bfe) HCHK(hipStreamWaitEvent(s, hm_ready, 0));
   Fp4Entry* f1 = nullptr;
   uint8_t* f1bad = nullptr;
-  if (!bfe && (wsbuf(w, W_F1, 3 * gcap, &f1) || wsbuf(w, W_F1BAD, gcap, &f1bad))) return -1;
+  if (!bfe && (wsbuf(w, W_F1, 3 * 2 * gcap, &f1) || wsbuf(w, W_F1BAD, gcap, &f1bad))) return -1;
   for (size_t g0 = 0; g0 < n_groups; g0 += gcap) {
     const uint32_t ng = (uint32_t)std::min(gcap, n_groups - g0);
     GroupPrepArgs ga{};
@@ -1146,28 +1148,34 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
     }
     ga.skip_hm = 1;
     TIMED(d, "k_group_prep", s, launch_group_prep(ga, s));
+    // these calls are single Verifies and small batches, latency-bound: the signature side's
+    // Miller loop runs while the messages still hash, then each group's (P, H(m)) loop, then ONE
+    // six-lane final exponentiation of the two stored loops (f1[2g], f1[2g + 1])
+    Pair3Args ps{};
+    ps.sig_lines = glines;
+    ps.stride = ng;
+    ps.n = ng;
+    ps.f_out = f1;
+    ps.f_out_stride = 2;
+    ps.f_out_off = 1;
+    TIMED(d, "k_pair3", s, launch_pair3_mls(ps, s));
     if (hm_ready && g0 == 0) HCHK(hipStreamWaitEvent(s, hm_ready, 0));
-    // each group's two-pair Miller loop (3 lanes), then its final exponentiation in six lanes:
-    // about half the latency of one three-lane k_pair3 -- these calls are single Verifies and
-    // small batches, latency-bound
     Pair3Args pa{};
     pa.pk = gP;
     pa.pk_st = gst;
     pa.msg_idx = gmsg + g0;
     pa.hm = hm;
-    pa.sig_lines = glines;
-    pa.stride = ng;
     pa.n = ng;
-    pa.n_items = 0xffffffffu;
     pa.f_out = f1;
+    pa.f_out_stride = 2;
     pa.f_bad = f1bad;
-    TIMED(d, "k_pair3", s, launch_pair3_fml(pa, s));
+    TIMED(d, "k_pair3", s, launch_pair3_ml(pa, s));
     Pair3Args pf{};
     pf.pk_st = f1bad;
     pf.n = ng;
     pf.f_in = f1;
-    pf.f_range = 1;
-    pf.f_n = ng;
+    pf.f_range = 2;
+    pf.f_n = 2 * ng;
     pf.status = gver + g0;
     TIMED(d, "k_pair3", s, launch_pair6_fin(pf, s));
   }

@@ -179,14 +179,11 @@ struct Pair3Args {
   // so that a final exponentiation's two factors (product tree root, signature-side loop) sit side
   // by side
   uint32_t f_out_stride, f_out_off;
-  // FML: one byte per unit, nonzero when the unit fails without its pairing (state, P or H(m) at
-  // infinity); the six-lane final exponentiation takes it as pk_st
+  // ML (nullable): one byte per unit, nonzero when the unit fails without its pairing (state, P or
+  // H(m) at infinity); a six-lane final exponentiation over the stored loop takes it as pk_st
   uint8_t* f_bad;
 };
 void launch_pair3(const Pair3Args& a, hipStream_t s);
-// FML: the loop of launch_pair3 (both pairs), stored unexponentiated at f_out[e] with f_bad[e];
-// launch_pair6_fin over it (f_range 1, pk_st = f_bad) gives the same verdicts at half the latency
-void launch_pair3_fml(const Pair3Args& a, hipStream_t s);
 void launch_pair3_ml(const Pair3Args& a, hipStream_t s);
 void launch_pair3_fin(const Pair3Args& a, hipStream_t s);
 // PROD: f_out[e] = product of the stored values f_in of entries [e f_range, min((e + 1) f_range, f_n))

@@ -31,9 +31,7 @@ __global__ KB_OCC(HB_OCC_LINES) void k_lines_msg(MsgEntry* __restrict__ hm, uint
 // unexponentiated (entries with a nonzero pk_st byte contribute one).
 // P3_MLS: the (-g1, S) loop alone, stored (the final exponentiation's second factor, computed beside
 // the product tree instead of in front of the exponentiation).
-// P3_FML: the P3_FULL loop (both pairs) stored unexponentiated, with a per-unit byte saying the
-// unit fails without its pairing -- the small calls' group checks, exponentiated by k_pair6_fin.
-enum { P3_FULL = 0, P3_ML = 1, P3_FIN = 2, P3_PROD = 3, P3_MML = 4, P3_MLS = 5, P3_FML = 6 };
+enum { P3_FULL = 0, P3_ML = 1, P3_FIN = 2, P3_PROD = 3, P3_MML = 4, P3_MLS = 5 };
 
 __device__ __forceinline__ size_t f_out_index(const Pair3Args& a, uint32_t e) {
   return (size_t)e * (a.f_out_stride ? a.f_out_stride : 1u) + a.f_out_off;
@@ -145,15 +143,12 @@ __global__ KB_OCC(HB_OCC_PAIR3) void k_pair3(Pair3Args a) {
     Fp4 r;
     f4_select(r, a.pk_st && a.pk_st[e], f, g_one(g));
     if (valid) a.f_out[3 * f_out_index(a, e) + g.k] = Fp4Entry{r.x, r.y};
+    // groups of the small calls: the byte P3_FULL's verdict rules would fail without a pairing
+    if (a.f_bad && valid && g.k == 0) a.f_bad[e] = ((a.pk_st && a.pk_st[e]) || P.inf || a.hm[m].h.inf) ? 1 : 0;
     return;
   }
   if (MODE == P3_MLS) {
     if (valid) a.f_out[3 * f_out_index(a, e) + g.k] = Fp4Entry{f.x, f.y};
-    return;
-  }
-  if (MODE == P3_FML) {  // groups only (no items, no aggregates): the verdict byte of P3_FULL's rules
-    if (valid) a.f_out[3 * f_out_index(a, e) + g.k] = Fp4Entry{f.x, f.y};
-    if (valid && g.k == 0) a.f_bad[e] = ((a.pk_st && a.pk_st[e]) || P.inf || a.hm[m].h.inf) ? 1 : 0;
     return;
   }
   if (MODE == P3_FIN) {  // times the stored Miller loops of entries [e f_range, ...) (wave-uniform trip count)
@@ -263,6 +258,5 @@ void launch_pair3_fin(const Pair3Args& a, hipStream_t s) { pair3_launch<P3_FIN>(
 void launch_pair3_prod(const Pair3Args& a, hipStream_t s) { pair3_launch<P3_PROD>(a, s); }
 void launch_pair3_mml(const Pair3Args& a, hipStream_t s) { pair3_launch<P3_MML>(a, s); }
 void launch_pair3_mls(const Pair3Args& a, hipStream_t s) { pair3_launch<P3_MLS>(a, s); }
-void launch_pair3_fml(const Pair3Args& a, hipStream_t s) { pair3_launch<P3_FML>(a, s); }
 
 }  // namespace hb
