@@ -164,10 +164,10 @@ HD void fp_join28(uint32_t* w, const uint32_t* l) {  // 14 x 28 (normalised, < 2
   }                                                                                     \
   acc >>= 28;
 
-HD void fp_mul_core(uint32_t* out, const uint32_t* aw, const uint32_t* bw) {
-  uint32_t a[14], b[14], m[14], r[14];
-  fp_split28(a, aw);
-  fp_split28(b, bw);
+// the products on operands already in 14 x 28-bit limbs (values < 2p; the outputs are again
+// normalised 28-bit limbs of a value < 2p, so they chain without a join / split in between)
+HD void fp_mul28_core(uint32_t* r, const uint32_t* a, const uint32_t* b) {
+  uint32_t m[14];
   uint64_t acc = 0;
   HB_UNROLL for (int k = 0; k < 27; k++) {
     const int lo = k < 14 ? 0 : k - 13, hi = k < 14 ? k : 13;
@@ -177,13 +177,11 @@ HD void fp_mul_core(uint32_t* out, const uint32_t* aw, const uint32_t* bw) {
     HB_MONT28_TAIL(acc, m, k, r)
   }
   r[13] = (uint32_t)acc;
-  fp_join28(out, r);
 }
 
 // squaring: the cross products a_j a_{k-j}, j < k - j, once against the doubled limb
-HD void fp_sqr_core(uint32_t* out, const uint32_t* aw) {
-  uint32_t a[14], a2[14], m[14], r[14];
-  fp_split28(a, aw);
+HD void fp_sqr28_core(uint32_t* r, const uint32_t* a) {
+  uint32_t a2[14], m[14];
   HB_UNROLL for (int j = 0; j < 14; j++) a2[j] = a[j] << 1;
   uint64_t acc = 0;
   HB_UNROLL for (int k = 0; k < 27; k++) {
@@ -197,6 +195,20 @@ HD void fp_sqr_core(uint32_t* out, const uint32_t* aw) {
     HB_MONT28_TAIL(acc, m, k, r)
   }
   r[13] = (uint32_t)acc;
+}
+
+HD void fp_mul_core(uint32_t* out, const uint32_t* aw, const uint32_t* bw) {
+  uint32_t a[14], b[14], r[14];
+  fp_split28(a, aw);
+  fp_split28(b, bw);
+  fp_mul28_core(r, a, b);
+  fp_join28(out, r);
+}
+
+HD void fp_sqr_core(uint32_t* out, const uint32_t* aw) {
+  uint32_t a[14], r[14];
+  fp_split28(a, aw);
+  fp_sqr28_core(r, a);
   fp_join28(out, r);
 }
 
@@ -465,6 +477,55 @@ HD Fp fp_sqr(const Fp& a) {
   HB_UNROLL for (int i = 0; i < NL; i++) r.v[i] = rv[i];
   return r;
 }
+// chains of products in 28-bit limbs (the constant exponentiations): 14 limbs in a 16-wide vector
+typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
+__device__ __noinline__ static u32x16 fp_mul28_leaf(u32x16 a, u32x16 b) {
+  uint32_t x[14], y[14], r[14];
+  HB_UNROLL for (int i = 0; i < 14; i++) {
+    x[i] = a[i];
+    y[i] = b[i];
+  }
+  fp_mul28_core(r, x, y);
+  u32x16 o;
+  HB_UNROLL for (int i = 0; i < 14; i++) o[i] = r[i];
+  o[14] = o[15] = 0;
+  return o;
+}
+__device__ __noinline__ static u32x16 fp_sqr28_leaf(u32x16 a) {
+  uint32_t x[14], r[14];
+  HB_UNROLL for (int i = 0; i < 14; i++) x[i] = a[i];
+  fp_sqr28_core(r, x);
+  u32x16 o;
+  HB_UNROLL for (int i = 0; i < 14; i++) o[i] = r[i];
+  o[14] = o[15] = 0;
+  return o;
+}
+struct Fp28 {
+  u32x16 l;
+};
+HD Fp28 fp28_mul(const Fp28& a, const Fp28& b) {
+  HB_COUNT_FP_MUL();
+  return {fp_mul28_leaf(a.l, b.l)};
+}
+HD Fp28 fp28_sqr(const Fp28& a) {
+  HB_COUNT_FP_MUL();
+  return {fp_sqr28_leaf(a.l)};
+}
+HD Fp28 fp28_from(const Fp& a) {
+  uint32_t x[14];
+  fp_split28(x, a.v);
+  Fp28 r;
+  HB_UNROLL for (int i = 0; i < 14; i++) r.l[i] = x[i];
+  r.l[14] = r.l[15] = 0;
+  return r;
+}
+HD Fp fp28_to(const Fp28& a) {
+  uint32_t x[14];
+  HB_UNROLL for (int i = 0; i < 14; i++) x[i] = a.l[i];
+  Fp r;
+  fp_join28(r.v, x);
+  return r;
+}
 #else
 HD void fp2_mul_pair(Fp& r0, Fp& r1, const Fp& a0, const Fp& a1, const Fp& b0, const Fp& b1) {
   fp2_mul_core(r0.v, r1.v, a0.v, a1.v, b0.v, b1.v);
@@ -480,6 +541,31 @@ HD Fp fp_sqr(const Fp& a) {
   HB_COUNT_FP_MUL();
   Fp r;
   fp_sqr_core(r.v, a.v);
+  return r;
+}
+struct Fp28 {
+  uint32_t l[14];
+};
+HD Fp28 fp28_mul(const Fp28& a, const Fp28& b) {
+  HB_COUNT_FP_MUL();
+  Fp28 r;
+  fp_mul28_core(r.l, a.l, b.l);
+  return r;
+}
+HD Fp28 fp28_sqr(const Fp28& a) {
+  HB_COUNT_FP_MUL();
+  Fp28 r;
+  fp_sqr28_core(r.l, a.l);
+  return r;
+}
+HD Fp28 fp28_from(const Fp& a) {
+  Fp28 r;
+  fp_split28(r.l, a.v);
+  return r;
+}
+HD Fp fp28_to(const Fp28& a) {
+  Fp r;
+  fp_join28(r.v, a.l);
   return r;
 }
 #endif
@@ -539,19 +625,23 @@ HDNI Fp fp_pow_const(const Fp& a, const uint32_t* e, int top_bit) {
 // about 86 products against the 229 set bits the binary method above multiplies by.  The table
 // entry of the next window is read before that window's squarings, so its load (the table is
 // indexed by a wave-uniform digit) overlaps them.
+//
+// The whole chain stays in 14 x 28-bit limbs (fp28_*): every product's output is a valid input of
+// the next, so the split of both operands and the join of the result -- ~45 of a product's ~545
+// instructions -- happen once per exponentiation instead of once per product.
 HDNI Fp fp_pow_win(const Fp& a, const uint8_t* sch, int n) {
-  Fp tab[8];
-  tab[0] = a;
-  const Fp a2 = fp_sqr(a);
-  HB_UNROLL for (int i = 1; i < 8; i++) tab[i] = fp_mul(tab[i - 1], a2);
-  Fp r = tab[(sch[1] >> 1) & 7];
+  Fp28 tab[8];
+  tab[0] = fp28_from(a);
+  const Fp28 a2 = fp28_sqr(tab[0]);
+  HB_UNROLL for (int i = 1; i < 8; i++) tab[i] = fp28_mul(tab[i - 1], a2);
+  Fp28 r = tab[(sch[1] >> 1) & 7];
   HB_NOUNROLL for (int k = 1; k < n; k++) {
     const int sq = sch[2 * k], d = sch[2 * k + 1];
-    const Fp m = tab[(d >> 1) & 7];
-    HB_NOUNROLL for (int j = 0; j < sq; j++) r = fp_sqr(r);
-    if (d) r = fp_mul(r, m);
+    const Fp28 m = tab[(d >> 1) & 7];
+    HB_NOUNROLL for (int j = 0; j < sq; j++) r = fp28_sqr(r);
+    if (d) r = fp28_mul(r, m);
   }
-  return r;
+  return fp28_to(r);
 }
 
 HD Fp fp_inv(const Fp& a) { return fp_pow_win(a, WIN_P_MINUS_2, WIN_P_MINUS_2_N); }
