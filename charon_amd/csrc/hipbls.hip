@@ -266,6 +266,13 @@ bool g_stagger = false;
 // aggregates) the slot-wide check beats the per-batch one since the multi-Miller loops and the
 // six-lane final exponentiation (14.4 vs 15.3 ms per slot, profiles/r03s_ab_summary.txt)
 std::atomic<size_t> g_slot_msm_min{32768};
+// HBLS_ADAPTIVE=0: always try the slot-wide check.  Default: after a call whose slot-wide check
+// failed (invalid partials or aggregates that only a pairing catches), the next calls go straight
+// to the per-batch check -- a failing slot-wide check is work thrown away -- until a call passes
+// every batch; under a sustained attack (C5: 1 % of the partials invalid in every slot) that
+// saves the signature-side MSM, its lines and Miller loop, the product tree and one final
+// exponentiation per slot.  Verdicts are the same either way.
+std::atomic<bool> g_adaptive{true};
 // HBLS_FE6=0: the final exponentiations without lines in three lanes (k_pair3<FIN>) instead of six
 // (k_pair6_fin, pair6.h)
 bool g_fe6 = true;
@@ -332,6 +339,14 @@ struct Hc {
   bool busy = false;
 };
 
+// one record per call that could take the slot-wide check: did it fail (or, skipped, did any batch
+// fail the per-batch check)
+struct SlotRes {
+  uint8_t sfail, skipped, pad[2];
+  uint32_t gcount;
+};
+constexpr unsigned N_RES = 16;
+
 struct Dev {
   int ord = -1;
   int n_cu = 256;  // compute units (4 SIMDs each)
@@ -351,6 +366,12 @@ struct Dev {
   // public-key cache (hbls_pubkey_cache_add): decompressed entries + statuses, every device holds
   // all g_kc_n of them
   DevBuf kc_tab, kc_st;
+  // adaptive slot-wide check (HBLS_ADAPTIVE): outcomes of recent checked calls, copied to pinned host
+  // memory asynchronously and read once their event has completed -- never a synchronisation
+  SlotRes* res_host = nullptr;
+  hipEvent_t res_ev[N_RES] = {};
+  unsigned res_head = 0, res_tail = 0;  // records [tail, head) not yet read
+  bool attack = false;                  // the last known call had invalid items a pairing caught
   // timing (hbls_timing)
   bool timing = false;
   bool serial = false;  // timing mode 2: every timed launch completes before the next is enqueued
@@ -466,6 +487,8 @@ int dev_create(int ord, Dev** out) {
     HCHK(hipEventCreateWithFlags(&w.ev_msm, hipEventDisableTiming));
     HCHK(hipStreamCreateWithPriority(&d->hc[k_ws].s, hipStreamNonBlocking, prio_lo));
   }
+  HCHK(hipHostMalloc((void**)&d->res_host, N_RES * sizeof(SlotRes), hipHostMallocDefault));
+  for (unsigned k = 0; k < N_RES; k++) HCHK(hipEventCreateWithFlags(&d->res_ev[k], hipEventDisableTiming));
   *out = d;
   return 0;
 }
@@ -501,6 +524,7 @@ int init_mask(uint32_t mask) {
   g_fe6 = env_size("HBLS_FE6", 1) != 0;
   g_fe_batch_min = env_size("HBLS_FE_BATCH", g_fe_batch_min.load());
   g_slot_msm_min = env_size("HBLS_SLOT_MSM", g_slot_msm_min.load());
+  g_adaptive = env_size("HBLS_ADAPTIVE", 1) != 0;
   g_stagger = env_size("HBLS_STAGGER", 0) != 0;
   g_ws_sets = (int)std::min<size_t>(N_WS_MAX, std::max<size_t>(1, env_size("HBLS_WS_SETS", 3)));
   {
@@ -790,7 +814,19 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
                wsbuf(w, W_PBUF3, 3 * nb2, &pbuf3) ||
                wsbuf(w, W_SFAIL, 1, &sfail) || wsbuf(w, W_MLEV, N_LINES * gcap, &mlev)))
     return -1;
-  const int sides1 = smsm ? 1 : 3;  // first pass: the public-key side only when the MSM takes the other
+  // adaptive: the outcome of the last completed checked call decides whether this one tries the
+  // slot-wide check at all (skip: the fallback's kernels run unguarded, sfail set to 1)
+  bool skip_msm = false;
+  if (smsm && g_adaptive.load()) {
+    while (d.res_tail != d.res_head && hipEventQuery(d.res_ev[d.res_tail % N_RES]) == hipSuccess) {
+      const SlotRes& r = d.res_host[d.res_tail % N_RES];
+      d.attack = r.skipped ? r.gcount != 0 : r.sfail != 0;
+      d.res_tail++;
+    }
+    skip_msm = d.attack;
+  }
+  // first pass: the public-key side only when the MSM takes the other
+  const int sides1 = smsm && !skip_msm ? 1 : 3;
 
   // fork: decompression on the side streams (after the previous verification's decompression)
   if (d.dec_valid && g_stagger) HCHK(hipStreamWaitEvent(s, d.ev_dec, 0));
@@ -883,7 +919,7 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
     ra.always = item_always;
     ra.sides = sides1;
     TIMED(d, "k_rlc", s, launch_rlc_msm(ra, (uint32_t)max_chunks, s));
-    if (smsm) {  // the per-item signature side, only if the slot-wide check fails
+    if (smsm && !skip_msm) {  // the per-item signature side, only if the slot-wide check fails
       ra.sides = 2;
       ra.guard = sfail;
       rlc_fallback = ra;
@@ -901,7 +937,7 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
     // combined check exactly; with an invalid partial j beside it the check passes for one value
     // of the random r_j only) -- the group's items all take random coefficients (item_always)
     HCHK(hipStreamWaitEvent(s, w.ev_ta, 0));
-    uint2* acoef = smsm ? (coef_pi ? coef_pi : rlc_fallback.coef) + n : nullptr;
+    uint2* acoef = smsm && !skip_msm ? (coef_pi ? coef_pi : rlc_fallback.coef) + n : nullptr;
     TIMED(d, "k_rlc", s,
           launch_rlc(apk, apkst, asig, fold->ta_status, nullptr, nullptr, bfe ? 1 : 0, (uint32_t)n_agg, (uint32_t)n,
                      key, apr, asr, s, acoef, sides1));
@@ -956,8 +992,10 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
         // Miller loops and their product tree (s), the MSM of the signature side and its lines (side 0)
         ga.p_only = 1;
         TIMED(d, "k_group_prep", s, launch_group_prep(ga, s));
+        if (skip_msm) HCHK(hipMemsetAsync(sfail, 1, 1, s));  // the per-batch check runs unconditionally
         HCHK(hipEventRecord(w.ev_msm, s));
         hipStream_t sm = w.side[0];
+        if (!skip_msm) {
         HCHK(hipStreamWaitEvent(sm, w.ev_msm, 0));
         ma.sig = vsig;
         ma.agg_sig = asig;
@@ -986,6 +1024,7 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
           ps.f_out_off = 1;
           TIMED(d, "k_pair3_mls", sm, launch_pair3_mls(ps, sm));
         }
+        }
         HCHK(hipEventRecord(w.ev_side[0], sm));
         // multi-Miller loops over mmlk groups (shared squarings), then a product tree of fan-in
         // PROD_FAN down to ONE value, pfin[0] (ping-pong between pbuf1 and pbuf2): eight products
@@ -1004,7 +1043,7 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
         TIMED(d, "k_pair3_mml", s, launch_pair3_mml(pp, s));
         Fp4Entry* cur = pbuf1;
         uint32_t cur_n = pp.n;
-        do {
+        if (!skip_msm) do {
           Pair3Args pr{};
           pr.n = (cur_n + PROD_FAN - 1) / PROD_FAN;
           pr.f_in = cur;
@@ -1023,20 +1062,23 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
         pf.f_range = 2;
         pf.f_n = 2;
         pf.status = sfail;
-        TIMED(d, "k_pair3_fin", s, g_fe6 ? launch_pair6_fin(pf, s) : launch_pair3_fin(pf, s));
-        TIMED(d, "k_slot_verdict", s, launch_slot_verdict(gst, sfail, ng, gver + g0, s));
-        // the slot-wide check failed: the per-batch check (signature sides per item and group)
-        if (rlc_fallback_chunks) {
-          TIMED(d, "k_rlc", s, launch_rlc_msm(rlc_fallback, rlc_fallback_chunks, s));
-        } else {
-          TIMED(d, "k_rlc", s,
-                launch_rlc(vpk, vpkst, vsig, vsigst, igrp, dgoff, 1, (uint32_t)n, 0, key, pr, sr, s, coef_pi, 2,
-                           sfail));
+        if (!skip_msm) {
+          TIMED(d, "k_pair3_fin", s, g_fe6 ? launch_pair6_fin(pf, s) : launch_pair3_fin(pf, s));
+          TIMED(d, "k_slot_verdict", s, launch_slot_verdict(gst, sfail, ng, gver + g0, s));
+          // the slot-wide check failed: the per-batch check (signature sides per item and group;
+          // computed in the first pass when the check was skipped)
+          if (rlc_fallback_chunks) {
+            TIMED(d, "k_rlc", s, launch_rlc_msm(rlc_fallback, rlc_fallback_chunks, s));
+          } else {
+            TIMED(d, "k_rlc", s,
+                  launch_rlc(vpk, vpkst, vsig, vsigst, igrp, dgoff, 1, (uint32_t)n, 0, key, pr, sr, s, coef_pi, 2,
+                             sfail));
+          }
+          if (n_agg)
+            TIMED(d, "k_rlc", s,
+                  launch_rlc(apk, apkst, asig, fold->ta_status, nullptr, nullptr, 1, (uint32_t)n_agg, (uint32_t)n,
+                             key, apr, asr, s, const_cast<uint2*>(ma.coef) + n, 2, sfail));
         }
-        if (n_agg)
-          TIMED(d, "k_rlc", s,
-                launch_rlc(apk, apkst, asig, fold->ta_status, nullptr, nullptr, 1, (uint32_t)n_agg, (uint32_t)n, key,
-                           apr, asr, s, const_cast<uint2*>(ma.coef) + n, 2, sfail));
         ga.p_only = 0;
         ga.guard = sfail;
         pm.guard = sfail;
@@ -1070,6 +1112,15 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
         pm.list = glist;
         pm.count = gcount;
         TIMED(d, "k_pair3_ml", s, launch_pair3_ml(pm, s));
+        // the call's outcome for the next calls' choice (read when its event has completed)
+        if (g_adaptive.load() && d.res_head - d.res_tail < N_RES) {
+          const unsigned k = d.res_head % N_RES;
+          d.res_host[k].skipped = skip_msm ? 1 : 0;
+          HCHK(hipMemcpyAsync(&d.res_host[k].sfail, sfail, 1, hipMemcpyDeviceToHost, s));
+          HCHK(hipMemcpyAsync(&d.res_host[k].gcount, gcount, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+          HCHK(hipEventRecord(d.res_ev[k], s));
+          d.res_head++;
+        }
       }
       if (!smsm) {  // the per-batch check of FE_BATCH groups (below the slot-wide check's size)
         ga.gS = gS;
@@ -1238,7 +1289,7 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
       HCHK(hipStreamSynchronize(s));
       g_stats[3] += c;
     }
-    if (smsm) {
+    if (smsm && !skip_msm) {
       uint8_t f = 0;
       HCHK(hipMemcpyAsync(&f, sfail, 1, hipMemcpyDeviceToHost, s));
       HCHK(hipStreamSynchronize(s));
@@ -2197,7 +2248,15 @@ int hbls_stats(uint64_t* out, size_t n) {
 }
 
 size_t hbls_fe_batch(size_t min_groups) { return g_fe_batch_min.exchange(min_groups); }
-size_t hbls_slot_msm(size_t min_items) { return g_slot_msm_min.exchange(min_items); }
+size_t hbls_slot_msm(size_t min_items) {
+  // a new setting starts from a clean history (tests count the slot-wide checks that ran)
+  for (Dev* d : g_devs) {
+    std::lock_guard<std::mutex> lk(d->mu);
+    for (; d->res_tail != d->res_head; d->res_tail++) (void)hipEventSynchronize(d->res_ev[d->res_tail % N_RES]);
+    d->attack = false;
+  }
+  return g_slot_msm_min.exchange(min_items);
+}
 size_t hbls_ta_joint(size_t members) { return g_ta_joint.exchange(std::min<size_t>(members, 8)); }
 size_t hbls_rlc_lanes(size_t lanes) { return g_rlc_lanes.exchange(lanes ? lanes : 65536); }
 

@@ -419,7 +419,8 @@ def test_batched_fe_rejects_cancelling_errors(L, hipbls, monkeypatch):
 def test_slot_msm_clean_and_cancelling_errors(L, hipbls, monkeypatch):
     """The slot-wide check (HBLS_SLOT_MSM) on 300 groups of one: a clean call passes it with no
     per-batch or per-item check; two signatures with opposite errors (sig0 + D, sig1 - D) make it
-    fail, and the per-batch check then rejects exactly those two."""
+    fail, and the per-batch check then rejects exactly those two.  Then the adaptive choice: the
+    next calls skip the slot-wide check (same verdicts) until one passes every batch."""
     from oracle import bls12381 as B
     monkeypatch.setenv("HBLS_STATS", "1")
     prev_f, prev_s = L.hbls_fe_batch(128), L.hbls_slot_msm(1)
@@ -442,6 +443,20 @@ def test_slot_msm_clean_and_cancelling_errors(L, hipbls, monkeypatch):
         assert st == [NOT_VERIFIED if i < 2 else OK for i in range(n)]
         d = [b - a for a, b in zip(s0, _stats(L))]
         assert d[4] == 1 and d[5] == 1 and d[3] >= 1 and d[2] == 2, d
+        # adaptive (HBLS_ADAPTIVE, default on): after a failed slot-wide check the next calls skip it
+        # and run the per-batch check directly -- same verdicts -- until one passes every batch
+        s0 = _stats(L)
+        assert hipbls.verify_batch(pks, msgs, bad) == st
+        d = [b - a for a, b in zip(s0, _stats(L))]
+        assert d[4] == 0 and d[3] >= 1 and d[2] == 2, d
+        s0 = _stats(L)
+        assert hipbls.verify_batch(pks, msgs, sigs) == [OK] * n  # clean: skipped, every batch passes
+        d = [b - a for a, b in zip(s0, _stats(L))]
+        assert d[4] == 0 and d[3] == 0 and d[2] == 0, d
+        s0 = _stats(L)
+        assert hipbls.verify_batch(pks, msgs, sigs) == [OK] * n  # back to the slot-wide check
+        d = [b - a for a, b in zip(s0, _stats(L))]
+        assert d[4] == 1 and d[5] == 0 and d[2] == 0, d
     finally:
         L.hbls_fe_batch(prev_f)
         L.hbls_slot_msm(prev_s)
