@@ -840,7 +840,7 @@ def main(argv=None):
         "parity": parity, "roofline": None, "cpu_baseline": None,
     }
 
-    if args.host_api and rank == 0:
+    if args.host_api and rank == 0 and world == 1:
         st = np.zeros(NP, dtype=np.uint8)
         t0 = time.perf_counter()
         _chk(L, L.hbls_verify_batch(_p(d["pks"]), _p(d["sigs"]), _p(d["item_msgs"]), _p(d["item_off"]),
