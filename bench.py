@@ -851,7 +851,7 @@ def main(argv=None):
                                                  _p(tout_h), _p(tst_h)))
         out["host_buffer_items_per_s"] = round((NP + V) / (time.perf_counter() - t0), 1)
         if "exp_v" in d:
-            clean = d["exp_ta"] == 0
+            clean = d["exp_agg"] == 0  # members all valid: the aggregate is the root signature
             out["host_buffer_parity"] = bool(np.array_equal(st, d["exp_v"]) and np.array_equal(tst_h, d["exp_ta"]) and
                                              np.array_equal(tout_h.reshape(V, 96)[clean],
                                                             d["root_sigs"].reshape(V, 96)[clean]))
