@@ -201,6 +201,24 @@ int set_err(const char* what, hipError_t e) { return set_err(std::string(what) +
 
 inline unsigned blocks_for(size_t n) { return (unsigned)((n + BLOCK - 1) / BLOCK); }
 
+// Host-buffer Verify on one device: the caller's keys and signatures go up as they are, and the
+// device puts them in group order (one lane per item: 48 + 96 bytes as 16-byte words) and the
+// statuses back in the caller's order -- no host-side copy of the 144 bytes per item.
+__global__ KERNEL_BOUNDS void k_gather_items(const uint4* __restrict__ pk_in, const uint4* __restrict__ sig_in,
+                                             const uint32_t* __restrict__ order, uint32_t n, uint4* __restrict__ pk_out,
+                                             uint4* __restrict__ sig_out) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const uint32_t i = order[k];
+  HB_UNROLL for (int w = 0; w < 3; w++) pk_out[3ull * k + w] = pk_in[3ull * i + w];
+  HB_UNROLL for (int w = 0; w < 6; w++) sig_out[6ull * k + w] = sig_in[6ull * i + w];
+}
+__global__ KERNEL_BOUNDS void k_scatter_status(const uint8_t* __restrict__ st_in, const uint32_t* __restrict__ order,
+                                               uint32_t n, uint8_t* __restrict__ st_out) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < n) st_out[order[k]] = st_in[k];
+}
+
 #define LAUNCH(kern, n, stream, ...)                                                              \
   do {                                                                                            \
     if ((n) > 0) {                                                                                \
@@ -317,7 +335,7 @@ struct Ws {
 };
 
 // host-call staging buffers (inputs and outputs of the host-buffer entry points)
-enum IoId { I_PK, I_SIG, I_MSG, I_OFF, I_LEN, I_MIDX, I_HM, I_STAT, I_IDX, I_GOFF, I_OUT, I_SK, I_VGOFF, I_KC, I_COUNT };
+enum IoId { I_PK, I_SIG, I_MSG, I_OFF, I_LEN, I_MIDX, I_HM, I_STAT, I_IDX, I_GOFF, I_OUT, I_SK, I_VGOFF, I_KC, I_HM2, I_COUNT };
 
 constexpr int N_WS_MAX = 8;  // workspace sets per device: HBLS_WS_SETS (default 3)
 int g_ws_sets = 3;
@@ -1488,13 +1506,14 @@ int kc_fill(Dev& d, const uint8_t* keys, size_t first, size_t m) {
   return 0;
 }
 
-bool kc_lookup(const uint8_t* pks, size_t m, std::vector<uint32_t>& idx) {
+// (order: nullable; key k is pks + 48 * order[k] when given)
+bool kc_lookup(const uint8_t* pks, size_t m, std::vector<uint32_t>& idx, const uint32_t* order = nullptr) {
   std::lock_guard<std::mutex> lk(g_kc_mu);
   if (g_kc_map.empty()) return false;
   idx.assign(m, 0xffffffffu);
   bool any = false;
   for (size_t k = 0; k < m; k++) {
-    auto it = g_kc_map.find(std::string((const char*)pks + 48 * k, 48));
+    auto it = g_kc_map.find(std::string((const char*)pks + 48 * (order ? order[k] : k), 48));
     if (it != g_kc_map.end()) {
       idx[k] = it->second;
       any = true;
@@ -1519,38 +1538,81 @@ int verify_host(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msgs, co
     if (k == 0 || all.idx[order[k]] != all.idx[order[k - 1]] || k - gstart.back() >= g_gmax) gstart.push_back(k);
   const size_t n_groups = gstart.size();
   gstart.push_back(n);
+  if (n >= 0xffffffffull) return set_err("verify batch: too many items");
+  std::vector<uint32_t> order32(order.begin(), order.end());
   return for_each_device_hc(n_groups, [&](Dev& d, Hc& h, size_t gb, size_t ge, std::unique_lock<std::mutex>& lk) -> int {
     const size_t ib = gstart[gb], ie = gstart[ge], m = ie - ib;
     if (m == 0) return 0;
-    MsgTable t;
-    dedup_messages(msgs, msg_off, msg_len, m, order.data() + ib, t);
-    std::vector<uint8_t> hpk(48 * m), hsig(96 * m);
-    for (size_t k = 0; k < m; k++) {
-      memcpy(&hpk[48 * k], pks + 48 * order[ib + k], 48);
-      memcpy(&hsig[96 * k], sigs + 96 * order[ib + k], 96);
+    // host preparation without the device lock (other callers enqueue meanwhile): the shard's
+    // distinct messages and each item's message index in group order -- the whole call's table
+    // when one device takes every group
+    lk.unlock();
+    const bool whole = gb == 0 && ge == n_groups;
+    MsgTable tl;
+    std::vector<uint32_t> midx;
+    if (whole) {
+      midx.resize(m);
+      for (size_t k = 0; k < m; k++) midx[k] = all.idx[order[k]];
+    } else {
+      dedup_messages(msgs, msg_off, msg_len, m, order.data() + ib, tl);
+    }
+    const MsgTable& t = whole ? all : tl;
+    const std::vector<uint32_t>& tidx = whole ? midx : tl.idx;
+    std::vector<uint8_t> hpk, hsig;  // several devices: each uploads only its shard, in group order
+    if (!whole) {
+      hpk.resize(48 * m);
+      hsig.resize(96 * m);
+      for (size_t k = 0; k < m; k++) {
+        memcpy(&hpk[48 * k], pks + 48 * order[ib + k], 48);
+        memcpy(&hsig[96 * k], sigs + 96 * order[ib + k], 96);
+      }
     }
     std::vector<uint32_t> goff(ge - gb + 1);
     for (size_t g = gb; g <= ge; g++) goff[g - gb] = (uint32_t)(gstart[g] - ib);
+    std::vector<uint32_t> kc;
+    const bool use_kc = whole ? kc_lookup(pks, m, kc, order32.data()) : kc_lookup(hpk.data(), m, kc);
+    lk.lock();
     // the messages hash on a side stream while the keys and signatures decompress (latency of
     // one call: the two chains run side by side)
     Ws& w = ws_acquire(d, h.s);
     MsgEntry* hm;
     hipEvent_t hm_ready = nullptr;
     if (hash_table(d, t, &hm, true, &w, &hm_ready, &h)) return -1;
-    uint8_t *dpk, *dsig, *dst;
-    uint32_t *didx, *dgoff, *dkc = nullptr;
-    if (upload(d, I_PK, hpk.data(), hpk.size(), &dpk, &h) || upload(d, I_SIG, hsig.data(), hsig.size(), &dsig, &h) ||
-        upload(d, I_MIDX, t.idx.data(), m, &didx, &h) || upload(d, I_VGOFF, goff.data(), goff.size(), &dgoff, &h))
+    uint8_t *dpk, *dsig, *dst, *dst_out = nullptr;
+    uint32_t *didx, *dgoff, *dkc = nullptr, *dord = nullptr;
+    if (whole) {  // caller order up, group order on the device
+      uint8_t *rpk, *rsig;
+      void *p1, *p2, *p3;
+      if (upload(d, I_PK, pks, 48 * m, &rpk, &h) || upload(d, I_SIG, sigs, 96 * m, &rsig, &h) ||
+          upload(d, I_IDX, order32.data(), m, &dord, &h) || ensure_buf(h.io[I_OUT], 144 * m, &p1) ||
+          ensure_buf(h.io[I_HM2], m, &p2) || ensure_buf(h.io[I_STAT], m, &p3))
+        return -1;
+      dpk = (uint8_t*)p1;
+      dsig = dpk + 48 * m;
+      dst_out = (uint8_t*)p2;
+      dst = (uint8_t*)p3;
+      LAUNCH(k_gather_items, m, h.s, (const uint4*)rpk, (const uint4*)rsig, dord, (uint32_t)m, (uint4*)dpk,
+             (uint4*)dsig);
+    } else {
+      void* p;
+      if (upload(d, I_PK, hpk.data(), hpk.size(), &dpk, &h) || upload(d, I_SIG, hsig.data(), hsig.size(), &dsig, &h) ||
+          ensure_buf(h.io[I_STAT], m, &p))
+        return -1;
+      dst = (uint8_t*)p;
+    }
+    if (upload(d, I_MIDX, tidx.data(), m, &didx, &h) || upload(d, I_VGOFF, goff.data(), goff.size(), &dgoff, &h))
       return -1;
-    std::vector<uint32_t> kc;
-    if (kc_lookup(hpk.data(), m, kc) && upload(d, I_KC, kc.data(), m, &dkc, &h)) return -1;
-    void* p;
-    if (ensure_buf(h.io[I_STAT], m, &p)) return -1;
-    dst = (uint8_t*)p;
+    if (use_kc && upload(d, I_KC, kc.data(), m, &dkc, &h)) return -1;
     if (verify_pipeline(d, w, dpk, dsig, didx, hm, m, dgoff, ge - gb, dst, h.s, hm_ready, nullptr, dkc))
       return -1;
+    if (whole) LAUNCH(k_scatter_status, m, h.s, dst, dord, (uint32_t)m, dst_out);
     if (ws_release(w, h.s)) return -1;
     lk.unlock();  // enqueued: other callers may enqueue while this one waits for its stream
+    if (whole) {
+      HCHK(hipMemcpyAsync(status, dst_out, m, hipMemcpyDeviceToHost, h.s));
+      HCHK(hipStreamSynchronize(h.s));
+      return 0;
+    }
     std::vector<uint8_t> hst(m);
     HCHK(hipMemcpyAsync(hst.data(), dst, m, hipMemcpyDeviceToHost, h.s));
     HCHK(hipStreamSynchronize(h.s));
