@@ -156,6 +156,32 @@ def test_slot_c5_shard_adversarial(L, c4):
     assert B.verify(bytes(d["dv_pks"][48 * v:48 * v + 48]), root, agg) == NOT_VERIFIED == ast[v]
 
 
+def test_host_batches_c5_shard_adversarial(L, c4):
+    """The same C5 shard through the host-buffer entry points the Go shim binds
+    (hbls_verify_batch over the 875 000 partials, hbls_threshold_aggregate_batch over the 125 000
+    groups): every status exact against the construction, aggregates byte-equal to the root-key
+    signatures where every member is valid.  Verify runs twice: the first call fails its
+    slot-wide check, the second (adaptive) goes straight to the per-batch check -- same statuses."""
+    import bench
+    d = dict(c4)
+    d["sigs"] = c4["sigs"].copy()
+    bench.corrupt(L, d, 0.01, seed=11)
+    V, NP = d["V"], d["NP"]
+    for _ in range(2):
+        st = np.full(NP, 255, dtype=np.uint8)
+        _chk(L, L.hbls_verify_batch(_p(d["pks"]), _p(d["sigs"]), _p(d["item_msgs"]), _p(d["item_off"]),
+                                    _p(d["item_len"]), NP, _p(st)))
+        bad = np.nonzero(st != d["exp_v"])[0]
+        assert len(bad) == 0, [(int(i), int(st[i]), int(d["exp_v"][i])) for i in bad[:10]]
+    tout = np.zeros(V * 96, dtype=np.uint8)
+    tst = np.zeros(V, dtype=np.uint8)
+    _chk(L, L.hbls_threshold_aggregate_batch(_p(d["ta_sigs"]), _p(d["ta_idx"]), _p(d["grp_off"]), V, _p(tout),
+                                             _p(tst)))
+    assert np.array_equal(tst, d["exp_ta"])
+    clean = d["exp_agg"] == OK
+    assert np.array_equal(tout.reshape(V, 96)[clean], d["root_sigs"].reshape(V, 96)[clean])
+
+
 def _rand_sks(rng, count):
     raw = np.frombuffer(rng.randbytes(32 * count), dtype=np.uint8).reshape(count, 32).copy()
     raw[:, 0] &= 0x3F  # < 2^254 < r
