@@ -30,7 +30,7 @@ EXPORTS = (
     "hbls_verify_device", "hbls_threshold_aggregate_device", "hbls_verify_aggregate_device", "hbls_slot_device",
     "hbls_hm_entry_bytes", "hbls_sync",
     "hbls_timing", "hbls_timing_read", "hbls_comm_id_bytes", "hbls_comm_unique_id", "hbls_comm_init",
-    "hbls_allgather_device", "hbls_comm_destroy", "hbls_stats", "hbls_fe_batch", "hbls_slot_msm", "hbls_rlc_lanes", "hbls_ta_joint", "hbls_attestation_signing_roots",
+    "hbls_allgather_device", "hbls_comm_destroy", "hbls_stats", "hbls_fe_batch", "hbls_slot_msm", "hbls_adaptive", "hbls_rlc_lanes", "hbls_ta_joint", "hbls_attestation_signing_roots",
     "hbls_signing_roots", "hbls_attestation_signing_roots_device", "hbls_pk_entry_bytes",
     "hbls_decompress_pubkeys_device", "hbls_pubkey_cache_add", "hbls_pubkey_cache_clear", "hbls_pubkey_cache_size",
     "hbls_debug_split",
@@ -104,6 +104,7 @@ def _declare(lib):
         "hbls_stats": ([P, SZ], ctypes.c_int),
         "hbls_fe_batch": ([SZ], SZ),
         "hbls_slot_msm": ([SZ], SZ),
+        "hbls_adaptive": ([ctypes.c_int], ctypes.c_int),
         "hbls_rlc_lanes": ([SZ], SZ),
         "hbls_ta_joint": ([SZ], SZ),
     }

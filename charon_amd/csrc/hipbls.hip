@@ -2310,6 +2310,7 @@ int hbls_stats(uint64_t* out, size_t n) {
 }
 
 size_t hbls_fe_batch(size_t min_groups) { return g_fe_batch_min.exchange(min_groups); }
+int hbls_adaptive(int on) { return g_adaptive.exchange(on != 0) ? 1 : 0; }
 size_t hbls_slot_msm(size_t min_items) {
   // a new setting starts from a clean history (tests count the slot-wide checks that ran)
   for (Dev* d : g_devs) {

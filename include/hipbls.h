@@ -239,8 +239,13 @@ size_t hbls_fe_batch(size_t min_groups);
 /* Tuning: batched verifications of at least min_items items (partials + folded aggregates) first
  * check every group at once -- the signature side as one multi-scalar multiplication, one final
  * exponentiation for the call -- and take the per-batch check only if that fails (0 = never;
- * default 65536, HBLS_SLOT_MSM).  Returns the previous value.  Verdicts do not depend on it. */
+ * default 32768, HBLS_SLOT_MSM).  Returns the previous value and clears the adaptive history
+ * below.  Verdicts do not depend on it. */
 size_t hbls_slot_msm(size_t min_items);
+/* Tuning: adaptive slot-wide check (1 = on, the default; HBLS_ADAPTIVE): after a call whose
+ * slot-wide check failed, the next calls take the per-batch check directly until one passes every
+ * batch.  Returns the previous setting.  Verdicts do not depend on it. */
+int hbls_adaptive(int on);
 /* Tuning: the random linear combination's public-key side groups a verification group's items
  * into shared-doubling chunks sized to keep about `lanes` lanes busy (at most 16 items per chunk;
  * calls of fewer than 2 lanes' worth keep one ladder per item).  0 restores the default 65536
