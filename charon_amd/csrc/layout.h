@@ -197,6 +197,10 @@ void launch_mml_eval(const Pair3Args& a, LineEntry* ev, hipStream_t s);
 // stored unexponentiated; the final exponentiation then runs with sig_lines == nullptr (FIN: no loop
 // of its own, the product of its f_range stored values, exponentiated)
 void launch_pair3_mls(const Pair3Args& a, hipStream_t s);
+// the (-g1, S) loop of each of n Jacobian points S straight from the points (lines produced and
+// consumed in one two-wave workgroup per point): f_out[e f_stride + f_off], bad[e] = S infinite
+void launch_lml(const G2JEntry* pts, uint32_t n, Fp4Entry* f_out, uint32_t f_stride, uint32_t f_off, uint8_t* bad,
+                hipStream_t s, const uint8_t* guard = nullptr);
 constexpr uint32_t PROD_FAN = 8;  // fan-in of the product trees in front of a final exponentiation
 // FIN without sig_lines over six lanes per unit (pair6.h: Fp2 products split across lane pairs):
 // the same statuses at about half the latency
@@ -294,7 +298,12 @@ void launch_slot_verdict(const uint8_t* gst, const uint8_t* sfail, uint32_t ng, 
 // with MSM_WINDOWS windows of MSM_C bits.
 constexpr uint32_t MSM_C = 16, MSM_WINDOWS = 2, MSM_MASK = (1u << MSM_C) - 1;
 constexpr uint32_t MSM_KEYS = MSM_WINDOWS << MSM_C;  // buckets (window, digit); digit 0 unused
-constexpr uint32_t MSM_CHUNK = 16;                   // buckets per lane of the weighing pass
+// buckets per lane of the weighing pass: 4 (32 768 lanes) rather than 16 -- the pass is a latency
+// tail of every slot (one round of waves), so more, shorter lanes halve it for ~20 M more products
+#ifndef HB_MSM_CHUNK
+#define HB_MSM_CHUNK 4
+#endif
+constexpr uint32_t MSM_CHUNK = HB_MSM_CHUNK;
 constexpr uint32_t MSM_PARTS = MSM_KEYS / MSM_CHUNK;
 struct G2MsmArgs {
   const HmEntry* sig;      // items [0, n)

@@ -187,11 +187,11 @@ void launch_msm_bucket(const G2MsmArgs& a, hipStream_t s) {
 void launch_msm_reduce(const G2MsmArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_msm_reduce, dim3(blocks_for(MSM_PARTS)), dim3(BLOCK), 0, s, a);
 }
-// part[MSM_PARTS] -> part2[MSM_PARTS / 128] -> total[0]
+// part[MSM_PARTS] -> part2[n2 <= 64] -> total[0]: q entries per lane in the first pass
 void launch_msm_sum(const G2MsmArgs& a, hipStream_t s) {
-  constexpr uint32_t n2 = MSM_PARTS / 128;
-  static_assert(MSM_PARTS % 128 == 0 && n2 <= 64, "two butterfly passes");
-  hipLaunchKernelGGL(k_msm_sum, dim3(n2), dim3(BLOCK), 0, s, (const G2JEntry*)a.part, MSM_PARTS, 2u, a.part2);
+  constexpr uint32_t q = MSM_PARTS >= 64 * 64 ? MSM_PARTS / (64 * 64) : 1u, n2 = MSM_PARTS / (64 * q);
+  static_assert(MSM_PARTS % (64 * q) == 0 && n2 <= 64 && n2 <= MSM_PARTS / 128, "two butterfly passes");
+  hipLaunchKernelGGL(k_msm_sum, dim3(n2), dim3(BLOCK), 0, s, (const G2JEntry*)a.part, MSM_PARTS, q, a.part2);
   hipLaunchKernelGGL(k_msm_sum, dim3(1), dim3(BLOCK), 0, s, (const G2JEntry*)a.part2, n2, 1u, a.total);
 }
 

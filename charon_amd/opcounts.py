@@ -131,7 +131,7 @@ def rlc_msm(b=BLOCKS, chunk=1, sides=3):
 
 # The slot-wide check's multi-scalar multiplication of the signature side (msm.hip): two windows of
 # 16 bits over the two 32-bit halves of every coefficient, i.e. 4 bucket entries per item.
-MSM_C, MSM_WINDOWS, MSM_CHUNK = 16, 2, 16
+MSM_C, MSM_WINDOWS, MSM_CHUNK = 16, 2, 4
 MSM_KEYS = MSM_WINDOWS << MSM_C
 MSM_PARTS = MSM_KEYS // MSM_CHUNK
 MSM_ENTRIES_PER_ITEM = 2 * MSM_WINDOWS

@@ -1,5 +1,5 @@
 """The slot-wide check's bucket method (charon_amd/csrc/msm.hip) restated over the integers: the
-scalar digits, the counting sort into buckets, the running-sum weighing of chunks of 16 buckets
+scalar digits, the counting sort into buckets, the running-sum weighing of chunks of MSM_CHUNK buckets
 plus one (lo - 1) multiple, the window shift and the final sum must give sum_i r_i x_i exactly.
 Group elements are replaced by integers (the method only adds, doubles and scales), so this pins
 the index arithmetic of k_msm_count / k_msm_fill / k_msm_order / k_msm_bucket / k_msm_reduce /
