@@ -762,7 +762,8 @@ def main(argv=None):
             n_prod = opcounts.prod_tree_inputs(-(-V // mmlk))
             fin = opcounts.pair3_fin(batch=2, lines=False)
             units.update({"k_group_prep": (V, prep_units["k_group_prep_p"]),
-                          "k_pair3_mls": (1, per_unit["k_pair3_mls"]),
+                          # the signature side's lines and loop in one kernel (k_lml)
+                          "k_pair3_mls": (1, tuple(a + b for a, b in zip(per_unit["k_pair3_mls"], per_unit["k_slines"]))),
                           "k_pair3_mml": (V, opcounts.pair3_mml(pairs=mmlk)),
                           "k_mml_eval": (V, per_unit["k_mml_eval"]),
                           "k_pair3_prod": (n_prod, per_unit["k_pair3_prod"]),

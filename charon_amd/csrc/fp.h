@@ -390,12 +390,17 @@ typedef uint32_t u32x24 __attribute__((ext_vector_type(24)));
 // on the scratch stack (dword stores and loads around every call).  The second operand therefore
 // travels through this per-lane LDS slot instead (k-major pairs: conflict-free 64-bit accesses).
 // Every kernel runs 64-lane workgroups, one wave each (BLOCK / dim3(64) at every launch).
-__shared__ uint2 hb_fp2_arg[12 * 64];
+// HB_ARG_LANES: threads of the largest workgroup of the translation unit (64: one wave; the
+// pairing unit's two-wave producer/consumer kernel needs a slot per thread of both waves)
+#ifndef HB_ARG_LANES
+#define HB_ARG_LANES 64
+#endif
+__shared__ uint2 hb_fp2_arg[12 * HB_ARG_LANES];
 __device__ __noinline__ static u32x24 fp2_mul_leaf(u32x24 a) {
   uint32_t x0[12], x1[12], y0[12], y1[12], r0[12], r1[12];
-  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t lane = threadIdx.x & (HB_ARG_LANES - 1u);
   HB_UNROLL for (int k = 0; k < 6; k++) {
-    const uint2 v = hb_fp2_arg[k * 64 + lane], w = hb_fp2_arg[(6 + k) * 64 + lane];
+    const uint2 v = hb_fp2_arg[k * HB_ARG_LANES + lane], w = hb_fp2_arg[(6 + k) * HB_ARG_LANES + lane];
     y0[2 * k] = v.x;
     y0[2 * k + 1] = v.y;
     y1[2 * k] = w.x;
@@ -433,10 +438,10 @@ HD void fp2_mul_pair(Fp& r0, Fp& r1, const Fp& a0, const Fp& a1, const Fp& b0, c
     av[i] = a0.v[i];
     av[12 + i] = a1.v[i];
   }
-  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t lane = threadIdx.x & (HB_ARG_LANES - 1u);
   HB_UNROLL for (int k = 0; k < 6; k++) {
-    hb_fp2_arg[k * 64 + lane] = make_uint2(b0.v[2 * k], b0.v[2 * k + 1]);
-    hb_fp2_arg[(6 + k) * 64 + lane] = make_uint2(b1.v[2 * k], b1.v[2 * k + 1]);
+    hb_fp2_arg[k * HB_ARG_LANES + lane] = make_uint2(b0.v[2 * k], b0.v[2 * k + 1]);
+    hb_fp2_arg[(6 + k) * HB_ARG_LANES + lane] = make_uint2(b1.v[2 * k], b1.v[2 * k + 1]);
   }
   u32x24 rv = fp2_mul_leaf(av);
   HB_UNROLL for (int i = 0; i < NL; i++) {

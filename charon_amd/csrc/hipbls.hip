@@ -314,7 +314,7 @@ enum WsId {
   W_FBUF, W_GS, W_BS, W_BLINES, W_BBAD, W_BVER, W_GLIST, W_GCOUNT,  // batched final exponentiation
   W_MCNT, W_MOFF, W_MCUR, W_MORDER, W_MENT, W_MBUCKET, W_MPART, W_MPART2, W_MTOT, W_PBUF1, W_PBUF2, W_PBUF3, W_SFAIL,  // slot-wide check
   W_MLEV,                                                                          // its evaluated Miller lines
-  W_PFIN, W_TBUF, W_F1, W_F1BAD,                                                                  // final exponentiations' factors
+  W_PFIN, W_TBUF, W_F1, W_F1BAD, W_F1S,                                                                  // final exponentiations' factors
   W_COUNT_
 };
 
@@ -332,6 +332,7 @@ struct Ws {
   bool used = false;
   hipStream_t side[N_SIDE] = {};
   hipEvent_t ev_fork = nullptr, ev_side[N_SIDE] = {}, ev_ta = nullptr, ev_msm = nullptr;
+  hipEvent_t ev_h = nullptr;  // host calls: the hashing done (before the messages' lines)
 };
 
 // host-call staging buffers (inputs and outputs of the host-buffer entry points)
@@ -503,6 +504,7 @@ int dev_create(int ord, Dev** out) {
     HCHK(hipEventCreateWithFlags(&w.ev_fork, hipEventDisableTiming));
     HCHK(hipEventCreateWithFlags(&w.ev_ta, hipEventDisableTiming));
     HCHK(hipEventCreateWithFlags(&w.ev_msm, hipEventDisableTiming));
+    HCHK(hipEventCreateWithFlags(&w.ev_h, hipEventDisableTiming));
     HCHK(hipStreamCreateWithPriority(&d->hc[k_ws].s, hipStreamNonBlocking, prio_lo));
   }
   HCHK(hipHostMalloc((void**)&d->res_host, N_RES * sizeof(SlotRes), hipHostMallocDefault));
@@ -747,7 +749,8 @@ int ta_tail(Dev& d, Ws& w, const HmEntry* pts, const uint32_t* src, const uint8_
 
 int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, const uint32_t* didx,
                     const MsgEntry* hm, size_t n, const uint32_t* dgoff, size_t n_groups, uint8_t* dst,
-                    hipStream_t s, hipEvent_t hm_ready, const TaFold* fold, const uint32_t* kc_idx = nullptr) {
+                    hipStream_t s, hipEvent_t hm_ready, const TaFold* fold, const uint32_t* kc_idx = nullptr,
+                    hipEvent_t h_ready = nullptr) {
   if (!dgoff) n_groups = n;
   G1AEntry* vpk;
   HmEntry* vsig;
@@ -965,7 +968,9 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
   if (hm_ready && bfe) HCHK(hipStreamWaitEvent(s, hm_ready, 0));
   Fp4Entry* f1 = nullptr;
   uint8_t* f1bad = nullptr;
-  if (!bfe && (wsbuf(w, W_F1, 3 * 2 * gcap, &f1) || wsbuf(w, W_F1BAD, gcap, &f1bad))) return -1;
+  G2JEntry* f1S = nullptr;
+  if (!bfe && (wsbuf(w, W_F1, 3 * 2 * gcap, &f1) || wsbuf(w, W_F1BAD, gcap, &f1bad) || wsbuf(w, W_F1S, gcap, &f1S)))
+    return -1;
   for (size_t g0 = 0; g0 < n_groups; g0 += gcap) {
     const uint32_t ng = (uint32_t)std::min(gcap, n_groups - g0);
     GroupPrepArgs ga{};
@@ -1030,9 +1035,10 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
         TIMED(d, "k_msm_bucket", sm, launch_msm_bucket(ma, sm));
         TIMED(d, "k_msm_reduce", sm, launch_msm_reduce(ma, sm));
         TIMED(d, "k_msm_sum", sm, launch_msm_sum(ma, sm));
-        TIMED(d, "k_slines", sm, launch_slines(ma.total, nullptr, nullptr, 1, blines, 1, bbad, sm));
         // the signature side's Miller loop, beside the multi-Miller loops and their product tree:
-        // the final exponentiation's second factor, pfin[1]
+        // the final exponentiation's second factor, pfin[1] (lines and loop in one kernel, k_lml)
+#if defined(HB_NO_LML)
+        TIMED(d, "k_slines", sm, launch_slines(ma.total, nullptr, nullptr, 1, blines, 1, bbad, sm));
         {
           Pair3Args ps{};
           ps.sig_lines = blines;
@@ -1042,6 +1048,9 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
           ps.f_out_off = 1;
           TIMED(d, "k_pair3_mls", sm, launch_pair3_mls(ps, sm));
         }
+#else
+        TIMED(d, "k_pair3_mls", sm, launch_lml(ma.total, 1, pfin, 1, 1, bbad, sm));
+#endif
         }
         HCHK(hipEventRecord(w.ev_side[0], sm));
         // multi-Miller loops over mmlk groups (shared squarings), then a product tree of fan-in
@@ -1216,29 +1225,27 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
       continue;
     }
     ga.skip_hm = 1;
+    // these calls are single Verifies and small batches, latency-bound: each group's sums (S kept
+    // Jacobian, no lines), then its signature side's Miller loop -- lines produced and consumed in
+    // one kernel (k_lml) -- while the messages still hash; after the hashing (not its lines) the
+    // (P, H(m)) loop the same way, then ONE six-lane final exponentiation of the two stored loops
+    // (f1[2g], f1[2g + 1])
+    ga.gS = f1S;
+    ga.bS = nullptr;
+    ga.fe_batch = 1;
     TIMED(d, "k_group_prep", s, launch_group_prep(ga, s));
-    // these calls are single Verifies and small batches, latency-bound: the signature side's
-    // Miller loop runs while the messages still hash, then each group's (P, H(m)) loop, then ONE
-    // six-lane final exponentiation of the two stored loops (f1[2g], f1[2g + 1])
-    Pair3Args ps{};
-    ps.sig_lines = glines;
-    ps.stride = ng;
-    ps.n = ng;
-    ps.f_out = f1;
-    ps.f_out_stride = 2;
-    ps.f_out_off = 1;
-    TIMED(d, "k_pair3", s, launch_pair3_mls(ps, s));
-    if (hm_ready && g0 == 0) HCHK(hipStreamWaitEvent(s, hm_ready, 0));
-    Pair3Args pa{};
+    TIMED(d, "k_pair3", s, launch_lml(f1S, ng, f1, 2, 1, nullptr, s));
+    if (g0 == 0 && (h_ready || hm_ready)) HCHK(hipStreamWaitEvent(s, h_ready ? h_ready : hm_ready, 0));
+    LmlArgs pa{};
     pa.pk = gP;
     pa.pk_st = gst;
     pa.msg_idx = gmsg + g0;
     pa.hm = hm;
     pa.n = ng;
     pa.f_out = f1;
-    pa.f_out_stride = 2;
-    pa.f_bad = f1bad;
-    TIMED(d, "k_pair3", s, launch_pair3_ml(pa, s));
+    pa.f_stride = 2;
+    pa.bad = f1bad;
+    TIMED(d, "k_pair3", s, launch_lml_p(pa, s));
     Pair3Args pf{};
     pf.pk_st = f1bad;
     pf.n = ng;
@@ -1248,6 +1255,8 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
     pf.status = gver + g0;
     TIMED(d, "k_pair3", s, launch_pair6_fin(pf, s));
   }
+  // the per-item fallback reads the messages' lines (the small calls' group checks did not wait)
+  if (!bfe && hm_ready && h_ready) HCHK(hipStreamWaitEvent(s, hm_ready, 0));
   HCHK(hipMemsetAsync(count, 0, sizeof(uint32_t), s));
   ScatterArgs sa{};
   sa.n = (uint32_t)n;
@@ -1391,7 +1400,7 @@ void dedup_messages(const uint8_t* msgs, const uint64_t* off, const uint32_t* le
 // runs on its side stream 2 (beside the decompression the verification forks next) and *ready is
 // the event the verification waits on before it needs H(m).
 int hash_table(Dev& d, const MsgTable& t, MsgEntry** hm_out, bool lines, Ws* w = nullptr,
-               hipEvent_t* ready = nullptr, Hc* h = nullptr) {
+               hipEvent_t* ready = nullptr, Hc* h = nullptr, hipEvent_t* h_ready = nullptr) {
   uint8_t* dmsg;
   uint64_t* doff;
   uint32_t* dlen;
@@ -1407,6 +1416,10 @@ int hash_table(Dev& d, const MsgTable& t, MsgEntry** hm_out, bool lines, Ws* w =
     HCHK(hipStreamWaitEvent(hs, w->ev_ta, 0));
   }
   TIMED(d, "k_hash_to_g2", hs, launch_hash_to_g2(dmsg, doff, dlen, (uint32_t)t.len.size(), (MsgEntry*)hm, hs));
+  if (w && h_ready) {
+    HCHK(hipEventRecord(w->ev_h, hs));
+    *h_ready = w->ev_h;
+  }
   if (lines) TIMED(d, "k_lines_msg", hs, launch_lines_msg((MsgEntry*)hm, (uint32_t)t.len.size(), hs));
   if (w) {
     HCHK(hipEventRecord(w->ev_side[2], hs));
@@ -1599,8 +1612,8 @@ int verify_host(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msgs, co
     // one call: the two chains run side by side)
     Ws& w = ws_acquire(d, h.s);
     MsgEntry* hm;
-    hipEvent_t hm_ready = nullptr;
-    if (hash_table(d, t, &hm, true, &w, &hm_ready, &h)) return -1;
+    hipEvent_t hm_ready = nullptr, h_ready = nullptr;
+    if (hash_table(d, t, &hm, true, &w, &hm_ready, &h, &h_ready)) return -1;
     uint8_t *dpk, *dsig, *dst, *dst_out = nullptr;
     uint32_t *didx, *dgoff, *dkc = nullptr, *dord = nullptr;
     if (whole) {  // caller order up, group order on the device
@@ -1626,7 +1639,7 @@ int verify_host(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msgs, co
     if (upload(d, I_MIDX, tidx.data(), m, &didx, &h) || upload(d, I_VGOFF, goff.data(), goff.size(), &dgoff, &h))
       return -1;
     if (use_kc && upload(d, I_KC, kc.data(), m, &dkc, &h)) return -1;
-    if (verify_pipeline(d, w, dpk, dsig, didx, hm, m, dgoff, ge - gb, dst, h.s, hm_ready, nullptr, dkc))
+    if (verify_pipeline(d, w, dpk, dsig, didx, hm, m, dgoff, ge - gb, dst, h.s, hm_ready, nullptr, dkc, h_ready))
       return -1;
     if (whole) LAUNCH(k_scatter_status, m, h.s, dst, dord, (uint32_t)m, dst_out);
     if (ws_release(w, h.s)) return -1;

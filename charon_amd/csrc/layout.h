@@ -201,6 +201,20 @@ void launch_pair3_mls(const Pair3Args& a, hipStream_t s);
 // consumed in one two-wave workgroup per point): f_out[e f_stride + f_off], bad[e] = S infinite
 void launch_lml(const G2JEntry* pts, uint32_t n, Fp4Entry* f_out, uint32_t f_stride, uint32_t f_off, uint8_t* bad,
                 hipStream_t s, const uint8_t* guard = nullptr);
+struct LmlArgs {
+  const G2JEntry* pts;     // side 0: the points S
+  const G1AEntry* pk;      // side 1: P per unit, its state (pk_st), message (msg_idx) and table (hm)
+  const uint8_t* pk_st;
+  const uint32_t* msg_idx;
+  const MsgEntry* hm;
+  uint32_t n;
+  Fp4Entry* f_out;
+  uint32_t f_stride, f_off;
+  uint8_t* bad;
+  const uint8_t* guard;
+};
+// side 1: the (P, H(m)) loop of each unit, H(m) affine (its lines are produced in the kernel)
+void launch_lml_p(const LmlArgs& a, hipStream_t s);
 constexpr uint32_t PROD_FAN = 8;  // fan-in of the product trees in front of a final exponentiation
 // FIN without sig_lines over six lanes per unit (pair6.h: Fp2 products split across lane pairs):
 // the same statuses at about half the latency

@@ -53,9 +53,9 @@ HD void fp_dot2_core(uint32_t* out, const uint32_t* x0w, const uint32_t* y0w, co
 // leaf: x0, x1 in registers, y0, y1 through the per-lane LDS slot of fp2_mul_leaf
 __device__ __noinline__ static u32x12 fp_dot2_leaf(u32x24 a, uint32_t neg) {
   uint32_t x0[12], x1[12], y0[12], y1[12], r[12];
-  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t lane = threadIdx.x & (HB_ARG_LANES - 1u);
   HB_UNROLL for (int k = 0; k < 6; k++) {
-    const uint2 v = hb_fp2_arg[k * 64 + lane], w = hb_fp2_arg[(6 + k) * 64 + lane];
+    const uint2 v = hb_fp2_arg[k * HB_ARG_LANES + lane], w = hb_fp2_arg[(6 + k) * HB_ARG_LANES + lane];
     y0[2 * k] = v.x;
     y0[2 * k + 1] = v.y;
     y1[2 * k] = w.x;
@@ -77,10 +77,10 @@ __device__ __forceinline__ Fp fp_dot2(const Fp& x0, const Fp& y0, const Fp& x1, 
     av[i] = x0.v[i];
     av[12 + i] = x1.v[i];
   }
-  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t lane = threadIdx.x & (HB_ARG_LANES - 1u);
   HB_UNROLL for (int k = 0; k < 6; k++) {
-    hb_fp2_arg[k * 64 + lane] = make_uint2(y0.v[2 * k], y0.v[2 * k + 1]);
-    hb_fp2_arg[(6 + k) * 64 + lane] = make_uint2(y1.v[2 * k], y1.v[2 * k + 1]);
+    hb_fp2_arg[k * HB_ARG_LANES + lane] = make_uint2(y0.v[2 * k], y0.v[2 * k + 1]);
+    hb_fp2_arg[(6 + k) * HB_ARG_LANES + lane] = make_uint2(y1.v[2 * k], y1.v[2 * k + 1]);
   }
   const u32x12 rv = fp_dot2_leaf(av, neg ? 1u : 0u);
   Fp r;

@@ -4,6 +4,7 @@
 // Compiled with HB_FAST_FPMUL: every field / curve / tower function is inlined; the Fp product and
 // square are the only calls (fp.h fp_mul_leaf / fp_sqr_leaf, compiler-visible C++).
 #define HB_FAST_FPMUL 1
+#define HB_ARG_LANES 128  // k_lml: two-wave workgroups
 #include "lines.h"
 #include "pair3.h"
 #include "pair6.h"
@@ -241,6 +242,99 @@ static inline unsigned blocks_for(size_t n) { return (unsigned)((n + BLOCK - 1) 
 void launch_mml_eval(const Pair3Args& a, LineEntry* ev, hipStream_t s) {
   const size_t n = (size_t)N_LINES * a.f_n;
   if (n) hipLaunchKernelGGL(k_mml_eval, dim3(blocks_for(n)), dim3(BLOCK), 0, s, a.pk, a.pk_st, a.msg_idx, a.hm, a.f_n, ev);
+}
+
+// The (-g1, S) Miller loop of ONE point S (Jacobian), its lines produced and consumed at once: a
+// two-wave workgroup per point -- wave 0 steps T through the chain of S (affine first) and hands
+// each line, evaluated at -g1, over through LDS; wave 1 (three lanes, pair3.h) squares and
+// multiplies it into f while wave 0 already computes the next.  The chain's latency is then about
+// one of the two halves instead of k_slines followed by k_pair3<MLS> (the slot-wide check's signature
+// side: a tail of every slot, on the critical path of small slots).  bad[e] = 1 for S at infinity.
+// SIDE 1 (the small calls' group checks): the (P_g, H(m_g)) loop instead, H(m_g) affine from the
+// message table (its lines need not exist yet: only the hashing is waited for), the lines
+// evaluated at P_g by the consumer; bad[e] = the group fails without a pairing (state, P or H(m)
+// at infinity), as k_pair3<ML>'s f_bad.
+template <int SIDE>
+__global__ __launch_bounds__(128, 1) void k_lml(LmlArgs a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (a.guard && *a.guard == 0) return;
+  const uint32_t e = blockIdx.x;
+  if (e >= a.n) return;  // workgroup-uniform
+  __shared__ LineEntry buf[2];
+  __shared__ uint32_t sinf;
+  const bool producer = threadIdx.x < 64;
+  G2Proj T;
+  G2A Q;
+  if (producer) {
+    if (SIDE == 0) {
+      const G2JEntry pe = a.pts[e];
+      Q = jac_to_aff(G2J{pe.X, pe.Y, pe.Z});
+    } else {
+      Q = hm_load(a.hm[a.msg_idx[e]].h);
+    }
+    T = {Q.x, Q.y, f2_one()};
+    if (threadIdx.x == 0) sinf = Q.inf ? 1u : 0u;
+  }
+  G1AEntry P{};
+  if (SIDE == 1 && !producer) P = a.pk[e];
+  Grp g = grp_make();
+  Fp4 f = g_one(g);
+  int bit = 62;        // consumer: the loop schedule of k_pair3
+  bool pending_add = false;
+  int pbit = 62;       // producer: the chain schedule of line_chain
+  bool padd = false;
+  HB_NOUNROLL for (int j = 0; j <= N_LINES; j++) {
+    if (producer && j < N_LINES) {
+      LineCoeffs l;
+      if (!padd) {
+        l = miller_dbl_c(T);
+        padd = ((HB_X_ABS >> pbit) & 1) != 0;
+        pbit--;
+      } else {
+        l = miller_add_c(T, Q.x, Q.y);
+        padd = false;
+      }
+      if (SIDE == 0) line_eval(l, fp_from_const(G1_GEN_X), fp_from_const(G1_GEN_NEG_Y));
+      if (threadIdx.x == 0) buf[j & 1] = {l.a0, l.a1, l.b1};
+    }
+    if (!producer && j > 0) {
+      const LineEntry L = buf[(j - 1) & 1];
+      const bool dbl = !pending_add;
+      if (dbl && j > 1) f = g_sqr(g, f);
+      if (SIDE == 0) f = g_mul_line(g, f, L.a0, L.a1, L.b1);
+      else f = g_mul_line(g, f, L.a0, f2_mul_fp(L.a1, P.x), f2_mul_fp(L.b1, P.y));
+      if (dbl) {
+        pending_add = ((HB_X_ABS >> bit) & 1) != 0;
+        bit--;
+      } else {
+        pending_add = false;
+      }
+    }
+    __syncthreads();
+  }
+  if (!producer && threadIdx.x < 64 + 3) {
+    const size_t o = (size_t)e * (a.f_stride ? a.f_stride : 1u) + a.f_off;
+    a.f_out[3 * o + g.k] = Fp4Entry{f.x, f.y};
+    if (threadIdx.x == 64 && a.bad)
+      a.bad[e] = SIDE == 0 ? (uint8_t)sinf : (uint8_t)((a.pk_st && a.pk_st[e]) || P.inf || sinf ? 1 : 0);
+  }
+#endif
+}
+
+void launch_lml(const G2JEntry* pts, uint32_t n, Fp4Entry* f_out, uint32_t f_stride, uint32_t f_off, uint8_t* bad,
+                hipStream_t s, const uint8_t* guard) {
+  LmlArgs a{};
+  a.pts = pts;
+  a.n = n;
+  a.f_out = f_out;
+  a.f_stride = f_stride;
+  a.f_off = f_off;
+  a.bad = bad;
+  a.guard = guard;
+  if (n) hipLaunchKernelGGL(k_lml<0>, dim3(n), dim3(128), 0, s, a);
+}
+void launch_lml_p(const LmlArgs& a, hipStream_t s) {
+  if (a.n) hipLaunchKernelGGL(k_lml<1>, dim3(a.n), dim3(128), 0, s, a);
 }
 
 void launch_lines_msg(MsgEntry* hm, uint32_t n, hipStream_t s) {
