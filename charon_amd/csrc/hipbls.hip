@@ -1724,6 +1724,7 @@ struct Coalescer {
   std::deque<VReq*> q;
   size_t queued = 0;
   bool running = false;
+  std::chrono::steady_clock::time_point last_end{};  // when the previous batch finished
 };
 Coalescer g_vq;
 size_t g_coalesce_us = (size_t)-1, g_coalesce_max = 0;
@@ -1782,7 +1783,12 @@ int verify_coalesced(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msg
   while (!me.done) {
     if (!c.running) {
       c.running = true;
-      auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(g_coalesce_us);
+      // gather more requests only in a busy period (a batch finished within the last few windows):
+      // a lone caller on an idle library runs at once, and under load the requests that queue up
+      // while a batch runs form the next one anyway
+      const auto now = std::chrono::steady_clock::now();
+      const bool busy = now - c.last_end < std::chrono::microseconds(4 * g_coalesce_us) || c.q.size() > 1;
+      auto deadline = now + std::chrono::microseconds(busy ? g_coalesce_us : 0);
       while (c.queued < g_coalesce_max && std::chrono::steady_clock::now() < deadline) c.cv.wait_until(lk, deadline);
       std::vector<VReq*> batch(c.q.begin(), c.q.end());
       c.q.clear();
@@ -1792,6 +1798,7 @@ int verify_coalesced(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msg
       lk.lock();
       for (VReq* r : batch) r->done = true;
       c.running = false;
+      c.last_end = std::chrono::steady_clock::now();
       c.cv.notify_all();
     } else {
       c.cv.wait(lk);
