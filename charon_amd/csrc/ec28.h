@@ -1,0 +1,238 @@
+// Lazily reduced 28-bit-limb point arithmetic for the subgroup ladders (round 3).
+//
+// fp.h stores Fp in 12 x 32-bit words reduced to [0, 2p): every Montgomery product re-splits its
+// operands into 14 limbs of 28 bits and joins its result back (≈ 80 of its ≈ 540 VALU
+// instructions), and every addition is a 12-word carry chain plus a conditional subtraction of
+// 2p (36 instructions).  Here the G1 Jacobian coordinates stay in 14 x 28-bit limbs across a
+// whole ladder: the products take and return limbs directly (fp_mul28_leaf / fp_sqr28_leaf), an
+// addition is 14 independent limb additions, a subtraction a + K - b adds a multiple K = s p of p
+// whose limbs are spread so that each dominates the subtrahend's (no borrows), and a carry pass
+// (`l_norm`) runs only where a value feeds a subtraction or must fit a product's input bound.
+// Nothing is reduced modulo p outside the products, so values grow up to VMAX p between them;
+// charon_amd/tools/lazy28.py restates every formula below over per-limb intervals and proves
+// (tests/test_lazy28.py) that no limb exceeds 32 bits, no product column 64 bits, every K
+// dominates its subtrahend and the coordinates return below VMAX p -- the ladders' invariant.
+// The site constants K28<s, t> below are the ones lazy28.KSITE holds (the test compares them).
+#pragma once
+#include "ec.h"
+
+namespace hb {
+
+struct L28 {
+  uint32_t l[14];
+};
+
+// K = s p as 14 limbs of 28 bits spread with redundancy t: K_0 = c_0 + t 2^28,
+// K_i = c_i + t 2^28 - t (0 < i < 13), K_13 = c_13 - t (lazy28.py kconst)
+struct K28v {
+  uint32_t l[14];
+};
+constexpr uint32_t kP28_[14] = {0x0fffaaabu, 0x0fefffffu, 0x03ffffb9u, 0x0fffeb15u, 0x06241eabu,
+                                0x0a0f6b0fu, 0x0f6730d2u, 0x0f38512bu, 0x04774b84u, 0x04bacd76u,
+                                0x0ba7b643u, 0x0e69a4b1u, 0x01ea397fu, 0x0001a011u};  // = P28
+constexpr K28v k28_make(uint32_t s, uint32_t t) {
+  K28v k{};
+  uint64_t c = 0;
+  for (int i = 0; i < 14; i++) {
+    const uint64_t v = (uint64_t)kP28_[i] * s + c;
+    k.l[i] = (uint32_t)(v & 0x0FFFFFFFu);
+    c = v >> 28;
+  }
+  k.l[13] += (uint32_t)(c << 28);  // s p < 2^392: no carry out of the top limb
+  k.l[0] += t << 28;
+  for (int i = 1; i < 13; i++) k.l[i] += (t << 28) - t;
+  k.l[13] -= t;
+  return k;
+}
+template <uint32_t S, uint32_t T>
+struct K28 {
+  static constexpr K28v v = k28_make(S, T);
+};
+
+HD L28 l_add(const L28& a, const L28& b) {
+  L28 r;
+  HB_UNROLL for (int i = 0; i < 14; i++) r.l[i] = a.l[i] + b.l[i];
+  return r;
+}
+HD L28 l_shl(const L28& a, int s) {
+  L28 r;
+  HB_UNROLL for (int i = 0; i < 14; i++) r.l[i] = a.l[i] << s;
+  return r;
+}
+template <uint32_t S, uint32_t T>
+HD L28 l_sub(const L28& a, const L28& b) {  // a + S p - b, limb-wise
+  L28 r;
+  HB_UNROLL for (int i = 0; i < 14; i++) r.l[i] = a.l[i] + (K28<S, T>::v.l[i] - b.l[i]);
+  return r;
+}
+HD L28 l_norm(L28 a) {  // carries: limbs 0..12 below 2^28, the value unchanged
+  HB_UNROLL for (int i = 0; i < 13; i++) {
+    a.l[i + 1] += a.l[i] >> 28;
+    a.l[i] &= 0x0FFFFFFFu;
+  }
+  return a;
+}
+HD L28 l_from(const Fp& a) {
+  L28 r;
+  fp_split28(r.l, a.v);
+  return r;
+}
+
+#if defined(__HIP_DEVICE_COMPILE__)
+HD L28 l_mul(const L28& a, const L28& b) {
+  HB_COUNT_FP_MUL();
+  u32x16 x, y;
+  HB_UNROLL for (int i = 0; i < 14; i++) {
+    x[i] = a.l[i];
+    y[i] = b.l[i];
+  }
+  x[14] = x[15] = y[14] = y[15] = 0;
+  const u32x16 o = fp_mul28_leaf(x, y);
+  L28 r;
+  HB_UNROLL for (int i = 0; i < 14; i++) r.l[i] = o[i];
+  return r;
+}
+HD L28 l_sqr(const L28& a) {
+  HB_COUNT_FP_MUL();
+  u32x16 x;
+  HB_UNROLL for (int i = 0; i < 14; i++) x[i] = a.l[i];
+  x[14] = x[15] = 0;
+  const u32x16 o = fp_sqr28_leaf(x);
+  L28 r;
+  HB_UNROLL for (int i = 0; i < 14; i++) r.l[i] = o[i];
+  return r;
+}
+#else
+HD L28 l_mul(const L28& a, const L28& b) {
+  HB_COUNT_FP_MUL();
+  L28 r;
+  fp_mul28_core(r.l, a.l, b.l);
+  return r;
+}
+HD L28 l_sqr(const L28& a) {
+  HB_COUNT_FP_MUL();
+  L28 r;
+  fp_sqr28_core(r.l, a.l);
+  return r;
+}
+#endif
+
+// a mod p == 0: the Montgomery product by the integer 1 is a R^-1 mod p and lies in [0, p]
+HD bool l_is_zero(const L28& a) {
+  L28 one;
+  one.l[0] = 1;
+  HB_UNROLL for (int i = 1; i < 14; i++) one.l[i] = 0;
+  const L28 t = l_mul(a, one);
+  uint32_t z = 0, q = 0;
+  HB_UNROLL for (int i = 0; i < 14; i++) {
+    z |= t.l[i];
+    q |= t.l[i] ^ kP28_[i];
+  }
+  return z == 0 || q == 0;
+}
+// back to the stored form: the product by R mod p (Montgomery one) is < p + 1 -> [0, 2p) words
+HD Fp l_to(const L28& a) {
+  const L28 t = l_mul(a, l_from(fp_one()));
+  Fp r;
+  fp_join28(r.v, t.l);
+  return r;
+}
+
+// ---- G1 Jacobian points in lazy limbs; infinity as a flag (E(Fp) has no 2-torsion: the
+// cofactor (x - 1)^2 / 3 and r are odd, so a doubling never reaches Z = 0 from a finite point)
+struct G1L {
+  L28 X, Y, Z;
+  bool inf;
+};
+
+// dbl-2009-l (lazy28.py dbl)
+HDNI G1L g1l_dbl(const G1L& p) {
+  const L28 A = l_sqr(p.X), B = l_sqr(p.Y), C = l_sqr(B);
+  const L28 T = l_sqr(l_add(p.X, B));
+  const L28 E = l_add(l_add(A, A), A);
+  const L28 F = l_sqr(E);
+  const L28 D = l_norm(l_shl(l_sub<3, 2>(T, l_add(A, C)), 1));
+  G1L r;
+  r.X = l_norm(l_sub<17, 2>(F, l_shl(D, 1)));
+  const L28 W = l_sub<19, 1>(D, r.X);
+  r.Y = l_norm(l_sub<9, 8>(l_mul(E, W), l_shl(C, 3)));
+  r.Z = l_mul(l_shl(p.Y, 1), p.Z);
+  r.inf = p.inf;
+  return r;
+}
+
+// the common tail of the additions (I = 4 HH folded into shifts: J = 4 H HH, V = 4 U1 HH)
+HD G1L g1l_add_tail(const L28& H, const L28& rr, const L28& U1, const L28& S1, const L28& Zs) {
+  const L28 HH = l_sqr(H);
+  const L28 J1 = l_mul(H, HH), V1 = l_mul(U1, HH);
+  G1L r;
+  r.X = l_norm(l_sub<13, 12>(l_sqr(rr), l_add(l_shl(J1, 2), l_shl(V1, 3))));
+  r.Y = l_norm(l_sub<9, 8>(l_mul(rr, l_sub<15, 1>(l_shl(V1, 2), r.X)), l_shl(l_mul(S1, J1), 3)));
+  r.Z = l_mul(Zs, H);
+  r.inf = false;
+  return r;
+}
+
+HD G1L g1l_infinity() {
+  G1L r;
+  HB_UNROLL for (int i = 0; i < 14; i++) r.X.l[i] = r.Y.l[i] = r.Z.l[i] = 0;
+  r.inf = true;
+  return r;
+}
+
+// madd-2007-bl: p + (x2, y2), the affine point finite and normalised below 2p (lazy28.py madd)
+HDNI G1L g1l_madd(const G1L& p, const L28& x2, const L28& y2) {
+  if (p.inf) return {x2, y2, l_from(fp_one()), false};
+  const L28 Z1Z1 = l_sqr(p.Z);
+  const L28 U2 = l_mul(x2, Z1Z1);
+  const L28 S2 = l_mul(l_mul(y2, p.Z), Z1Z1);
+  const L28 H = l_sub<21, 1>(U2, p.X);
+  const L28 rr = l_norm(l_sub<41, 2>(l_shl(S2, 1), l_shl(p.Y, 1)));
+  if (l_is_zero(H)) {
+    if (l_is_zero(rr)) return g1l_dbl(p);
+    return g1l_infinity();
+  }
+  return g1l_add_tail(H, rr, p.X, p.Y, l_shl(p.Z, 1));
+}
+
+// add-2007-bl (lazy28.py jadd)
+HDNI G1L g1l_add(const G1L& p, const G1L& q) {
+  if (p.inf) return q;
+  if (q.inf) return p;
+  const L28 Z1Z1 = l_sqr(p.Z), Z2Z2 = l_sqr(q.Z);
+  const L28 U1 = l_mul(p.X, Z2Z2), U2 = l_mul(q.X, Z1Z1);
+  const L28 S1 = l_mul(l_mul(p.Y, q.Z), Z2Z2);
+  const L28 S2 = l_mul(l_mul(q.Y, p.Z), Z1Z1);
+  const L28 H = l_sub<21, 1>(U2, U1);
+  const L28 rr = l_norm(l_sub<41, 2>(l_shl(S2, 1), l_shl(S1, 1)));
+  if (l_is_zero(H)) {
+    if (l_is_zero(rr)) return g1l_dbl(p);
+    return g1l_infinity();
+  }
+  return g1l_add_tail(H, rr, U1, S1, l_mul(l_shl(p.Z, 1), q.Z));
+}
+
+HD G1J g1l_to_jac(const G1L& p) {
+  if (p.inf) return jac_infinity<Fp>();
+  return {l_to(p.X), l_to(p.Y), l_to(p.Z)};
+}
+
+// P in G1  <=>  phi(P) == [-x^2] P (ec.h g1_in_subgroup), the two ladders in lazy limbs
+HDNI bool g1_in_subgroup28(const G1A& p) {
+  if (p.inf) return true;
+  const L28 x = l_from(p.x), y = l_from(p.y);
+  G1L t = {x, y, l_from(fp_one()), false};
+  HB_NOUNROLL for (int i = 62; i >= 0; i--) {
+    t = g1l_dbl(t);
+    if ((HB_X_ABS >> i) & 1) t = g1l_madd(t, x, y);
+  }
+  G1L u = t;
+  HB_NOUNROLL for (int i = 62; i >= 0; i--) {
+    u = g1l_dbl(u);
+    if ((HB_X_ABS >> i) & 1) u = g1l_add(u, t);
+  }
+  const G1J phi = jac_from_aff(G1A{fp_mul(p.x, fp_from_const(G1_BETA)), p.y, false});
+  return jac_eq(phi, jac_neg(g1l_to_jac(u)));
+}
+
+}  // namespace hb

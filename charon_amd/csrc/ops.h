@@ -5,6 +5,7 @@
 #include "h2c.h"
 #include "pairing.h"
 #include "fr.h"
+#include "ec28.h"
 
 namespace hb {
 
@@ -58,7 +59,7 @@ HDNI uint8_t g1_decompress(G1A& out, const uint8_t* b, bool subgroup_check = tru
   out.x = x;
   out.y = y;
   out.inf = false;
-  if (subgroup_check && !g1_in_subgroup(out)) return 1;
+  if (subgroup_check && !g1_in_subgroup28(out)) return 1;
   return 0;
 }
 

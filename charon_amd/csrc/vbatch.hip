@@ -65,13 +65,17 @@ __global__ KB_OCC(HB_OCC_DECPK) void k_dec_pk(const uint8_t* __restrict__ pks, u
 }
 
 // The subgroup check of k_dec_pk's points, a kernel of its own like k_g2_subgroup (the fused
-// kernel spilled the square root's window table beside the ladder).
+// kernel spilled the square root's window table beside the ladder).  The ladders run in lazily
+// reduced 28-bit limbs (ec28.h; HB_G1_LAZY=0: the stored-word ec.h test, for A/B runs).
+#ifndef HB_G1_LAZY
+#define HB_G1_LAZY 1
+#endif
 __global__ KB_OCC(HB_OCC_SUBG) void k_g1_subgroup(uint32_t n, G1AEntry* __restrict__ pts, uint8_t* __restrict__ st) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const G1AEntry e = pts[i];
   if (st[i] || e.inf) return;
-  if (!g1_in_subgroup(G1A{e.x, e.y, false})) {
+  if (!(HB_G1_LAZY ? g1_in_subgroup28(G1A{e.x, e.y, false}) : g1_in_subgroup(G1A{e.x, e.y, false}))) {
     const G1A g = g1_generator();
     G1AEntry z;
     z.x = g.x;

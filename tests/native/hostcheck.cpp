@@ -497,3 +497,18 @@ extern "C" int hc_lagrange_g2_small(const uint8_t* sigs, const int64_t* idx, int
   g2_compress(out96, jac_to_aff(qa.inf ? jac_infinity<Fp2>() : jac_mul_aff(qa, sc.v, 256)));
   return 0;
 }
+
+// the G1 subgroup test both ways for an affine point given as big-endian x || y (on the curve,
+// not checked): out[0] = ec.h g1_in_subgroup (stored words), out[1] = ec28.h lazy limbs,
+// out[2] = the Fp products the lazy test spent
+extern "C" int hc_g1_subgroup2(const uint8_t* xy96, int* out) {
+  Fp xr, yr;
+  fp_from_be_raw(xr, xy96);
+  fp_from_be_raw(yr, xy96 + 48);
+  const G1A p = {fp_to_mont(xr), fp_to_mont(yr), false};
+  out[0] = g1_in_subgroup(p) ? 1 : 0;
+  g_cnt_fp_mul = 0;
+  out[1] = g1_in_subgroup28(p) ? 1 : 0;
+  out[2] = (int)g_cnt_fp_mul;
+  return 0;
+}
