@@ -241,4 +241,188 @@ HDNI bool g1_in_subgroup28(const G1A& p) {
   return jac_eq(phi, jac_neg(g1l_to_jac(u)));
 }
 
+
+// ---- Fp2 (u^2 = -1) in lazy limbs (lazy28.py Fp2Ops)
+struct F2L {
+  L28 c0, c1;
+};
+HD F2L f2l_add(const F2L& a, const F2L& b) { return {l_add(a.c0, b.c0), l_add(a.c1, b.c1)}; }
+HD F2L f2l_shl(const F2L& a, int s) { return {l_shl(a.c0, s), l_shl(a.c1, s)}; }
+template <uint32_t S, uint32_t T>
+HD F2L f2l_sub(const F2L& a, const F2L& b) {
+  return {l_sub<S, T>(a.c0, b.c0), l_sub<S, T>(a.c1, b.c1)};
+}
+HD F2L f2l_norm(const F2L& a) { return {l_norm(a.c0), l_norm(a.c1)}; }
+HD F2L f2l_from(const Fp2& a) { return {l_from(a.c0), l_from(a.c1)}; }
+HD Fp2 f2l_to(const F2L& a) { return {l_to(a.c0), l_to(a.c1)}; }
+HD bool f2l_is_zero(const F2L& a) { return l_is_zero(a.c0) && l_is_zero(a.c1); }
+
+// (a0 + a1 u)(b0 + b1 u) in one product-scanning pass with two accumulators:
+//   real = a0 b0 + (K - a1) b1,   imag = a0 b1 + a1 b0,   K = 33 p (lazy28.KSITE["2N"]),
+// so both columns are sums of non-negative terms (no signed accumulator, no final correction)
+// and both results come out normalised.
+constexpr K28v kF2N = k28_make(33, 6);
+HD void f2l_dot_core(uint32_t* r, const uint32_t* a0, const uint32_t* a1, const uint32_t* b0, const uint32_t* b1) {
+  uint32_t m[14];  // r = (a0 b0 + a1 b1) / R: one column pass, one accumulator
+  uint64_t acc = 0;
+  HB_UNROLL for (int k = 0; k < 27; k++) {
+    const int lo = k < 14 ? 0 : k - 13, hi = k < 14 ? k : 13;
+    HB_UNROLL for (int j = lo; j <= hi; j++) {
+      acc += (uint64_t)a0[j] * b0[k - j];
+      acc += (uint64_t)a1[j] * b1[k - j];
+    }
+    HB_UNROLL for (int j = lo; j <= hi; j++)
+      if (j < k || k >= 14) acc += (uint64_t)m[j] * P28[k - j];
+    HB_MONT28_TAIL(acc, m, k, r)
+  }
+  r[13] = (uint32_t)acc;
+}
+HD void f2l_mul_core(uint32_t* r0, uint32_t* r1, const uint32_t* a0, const uint32_t* a1, const uint32_t* b0,
+                     const uint32_t* b1) {
+  uint32_t na1[14];
+  HB_UNROLL for (int j = 0; j < 14; j++) na1[j] = kF2N.l[j] - a1[j];
+  f2l_dot_core(r0, a0, na1, b0, b1);  // real = a0 b0 + (K - a1) b1
+  f2l_dot_core(r1, a0, a1, b1, b0);   // imag = a0 b1 + a1 b0
+}
+
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef uint32_t u32x32 __attribute__((ext_vector_type(32)));
+// first operand in the 32 argument VGPRs (limbs 0..13 | 16..29), the second through the per-lane
+// LDS slot of fp.h (14 pairs (b0_k, b1_k), k-major: conflict-free 64-bit accesses)
+static_assert(HB_FP2_ARG_SLOTS >= 14, "hb_fp2_arg holds 14 pairs per lane");
+__device__ __noinline__ static u32x32 f2l_mul_leaf(u32x32 a) {
+  uint32_t x0[14], x1[14], y0[14], y1[14], r0[14], r1[14];
+  const uint32_t lane = threadIdx.x & (HB_ARG_LANES - 1u);
+  HB_UNROLL for (int k = 0; k < 14; k++) {
+    const uint2 v = hb_fp2_arg[k * HB_ARG_LANES + lane];
+    y0[k] = v.x;
+    y1[k] = v.y;
+    x0[k] = a[k];
+    x1[k] = a[16 + k];
+  }
+  f2l_mul_core(r0, r1, x0, x1, y0, y1);
+  u32x32 o;
+  HB_UNROLL for (int k = 0; k < 14; k++) {
+    o[k] = r0[k];
+    o[16 + k] = r1[k];
+  }
+  o[14] = o[15] = o[30] = o[31] = 0;
+  return o;
+}
+HD F2L f2l_mul(const F2L& a, const F2L& b) {
+  HB_COUNT_FP_MUL();
+  HB_COUNT_FP_MUL();
+  HB_COUNT_FP_MUL();
+  u32x32 av;
+  const uint32_t lane = threadIdx.x & (HB_ARG_LANES - 1u);
+  HB_UNROLL for (int k = 0; k < 14; k++) {
+    av[k] = a.c0.l[k];
+    av[16 + k] = a.c1.l[k];
+    hb_fp2_arg[k * HB_ARG_LANES + lane] = make_uint2(b.c0.l[k], b.c1.l[k]);
+  }
+  av[14] = av[15] = av[30] = av[31] = 0;
+  const u32x32 o = f2l_mul_leaf(av);
+  F2L r;
+  HB_UNROLL for (int k = 0; k < 14; k++) {
+    r.c0.l[k] = o[k];
+    r.c1.l[k] = o[16 + k];
+  }
+  return r;
+}
+#else
+HD F2L f2l_mul(const F2L& a, const F2L& b) {
+  HB_COUNT_FP_MUL();
+  HB_COUNT_FP_MUL();
+  HB_COUNT_FP_MUL();
+  F2L r;
+  f2l_mul_core(r.c0.l, r.c1.l, a.c0.l, a.c1.l, b.c0.l, b.c1.l);
+  return r;
+}
+#endif
+// (a0 + a1)(a0 + K - a1) + 2 a0 a1 u, K = 36 p (lazy28.KSITE["2Q"]): two Fp products
+HD F2L f2l_sqr(const F2L& a) {
+  return {l_mul(l_add(a.c0, a.c1), l_sub<36, 1>(a.c0, a.c1)), l_mul(l_shl(a.c0, 1), a.c1)};
+}
+
+// ---- G2 Jacobian points in lazy limbs (E'(Fp2) has no 2-torsion either: h2 and r are odd)
+struct G2L {
+  F2L X, Y, Z;
+  bool inf;
+};
+
+// lazy28.py dbl2: D = 4 X B from one product, E = 3A normalised before its square, E W = 3 (A W);
+// the products in the order that ends the inputs' live ranges first (Z3 before B = Y^2, D1 right
+// after A) so that fewer values are held across the product calls
+HDNI G2L g2l_dbl(const G2L& p) {
+  G2L r;
+  r.Z = f2l_mul(f2l_shl(p.Y, 1), p.Z);
+  const F2L B = f2l_sqr(p.Y);
+  const F2L A = f2l_sqr(p.X);
+  const F2L D1 = f2l_mul(p.X, B);
+  const F2L C = f2l_sqr(B);
+  const F2L F = f2l_sqr(f2l_norm(f2l_add(f2l_shl(A, 1), A)));
+  r.X = f2l_norm(f2l_sub<9, 8>(F, f2l_shl(D1, 3)));
+  const F2L AW = f2l_mul(f2l_sub<11, 1>(f2l_shl(D1, 2), r.X), A);
+  r.Y = f2l_norm(f2l_sub<9, 8>(f2l_add(f2l_shl(AW, 1), AW), f2l_shl(C, 3)));
+  r.inf = p.inf;
+  return r;
+}
+
+HD G2L g2l_infinity() {
+  G2L r;
+  HB_UNROLL for (int i = 0; i < 14; i++)
+    r.X.c0.l[i] = r.X.c1.l[i] = r.Y.c0.l[i] = r.Y.c1.l[i] = r.Z.c0.l[i] = r.Z.c1.l[i] = 0;
+  r.inf = true;
+  return r;
+}
+
+// lazy28.py madd2: madd-2007-bl with H normalised (its square is an Fp2 square)
+HDNI G2L g2l_madd(const G2L& p, const F2L& x2, const F2L& y2) {
+  if (p.inf) return {x2, y2, {l_from(fp_one()), l_from(fp_zero())}, false};
+  const F2L Z1Z1 = f2l_sqr(p.Z);
+  const F2L U2 = f2l_mul(x2, Z1Z1);
+  const F2L S2 = f2l_mul(f2l_mul(y2, p.Z), Z1Z1);
+  const F2L H = f2l_norm(f2l_sub<17, 1>(U2, p.X));
+  const F2L rr = f2l_norm(f2l_sub<33, 2>(f2l_shl(S2, 1), f2l_shl(p.Y, 1)));
+  if (f2l_is_zero(H)) {
+    if (f2l_is_zero(rr)) return g2l_dbl(p);
+    return g2l_infinity();
+  }
+  const F2L HH = f2l_sqr(H);
+  const F2L J1 = f2l_mul(H, HH), V1 = f2l_mul(p.X, HH);
+  G2L r;
+  r.X = f2l_norm(f2l_sub<13, 12>(f2l_sqr(rr), f2l_add(f2l_shl(J1, 2), f2l_shl(V1, 3))));
+  r.Y = f2l_norm(
+      f2l_sub<9, 8>(f2l_mul(f2l_sub<16, 1>(f2l_shl(V1, 2), r.X), rr), f2l_shl(f2l_mul(p.Y, J1), 3)));
+  r.Z = f2l_mul(f2l_shl(p.Z, 1), H);
+  r.inf = false;
+  return r;
+}
+
+// Q in G2  <=>  psi(Q) == [x] Q (ec.h g2_in_subgroup), the ladder in lazy limbs.  `load` returns
+// Q again at each of the five mixed additions instead of the ladder holding its 56 limbs across
+// every product call (the kernel re-reads its entry; LICM is kept from hoisting that read)
+template <class LoadQ>
+HDNI bool g2_in_subgroup28_l(const LoadQ& load) {
+  const G2A q = load();
+  if (q.inf) return true;
+  G2L t = {f2l_from(q.x), f2l_from(q.y), {l_from(fp_one()), l_from(fp_zero())}, false};
+  HB_NOUNROLL for (int i = 62; i >= 0; i--) {
+    t = g2l_dbl(t);
+    if ((HB_X_ABS >> i) & 1) {
+#if defined(__HIP_DEVICE_COMPILE__)
+      __asm__ volatile("" ::: "memory");
+#endif
+      const G2A q2 = load();
+      t = g2l_madd(t, f2l_from(q2.x), f2l_from(q2.y));
+    }
+  }
+  const G2A q3 = load();
+  const G2J xq = t.inf ? jac_infinity<Fp2>() : G2J{f2l_to(t.X), f2l_to(t.Y), f2l_to(t.Z)};
+  return jac_eq(g2_psi(jac_from_aff(q3)), jac_neg(xq));
+}
+HDNI bool g2_in_subgroup28(const G2A& q) {
+  return g2_in_subgroup28_l([&]() { return q; });
+}
+
 }  // namespace hb

@@ -395,7 +395,8 @@ typedef uint32_t u32x24 __attribute__((ext_vector_type(24)));
 #ifndef HB_ARG_LANES
 #define HB_ARG_LANES 64
 #endif
-__shared__ uint2 hb_fp2_arg[12 * HB_ARG_LANES];
+#define HB_FP2_ARG_SLOTS 14  // 12 pairs for the stored-word product, 14 for ec28.h's lazy one
+__shared__ uint2 hb_fp2_arg[HB_FP2_ARG_SLOTS * HB_ARG_LANES];
 __device__ __noinline__ static u32x24 fp2_mul_leaf(u32x24 a) {
   uint32_t x0[12], x1[12], y0[12], y1[12], r0[12], r1[12];
   const uint32_t lane = threadIdx.x & (HB_ARG_LANES - 1u);

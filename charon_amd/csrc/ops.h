@@ -87,7 +87,7 @@ HDNI uint8_t g2_decompress(G2A& out, const uint8_t* b, bool subgroup_check = tru
   out.x = x;
   out.y = y;
   out.inf = false;
-  if (subgroup_check && !g2_in_subgroup(out)) return 1;
+  if (subgroup_check && !g2_in_subgroup28(out)) return 1;
   return 0;
 }
 

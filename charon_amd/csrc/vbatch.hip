@@ -70,6 +70,9 @@ __global__ KB_OCC(HB_OCC_DECPK) void k_dec_pk(const uint8_t* __restrict__ pks, u
 #ifndef HB_G1_LAZY
 #define HB_G1_LAZY 1
 #endif
+#ifndef HB_G2_LAZY
+#define HB_G2_LAZY 1  // k_g2_subgroup likewise (ec28.h g2_in_subgroup28)
+#endif
 __global__ KB_OCC(HB_OCC_SUBG) void k_g1_subgroup(uint32_t n, G1AEntry* __restrict__ pts, uint8_t* __restrict__ st) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -113,7 +116,12 @@ __global__ KB_OCC(HB_OCC_SUBG) void k_g2_subgroup(uint32_t n, HmEntry* __restric
   if (i >= n) return;
   const HmEntry e = pts[i];
   if (st[i] || e.inf) return;
+#if HB_G2_LAZY
+  const HmEntry* src = pts + i;
+  if (!g2_in_subgroup28_l([src]() { return G2A{src->x, src->y, false}; })) {
+#else
   if (!g2_in_subgroup(G2A{e.x, e.y, false})) {
+#endif
     HmEntry z;
     z.x = f2_zero();
     z.y = f2_zero();

@@ -196,10 +196,13 @@ class Fp2Ops:
 
 # K = s p with redundancy t per subtraction site (ec28.h K28<s, t>; kept in sync by
 # tests/test_lazy28.py, found by `python lazy28.py --search`)
-VMAX = 20
+VMAX = {"Fp": 20, "Fp2": 16}  # coordinates stay below VMAX p between the ladder steps
 KSITE = {
     "1D_D": (3, 2), "1D_X": (17, 2), "1D_W": (19, 1), "1D_Y": (9, 8),
     "1A_H": (21, 1), "1A_R": (41, 2), "1A_X": (13, 12), "1A_W": (15, 1), "1A_Y": (9, 8),
+    "2D_X": (9, 8), "2D_W": (11, 1), "2D_Y": (9, 8),
+    "2A_H": (17, 1), "2A_R": (33, 2), "2A_X": (13, 12), "2A_W": (16, 1), "2A_Y": (9, 8),
+    "2N": (33, 6), "2Q": (36, 1),
 }
 
 
@@ -261,6 +264,39 @@ def jadd(F, X1, Y1, Z1, X2, Y2, Z2):
     return _add_tail(F, H, rr, U1, S1, F.mul(F.shl(Z1, 1), Z2))
 
 
+def dbl2(F, X, Y, Z):
+    """g2l_dbl: dbl-2009-l rearranged for the Fp2 products' bounds -- D = 4 X B from one product
+    (the (X + B)^2 - A - C form grows D by its subtraction constant), E = 3A normalised before
+    its square, E W = 3 (A W)"""
+    A = F.sqr(X)
+    B = F.sqr(Y)
+    C = F.sqr(B)
+    D1 = F.mul(X, B)                                  # D = 4 D1
+    Fv = F.sqr(F.norm(F.add(F.shl(A, 1), A)))
+    X3 = F.norm(F.sub(Fv, F.shl(D1, 3), "D_X"))
+    W = F.sub(F.shl(D1, 2), X3, "D_W")
+    AW = F.mul(W, A)
+    Y3 = F.norm(F.sub(F.add(F.shl(AW, 1), AW), F.shl(C, 3), "D_Y"))
+    Z3 = F.mul(F.shl(Y, 1), Z)
+    return X3, Y3, Z3
+
+
+def madd2(F, X1, Y1, Z1, x2, y2):
+    """g2l_madd: madd-2007-bl as madd() with H normalised (its square is an Fp2 square)"""
+    Z1Z1 = F.sqr(Z1)
+    U2 = F.mul(x2, Z1Z1)
+    S2 = F.mul(F.mul(y2, Z1), Z1Z1)
+    H = F.norm(F.sub(U2, X1, "A_H"))
+    rr = F.norm(F.sub(F.shl(S2, 1), F.shl(Y1, 1), "A_R"))
+    HH = F.sqr(H)
+    J1 = F.mul(H, HH)
+    V1 = F.mul(X1, HH)
+    X3 = F.norm(F.sub(F.sqr(rr), F.add(F.shl(J1, 2), F.shl(V1, 3)), "A_X"))
+    Y3 = F.norm(F.sub(F.mul(F.sub(F.shl(V1, 2), X3, "A_W"), rr), F.shl(F.mul(Y1, J1), 3), "A_Y"))
+    Z3 = F.mul(F.shl(Z1, 1), H)
+    return X3, Y3, Z3
+
+
 def fits(x, vmax):
     return vmax_of(x) <= vmax and all(
         all(l <= M28 for l in b.lb[:13]) and b.lb[13] <= (vmax >> 364) for b in ([x] if isinstance(x, Bound) else x))
@@ -276,8 +312,11 @@ def check(vmax, fields=("Fp", "Fp2")):
         vm = vmax * P
         X = Y = Z = F.nrm(vm)
         aff = F.nrm(2 * P)
-        for op, fn in (("dbl", lambda: dbl(F, X, Y, Z)), ("madd", lambda: madd(F, X, Y, Z, aff, aff)),
-                       ("add", lambda: jadd(F, X, Y, Z, X, Y, Z))):
+        ops = (("dbl", lambda: dbl(F, X, Y, Z)), ("madd", lambda: madd(F, X, Y, Z, aff, aff)),
+               ("add", lambda: jadd(F, X, Y, Z, X, Y, Z)))
+        if name == "Fp2":
+            ops = (("dbl", lambda: dbl2(F, X, Y, Z)), ("madd", lambda: madd2(F, X, Y, Z, aff, aff)))
+        for op, fn in ops:
             res = fn()
             for c in res:
                 assert fits(c, vm), (name, op, vmax_of(c) / P)
@@ -320,5 +359,6 @@ if __name__ == "__main__":
             except AssertionError as e:
                 print(vm, "fails:", e)
     else:
-        for k, v in check(VMAX).items():
-            print(k, f"outputs < {v:.2f} p")
+        for f in ("Fp", "Fp2"):
+            for k, v in check(VMAX[f], (f,)).items():
+                print(k, f"outputs < {v:.2f} p (VMAX {VMAX[f]})")

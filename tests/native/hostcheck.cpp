@@ -512,3 +512,20 @@ extern "C" int hc_g1_subgroup2(const uint8_t* xy96, int* out) {
   out[2] = (int)g_cnt_fp_mul;
   return 0;
 }
+
+// the G2 subgroup test both ways, affine point as big-endian x0 || x1 || y0 || y1 (on the twist,
+// not checked): out[0] = ec.h g2_in_subgroup, out[1] = ec28.h lazy limbs, out[2] = its Fp products
+extern "C" int hc_g2_subgroup2(const uint8_t* xy192, int* out) {
+  Fp w[4];
+  for (int i = 0; i < 4; i++) {
+    Fp r;
+    fp_from_be_raw(r, xy192 + 48 * i);
+    w[i] = fp_to_mont(r);
+  }
+  const G2A q = {{w[0], w[1]}, {w[2], w[3]}, false};
+  out[0] = g2_in_subgroup(q) ? 1 : 0;
+  g_cnt_fp_mul = 0;
+  out[1] = g2_in_subgroup28(q) ? 1 : 0;
+  out[2] = (int)g_cnt_fp_mul;
+  return 0;
+}

@@ -22,22 +22,45 @@ import lazy28  # noqa: E402
 from oracle import bls12381 as B  # noqa: E402
 
 
-def test_bounds_fp():
-    out = lazy28.check(lazy28.VMAX, ("Fp",))
-    assert all(v <= lazy28.VMAX for v in out.values()), out
+@pytest.mark.parametrize("field", ["Fp", "Fp2"])
+def test_bounds(field):
+    out = lazy28.check(lazy28.VMAX[field], (field,))
+    assert all(v <= lazy28.VMAX[field] for v in out.values()), out
 
 
-def test_search_finds_no_smaller_constants():
+@pytest.mark.parametrize("field,prefix", [("Fp", "1"), ("Fp2", "2")])
+def test_search_finds_no_smaller_constants(field, prefix):
     """the committed constants are the smallest the interval analysis admits at VMAX"""
-    found = lazy28.search(lazy28.VMAX, ("Fp",))
-    assert found == {k: v for k, v in lazy28.KSITE.items() if k.startswith("1")}
+    saved = dict(lazy28.KSITE)
+    try:
+        found = lazy28.search(lazy28.VMAX[field], (field,))
+    finally:
+        lazy28.KSITE.clear()
+        lazy28.KSITE.update(saved)
+    assert found == {k: v for k, v in saved.items() if k.startswith(prefix)}
+
+
+def _fn(src, name):
+    i = src.index(name + "(")
+    return src[i:src.index("\n}\n", i)]
 
 
 def test_constants_match_ec28():
+    """each ec28.h formula uses exactly the constants lazy28.py proves for its sites"""
     src = open(os.path.join(ROOT, "charon_amd", "csrc", "ec28.h")).read()
-    used = {tuple(map(int, m)) for m in re.findall(r"l_sub<(\d+), (\d+)>", src)}
-    want = {v for k, v in lazy28.KSITE.items() if k.startswith("1")}
-    assert used == want, (used, want)
+    k = lazy28.KSITE
+
+    def used(*names, pat=r"l_sub<(\d+), (\d+)>"):
+        return sorted(tuple(map(int, m)) for n in names for m in re.findall(pat, _fn(src, n)))
+
+    assert used("HDNI G1L g1l_dbl") == sorted([k["1D_D"], k["1D_X"], k["1D_W"], k["1D_Y"]])
+    assert used("HD G1L g1l_add_tail") == sorted([k["1A_X"], k["1A_Y"], k["1A_W"]])
+    assert used("HDNI G1L g1l_madd") == used("HDNI G1L g1l_add") == sorted([k["1A_H"], k["1A_R"]])
+    assert used("HDNI G2L g2l_dbl", pat=r"f2l_sub<(\d+), (\d+)>") == sorted([k["2D_X"], k["2D_W"], k["2D_Y"]])
+    assert used("HDNI G2L g2l_madd", pat=r"f2l_sub<(\d+), (\d+)>") == sorted(
+        [k["2A_H"], k["2A_R"], k["2A_X"], k["2A_W"], k["2A_Y"]])
+    assert used("HD F2L f2l_sqr") == [k["2Q"]]
+    assert re.search(r"kF2N = k28_make\((\d+), (\d+)\)", src).groups() == tuple(map(str, k["2N"]))
     kp = [int(x, 16) for x in re.search(r"kP28_\[14\] = \{([^}]*)\}", src).group(1).replace("u", "").split(",")]
     assert kp == lazy28.P28
 
@@ -84,3 +107,35 @@ def test_g1_subgroup_lazy_matches(lib):
             pts += [t, B.g1_add(t, B.g1_mul(B.G1_GEN, rng.randrange(1, B.R)))]
     fpm = [_check(lib, p) for p in pts]
     assert max(fpm) <= 1040  # two 63-step ladders: 126 doublings x 7 + 5 x 11 + 5 x 16 + phi/eq 8
+
+
+def _random_twist_point(rng):
+    while True:
+        x = (rng.randrange(B.P), rng.randrange(B.P))
+        y = B.f2_sqrt(B.f2_add(B.f2_mul(B.f2_sqr(x), x), B.B_G2))
+        if y is not None:
+            return (x, y)
+
+
+def _check2(lib, pt):
+    out = (ctypes.c_int * 3)()
+    (x0, x1), (y0, y1) = pt
+    raw = b"".join(v.to_bytes(48, "big") for v in (x0, x1, y0, y1))
+    lib.hc_g2_subgroup2(raw, out)
+    want = B.g2_in_subgroup(pt)
+    assert out[0] == want and out[1] == want, (out[0], out[1], want)
+    return out[2]
+
+
+def test_g2_subgroup_lazy_matches(lib):
+    """subgroup points, random twist points (not in G2) and the committed off-subgroup fixture"""
+    import json
+    lib.hc_g2_subgroup2.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]
+    rng = random.Random(282)
+    pts = [B.G2_GEN, B.g2_neg(B.G2_GEN)] + [B.g2_mul(B.G2_GEN, rng.randrange(1, B.R)) for _ in range(3)]
+    pts += [_random_twist_point(rng) for _ in range(6)]
+    with open(os.path.join(ROOT, "tests", "golden", "off_subgroup_g2.json")) as f:
+        for h in json.load(f)["points"][:4]:
+            pts.append(B.g2_decompress(bytes.fromhex(h), subgroup_check=False))
+    fpm = [_check2(lib, p) for p in pts]
+    assert max(fpm) <= 1250  # 63 doublings x 17 + 5 mixed additions x 30 + psi / eq
