@@ -123,8 +123,28 @@ HD L28 l_sqr(const L28& a) {
 }
 #endif
 
-// a mod p == 0: the Montgomery product by the integer 1 is a R^-1 mod p and lies in [0, p]
-HD bool l_is_zero(const L28& a) {
+// a == 0 mod p for a NORMALISED value a < 2^392 without a product: a is k p only for
+// k = rint(a / p), read off the top 56 bits (the low 336 bits of p move the ratio by < 2^-38 for
+// the k < 2^20 of any lazy value), then one pass compares a with k p limb by limb
+constexpr double kInvPTop = 1.0 / (double)(((uint64_t)0x0001a011u << 28) | 0x01ea397fu);  // 1 / (p >> 336)
+HD bool l_is_zero_n(const L28& a) {
+  const double top = (double)a.l[13] * 268435456.0 + (double)a.l[12];
+  const uint32_t k = (uint32_t)__builtin_rint(top * kInvPTop);
+  uint64_t c = 0;
+  uint32_t diff = 0;
+  HB_UNROLL for (int i = 0; i < 13; i++) {
+    c += (uint64_t)k * kP28_[i];
+    diff |= ((uint32_t)c & 0x0FFFFFFFu) ^ a.l[i];
+    c >>= 28;
+  }
+  c += (uint64_t)k * kP28_[13];
+  diff |= (uint32_t)c ^ a.l[13];
+  return diff == 0;
+}
+HD bool l_is_zero(const L28& a) { return l_is_zero_n(l_norm(a)); }
+// reference form of the same test (the Montgomery product by the integer 1 is a R^-1 mod p and
+// lies in [0, p]), for tests/test_lazy28.py
+HD bool l_is_zero_mul(const L28& a) {
   L28 one;
   one.l[0] = 1;
   HB_UNROLL for (int i = 1; i < 14; i++) one.l[i] = 0;
@@ -397,6 +417,26 @@ HDNI G2L g2l_madd(const G2L& p, const F2L& x2, const F2L& y2) {
   r.Z = f2l_mul(f2l_shl(p.Z, 1), H);
   r.inf = false;
   return r;
+}
+
+// sum_i [a_i] T_i1 + [b_i] T_i2 over a chunk, the joint 32-step ladder of vbatch.hip k_rlc_msm in
+// lazy limbs: tab[3i + s - 1] is the affine point (Z = 1 record) added for bit pair s = a_i | 2 b_i
+// (T_i1, T_i2, T_i1 + T_i2); the same group element as its stored-word msm_ladder<Fp, true>
+template <class Pair>  // uint2 on the device
+HD G1J g1l_msm_ladder(const G1J* __restrict__ tab, const Pair* __restrict__ coef, uint32_t first, uint32_t cnt) {
+  G1L R = g1l_infinity();
+  HB_NOUNROLL for (int bit = 31; bit >= 0; bit--) {
+    R = g1l_dbl(R);
+    HB_NOUNROLL for (uint32_t k = 0; k < cnt; k++) {
+      const uint32_t i = first + k;
+      const Pair ab = coef[i];
+      const uint32_t sel = ((ab.x >> bit) & 1u) | (((ab.y >> bit) & 1u) << 1);
+      const G1J T = tab[3ull * i + (sel ? sel - 1u : 0u)];
+      const G1L S = g1l_madd(R, l_from(T.X), l_from(T.Y));
+      if (sel) R = S;
+    }
+  }
+  return g1l_to_jac(R);
 }
 
 // Q in G2  <=>  psi(Q) == [x] Q (ec.h g2_in_subgroup), the ladder in lazy limbs.  `load` returns

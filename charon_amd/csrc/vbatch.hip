@@ -360,7 +360,7 @@ __global__ KB_OCC(HB_OCC_RLC) void k_rlc_msm(RlcMsmArgs a) {
       a.t1[3ull * i] = J1;
       a.t1[3ull * i + 2] = {fp_mul(J3.X, zi2), fp_mul(J3.Y, fp_mul(zi2, zi)), fp_one()};
     }
-    const G1J rp = msm_ladder<Fp, true>(a.t1, a.coef, first, cnt);
+    const G1J rp = HB_G1_LAZY ? g1l_msm_ladder(a.t1, a.coef, first, cnt) : msm_ladder<Fp, true>(a.t1, a.coef, first, cnt);
     a.pout[first] = {rp.X, rp.Y, rp.Z};
     const G1J zi = jac_infinity<Fp>();
     for (uint32_t k = 1; k < cnt; k++) a.pout[first + k] = {zi.X, zi.Y, zi.Z};

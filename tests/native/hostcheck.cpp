@@ -529,3 +529,36 @@ extern "C" int hc_g2_subgroup2(const uint8_t* xy192, int* out) {
   out[2] = (int)g_cnt_fp_mul;
   return 0;
 }
+
+// ec28.h zero tests on a 14-limb value: out[0] = l_is_zero (carries + k p comparison),
+// out[1] = l_is_zero_mul (the Montgomery product by 1)
+extern "C" int hc_l28_is_zero(const uint32_t* limbs, int* out) {
+  L28 a;
+  for (int i = 0; i < 14; i++) a.l[i] = limbs[i];
+  out[0] = l_is_zero(a) ? 1 : 0;
+  out[1] = l_is_zero_mul(a) ? 1 : 0;
+  return 0;
+}
+
+// sum over k items of [a_i + b_i lambda] pk_i through ec28.h's lazy chunk ladder (the table built
+// as vbatch.hip k_rlc_msm builds it: P, phi(P), P + phi(P) affine), compressed
+extern "C" int hc_rlc_sum_g1_lazy(int k, const uint8_t* pks, const uint32_t* ab, uint8_t* out48) {
+  struct Pair {
+    uint32_t x, y;
+  };
+  G1J tab[3 * 64];
+  Pair coef[64];
+  if (k > 64) return 1;
+  for (int i = 0; i < k; i++) {
+    G1A p;
+    if (g1_decompress(p, pks + 48 * i)) return 1;
+    const G1A p2 = {fp_mul(p.x, fp_from_const(G1_BETA)), p.y, false};
+    const G1A p3 = jac_to_aff(jac_add_aff(jac_from_aff(p), p2));
+    tab[3 * i] = jac_from_aff(p);
+    tab[3 * i + 1] = jac_from_aff(p2);
+    tab[3 * i + 2] = jac_from_aff(p3);
+    coef[i] = {ab[2 * i], ab[2 * i + 1]};
+  }
+  g1_compress(out48, jac_to_aff(g1l_msm_ladder(tab, coef, 0, (uint32_t)k)));
+  return 0;
+}

@@ -139,3 +139,56 @@ def test_g2_subgroup_lazy_matches(lib):
             pts.append(B.g2_decompress(bytes.fromhex(h), subgroup_check=False))
     fpm = [_check2(lib, p) for p in pts]
     assert max(fpm) <= 1250  # 63 doublings x 17 + 5 mixed additions x 30 + psi / eq
+
+
+def test_zero_test(lib):
+    """l_is_zero (no product) agrees with the Montgomery-product form and with v % p on multiples
+    of p up to 64 p, their neighbours, random values and lazy (uncarried) limb layouts"""
+    lib.hc_l28_is_zero.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_int)]
+    rng = random.Random(2828)
+    vals = []
+    for k in range(65):
+        for d in (0, 1, -1, 1 << 336, -(1 << 336), 1 << 200, rng.randrange(1, 1 << 300)):
+            v = k * B.P + d
+            if 0 <= v < (1 << 391):
+                vals.append(v)
+    vals += [rng.randrange(1 << 391) for _ in range(200)]
+    for v in vals:
+        limbs = lazy28.limbs28(v)
+        layouts = [limbs]
+        j = rng.randrange(13)  # the same value with a borrowed carry: limb j + 2^28, limb j+1 - 1
+        if limbs[j + 1] > 0:
+            l2 = list(limbs)
+            l2[j] += 1 << 28
+            l2[j + 1] -= 1
+            layouts.append(l2)
+        for lb in layouts:
+            out = (ctypes.c_int * 2)()
+            lib.hc_l28_is_zero((ctypes.c_uint32 * 14)(*lb), out)
+            assert out[0] == out[1] == (v % B.P == 0), (v, lb, out[0], out[1])
+
+
+def test_rlc_chunk_ladder_lazy(lib):
+    """ec28.h g1l_msm_ladder (k_rlc_msm's G1 chunk ladder): sum [a_i + b_i lambda] P_i over chunks
+    of 1, 2, 10 and 11 keys, including repeated keys and coefficients whose ladder meets +-T
+    (equal keys, all-ones, single bits), against the oracle"""
+    lib.hc_rlc_sum_g1_lazy.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint32), ctypes.c_char_p]
+    lam = (-B.X_PARAM ** 2) % B.R
+    rng = random.Random(2829)
+    keys = [B.g1_mul(B.G1_GEN, rng.randrange(1, B.R)) for _ in range(6)]
+    cases = []
+    for k in (1, 2, 10, 11):
+        pts = [keys[rng.randrange(len(keys))] for _ in range(k)]
+        cases.append((pts, [(rng.getrandbits(32), rng.getrandbits(32)) for _ in range(k)]))
+    cases.append(([keys[0]] * 4, [(1, 0), (1, 0), (0xFFFFFFFF, 0), (0, 1)]))   # R meets T: doubling
+    cases.append(([keys[1], B.g1_neg(keys[1])], [(5, 0), (5, 0)]))             # sum is infinity
+    cases.append(([keys[2]] * 3, [(0xFFFFFFFF, 0xFFFFFFFF)] * 3))
+    for pts, ab in cases:
+        buf = b"".join(B.g1_compress(p) for p in pts)
+        flat = (ctypes.c_uint32 * (2 * len(ab)))(*[x for pair in ab for x in pair])
+        out = ctypes.create_string_buffer(48)
+        assert lib.hc_rlc_sum_g1_lazy(len(pts), buf, flat, out) == 0
+        want = None
+        for p, (a, b) in zip(pts, ab):
+            want = B.g1_add(want, B.g1_mul(p, (a + b * lam) % B.R))
+        assert out.raw == B.g1_compress(want)
