@@ -439,6 +439,56 @@ HD G1J g1l_msm_ladder(const G1J* __restrict__ tab, const Pair* __restrict__ coef
   return g1l_to_jac(R);
 }
 
+// lazy28.py jadd2: add-2007-bl as g1l_add with H normalised (its square is an Fp2 square)
+HDNI G2L g2l_add(const G2L& p, const G2L& q) {
+  if (p.inf) return q;
+  if (q.inf) return p;
+  const F2L Z1Z1 = f2l_sqr(p.Z), Z2Z2 = f2l_sqr(q.Z);
+  const F2L U1 = f2l_mul(p.X, Z2Z2), U2 = f2l_mul(q.X, Z1Z1);
+  const F2L S1 = f2l_mul(f2l_mul(p.Y, q.Z), Z2Z2);
+  const F2L S2 = f2l_mul(f2l_mul(q.Y, p.Z), Z1Z1);
+  const F2L H = f2l_norm(f2l_sub<2, 1>(U2, U1));
+  const F2L rr = f2l_norm(f2l_sub<3, 2>(f2l_shl(S2, 1), f2l_shl(S1, 1)));
+  if (f2l_is_zero(H)) {
+    if (f2l_is_zero(rr)) return g2l_dbl(p);
+    return g2l_infinity();
+  }
+  const F2L HH = f2l_sqr(H);
+  const F2L J1 = f2l_mul(H, HH), V1 = f2l_mul(U1, HH);
+  G2L r;
+  r.X = f2l_norm(f2l_sub<13, 12>(f2l_sqr(rr), f2l_add(f2l_shl(J1, 2), f2l_shl(V1, 3))));
+  r.Y = f2l_norm(
+      f2l_sub<9, 8>(f2l_mul(f2l_sub<15, 1>(f2l_shl(V1, 2), r.X), rr), f2l_shl(f2l_mul(S1, J1), 3)));
+  r.Z = f2l_mul(f2l_mul(f2l_shl(p.Z, 1), q.Z), H);
+  r.inf = false;
+  return r;
+}
+
+HD G2L g2l_from_jac(const G2J& p) {
+  return {f2l_from(p.X), f2l_from(p.Y), f2l_from(p.Z), f2_is_zero(p.Z)};
+}
+HD G2J g2l_to_jac(const G2L& p) {
+  if (p.inf) return jac_infinity<Fp2>();
+  return {f2l_to(p.X), f2l_to(p.Y), f2l_to(p.Z)};
+}
+
+// [|x|] P for a Jacobian P in stored words (ec.h jac_mul_by_xabs), the ladder in lazy limbs;
+// `load` returns P again at each of the five additions (not held across the product calls)
+template <class LoadP>
+HDNI G2J g2l_mul_by_xabs_l(const LoadP& load) {
+  G2L t = g2l_from_jac(load());
+  HB_NOUNROLL for (int i = 62; i >= 0; i--) {
+    t = g2l_dbl(t);
+    if ((HB_X_ABS >> i) & 1) {
+#if defined(__HIP_DEVICE_COMPILE__)
+      __asm__ volatile("" ::: "memory");
+#endif
+      t = g2l_add(t, g2l_from_jac(load()));
+    }
+  }
+  return g2l_to_jac(t);
+}
+
 // Q in G2  <=>  psi(Q) == [x] Q (ec.h g2_in_subgroup), the ladder in lazy limbs.  `load` returns
 // Q again at each of the five mixed additions instead of the ladder holding its 56 limbs across
 // every product call (the kernel re-reads its entry; LICM is kept from hoisting that read)

@@ -318,7 +318,8 @@ def per_unit(b=BLOCKS, group_size=1, t=1):
         "k_fb_lines": (b["lines_eval"],) * 2,
         "k_ta_straus": (ta_msm(b, 1),) * 2,  # one ladder per member (HBLS_TA_MSM off)
         "k_group_sum": (gsum,) * 2,
-        "k_hash_to_g2": (HASH_TO_G2,) * 2,
+        # the two cofactor ladders in lazy limbs (ec28.h): one product more per doubling / addition
+        "k_hash_to_g2": (HASH_TO_G2, HASH_TO_G2 + 2 * G2_DEC_LAZY_EXTRA),
         "k_lines_msg": (b["lines_uneval"],) * 2,
         # VerifyAggregate at scale (vbatch.hip): per key one mixed addition in pass 1 (later passes
         # add 1/32 as many Jacobian partials), per group the affine sum and the signature's lines

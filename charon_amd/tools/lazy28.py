@@ -202,6 +202,7 @@ KSITE = {
     "1A_H": (21, 1), "1A_R": (41, 2), "1A_X": (13, 12), "1A_W": (15, 1), "1A_Y": (9, 8),
     "2D_X": (9, 8), "2D_W": (11, 1), "2D_Y": (9, 8),
     "2A_H": (17, 1), "2A_R": (33, 2), "2A_X": (13, 12), "2A_W": (16, 1), "2A_Y": (9, 8),
+    "2J_H": (2, 1), "2J_R": (3, 2), "2J_X": (13, 12), "2J_W": (15, 1), "2J_Y": (9, 8),
     "2N": (33, 6), "2Q": (36, 1),
 }
 
@@ -297,6 +298,25 @@ def madd2(F, X1, Y1, Z1, x2, y2):
     return X3, Y3, Z3
 
 
+def jadd2(F, X1, Y1, Z1, X2, Y2, Z2):
+    """g2l_add: add-2007-bl as jadd() with H normalised (its square is an Fp2 square)"""
+    Z1Z1 = F.sqr(Z1)
+    Z2Z2 = F.sqr(Z2)
+    U1 = F.mul(X1, Z2Z2)
+    U2 = F.mul(X2, Z1Z1)
+    S1 = F.mul(F.mul(Y1, Z2), Z2Z2)
+    S2 = F.mul(F.mul(Y2, Z1), Z1Z1)
+    H = F.norm(F.sub(U2, U1, "J_H"))
+    rr = F.norm(F.sub(F.shl(S2, 1), F.shl(S1, 1), "J_R"))
+    HH = F.sqr(H)
+    J1 = F.mul(H, HH)
+    V1 = F.mul(U1, HH)
+    X3 = F.norm(F.sub(F.sqr(rr), F.add(F.shl(J1, 2), F.shl(V1, 3)), "J_X"))
+    Y3 = F.norm(F.sub(F.mul(F.sub(F.shl(V1, 2), X3, "J_W"), rr), F.shl(F.mul(S1, J1), 3), "J_Y"))
+    Z3 = F.mul(F.mul(F.shl(Z1, 1), Z2), H)
+    return X3, Y3, Z3
+
+
 def fits(x, vmax):
     return vmax_of(x) <= vmax and all(
         all(l <= M28 for l in b.lb[:13]) and b.lb[13] <= (vmax >> 364) for b in ([x] if isinstance(x, Bound) else x))
@@ -315,7 +335,8 @@ def check(vmax, fields=("Fp", "Fp2")):
         ops = (("dbl", lambda: dbl(F, X, Y, Z)), ("madd", lambda: madd(F, X, Y, Z, aff, aff)),
                ("add", lambda: jadd(F, X, Y, Z, X, Y, Z)))
         if name == "Fp2":
-            ops = (("dbl", lambda: dbl2(F, X, Y, Z)), ("madd", lambda: madd2(F, X, Y, Z, aff, aff)))
+            ops = (("dbl", lambda: dbl2(F, X, Y, Z)), ("madd", lambda: madd2(F, X, Y, Z, aff, aff)),
+                   ("add", lambda: jadd2(F, X, Y, Z, X, Y, Z)))
         for op, fn in ops:
             res = fn()
             for c in res:

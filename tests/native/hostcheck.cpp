@@ -562,3 +562,21 @@ extern "C" int hc_rlc_sum_g1_lazy(int k, const uint8_t* pks, const uint32_t* ab,
   g1_compress(out48, jac_to_aff(g1l_msm_ladder(tab, coef, 0, (uint32_t)k)));
   return 0;
 }
+
+// [|x|] P both ways for a Jacobian G2 point given as the affine point (x0 x1 y0 y1, big-endian)
+// scaled by z = (z0, z1) (z = 0: infinity): out96x2 = compressed results of ec.h jac_mul_by_xabs
+// and ec28.h g2l_mul_by_xabs_l
+extern "C" int hc_g2_mul_xabs2(const uint8_t* xyz288, uint8_t* out192) {
+  Fp w[6];
+  for (int i = 0; i < 6; i++) {
+    Fp r;
+    fp_from_be_raw(r, xyz288 + 48 * i);
+    w[i] = fp_to_mont(r);
+  }
+  const Fp2 x = {w[0], w[1]}, y = {w[2], w[3]}, z = {w[4], w[5]};
+  const Fp2 z2 = f2_sqr(z);
+  const G2J P = {f2_mul(x, z2), f2_mul(y, f2_mul(z2, z)), z};
+  g2_compress(out192, jac_to_aff(jac_mul_by_xabs(P)));
+  g2_compress(out192 + 96, jac_to_aff(g2l_mul_by_xabs_l([&]() { return P; })));
+  return 0;
+}

@@ -59,6 +59,8 @@ def test_constants_match_ec28():
     assert used("HDNI G2L g2l_dbl", pat=r"f2l_sub<(\d+), (\d+)>") == sorted([k["2D_X"], k["2D_W"], k["2D_Y"]])
     assert used("HDNI G2L g2l_madd", pat=r"f2l_sub<(\d+), (\d+)>") == sorted(
         [k["2A_H"], k["2A_R"], k["2A_X"], k["2A_W"], k["2A_Y"]])
+    assert used("HDNI G2L g2l_add", pat=r"f2l_sub<(\d+), (\d+)>") == sorted(
+        [k["2J_H"], k["2J_R"], k["2J_X"], k["2J_W"], k["2J_Y"]])
     assert used("HD F2L f2l_sqr") == [k["2Q"]]
     assert re.search(r"kF2N = k28_make\((\d+), (\d+)\)", src).groups() == tuple(map(str, k["2N"]))
     kp = [int(x, 16) for x in re.search(r"kP28_\[14\] = \{([^}]*)\}", src).group(1).replace("u", "").split(",")]
@@ -192,3 +194,20 @@ def test_rlc_chunk_ladder_lazy(lib):
         for p, (a, b) in zip(pts, ab):
             want = B.g1_add(want, B.g1_mul(p, (a + b * lam) % B.R))
         assert out.raw == B.g1_compress(want)
+
+
+def test_g2_xabs_ladder_lazy(lib):
+    """ec28.h g2l_mul_by_xabs_l (the hash's cofactor ladders, general Jacobian additions) against
+    ec.h jac_mul_by_xabs and the oracle, on random twist points with random Z, subgroup points and
+    infinity"""
+    lib.hc_g2_mul_xabs2.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+    rng = random.Random(2830)
+    pts = [_random_twist_point(rng) for _ in range(4)] + [B.G2_GEN, B.g2_mul(B.G2_GEN, 12345)]
+    for pt in pts + [None]:
+        (x0, x1), (y0, y1) = pt if pt else ((0, 0), (1, 0))
+        z = (rng.randrange(B.P), rng.randrange(B.P)) if pt else (0, 0)
+        raw = b"".join(v.to_bytes(48, "big") for v in (x0, x1, y0, y1) + z)
+        out = ctypes.create_string_buffer(192)
+        assert lib.hc_g2_mul_xabs2(raw, out) == 0
+        want = B.g2_compress(B.g2_mul(pt, -B.X_PARAM)) if pt else B.g2_compress(None)
+        assert out.raw[:96] == want and out.raw[96:] == want
