@@ -726,6 +726,9 @@ __global__ KB_OCC(HB_OCC_STRAUS) void k_ta_stab(const G2JEntry* __restrict__ q, 
 
 // One lane per validator of a wave k_ta_small took: [s] Q over Q's tables (k_ta_jladder's schedule
 // for one member), into the validator's first member slot of `out`, infinity into the others.
+#ifndef HB_TA_LAZY
+#define HB_TA_LAZY 1  // k_ta_sladder's ladder in ec28.h lazy limbs (0: stored words, A/B runs)
+#endif
 __global__ KB_OCC(HB_OCC_STRAUS) void k_ta_sladder(const TaDigits* __restrict__ sdig, const uint8_t* __restrict__ done,
                                                       uint32_t n_groups, uint32_t t, uint4* __restrict__ tab,
                                                       G2JEntry* __restrict__ out) {
@@ -746,21 +749,36 @@ __global__ KB_OCC(HB_OCC_STRAUS) void k_ta_sladder(const TaDigits* __restrict__ 
   }
   __syncthreads();
   const uint4* wt = tab + (size_t)blockIdx.x * 16 * TA_TAB_QUADS * 64 + lane;
+#if HB_TA_LAZY
+  G2L RL = g2l_infinity();  // the ladder in lazily reduced 28-bit limbs (ec28.h)
+#else
   G2J R = jac_infinity<Fp2>();
+#endif
   const int top = naf_top;
   HB_NOUNROLL for (int i = top; i >= 0; i--) {
+#if HB_TA_LAZY
+    RL = g2l_dbl(RL);
+#else
     R = jac_dbl(R);
+#endif
     HB_NOUNROLL for (int b = 0; b < 4; b++) {
       const int dg = naf[b][i];
       if (dg != 0) {  // wave-uniform
         const int e = 4 * b + ((dg < 0 ? -dg : dg) >> 1);
         G2A T = {f2_load_q(wt, e, 0), f2_load_q(wt, e, 6), false};
         if (dg < 0) T.y = f2_neg(T.y);
+#if HB_TA_LAZY
+        RL = g2l_madd(RL, f2l_from(T.x), f2l_from(T.y));
+#else
         R = jac_add_aff(R, T);
+#endif
       }
     }
   }
   if (!valid) return;
+#if HB_TA_LAZY
+  G2J R = g2l_to_jac(RL);
+#endif
   if (dn == 2) R = jac_infinity<Fp2>();
   out[(size_t)v * t] = {R.X, R.Y, R.Z};
   const G2J z = jac_infinity<Fp2>();
