@@ -489,6 +489,25 @@ HDNI G2J g2l_mul_by_xabs_l(const LoadP& load) {
   return g2l_to_jac(t);
 }
 
+// the G2 twin of g1l_msm_ladder (k_rlc_msm's per-group signature side): tab[3i + s - 1] affine
+template <class Pair>
+HD G2J g2l_msm_ladder(const G2J* __restrict__ tab, const Pair* __restrict__ coef, uint32_t first, uint32_t cnt) {
+  G2L R = g2l_infinity();
+  HB_NOUNROLL for (int bit = 31; bit >= 0; bit--) {
+    R = g2l_dbl(R);
+    HB_NOUNROLL for (uint32_t k = 0; k < cnt; k++) {
+      const uint32_t i = first + k;
+      const Pair ab = coef[i];
+      const uint32_t sel = ((ab.x >> bit) & 1u) | (((ab.y >> bit) & 1u) << 1);
+      if (sel) {
+        const G2J T = tab[3ull * i + sel - 1u];
+        R = g2l_madd(R, f2l_from(T.X), f2l_from(T.Y));
+      }
+    }
+  }
+  return g2l_to_jac(R);
+}
+
 // Q in G2  <=>  psi(Q) == [x] Q (ec.h g2_in_subgroup), the ladder in lazy limbs.  `load` returns
 // Q again at each of the five mixed additions instead of the ladder holding its 56 limbs across
 // every product call (the kernel re-reads its entry; LICM is kept from hoisting that read)

@@ -394,7 +394,7 @@ __global__ KB_OCC(HB_OCC_RLC) void k_rlc_msm(RlcMsmArgs a) {
     a.t2[3ull * i] = J1;
     a.t2[3ull * i + 2] = {f2_mul(J3.X, zi2), f2_mul(J3.Y, f2_mul(zi2, zi)), f2_one()};
   }
-  const G2J rs = msm_ladder<Fp2, true>(a.t2, a.coef, first, cnt);
+  const G2J rs = HB_G2_LAZY ? g2l_msm_ladder(a.t2, a.coef, first, cnt) : msm_ladder<Fp2, true>(a.t2, a.coef, first, cnt);
   a.sout[first] = {rs.X, rs.Y, rs.Z};
   const G2J zs = jac_infinity<Fp2>();
   for (uint32_t k = 1; k < cnt; k++) a.sout[first + k] = {zs.X, zs.Y, zs.Z};

@@ -580,3 +580,26 @@ extern "C" int hc_g2_mul_xabs2(const uint8_t* xyz288, uint8_t* out192) {
   g2_compress(out192 + 96, jac_to_aff(g2l_mul_by_xabs_l([&]() { return P; })));
   return 0;
 }
+
+// sum over k items of [a_i + b_i lambda] S_i (G2) through ec28.h's lazy chunk ladder, the table
+// as k_rlc_msm builds it (S, -psi^2(S), S - psi^2(S) affine), compressed
+extern "C" int hc_rlc_sum_g2_lazy(int k, const uint8_t* sigs, const uint32_t* ab, uint8_t* out96) {
+  struct Pair {
+    uint32_t x, y;
+  };
+  G2J tab[3 * 64];
+  Pair coef[64];
+  if (k > 64) return 1;
+  for (int i = 0; i < k; i++) {
+    G2A p;
+    if (g2_decompress(p, sigs + 96 * i)) return 1;
+    const G2A p2 = {f2_mul(p.x, f2_from_const(PSI2_CX)), f2_neg(f2_mul(p.y, f2_from_const(PSI2_CY))), false};
+    const G2A p3 = jac_to_aff(jac_add_aff(jac_from_aff(p), p2));
+    tab[3 * i] = jac_from_aff(p);
+    tab[3 * i + 1] = jac_from_aff(p2);
+    tab[3 * i + 2] = jac_from_aff(p3);
+    coef[i] = {ab[2 * i], ab[2 * i + 1]};
+  }
+  g2_compress(out96, jac_to_aff(g2l_msm_ladder(tab, coef, 0, (uint32_t)k)));
+  return 0;
+}

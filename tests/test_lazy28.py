@@ -211,3 +211,24 @@ def test_g2_xabs_ladder_lazy(lib):
         assert lib.hc_g2_mul_xabs2(raw, out) == 0
         want = B.g2_compress(B.g2_mul(pt, -B.X_PARAM)) if pt else B.g2_compress(None)
         assert out.raw[:96] == want and out.raw[96:] == want
+
+
+def test_rlc_chunk_ladder_g2_lazy(lib):
+    """ec28.h g2l_msm_ladder (k_rlc_msm's per-group signature side) against the oracle, incl. equal
+    points (the ladder meets T) and a sum at infinity"""
+    lib.hc_rlc_sum_g2_lazy.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint32), ctypes.c_char_p]
+    lam = (-B.X_PARAM ** 2) % B.R
+    rng = random.Random(2831)
+    pts_all = [B.g2_mul(B.G2_GEN, rng.randrange(1, B.R)) for _ in range(4)]
+    cases = [([pts_all[rng.randrange(4)] for _ in range(7)], [(rng.getrandbits(32), rng.getrandbits(32)) for _ in range(7)]),
+             ([pts_all[0]] * 3, [(1, 0), (1, 0), (0, 1)]),
+             ([pts_all[1], B.g2_neg(pts_all[1])], [(9, 0), (9, 0)])]
+    for pts, ab in cases:
+        buf = b"".join(B.g2_compress(p) for p in pts)
+        flat = (ctypes.c_uint32 * (2 * len(ab)))(*[x for pair in ab for x in pair])
+        out = ctypes.create_string_buffer(96)
+        assert lib.hc_rlc_sum_g2_lazy(len(pts), buf, flat, out) == 0
+        want = None
+        for p, (a, b) in zip(pts, ab):
+            want = B.g2_add(want, B.g2_mul(p, (a + b * lam) % B.R))
+        assert out.raw == B.g2_compress(want)
