@@ -79,13 +79,13 @@ HD L28 l_from(const Fp& a) {
 }
 
 #if defined(__HIP_DEVICE_COMPILE__)
+// (lanes 14, 15 of the argument vectors are left undefined: no moves for them around the call)
 HD L28 l_mul_nc(const L28& a, const L28& b) {  // not counted: membership / conversion helpers
   u32x16 x, y;
   HB_UNROLL for (int i = 0; i < 14; i++) {
     x[i] = a.l[i];
     y[i] = b.l[i];
   }
-  x[14] = x[15] = y[14] = y[15] = 0;
   const u32x16 o = fp_mul28_leaf(x, y);
   L28 r;
   HB_UNROLL for (int i = 0; i < 14; i++) r.l[i] = o[i];
@@ -99,7 +99,6 @@ HD L28 l_sqr(const L28& a) {
   HB_COUNT_FP_MUL();
   u32x16 x;
   HB_UNROLL for (int i = 0; i < 14; i++) x[i] = a.l[i];
-  x[14] = x[15] = 0;
   const u32x16 o = fp_sqr28_leaf(x);
   L28 r;
   HB_UNROLL for (int i = 0; i < 14; i++) r.l[i] = o[i];
@@ -326,7 +325,6 @@ __device__ __noinline__ static u32x32 f2l_mul_leaf(u32x32 a) {
     o[k] = r0[k];
     o[16 + k] = r1[k];
   }
-  o[14] = o[15] = o[30] = o[31] = 0;
   return o;
 }
 HD F2L f2l_mul(const F2L& a, const F2L& b) {
@@ -340,7 +338,6 @@ HD F2L f2l_mul(const F2L& a, const F2L& b) {
     av[16 + k] = a.c1.l[k];
     hb_fp2_arg[k * HB_ARG_LANES + lane] = make_uint2(b.c0.l[k], b.c1.l[k]);
   }
-  av[14] = av[15] = av[30] = av[31] = 0;
   const u32x32 o = f2l_mul_leaf(av);
   F2L r;
   HB_UNROLL for (int k = 0; k < 14; k++) {

@@ -494,7 +494,6 @@ __device__ __noinline__ static u32x16 fp_mul28_leaf(u32x16 a, u32x16 b) {
   fp_mul28_core(r, x, y);
   u32x16 o;
   HB_UNROLL for (int i = 0; i < 14; i++) o[i] = r[i];
-  o[14] = o[15] = 0;
   return o;
 }
 __device__ __noinline__ static u32x16 fp_sqr28_leaf(u32x16 a) {
@@ -503,7 +502,6 @@ __device__ __noinline__ static u32x16 fp_sqr28_leaf(u32x16 a) {
   fp_sqr28_core(r, x);
   u32x16 o;
   HB_UNROLL for (int i = 0; i < 14; i++) o[i] = r[i];
-  o[14] = o[15] = 0;
   return o;
 }
 struct Fp28 {
