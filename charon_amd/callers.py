@@ -34,7 +34,7 @@ from __future__ import annotations
 from dataclasses import dataclass
 from typing import Dict, List, Mapping, Optional, Sequence, Tuple
 
-from .tbls import TblsError, _TA_ERR, _VERIFY_AGG_ERR, _VERIFY_ERR
+from .tbls import TblsError, status_error
 
 OK = 0
 ZERO_SIG = bytes(96)
@@ -50,7 +50,7 @@ def _wrap(outer: str, inner: str) -> CallerError:
 
 
 def _verr(st: int) -> str:
-    return _VERIFY_ERR.get(st, "signature not verified")
+    return status_error("verify", st)
 
 
 @dataclass
@@ -126,7 +126,7 @@ def sigagg_aggregate(impl, threshold: int, dv_pubkeys: Mapping[bytes, bytes],
                                          [outs[k] for k in ok]))) if ok else {}
     for k in range(len(done)):
         if sts[k] != OK:
-            raise _wrap("threshold aggregate", _TA_ERR.get(sts[k], "cannot combine signatures"))
+            raise _wrap("threshold aggregate", status_error("threshold_aggregate", sts[k]))
         if vst[k] != OK:
             raise _wrap("threshold aggregate", "aggregate signature verification failed: " + _verr(vst[k]))
     if pre is not None:
@@ -167,7 +167,7 @@ def lock_verify_signatures(impl, public_shares: Sequence[bytes], signature_aggre
     validator's every public share against the lock hash."""
     st = impl.verify_aggregate_batch([list(public_shares)], [signature_aggregate], [lock_hash])[0]
     if st != OK:
-        raise _wrap("verify lock signature aggregate", _VERIFY_AGG_ERR.get(st, "signature verification failed"))
+        raise _wrap("verify lock signature aggregate", status_error("verify_aggregate", st))
 
 
 def _dkg_partials(pubshares_by_dv, partials, roots, what: str, missing_msg: Optional[str],
@@ -215,7 +215,7 @@ def _dkg_threshold_aggregate(impl, pubshares_by_dv, partials, roots, what, missi
         if d >= complete:
             break
         if tst[d] != OK:
-            raise CallerError(_TA_ERR.get(tst[d], "cannot combine signatures"))
+            raise CallerError(status_error("threshold_aggregate", tst[d]))
         if ast[d] != OK:
             raise _wrap(agg_err, _verr(ast[d]))
     if pre is not None:
@@ -259,7 +259,7 @@ def dkg_agg_lock_hash_sig(impl, pubshares_by_dv: Mapping[bytes, Mapping[int, byt
         raise CallerError(pre)
     outs, sts = impl.aggregate_batch([[s for _, _, _, s in items]])
     if sts[0] != OK:
-        raise _wrap("bls aggregate Signatures", "cannot unmarshal signature into Herumi signature")
+        raise _wrap("bls aggregate Signatures", status_error("aggregate", sts[0]))
     return outs[0], [p for _, p, _, _ in items]
 
 
@@ -267,7 +267,7 @@ def dkg_verify_lock_multisig(impl, pubkeys: Sequence[bytes], agg_sig: bytes, loc
     """signAndAggLockHash's check of that aggregate (dkg.go:595-598)."""
     st = impl.verify_aggregate_batch([list(pubkeys)], [agg_sig], [lock_hash])[0]
     if st != OK:
-        raise _wrap("verify multisignature", _VERIFY_AGG_ERR.get(st, "signature verification failed"))
+        raise _wrap("verify multisignature", status_error("verify_aggregate", st))
 
 
 def exit_aggregate(impl, partial_sigs: Sequence[Optional[bytes]]) -> bytes:
@@ -282,7 +282,7 @@ def exit_aggregate(impl, partial_sigs: Sequence[Optional[bytes]]) -> bytes:
         group[i + 1] = s
     outs, sts = impl.threshold_aggregate_batch([group])
     if sts[0] != OK:
-        raise _wrap("partial signatures threshold aggregate", _TA_ERR.get(sts[0], "cannot combine signatures"))
+        raise _wrap("partial signatures threshold aggregate", status_error("threshold_aggregate", sts[0]))
     return outs[0]
 
 
@@ -293,18 +293,24 @@ def exit_aggregate_batch(impl, validators: Sequence[Tuple[str, Sequence[Optional
     fails aborts with "load full exit data from Obol API: partial signatures threshold aggregate:
     <error>"."""
     groups = []
-    for _, partial_sigs in validators:
+    pre: Optional[str] = None
+    for _, partial_sigs in validators:  # the length pre-check in lock order, up to the first failure
         group = {}
         for i, s in enumerate(partial_sigs):
             if not s:
                 continue
             if len(s) != 96:
-                raise _wrap("load full exit data from Obol API", _wrap("invalid partial signature", _LEN_ERR).args[0])
+                pre = _wrap("invalid partial signature", _LEN_ERR).args[0]
+                break
             group[i + 1] = s
+        if pre is not None:
+            break
         groups.append(group)
     outs, sts = impl.threshold_aggregate_batch(groups) if groups else ([], [])
-    for st in sts:
+    for st in sts:  # an earlier validator's aggregation error comes first (exit_fetch.go:122-132)
         if st != OK:
             raise _wrap("load full exit data from Obol API",
-                        "partial signatures threshold aggregate: " + _TA_ERR.get(st, "cannot combine signatures"))
+                        "partial signatures threshold aggregate: " + status_error("threshold_aggregate", st))
+    if pre is not None:
+        raise _wrap("load full exit data from Obol API", pre)
     return outs

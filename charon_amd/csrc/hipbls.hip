@@ -245,8 +245,10 @@ std::atomic<size_t> g_rlc_lanes{65536};   // HBLS_RLC_LANES: lanes the chunk siz
 // public-key cache: compressed key -> entry index (the same on every device).  Lock order: an
 // adder (or clear) takes g_kc_add_mu, then one Dev::mu at a time to fill that device's table, then
 // g_kc_mu to publish; verifications hold their Dev::mu and take g_kc_mu for the lookup.  g_kc_mu is
-// always the innermost lock, so adds and verifications never wait on each other in a cycle; a
-// lookup made under a Dev::mu stays valid while it is held (entries are only written under it).
+// always the innermost lock, so adds and verifications never wait on each other in a cycle.  A
+// lookup made under a Dev::mu stays valid for everything enqueued while it is held: entries are
+// only written under it, and kc_fill first waits for every launch already enqueued on the device
+// (which covers indices reused after hbls_pubkey_cache_clear).
 std::mutex g_kc_add_mu;
 std::mutex g_kc_mu;
 std::unordered_map<std::string, uint32_t> g_kc_map;
@@ -399,7 +401,14 @@ struct Dev {
 };
 
 std::mutex g_init_mu;
-std::vector<Dev*> g_devs;  // in device-mask order (hbls_debug_split: each ordinal repeated)
+std::vector<Dev*> g_devs;  // in device-mask order (hbls_debug_split: each ordinal repeated); g_devs_mu
+std::mutex g_devs_mu;      // hbls_debug_split swaps g_devs while calls may be in flight
+// a snapshot of g_devs: Dev objects are never freed (split contexts are pooled), so the pointers
+// stay valid after the lock is released
+std::vector<Dev*> devs() {
+  std::lock_guard<std::mutex> l(g_devs_mu);
+  return g_devs;
+}
 std::vector<Dev*> g_base_devs;   // one per device of the mask
 std::vector<std::vector<Dev*>> g_split_pool;  // per base device: extra contexts of hbls_debug_split (reused)
 uint32_t g_mask = 0;
@@ -560,7 +569,10 @@ int init_mask(uint32_t mask) {
       if (dev_create(k, &d)) return -1;
       devs.push_back(d);
     }
-  g_devs = devs;
+  {
+    std::lock_guard<std::mutex> l(g_devs_mu);
+    g_devs = devs;
+  }
   g_base_devs = devs;
   g_mask = mask;
   g_ready.store(true);
@@ -572,13 +584,14 @@ int ensure_init() { return g_ready.load() ? 0 : init_mask(0); }
 // the device of a caller's stream (device entry points); stream 0: the first device
 int dev_of_stream(hipStream_t s, Dev** out) {
   if (ensure_init()) return -1;
-  int ord = g_devs[0]->ord;
+  const std::vector<Dev*> ds = devs();
+  int ord = ds[0]->ord;
   if (s) {
     hipDevice_t dv;
     HCHK(hipStreamGetDevice(s, &dv));
     ord = (int)dv;
   }
-  for (Dev* d : g_devs)
+  for (Dev* d : ds)
     if (d->ord == ord) {
       HCHK(hipSetDevice(ord));
       *out = d;
@@ -1431,9 +1444,10 @@ int hash_table(Dev& d, const MsgTable& t, MsgEntry** hm_out, bool lines, Ws* w =
 
 // Run fn(dev, shard) for each device's shard concurrently (one host thread per extra device).
 int for_each_device(size_t n_units, const std::function<int(Dev&, size_t, size_t)>& fn) {
-  const size_t nd = std::min(g_devs.size(), std::max<size_t>(n_units, 1));
+  const std::vector<Dev*> ds = devs();
+  const size_t nd = std::min(ds.size(), std::max<size_t>(n_units, 1));
   if (nd <= 1) {
-    Dev& d = *g_devs[0];
+    Dev& d = *ds[0];
     std::lock_guard<std::mutex> lk(d.mu);
     if (hipSetDevice(d.ord) != hipSuccess) return set_err("hipSetDevice failed");
     return fn(d, 0, n_units);
@@ -1444,7 +1458,7 @@ int for_each_device(size_t n_units, const std::function<int(Dev&, size_t, size_t
   for (size_t k = 0; k < nd; k++) {
     const size_t b = n_units * k / nd, e = n_units * (k + 1) / nd;
     th.emplace_back([&, k, b, e]() {
-      Dev& d = *g_devs[k];
+      Dev& d = *ds[k];
       std::lock_guard<std::mutex> lk(d.mu);
       if (hipSetDevice(d.ord) != hipSuccess) {
         rc[k] = -1;
@@ -1457,7 +1471,7 @@ int for_each_device(size_t n_units, const std::function<int(Dev&, size_t, size_t
   }
   for (auto& t : th) t.join();
   for (size_t k = 0; k < nd; k++)
-    if (rc[k]) return set_err("device " + std::to_string(g_devs[k]->ord) + ": " + errs[k]);
+    if (rc[k]) return set_err("device " + std::to_string(ds[k]->ord) + ": " + errs[k]);
   return 0;
 }
 
@@ -1477,21 +1491,22 @@ int for_each_device_hc(size_t n_units, const HcFn& fn) {
     if (hipSetDevice(d.ord) != hipSuccess) return set_err("hipSetDevice failed");
     return fn(d, h, b, e, lk);
   };
-  const size_t nd = std::min(g_devs.size(), std::max<size_t>(n_units, 1));
-  if (nd <= 1) return run(*g_devs[0], 0, n_units);
+  const std::vector<Dev*> ds = devs();
+  const size_t nd = std::min(ds.size(), std::max<size_t>(n_units, 1));
+  if (nd <= 1) return run(*ds[0], 0, n_units);
   std::vector<int> rc(nd, 0);
   std::vector<std::string> errs(nd);
   std::vector<std::thread> th;
   for (size_t k = 0; k < nd; k++) {
     const size_t b = n_units * k / nd, e = n_units * (k + 1) / nd;
     th.emplace_back([&, k, b, e]() {
-      rc[k] = run(*g_devs[k], b, e);
+      rc[k] = run(*ds[k], b, e);
       if (rc[k]) errs[k] = g_err;
     });
   }
   for (auto& t : th) t.join();
   for (size_t k = 0; k < nd; k++)
-    if (rc[k]) return set_err("device " + std::to_string(g_devs[k]->ord) + ": " + errs[k]);
+    if (rc[k]) return set_err("device " + std::to_string(ds[k]->ord) + ": " + errs[k]);
   return 0;
 }
 
@@ -1503,6 +1518,10 @@ int for_each_device_hc(size_t n_units, const HcFn& fn) {
 // the entries before `first`).  Caller holds d.mu.
 int kc_fill(Dev& d, const uint8_t* keys, size_t first, size_t m) {
   HCHK(hipSetDevice(d.ord));
+  // launches enqueued earlier (on host-call or caller streams) may still read the table: let them
+  // finish before any entry is rewritten or the table moves.  No new reader can be enqueued
+  // meanwhile (they look indices up under d.mu, held here); cache adds are rare (cluster locks).
+  HCHK(hipDeviceSynchronize());
   const size_t tot = first + m;
   if (d.kc_tab.cap < tot * sizeof(G1AEntry) || d.kc_st.cap < tot) {  // grow, keeping the old entries
     DevBuf nt, ns;
@@ -1603,11 +1622,14 @@ int verify_host(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msgs, co
     }
     std::vector<uint32_t> goff(ge - gb + 1);
     for (size_t g = gb; g <= ge; g++) goff[g - gb] = (uint32_t)(gstart[g] - ib);
-    std::vector<uint32_t> kc;
-    const bool use_kc = whole ? kc_lookup(pks, m, kc, order32.data()) : kc_lookup(hpk.data(), m, kc);
     const double t_prep = now_ms();
     lk.lock();
     const double t_locked = now_ms();
+    // the key-cache lookup under Dev::mu: entries of d's table are only (re)written under it, after
+    // every launch that may still read them has completed (kc_fill), so the indices stay valid for
+    // what this call enqueues
+    std::vector<uint32_t> kc;
+    const bool use_kc = whole ? kc_lookup(pks, m, kc, order32.data()) : kc_lookup(hpk.data(), m, kc);
     // the messages hash on a side stream while the keys and signatures decompress (latency of
     // one call: the two chains run side by side)
     Ws& w = ws_acquire(d, h.s);
@@ -1930,7 +1952,7 @@ const char* hbls_last_error(void) { return g_err.c_str(); }
 
 int hbls_available(void) { return ensure_init() == 0 ? 1 : 0; }
 
-int hbls_device_count(void) { return ensure_init() ? -1 : (int)g_devs.size(); }
+int hbls_device_count(void) { return ensure_init() ? -1 : (int)devs().size(); }
 
 size_t hbls_hm_entry_bytes(void) { return sizeof(MsgEntry); }
 
@@ -2164,7 +2186,7 @@ int hbls_pubkey_cache_add(const uint8_t* pks, size_t n) {
   const size_t m = add.size();
   if (m == 0) return 0;
   if (g_kc_n + m > 0xffffffffull) return set_err("pubkey cache full");
-  for (Dev* dp : g_devs) {  // the device work under each Dev::mu in turn, g_kc_mu not held
+  for (Dev* dp : devs()) {  // the device work under each Dev::mu in turn, g_kc_mu not held
     std::lock_guard<std::mutex> dl(dp->mu);
     if (kc_fill(*dp, fresh.data(), g_kc_n, m)) return -1;
   }
@@ -2218,6 +2240,7 @@ int hbls_debug_split(uint32_t copies) {
       devs.push_back(d);
     }
   }
+  std::lock_guard<std::mutex> l(g_devs_mu);
   g_devs = devs;
   return 0;
 }
@@ -2324,7 +2347,7 @@ int hbls_slot_device(const hbls_slot* a, void* stream) {
 
 int hbls_timing(int enable) {
   if (ensure_init()) return -1;
-  for (Dev* d : g_devs) {
+  for (Dev* d : devs()) {
     std::lock_guard<std::mutex> lk(d->mu);
     d->timing = enable != 0;
     d->serial = enable == 2;
@@ -2338,7 +2361,7 @@ int hbls_timing(int enable) {
 int hbls_timing_read(const char** names, float* ms, size_t max_n, size_t* n_out) {
   if (ensure_init()) return -1;
   size_t k = 0;
-  for (Dev* d : g_devs) {
+  for (Dev* d : devs()) {
     std::lock_guard<std::mutex> lk(d->mu);
     HCHK(hipSetDevice(d->ord));
     for (size_t i = 0; i < d->tev_used && k < max_n; i++, k++) {
@@ -2360,7 +2383,7 @@ size_t hbls_fe_batch(size_t min_groups) { return g_fe_batch_min.exchange(min_gro
 int hbls_adaptive(int on) { return g_adaptive.exchange(on != 0) ? 1 : 0; }
 size_t hbls_slot_msm(size_t min_items) {
   // a new setting starts from a clean history (tests count the slot-wide checks that ran)
-  for (Dev* d : g_devs) {
+  for (Dev* d : devs()) {
     std::lock_guard<std::mutex> lk(d->mu);
     for (; d->res_tail != d->res_head; d->res_tail++) (void)hipEventSynchronize(d->res_ev[d->res_tail % N_RES]);
     d->attack = false;
@@ -2387,9 +2410,10 @@ int hbls_comm_unique_id(uint8_t* id) {
 
 int hbls_comm_init(int nranks, int rank, const uint8_t* id) {
   if (ensure_init()) return -1;
-  if (g_devs.size() != 1) return set_err("hbls_comm_init: one device per process");
+  const std::vector<Dev*> ds = devs();
+  if (ds.size() != 1) return set_err("hbls_comm_init: one device per process");
   if (g_comm) return g_comm_ranks == nranks ? 0 : set_err("communicator already initialised");
-  HCHK(hipSetDevice(g_devs[0]->ord));
+  HCHK(hipSetDevice(ds[0]->ord));
   ncclUniqueId u;
   memcpy(&u, id, sizeof(u));
   NCHK(ncclCommInitRank(&g_comm, nranks, u, rank));

@@ -43,6 +43,9 @@ HD bool ta_small_split(const int64_t* x, int t, int64_t* c, Fr& s) {
       if (d == 0) return false;
       if (__builtin_mul_overflow(e, d, &e)) return false;
     }
+    // E_j = -2^63 passes the overflow checks (e.g. x_j = -2^30 among {2^30, -2^30 + 1, -2^30 + 4}),
+    // but its magnitude does not fit: refuse it (the general path aggregates the group)
+    if (e == INT64_MIN) return false;
     c[j] = e;  // E_j for now
     const int64_t ae = e < 0 ? -e : e;
     const int64_t g = ta_gcd(L, ae);

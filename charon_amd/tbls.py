@@ -34,21 +34,33 @@ class TblsError(Exception):
     """Raised where the Go implementation returns a non-nil error."""
 
 
-# herumi.go error strings, by status code and call site
-_VERIFY_ERR = {
-    BAD_PUBKEY: "cannot set compressed public key in Herumi format",   # herumi.go:291
-    BAD_SIGNATURE: "cannot unmarshal signature into Herumi signature",  # herumi.go:296
-    NOT_VERIFIED: "signature not verified",                            # herumi.go:300
+# herumi.go error strings, by status code and call site.  ONE table: the Python mirror, the caller
+# mirrors (callers.py) and the Go shim's switches (INTEGRATION.md verifyStatusErr /
+# verifyAggStatusErr / ThresholdAggregateBatch / Aggregate) must all say the same;
+# tests/test_go_shim.py parses the Go switches and compares them with this table.
+#   kind -> ({status: message}, message of every other non-OK status)
+STATUS_ERRORS = {
+    "verify": ({
+        BAD_PUBKEY: "cannot set compressed public key in Herumi format",   # herumi.go:291
+        BAD_SIGNATURE: "cannot unmarshal signature into Herumi signature",  # herumi.go:296
+    }, "signature not verified"),                                          # herumi.go:300
+    "verify_aggregate": ({
+        BAD_PUBKEY: "cannot set compressed public key in Herumi format",   # herumi.go:331
+        BAD_SIGNATURE: "cannot unmarshal signature into Herumi signature",  # herumi.go:325
+    }, "signature verification failed"),                                   # herumi.go:338
+    "threshold_aggregate": ({
+        BAD_SIGNATURE: "cannot unmarshal signature into Herumi signature",  # herumi.go:258-262
+    }, "cannot combine signatures"),                                       # herumi.go:282
+    "aggregate": ({}, "cannot unmarshal signature into Herumi signature"),  # herumi.go:236
 }
-_VERIFY_AGG_ERR = {
-    BAD_PUBKEY: "cannot set compressed public key in Herumi format",   # herumi.go:331
-    BAD_SIGNATURE: "cannot unmarshal signature into Herumi signature",  # herumi.go:325
-    NOT_VERIFIED: "signature verification failed",                     # herumi.go:338
-}
-_TA_ERR = {
-    BAD_SIGNATURE: "cannot unmarshal signature into Herumi signature",  # herumi.go:258-262
-    COMBINE_FAILED: "cannot combine signatures",                       # herumi.go:282
-}
+
+
+def status_error(kind: str, st: int):
+    """herumi's error message for status `st` of a `kind` call (None for OK)."""
+    if st == OK:
+        return None
+    table, other = STATUS_ERRORS[kind]
+    return table.get(st, other)
 
 
 def _buf(data: bytes):
@@ -196,7 +208,7 @@ class HIPBLS:
         """herumi.go:288-304; raises TblsError with herumi's message, returns None on success."""
         st = self.verify_batch([compressed_public_key], [data], [signature])[0]
         if st != OK:
-            raise TblsError(_VERIFY_ERR.get(st, "signature not verified"))
+            raise TblsError(status_error("verify", st))
 
     def verify_batch(self, pks: Sequence[bytes], msgs: Sequence[bytes], sigs: Sequence[bytes]) -> List[int]:
         """Batch tbls.Verify: one status code per item (0 = verified)."""
@@ -216,7 +228,7 @@ class HIPBLS:
         """herumi.go:249-286."""
         outs, sts = self.threshold_aggregate_batch([partial_signatures_by_index])
         if sts[0] != OK:
-            raise TblsError(_TA_ERR.get(sts[0], "cannot combine signatures"))
+            raise TblsError(status_error("threshold_aggregate", sts[0]))
         return outs[0]
 
     def threshold_aggregate_batch(self, groups: Sequence[Mapping[int, bytes]]) -> Tuple[List[bytes], List[int]]:
@@ -240,7 +252,7 @@ class HIPBLS:
         """herumi.go:225-247 (empty input -> infinity encoding)."""
         outs, sts = self.aggregate_batch([signs])
         if sts[0] != OK:
-            raise TblsError("cannot unmarshal signature into Herumi signature")
+            raise TblsError(status_error("aggregate", sts[0]))
         return outs[0]
 
     def aggregate_batch(self, groups: Sequence[Sequence[bytes]]) -> Tuple[List[bytes], List[int]]:
@@ -261,7 +273,7 @@ class HIPBLS:
         """herumi.go:318-342 (FastAggregateVerify)."""
         st = self.verify_aggregate_batch([public_shares], [signature], [data])[0]
         if st != OK:
-            raise TblsError(_VERIFY_AGG_ERR.get(st, "signature verification failed"))
+            raise TblsError(status_error("verify_aggregate", st))
 
     def verify_aggregate_batch(self, pk_groups: Sequence[Sequence[bytes]], sigs: Sequence[bytes],
                                msgs: Sequence[bytes]) -> List[int]:

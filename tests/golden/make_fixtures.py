@@ -4,9 +4,12 @@ Cases (status codes as in include/hipbls.h):
   verify:  valid / wrong message / wrong share index / random 96 bytes / all-zero signature /
            off-subgroup G2 signature / infinity signature / infinity public key /
            x >= p / no-sqrt x / missing compression flag / off-subgroup G1 pk /
-           non-canonical infinity / 11-byte "hello obol!" message (tbls_test.go:73)
+           non-canonical infinity / 11-byte "hello obol!" message (tbls_test.go:73) /
+           the G2-side encoding rejects: x.c1 >= p, x.c0 >= p, no square root, compression
+           flag clear, infinity with nonzero bits (three placements), a flipped sign bit
   threshold_aggregate: t-of-n subsets, n > t (sigagg_test.go passes all n), k = 1, index 0,
-           negative index, undecodable partial, empty group
+           negative index, undecodable partial, empty group, a member of every G2-side
+           encoding class
   aggregate / verify_aggregate: tbls_test.go:129-167 shape (10 keys), empty inputs
 Deterministic (seeded); run time ~2-3 minutes.
 
@@ -65,6 +68,43 @@ def no_sqrt_x_g1() -> bytes:
             return bytes(b)
 
 
+def g2_bytes(x0: int, x1: int, flags: int = 0x80) -> bytearray:
+    """ZCash G2 layout: x.c1 then x.c0, 48 B each, flags in the top three bits."""
+    b = bytearray(x1.to_bytes(48, "big") + x0.to_bytes(48, "big"))
+    b[0] |= flags
+    return b
+
+
+def no_sqrt_x_g2(r: random.Random) -> bytes:
+    while True:
+        x = (r.randrange(B.P), r.randrange(B.P))
+        if B.f2_sqrt(B.f2_add(B.f2_mul(B.f2_sqr(x), x), B.B_G2)) is None:
+            return bytes(g2_bytes(*x))
+
+
+def g2_encoding_rejects(sig: bytes, r: random.Random):
+    """The Sign.Deserialize rejects behind herumi.go:294-297 (parsigex_test.go:285-289 feeds
+    undecodable partials): (name, 96 bytes) -- x.c1 >= p, x.c0 >= p, no square root, compression
+    flag clear, infinity with nonzero bits, plus a flipped sign bit (a valid point, -sigma)."""
+    x1 = int.from_bytes(sig[:48], "big") & ((1 << 381) - 1)
+    x0 = int.from_bytes(sig[48:], "big")
+    out = [("sig_x_c1_ge_p", bytes(g2_bytes(x0, x1 + B.P if x1 + B.P < 2 ** 381 else B.P))),
+           ("sig_x_c1_eq_p", bytes(g2_bytes(x0, B.P))),
+           ("sig_x_c0_ge_p", bytes(g2_bytes(x0 + B.P if x0 + B.P < 2 ** 384 else B.P, x1, sig[0] & 0xE0))),
+           ("sig_x_c0_all_ones", bytes(g2_bytes((1 << 384) - 1, x1, sig[0] & 0xE0))),
+           ("sig_no_sqrt", no_sqrt_x_g2(r))]
+    nc = bytearray(sig)
+    nc[0] &= 0x7F
+    out.append(("sig_uncompressed_flag", bytes(nc)))
+    out.append(("sig_noncanonical_infinity_low", bytes([0xC0]) + bytes(94) + b"\x01"))
+    out.append(("sig_noncanonical_infinity_c0", bytes([0xC0]) + bytes(47) + b"\x80" + bytes(47)))
+    out.append(("sig_noncanonical_infinity_top", bytes([0xC1]) + bytes(95)))
+    neg = bytearray(sig)
+    neg[0] ^= 0x20
+    out.append(("sig_sign_bit_flipped", bytes(neg)))
+    return out
+
+
 def main():
     cases = []
     # a 4-of-3 cluster for one validator (C1 shape)
@@ -104,6 +144,12 @@ def main():
     add_verify("empty_message", dv_pk, b"", B.sign(secret, b""), B.ST_OK)
     long_msg = bytes(rng.randrange(256) for _ in range(300))
     add_verify("long_message", pubshares[3], long_msg, B.sign(shares[3], long_msg), B.ST_OK)
+    # G2-side non-canonical encodings (their own RNG stream: the cases above stay as they were)
+    rng2 = random.Random(0x6253_4947)
+    g2_rejects = g2_encoding_rejects(parts[1], rng2)
+    for name, sig in g2_rejects:
+        add_verify(name, pubshares[1], msg, sig,
+                   B.ST_NOT_VERIFIED if name == "sig_sign_bit_flipped" else B.ST_BAD_SIGNATURE)
 
     # threshold aggregate
     ta = []
@@ -133,6 +179,14 @@ def main():
     p7 = {i: B.sign(sh7[i], msg7) for i in (2, 3, 5, 7, 8, 9, 10)}
     st, out = add_ta("t7_of_10", p7)
     assert out == B.sign(secret7, msg7)
+    # an undecodable member of every G2-side encoding class (herumi.go:262-268, via Sign.Deserialize)
+    for name, sig in g2_rejects:
+        if name == "sig_sign_bit_flipped":  # decodes: a wrong (but valid) aggregate, status OK
+            st, out = add_ta("member_" + name, {1: parts[1], 2: sig, 3: parts[3]})
+            assert st == B.ST_OK and out != B.sign(secret, msg)
+            continue
+        st, _ = add_ta("member_" + name, {1: parts[1], 2: sig, 3: parts[3]})
+        assert st == B.ST_BAD_SIGNATURE, name
 
     # aggregate + verify_aggregate (tbls_test.go:129-167 shape)
     agg_cases = []

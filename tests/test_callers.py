@@ -120,6 +120,16 @@ def _flows(impl, sign, pub):
                                           "aggregate: cannot unmarshal signature into Herumi signature$"):
         callers.exit_aggregate_batch(impl, [("0xa", [parts[1], parts[2], None, parts[4]]),
                                             ("0xb", [b"\x11" * 96, parts[2], parts[3], None])])
+    # validator 0's aggregation error comes before validator 1's length error (exit_fetch.go:122-132)
+    with pytest.raises(CallerError, match="^load full exit data from Obol API: partial signatures threshold "
+                                          "aggregate: cannot unmarshal signature into Herumi signature$"):
+        callers.exit_aggregate_batch(impl, [("0xa", [b"\x11" * 96, parts[2], parts[3], None]),
+                                            ("0xb", [parts[1], parts[2][:95], parts[3], None])])
+    # ... and a length error of an earlier validator before a later aggregation error
+    with pytest.raises(CallerError, match="^load full exit data from Obol API: invalid partial signature: "
+                                          "data is not of the correct length$"):
+        callers.exit_aggregate_batch(impl, [("0xa", [parts[1], parts[2][:95], parts[3], None]),
+                                            ("0xb", [b"\x11" * 96, parts[2], parts[3], None])])
 
     # --- DKG deposit data / registrations: verify + aggregate + verify per DV (dkg.go:820-984)
     roots = {dv: root}

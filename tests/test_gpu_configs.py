@@ -6,6 +6,8 @@ C4: 1M validators of a 7-operator threshold-5 cluster over 8 GPUs = 125 000 vali
     the aggregated share set a non-prefix 5-subset (bench.py ta_share_positions: its Lagrange
     coefficients are not integers).  875 000 partial Verify + 125 000 ThresholdAggregate + 125 000
     aggregate Verify under the DV keys (core/sigagg/sigagg.go:105,117).
+C3 adversarial: configs[2]'s geometry (100 000 validators, 10-of-7, distinct messages, the
+    non-prefix share set) with the C5 mix below.
 C5: the same shard with 1 % of the partials corrupted in equal fifths (bench.py corrupt: random
     bytes, on-curve points outside G2, wrong message, another share's partial, infinity;
     core/parsigex/parsigex_test.go:285-289, core/sigagg/sigagg_test.go:46-67), every status exact
@@ -154,6 +156,62 @@ def test_slot_c5_shard_adversarial(L, c4):
     assert st == OK and agg == bytes(tout[v])
     root = bytes(d["msgs"].reshape(d["M"], 32)[int(d["midx"][v * n])])
     assert B.verify(bytes(d["dv_pks"][48 * v:48 * v + 48]), root, agg) == NOT_VERIFIED == ast[v]
+
+
+def test_slot_c3_adversarial(L):
+    """BASELINE configs[2] geometry with the C5 adversarial mix: 100 000 validators of a 10-operator
+    threshold-7 cluster over distinct per-validator messages, the non-prefix aggregated share set
+    {1, 2, 3, 4, 8, 9, 10}, 1 % of the 1 M partials corrupted in equal fifths (bench.corrupt), the
+    aggregated members among them.  This drives the failure paths at 10-item groups: the failing
+    slot-wide check, the per-batch check, the per-group and per-item fallbacks, the 10-member chunk
+    ladders, and the small-scalar aggregation over groups with a bad member.  The slot runs twice:
+    the second call takes the per-batch check directly (adaptive).  Every status is exact against the
+    construction; the oracle recomputes two partials of every class, 16 clean partials and 8
+    aggregates (clean, with an undecodable member, with a decodable wrong member)."""
+    import bench
+    from oracle import bls12381 as B
+    wl = bench.WORKLOADS["c3"]
+    d = bench.setup_inputs(L, wl, wl["validators"], 0)
+    V, NP, n, t = d["V"], d["NP"], d["n"], d["t"]
+    assert (V, n, t, d["M"]) == (100_000, 10, 7, 100_000)
+    assert [int(x) for x in d["ta_idx"][:t]] == [1, 2, 3, 4, 8, 9, 10]
+    bench.corrupt(L, d, 0.01, seed=303)
+    assert d["n_corrupted"] == NP // 100
+    members = np.asarray(d["ta_src"], dtype=np.int64).reshape(V, t)
+    rng = random.Random(303)
+    bad_items = rng.sample(range(NP), int(NP * 0.01))
+    assert len(set(bad_items) & set(members.reshape(-1).tolist())) > 0.6 * len(bad_items)  # aggregated members
+    for _ in range(2):
+        vst, tst, ast, tout = _run_slot(L, d, sigs=d["sigs"])
+        bad = np.nonzero(vst != d["exp_v"])[0]
+        assert len(bad) == 0, [(int(i), int(vst[i]), int(d["exp_v"][i])) for i in bad[:10]]
+        assert np.array_equal(tst, d["exp_ta"])
+        assert np.array_equal(ast, d["exp_agg"])
+        clean = d["exp_agg"] == OK
+        assert np.array_equal(tout[clean], d["root_sigs"].reshape(V, 96)[clean])
+    assert {int(x) for x in np.unique(d["exp_agg"])} == {OK, BAD_SIGNATURE, NOT_VERIFIED}
+    # oracle: two partials of every class (class k % 5 in sample order), 16 clean partials
+    sample = [bad_items[k] for k in range(10)]
+    cl = random.Random(304)
+    sample += cl.sample([i for i in range(NP) if d["exp_v"][i] == OK][:200_000], 16)
+    for i in sample:
+        st = B.verify(bytes(d["pks"][48 * i:48 * i + 48]), bytes(d["item_msgs"][32 * i:32 * i + 32]),
+                      bytes(d["sigs"][96 * i:96 * i + 96]))
+        assert st == vst[i] == d["exp_v"][i], (i, st, int(vst[i]))
+    # 8 aggregates: 4 clean, 2 with an undecodable member, 2 with a decodable wrong member; each
+    # recomputed from its seven members and verified under the DV key by the oracle
+    pick = (cl.sample([v for v in range(V) if d["exp_agg"][v] == OK], 4) +
+            [v for v in range(V) if d["exp_ta"][v] == BAD_SIGNATURE][:2] +
+            [v for v in range(V) if d["exp_agg"][v] == NOT_VERIFIED][:2])
+    for v in pick:
+        st, agg = B.threshold_aggregate(_oracle_members(d, v))
+        assert st == tst[v], v
+        if st != OK:
+            assert ast[v] == st
+            continue
+        assert agg == bytes(tout[v]), v
+        root = bytes(d["msgs"].reshape(d["M"], 32)[int(d["midx"][v * n])])
+        assert B.verify(bytes(d["dv_pks"][48 * v:48 * v + 48]), root, agg) == ast[v], v
 
 
 def test_host_batches_c5_shard_adversarial(L, c4):

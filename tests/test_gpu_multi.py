@@ -144,8 +144,11 @@ def test_debug_split_same_results(L, hipbls):
 
 
 def test_cache_add_races_verification(hipbls):
-    """hbls_pubkey_cache_add on one thread while four threads verify: no deadlock (the add takes
-    the device locks one at a time and the key map last), every verdict right."""
+    """hbls_pubkey_cache_add and _clear on one thread while four threads verify: no deadlock (the
+    add takes the device locks one at a time and the key map last), every verdict right.  After each
+    clear the next add reuses table indices 0.. for OTHER keys, so a lookup made outside the device
+    lock, or a table rewritten under a verification still in flight, would check a signature against
+    the wrong key (hipbls.hip kc_lookup / kc_fill)."""
     rng = random.Random(21)
     keys, pks, msgs, sigs, items = _mixed_inputs(hipbls, rng, n_keys=64, n_items=200)
     P, M, S = zip(*items)
@@ -165,9 +168,9 @@ def test_cache_add_races_verification(hipbls):
 
     def adder():
         try:
-            for r in range(12):
+            for r in range(24):
                 hipbls.cache_pubkeys(pks[(r * 5) % 64:(r * 5) % 64 + 8])
-                if r % 4 == 3:
+                if r % 3 == 2:
                     hipbls.clear_pubkey_cache()
         except Exception as e:  # noqa: BLE001
             errs.append(repr(e))

@@ -163,7 +163,13 @@ def test_ta_small_split(hc):
         if max(map(abs, ids)) <= 10:
             worst = max(worst, max(abs(c[j]) for j in range(len(ids))))
     assert 0 < worst < 2 ** 22
-    for bad in ([0, 1, 2], [1, 1, 2], [5], list(range(1, 18))):
+    # E_j = -2^63 exactly for x_j = -2^30 (no multiplication overflows, but |E_j| does not fit)
+    edge = [-2 ** 30, 2 ** 30, -2 ** 30 + 1, -2 ** 30 + 4]
+    e0 = edge[0]
+    for m in edge[1:]:
+        e0 *= m - edge[0]
+    assert e0 == -2 ** 63
+    for bad in ([0, 1, 2], [1, 1, 2], [5], list(range(1, 18)), edge):
         arr = (ctypes.c_int64 * len(bad))(*bad)
         assert hc.hc_ta_small(arr, len(bad), c, s) == 0, bad
 

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summary of tools/gpu_r03_ab.sh results: per variant the value, ms/step, parity, selected kernel
+"""Summary of A/B bench results (bench_<variant>_<k>.json): per variant the value, ms/step, parity, selected kernel
 times and the single-call latency.  Usage: absum.py TAG"""
 import json
 import os

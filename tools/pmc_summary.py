@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summarise the rocprofv3 passes of tools/gpu_pmc.sh: per kernel of the LAST timed slot, the SQ
+"""Summarise the rocprofv3 passes of tools/gpu.sh pmc: per kernel of the LAST timed slot, the SQ
 counters, FETCH_SIZE (x2: gfx950 tallies 128-B requests at 64 B, MI355X_MICROARCH.md 'HBM'),
 WRITE_SIZE, and the kernel-trace duration.  Usage: pmc_summary.py <gpurun_out/pmc_TAG> [json]"""
 import collections

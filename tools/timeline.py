@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Print the kernel timeline of the last N slots of a rocprofv3 kernel trace (tools/gpu_trace.sh)."""
+"""Print the kernel timeline of the last N slots of a rocprofv3 kernel trace (tools/gpu.sh trace)."""
 import csv
 import sys
 
