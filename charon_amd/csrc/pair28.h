@@ -1,0 +1,247 @@
+// The Miller loop's arithmetic in lazily reduced 28-bit limbs (round 4).
+//
+// pairing.h / pair3.h run the Miller chain (G2 point + lines) and the three-lane Fp12 accumulator
+// on stored 12-word Fp: every Fp2 product splits its four operands into 28-bit limbs and joins
+// its two results, and every addition is a carry chain plus a conditional subtraction of 2p.
+// Here both stay in 14 x 28-bit limbs (ec28.h L28 / F2L): the products take and return limbs,
+// additions are limb-wise, subtractions add a multiple K = s p of p that dominates the
+// subtrahend limb by limb (ec28.h K28<s, t>), and carries run only where a bound needs them.
+// Values do not grow from step to step: every step ends with l_red, a partial reduction that
+// needs no product (q = floor(v / p) or one less, read off the top 56 bits; v - q p < 2p), so
+// the chain's point and the accumulator's lane values are below 2p at every step boundary.
+// Reduced values are valid stored words after a join (fp.h fp_join28): the lines written to
+// memory and the loop's result keep the stored-word layouts of layout.h without a product.
+//
+// charon_amd/tools/lazy28.py restates every formula here (ldbl, ladd, f4_mul, f4_sqr, g4_sqr,
+// g4_mul_line) over per-limb intervals and proves that no limb leaves 32 bits, no product column
+// 64 bits, every K dominates its subtrahend and the step outputs are reduced below 2p; the site
+// constants below are the ones lazy28.KSITE holds ("3*": the chain, "4*": the Fp4 lane values),
+// tests/test_lazy28.py compares them.
+#pragma once
+#include "pair3.h"
+
+namespace hb {
+
+// v mod p up to a multiple of p: the same residue, normalised, below 2p.  a: limbs below 2^32
+// (not necessarily carried), value below 2^390.  The top estimate l13 2^28 + l12 is within 17 of
+// v / 2^336 (the lower limbs carry at most 16 into limb 12), so top / (p >> 336) is within 2^-40
+// of v / p; minus 2^-20 and truncated it gives floor(v / p) or one less.  The subtraction runs
+// with a signed carry (q < 2^10, so q p_i < 2^38).
+HD L28 l_red(const L28& a) {
+  const double top = (double)a.l[13] * 268435456.0 + (double)a.l[12];
+  const double qd = top * kInvPTop - 0x1p-20;
+  const int32_t q = qd > 0.0 ? (int32_t)qd : 0;
+  L28 r;
+  int64_t c = 0;
+  HB_UNROLL for (int i = 0; i < 13; i++) {
+    c += (int64_t)a.l[i] - (int64_t)q * (int64_t)kP28_[i];
+    r.l[i] = (uint32_t)c & 0x0FFFFFFFu;
+    c >>= 28;
+  }
+  r.l[13] = (uint32_t)(c + (int64_t)a.l[13] - (int64_t)q * (int64_t)kP28_[13]);
+  return r;
+}
+
+HD L28 l_zero() {
+  L28 r;
+  HB_UNROLL for (int i = 0; i < 14; i++) r.l[i] = 0;
+  return r;
+}
+HD L28 l_select(bool take_b, const L28& a, const L28& b) {
+  L28 r;
+  HB_UNROLL for (int i = 0; i < 14; i++) r.l[i] = take_b ? b.l[i] : a.l[i];
+  return r;
+}
+// a reduced value (< 2p, normalised) as stored words, no product
+HD Fp l_join(const L28& a) {
+  Fp r;
+  fp_join28(r.v, a.l);
+  return r;
+}
+
+HD F2L f2l_red(const F2L& a) { return {l_red(a.c0), l_red(a.c1)}; }
+HD F2L f2l_zero() { return {l_zero(), l_zero()}; }
+HD F2L f2l_one() { return {l_from(fp_one()), l_zero()}; }
+HD F2L f2l_select(bool take_b, const F2L& a, const F2L& b) {
+  return {l_select(take_b, a.c0, b.c0), l_select(take_b, a.c1, b.c1)};
+}
+HD Fp2 f2l_join(const F2L& a) { return {l_join(a.c0), l_join(a.c1)}; }
+// (a0 + a1 u)(1 + u) = (a0 + K - a1) + (a0 + a1) u
+template <uint32_t S, uint32_t T>
+HD F2L f2l_xi(const F2L& a) {
+  return {l_sub<S, T>(a.c0, a.c1), l_add(a.c0, a.c1)};
+}
+// ec28.h f2l_sqr with the site's constant: (a0 + a1)(a0 + K - a1) + 2 a0 a1 u
+template <uint32_t S, uint32_t T>
+HD F2L f2l_sqr_k(const F2L& a) {
+  return {l_mul(l_add(a.c0, a.c1), l_sub<S, T>(a.c0, a.c1)), l_mul(l_shl(a.c0, 1), a.c1)};
+}
+
+// ---- the Miller chain: T in homogeneous projective coordinates on the twist (pairing.h
+// miller_dbl_c / miller_add_c), the line as (a0, c1, c2) -- evaluated at P it is
+// a0 + (c1 xP) v + (c2 yP) v w.  Coordinates and line coefficients reduced (< 2p).
+struct G2P28 {
+  F2L X, Y, Z;
+};
+struct Line28 {
+  F2L a0, a1, b1;
+};
+
+// lazy28.py ldbl: the doubling step scaled by 4 (X3 = 2 X Y (A - E), Y3 = (A + E)^2 - 12 C^2,
+// Z3 = 8 A D -- the same projective point as miller_dbl_c's, no halving), A = Y^2, B = Z^2,
+// C = 3 b' B = 12 xi B, E = 3 C, D = Y Z; line (A - C, -3 X^2, 2 D), handed to put(Line28) as
+// soon as it exists.  The products run in the order that ends their inputs' live ranges first.
+template <class Put>
+HD void l2_dbl_line(G2P28& T, const Put& put) {
+  const F2L XX = f2l_sqr_k<78, 1>(T.X);
+  const F2L XY = f2l_mul(f2l_shl(T.X, 1), T.Y);
+  const F2L D = f2l_mul(T.Y, T.Z);
+  const F2L A = f2l_sqr_k<78, 1>(T.Y);
+  const F2L B = f2l_sqr_k<78, 1>(T.Z);
+  const F2L xb = f2l_norm(f2l_xi<2, 1>(B));
+  const F2L C = f2l_norm(f2l_add(f2l_shl(xb, 3), f2l_shl(xb, 2)));
+  put(Line28{f2l_red(f2l_sub<38, 1>(A, C)), f2l_red(f2l_sub<4, 3>(f2l_zero(), f2l_add(f2l_shl(XX, 1), XX))),
+             f2l_red(f2l_shl(D, 1))});
+  T.Z = f2l_red(f2l_shl(f2l_mul(A, D), 3));
+  const F2L E = f2l_add(f2l_shl(C, 1), C);
+  T.X = f2l_red(f2l_mul(XY, f2l_norm(f2l_sub<113, 3>(A, E))));
+  const F2L C2 = f2l_sqr_k<78, 1>(C);
+  T.Y = f2l_red(f2l_sub<47, 12>(f2l_sqr_k<78, 1>(f2l_norm(f2l_add(A, E))), f2l_add(f2l_shl(C2, 3), f2l_shl(C2, 2))));
+}
+
+// lazy28.py ladd: T + Q (Q affine, reduced), the chord through T and Q, put(Line28) as above
+template <class Put>
+HD void l2_add_line(G2P28& T, const F2L& xq, const F2L& yq, const Put& put) {
+  const F2L th = f2l_norm(f2l_sub<2, 1>(T.Y, f2l_mul(yq, T.Z)));
+  const F2L la = f2l_norm(f2l_sub<2, 1>(T.X, f2l_mul(xq, T.Z)));
+  put(Line28{f2l_red(f2l_sub<2, 1>(f2l_mul(th, xq), f2l_mul(la, yq))), f2l_red(f2l_sub<5, 1>(f2l_zero(), th)),
+             f2l_red(la)});
+  const F2L C = f2l_sqr_k<78, 1>(th);
+  const F2L D = f2l_sqr_k<78, 1>(la);
+  const F2L E = f2l_mul(la, D);
+  const F2L G = f2l_mul(T.X, D);
+  const F2L H = f2l_norm(f2l_sub<3, 2>(f2l_add(E, f2l_mul(T.Z, C)), f2l_shl(G, 1)));
+  T.Z = f2l_red(f2l_mul(T.Z, E));
+  T.Y = f2l_red(f2l_sub<2, 1>(f2l_mul(th, f2l_norm(f2l_sub<6, 1>(G, H))), f2l_mul(T.Y, E)));
+  T.X = f2l_red(f2l_mul(la, H));
+}
+
+// a chain line as stored words; EVAL: evaluated at -g1 (c1 xP, c2 yP: products of reduced values
+// are below 2p, joined as they are; counted like pairing.h line_eval's)
+template <bool EVAL>
+HD LineCoeffs line28_store(const Line28& l) {
+  if (EVAL) {
+    const L28 xp = l_from(fp_from_const(G1_GEN_X)), yp = l_from(fp_from_const(G1_GEN_NEG_Y));
+    return {f2l_join(l.a0), {l_join(l_mul(l.a1.c0, xp)), l_join(l_mul(l.a1.c1, xp))},
+            {l_join(l_mul(l.b1.c0, yp)), l_join(l_mul(l.b1.c1, yp))}};
+  }
+  return {f2l_join(l.a0), f2l_join(l.a1), f2l_join(l.b1)};
+}
+
+// The Miller chain of an affine G2 point (lines.h line_chain in lazy limbs): 68 lines, line j
+// handed to put(j, LineCoeffs) (the stored-word line, pairing.h / layout.h LineEntry layout).
+// load() returns Q again at each of the five additions (not held across the chain).
+template <bool EVAL, class LoadQ, class Put>
+HD void line_chain28(const LoadQ& load, const Put& put) {
+  const G2A Q = load();
+  G2P28 T = {f2l_from(Q.x), f2l_from(Q.y), f2l_one()};
+  int j = 0;
+  auto emit = [&](const Line28& l) { put(j++, line28_store<EVAL>(l)); };
+  HB_NOUNROLL for (int i = 62; i >= 0; i--) {
+    l2_dbl_line(T, emit);
+    if ((HB_X_ABS >> i) & 1) {
+#if defined(__HIP_DEVICE_COMPILE__)
+      __asm__ volatile("" ::: "memory");
+#endif
+      const G2A q2 = load();
+      l2_add_line(T, f2l_from(q2.x), f2l_from(q2.y), emit);
+    }
+  }
+}
+
+// ---- Fp4 = Fp2[s]/(s^2 - xi) in lazy limbs: the lane values of pair3.h's three-lane Fp12
+struct F4L {
+  F2L x, y;  // x + y s
+};
+HD F4L f4l_add(const F4L& a, const F4L& b) { return {f2l_add(a.x, b.x), f2l_add(a.y, b.y)}; }
+template <uint32_t S, uint32_t T>
+HD F4L f4l_sub(const F4L& a, const F4L& b) {
+  return {f2l_sub<S, T>(a.x, b.x), f2l_sub<S, T>(a.y, b.y)};
+}
+HD F4L f4l_norm(const F4L& a) { return {f2l_norm(a.x), f2l_norm(a.y)}; }
+HD F4L f4l_red(const F4L& a) { return {f2l_red(a.x), f2l_red(a.y)}; }
+HD F4L f4l_select(bool take_b, const F4L& a, const F4L& b) {
+  return {f2l_select(take_b, a.x, b.x), f2l_select(take_b, a.y, b.y)};
+}
+HD F4L f4l_from(const Fp2& x, const Fp2& y) { return {f2l_from(x), f2l_from(y)}; }
+// (x + y s) s = xi y + x s
+template <uint32_t S, uint32_t T>
+HD F4L f4l_mul_s(const F4L& a) {
+  return {f2l_xi<S, T>(a.y), a.x};
+}
+// lazy28.py f4_mul (Karatsuba, normalised): (t0 + xi t1, t2 - t0 - t1)
+template <uint32_t XS, uint32_t XT, uint32_t YS, uint32_t YT>
+HD F4L f4l_mul(const F4L& a, const F4L& b) {
+  const F2L t0 = f2l_mul(a.x, b.x), t1 = f2l_mul(a.y, b.y);
+  const F2L t2 = f2l_mul(f2l_add(a.x, a.y), f2l_add(b.x, b.y));
+  return f4l_norm({f2l_add(t0, f2l_xi<XS, XT>(t1)), f2l_sub<YS, YT>(t2, f2l_add(t0, t1))});
+}
+// lazy28.py f4_sqr: (x^2 + xi y^2, (x + y)^2 - x^2 - y^2), normalised
+template <uint32_t XS, uint32_t XT, uint32_t YS, uint32_t YT>
+HD F4L f4l_sqr(const F4L& a) {
+  const F2L t0 = f2l_sqr_k<9, 2>(a.x), t1 = f2l_sqr_k<9, 2>(a.y);
+  return f4l_norm({f2l_add(f2l_xi<XS, XT>(t1), t0),
+                   f2l_sub<YS, YT>(f2l_sqr_k<9, 2>(f2l_norm(f2l_add(a.x, a.y))), f2l_add(t0, t1))});
+}
+
+// The lane operations of pair3.h in two phases around their lane exchanges, so that the host
+// harness can run the three roles one after the other (tests/native/hostcheck.cpp) and the device
+// (g4_sqr / g4_mul_line below) between ds_bpermutes.
+// square (pair3.h g_sqr): phase 1 -- v = A^2, w = (A_p + A_q)^2 from the two roles != e(k);
+// phase 2 -- D = w - v_p - v_q, C = Y + [k != 2] s X with (X, Y) = (D, v_e) for k = 0, else
+// (v_e, D); reduced
+HD void g4_sqr_p1(const F4L& A, const F4L& Ap, const F4L& Aq, F4L& v, F4L& w) {
+  v = f4l_sqr<2, 1, 3, 2>(A);
+  w = f4l_sqr<2, 1, 3, 2>(f4l_add(Ap, Aq));
+}
+HD F4L g4_sqr_p2(int k, const F4L& w, const F4L& vp, const F4L& vq, const F4L& ve) {
+  const F4L D = f4l_sub<9, 2>(w, f4l_add(vp, vq));
+  const F4L X = f4l_select(k != 0, D, ve), Y = f4l_select(k != 0, ve, D);
+  const F4L sx = f4l_select(k == 2, f4l_mul_s<14, 4>(X), X);
+  return f4l_red(f4l_add(Y, sx));
+}
+// product by a sparse line a0 + a1 v + b1 v w (pair3.h g_mul_line): phase 1 -- F a1, sent to the
+// role before; phase 2 -- C = F (a0 + b1 s) + [k == 2 ? s : 1] (F_{k+1} a1); reduced
+HD F4L g4_line_p1(const F4L& F, const F2L& a1) { return {f2l_mul(F.x, a1), f2l_mul(F.y, a1)}; }
+HD F4L g4_line_p2(int k, const F4L& F, const F2L& a0, const F2L& b1, const F4L& Qn) {
+  const F4L Qs = f4l_select(k == 2, f4l_mul_s<2, 1>(Qn), Qn);  // k == 2 ? Qn : s Qn
+  return f4l_red(f4l_add(f4l_mul<2, 1, 3, 2>(F, F4L{a0, b1}), Qs));
+}
+HD F4L g4_one_role(int k) {
+  F4L r = {f2l_zero(), f2l_zero()};
+  if (k == 0) r.x = f2l_one();
+  return r;
+}
+
+#if defined(__HIP_DEVICE_COMPILE__)
+// The lane steps on the device: pair3.h's exchanges (ds_bpermute) around the two phases
+__device__ __forceinline__ L28 xch(const L28& a, int addr) {
+  L28 r;
+  HB_UNROLL for (int i = 0; i < 14; i++) r.l[i] = xch(a.l[i], addr);
+  return r;
+}
+__device__ __forceinline__ F2L xch(const F2L& a, int addr) { return {xch(a.c0, addr), xch(a.c1, addr)}; }
+__device__ __forceinline__ F4L xch(const F4L& a, int addr) { return {xch(a.x, addr), xch(a.y, addr)}; }
+
+__device__ __forceinline__ F4L g4_one(const Grp& g) { return g4_one_role(g.k); }
+__device__ __forceinline__ F4L g4_sqr(const Grp& g, const F4L& A) {
+  F4L v, w;
+  g4_sqr_p1(A, xch(A, g.p), xch(A, g.q), v, w);
+  return g4_sqr_p2(g.k, w, xch(v, g.p), xch(v, g.q), xch(v, g.e));
+}
+__device__ __forceinline__ F4L g4_mul_line(const Grp& g, const F4L& F, const F2L& a0, const F2L& a1, const F2L& b1) {
+  return g4_line_p2(g.k, F, a0, b1, xch(g4_line_p1(F, a1), g.n1));
+}
+#endif
+
+}  // namespace hb

@@ -13,11 +13,20 @@ namespace hb {
 
 constexpr int BLOCK = 64;
 
+// HB_MML28 / HB_LML28 = 0: the stored-word multi-Miller loop / fused lines+loop (A/B runs); default:
+// the lazy-limb arithmetic of pair28.h
+#ifndef HB_MML28
+#define HB_MML28 1
+#endif
+#ifndef HB_LML28
+#define HB_LML28 1
+#endif
+
 // One lane per distinct message: the unevaluated line chain of H(m).
 __global__ KB_OCC(HB_OCC_LINES) void k_lines_msg(MsgEntry* __restrict__ hm, uint32_t n) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  line_chain<false>(hm_load(hm[i].h), hm[i].lines, 1);
+  line_chain_ld<false>(&hm[i].h, hm[i].lines, 1);
 }
 
 // THREE lanes per pairing (pair3.h): Miller loop over the streamed lines of (P, H(m)) and
@@ -83,21 +92,38 @@ __global__ KB_OCC(HB_OCC_PAIR3) void k_pair3(Pair3Args a) {
     const uint32_t cnt = first < a.f_n ? min(a.f_range, a.f_n - first) : 0u;
     const LineEntry* ev = a.sig_lines;
     const size_t fn = a.f_n;
+#if HB_MML28
+    // the accumulator in lazy limbs (pair28.h g4_sqr / g4_mul_line), reduced below 2p after every
+    // step; the stored-word lines are split as they are read
+    F4L f = g4_one(g);
+#else
     Fp4 f = g_one(g);
+#endif
     int bit = 62;
     bool pending_add = false;
     LineEntry Ln = ev[first];
     HB_NOUNROLL for (int j = 0; j < N_LINES; j++) {
       const bool dbl = !pending_add;
+#if HB_MML28
+      if (dbl && j > 0) f = g4_sqr(g, f);
+#else
       if (dbl && j > 0) f = g_sqr(g, f);
+#endif
       HB_NOUNROLL for (uint32_t k = 0; k < a.f_range; k++) {
         const LineEntry L = Ln;
         // prefetch: the next pair of this line, else the first pair of the next line
         const uint32_t k1 = k + 1 < a.f_range ? k + 1 : 0u;
         const int j1 = k + 1 < a.f_range ? j : (j + 1 < N_LINES ? j + 1 : j);
         Ln = ev[(size_t)j1 * fn + (k1 < cnt ? first + k1 : first)];
+#if HB_MML28
+        F2L l0, l1, l2;
+        line_split(L, l0, l1, l2);
+        const F4L t = g4_mul_line(g, f, l0, l1, l2);
+        f = f4l_select(k < cnt, f, t);
+#else
         const Fp4 t = g_mul_line(g, f, L.a0, L.a1, L.b1);
         f4_select(f, k < cnt, f, t);
+#endif
       }
       if (dbl) {
         pending_add = ((HB_X_ABS >> bit) & 1) != 0;
@@ -106,7 +132,11 @@ __global__ KB_OCC(HB_OCC_PAIR3) void k_pair3(Pair3Args a) {
         pending_add = false;
       }
     }
+#if HB_MML28
+    if (valid) a.f_out[3 * f_out_index(a, e) + g.k] = f4l_store(f);
+#else
     if (valid) a.f_out[3 * f_out_index(a, e) + g.k] = Fp4Entry{f.x, f.y};
+#endif
     return;
   }
   if (MODE != P3_FIN && MODE != P3_MLS) {
@@ -263,7 +293,12 @@ __global__ __launch_bounds__(128, 1) void k_lml(LmlArgs a) {
   __shared__ LineEntry buf[2];
   __shared__ uint32_t sinf;
   const bool producer = threadIdx.x < 64;
+#if HB_LML28
+  G2P28 T;
+  __shared__ HmEntry qsh;  // the producer's affine point, re-read at the chain's additions
+#else
   G2Proj T;
+#endif
   G2A Q;
   if (producer) {
     if (SIDE == 0) {
@@ -272,19 +307,48 @@ __global__ __launch_bounds__(128, 1) void k_lml(LmlArgs a) {
     } else {
       Q = hm_load(a.hm[a.msg_idx[e]].h);
     }
+#if HB_LML28
+    T = {f2l_from(Q.x), f2l_from(Q.y), f2l_one()};
+    if (threadIdx.x == 0) qsh = HmEntry{Q.x, Q.y, 0u, {0u, 0u, 0u}};
+#else
     T = {Q.x, Q.y, f2_one()};
+#endif
     if (threadIdx.x == 0) sinf = Q.inf ? 1u : 0u;
   }
   G1AEntry P{};
   if (SIDE == 1 && !producer) P = a.pk[e];
   Grp g = grp_make();
+#if HB_LML28
+  F4L f = g4_one(g);
+  F2L px, py;  // SIDE 1: P's coordinates, the consumer evaluates at P
+  if (SIDE == 1) {
+    px = {l_from(P.x), l_zero()};
+    py = {l_from(P.y), l_zero()};
+  }
+#else
   Fp4 f = g_one(g);
+#endif
   int bit = 62;        // consumer: the loop schedule of k_pair3
   bool pending_add = false;
   int pbit = 62;       // producer: the chain schedule of line_chain
   bool padd = false;
   HB_NOUNROLL for (int j = 0; j <= N_LINES; j++) {
     if (producer && j < N_LINES) {
+#if HB_LML28
+      auto put = [&](const Line28& l28) {
+        const LineCoeffs l = SIDE == 0 ? line28_store<true>(l28) : line28_store<false>(l28);
+        if (threadIdx.x == 0) buf[j & 1] = {l.a0, l.a1, l.b1};
+      };
+      if (!padd) {
+        l2_dbl_line(T, put);
+        padd = ((HB_X_ABS >> pbit) & 1) != 0;
+        pbit--;
+      } else {
+        const HmEntry qe = qsh;
+        l2_add_line(T, f2l_from(qe.x), f2l_from(qe.y), put);
+        padd = false;
+      }
+#else
       LineCoeffs l;
       if (!padd) {
         l = miller_dbl_c(T);
@@ -296,13 +360,25 @@ __global__ __launch_bounds__(128, 1) void k_lml(LmlArgs a) {
       }
       if (SIDE == 0) line_eval(l, fp_from_const(G1_GEN_X), fp_from_const(G1_GEN_NEG_Y));
       if (threadIdx.x == 0) buf[j & 1] = {l.a0, l.a1, l.b1};
+#endif
     }
     if (!producer && j > 0) {
       const LineEntry L = buf[(j - 1) & 1];
       const bool dbl = !pending_add;
+#if HB_LML28
+      if (dbl && j > 1) f = g4_sqr(g, f);
+      F2L l0, l1, l2;
+      line_split(L, l0, l1, l2);
+      if (SIDE == 1) {  // c1 xP, c2 yP (products of reduced values: below 2p)
+        l1 = {l_mul(l1.c0, px.c0), l_mul(l1.c1, px.c0)};
+        l2 = {l_mul(l2.c0, py.c0), l_mul(l2.c1, py.c0)};
+      }
+      f = g4_mul_line(g, f, l0, l1, l2);
+#else
       if (dbl && j > 1) f = g_sqr(g, f);
       if (SIDE == 0) f = g_mul_line(g, f, L.a0, L.a1, L.b1);
       else f = g_mul_line(g, f, L.a0, f2_mul_fp(L.a1, P.x), f2_mul_fp(L.b1, P.y));
+#endif
       if (dbl) {
         pending_add = ((HB_X_ABS >> bit) & 1) != 0;
         bit--;
@@ -314,7 +390,11 @@ __global__ __launch_bounds__(128, 1) void k_lml(LmlArgs a) {
   }
   if (!producer && threadIdx.x < 64 + 3) {
     const size_t o = (size_t)e * (a.f_stride ? a.f_stride : 1u) + a.f_off;
+#if HB_LML28
+    a.f_out[3 * o + g.k] = f4l_store(f);
+#else
     a.f_out[3 * o + g.k] = Fp4Entry{f.x, f.y};
+#endif
     if (threadIdx.x == 64 && a.bad)
       a.bad[e] = SIDE == 0 ? (uint8_t)sinf : (uint8_t)((a.pk_st && a.pk_st[e]) || P.inf || sinf ? 1 : 0);
   }

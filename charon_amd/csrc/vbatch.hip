@@ -457,8 +457,7 @@ __global__ KB_OCC(HB_OCC_LINES) void k_fb_lines(const uint32_t* __restrict__ lis
   const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
   if (u >= cap || base + u >= *count) return;
   const uint32_t e = list[base + u];
-  const G2A S = e < n_items ? hm_load(sig[e]) : hm_load(agg_sig[e - n_items]);
-  line_chain<true>(S, lines + u, cap);
+  line_chain_ld<true>(e < n_items ? sig + e : agg_sig + (e - n_items), lines + u, cap);
 }
 
 static inline unsigned blocks_for(size_t n) { return (unsigned)((n + BLOCK - 1) / BLOCK); }
@@ -564,7 +563,7 @@ __global__ KB_OCC(HB_OCC_LINES) void k_sig_lines(const HmEntry* __restrict__ sig
                                uint32_t stride) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  line_chain<true>(hm_load(sig[i]), lines + i, stride);
+  line_chain_ld<true>(sig + i, lines + i, stride);
 }
 
 // One lane per group: herumi's order of checks -- signature decoding, public key decoding, then

@@ -204,6 +204,12 @@ KSITE = {
     "2A_H": (17, 1), "2A_R": (33, 2), "2A_X": (13, 12), "2A_W": (16, 1), "2A_Y": (9, 8),
     "2J_H": (2, 1), "2J_R": (3, 2), "2J_X": (13, 12), "2J_W": (15, 1), "2J_Y": (9, 8),
     "2N": (33, 6), "2Q": (36, 1),
+    # round 4 (pair28.h): the Miller chain ("3") and the three-lane Fp4 values ("4"), proven at 2p
+    "3A_GH": (6, 1), "3A_H": (3, 2), "3A_Y": (2, 1), "3A_a0": (2, 1), "3A_a1": (5, 1), "3A_la": (2, 1),
+    "3A_th": (2, 1), "3D_AE": (113, 3), "3D_Y": (47, 12), "3D_a0": (38, 1), "3D_a1": (4, 3), "3D_xi": (2, 1),
+    "3Q": (78, 1),
+    "4Lmxi": (2, 1), "4Lmy": (3, 2), "4Ls": (2, 1), "4Q": (9, 2), "4SD": (9, 2), "4Ss": (14, 4),
+    "4Svxi": (2, 1), "4Svy": (3, 2), "4Swxi": (2, 1), "4Swy": (3, 2),
 }
 
 
@@ -317,6 +323,184 @@ def jadd2(F, X1, Y1, Z1, X2, Y2, Z2):
     return X3, Y3, Z3
 
 
+# ------------------------------------------------------------------------------------------
+# Round 4: the Miller-loop arithmetic in lazy limbs (csrc/pair28.h).
+#
+# red(a): the partial reduction l_red of pair28.h -- a normalised value v < 2^390 becomes v - q p
+# with q = floor(v / p) or one less, read off the top 56 bits (no product): normalised, < 2p.
+def red(a):
+    assert a.v < (1 << 390)  # the limbs need no carry pass (Bound keeps them below 2^32)
+    return Bound.normalised(2 * P)
+
+
+def f2_red(a):
+    return (red(a[0]), red(a[1]))
+
+
+def bmax(a, b):
+    """the bound of a value that is a or b (the lane roles' selects of pair28.h)"""
+    if isinstance(a, Bound):
+        return Bound([max(x, y) for x, y in zip(a.lb, b.lb)], max(a.v, b.v))
+    return tuple(bmax(x, y) for x, y in zip(a, b))
+
+
+class LineOps(Fp2Ops):
+    """the Fp2 of the line chain and the Fp4 lane arithmetic: its own squaring constant"""
+
+    @staticmethod
+    def sqr(a):
+        return f2_sqr(a, "3Q")
+
+    @staticmethod
+    def sub(a, b, site):
+        return f2_sub(a, b, "3" + site)
+
+
+def f2_xi(F, a, site):
+    """(a0 + a1 u)(1 + u) = (a0 - a1) + (a0 + a1) u"""
+    return (sub(a[0], a[1], "3" + site), add(a[0], a[1]))
+
+
+ZERO2 = (Bound([0] * NLIMB, 0), Bound([0] * NLIMB, 0))
+
+
+def ldbl(F, X, Y, Z):
+    """pair28.h l2_dbl_line: the doubling step of the Miller chain in homogeneous projective
+    coordinates on the twist (b' = 4 xi), scaled by 4 so that no halving is needed:
+      A = Y^2, B = Z^2, C = 3 b' B = 12 xi B, E = 3 C, D = Y Z
+      line (a0, a1, b1) = (A - C, -3 X^2, 2 D)
+      X3 = 2 X Y (A - E), Y3 = (A + E)^2 - 12 C^2, Z3 = 8 A D
+    The point's coordinates are reduced (l_red) at the end of every step: they stay below 2p."""
+    A = F.sqr(Y)
+    B = F.sqr(Z)
+    xb = F.norm(f2_xi(F, B, "D_xi"))
+    C = F.norm(F.add(F.shl(xb, 3), F.shl(xb, 2)))
+    E = F.add(F.shl(C, 1), C)
+    D = F.mul(Y, Z)
+    XX = F.sqr(X)
+    a0 = F.sub(A, C, "D_a0")
+    a1 = F.sub(ZERO2, F.add(F.shl(XX, 1), XX), "D_a1")
+    b1 = F.shl(D, 1)
+    XY = F.mul(F.shl(X, 1), Y)
+    X3 = f2_red(F.mul(XY, F.norm(F.sub(A, E, "D_AE"))))
+    C2 = F.sqr(C)
+    Y3 = f2_red(F.sub(F.sqr(F.norm(F.add(A, E))), F.add(F.shl(C2, 3), F.shl(C2, 2)), "D_Y"))
+    Z3 = f2_red(F.shl(F.mul(A, D), 3))
+    return (X3, Y3, Z3), (f2_red(a0), f2_red(a1), f2_red(b1))
+
+
+def ladd(F, X, Y, Z, xq, yq):
+    """pair28.h l2_add_line: T + Q for an affine Q, the chord through T and Q:
+      th = Y - yq Z, la = X - xq Z, C = th^2, D = la^2, E = la D, F = Z C, G = X D,
+      H = E + F - 2G; line (th xq - la yq, -th, la); X3 = la H, Y3 = th (G - H) - Y E, Z3 = Z E"""
+    th = F.norm(F.sub(Y, F.mul(yq, Z), "A_th"))
+    la = F.norm(F.sub(X, F.mul(xq, Z), "A_la"))
+    C = F.sqr(th)
+    D = F.sqr(la)
+    E = F.mul(la, D)
+    Fv = F.mul(Z, C)
+    G = F.mul(X, D)
+    H = F.norm(F.sub(F.add(E, Fv), F.shl(G, 1), "A_H"))
+    a0 = F.sub(F.mul(th, xq), F.mul(la, yq), "A_a0")
+    a1 = F.sub(ZERO2, th, "A_a1")
+    X3 = f2_red(F.mul(la, H))
+    Y3 = f2_red(F.sub(F.mul(th, F.norm(F.sub(G, H, "A_GH"))), F.mul(Y, E), "A_Y"))
+    Z3 = f2_red(F.mul(Z, E))
+    return (X3, Y3, Z3), (f2_red(a0), f2_red(a1), f2_red(la))
+
+
+# Fp4 = Fp2[s]/(s^2 - xi) as (x, y); the lane values of pair28.h's three-lane Fp12
+def f4_add(a, b):
+    return (f2_add(a[0], b[0]), f2_add(a[1], b[1]))
+
+
+def f4_sub(a, b, site):
+    return (f2_sub(a[0], b[0], "4" + site), f2_sub(a[1], b[1], "4" + site))
+
+
+def f4_norm(a):
+    return (f2_norm(a[0]), f2_norm(a[1]))
+
+
+def f4_red(a):
+    return (f2_red(a[0]), f2_red(a[1]))
+
+
+def f4_xi(a, site):
+    return (sub(a[0], a[1], "4" + site), add(a[0], a[1]))
+
+
+def f4_mul(a, b, site):
+    """g4 Karatsuba: t0 = a.x b.x, t1 = a.y b.y, t2 = (a.x + a.y)(b.x + b.y);
+    (t0 + xi t1, t2 - t0 - t1), normalised"""
+    t0 = f2_mul(a[0], b[0], "2N")
+    t1 = f2_mul(a[1], b[1], "2N")
+    t2 = f2_mul(f2_add(a[0], a[1]), f2_add(b[0], b[1]), "2N")
+    return f4_norm((f2_add(t0, f4_xi(t1, site + "xi")), f2_sub(t2, f2_add(t0, t1), "4" + site + "y")))
+
+
+def f4_sqr(a, site):
+    """(x + y s)^2 = (x^2 + xi y^2, (x + y)^2 - x^2 - y^2), normalised"""
+    t0 = f2_sqr(a[0], "4Q")
+    t1 = f2_sqr(a[1], "4Q")
+    return f4_norm((f2_add(f4_xi(t1, site + "xi"), t0),
+                    f2_sub(f2_sqr(f2_norm(f2_add(a[0], a[1])), "4Q"), f2_add(t0, t1), "4" + site + "y")))
+
+
+def f4_mul_s(a, site):
+    return (f4_xi(a[1], site), a[0])
+
+
+def g4_sqr(A):
+    """pair28.h g4_sqr (pair3.h g_sqr): sa = A_p + A_q, v = A^2, w = sa^2, D = w - v_p - v_q,
+    C = Y + [k != 2] s X with (X, Y) = (D, v_e) or (v_e, D); reduced"""
+    sa = f4_add(A, A)
+    v = f4_sqr(A, "Sv")
+    w = f4_sqr(sa, "Sw")
+    D = f4_sub(w, f4_add(v, v), "SD")
+    X = bmax(D, v)
+    Y = bmax(v, D)
+    sx = bmax(f4_mul_s(X, "Ss"), X)
+    return f4_red(f4_add(Y, sx))
+
+
+def g4_mul_line(Fv, a0, a1, b1):
+    """pair28.h g4_mul_line (pair3.h g_mul_line): F (a0 + b1 s) + [s] F_n a1; reduced"""
+    Qn = (f2_mul(Fv[0], a1, "2N"), f2_mul(Fv[1], a1, "2N"))
+    Qs = bmax(f4_mul_s(Qn, "Ls"), Qn)
+    return f4_red(f4_add(f4_mul(Fv, (a0, b1), "Lm"), Qs))
+
+
+def check_lines(vmax):
+    """the chain's point stays normalised below vmax p; the lines come out reduced (< 2p)"""
+    F = LineOps
+    vm = vmax * P
+    X = Y = Z = F.nrm(vm)
+    q = F.nrm(2 * P)
+    out = {}
+    for op, fn in (("dbl", lambda: ldbl(F, X, Y, Z)), ("add", lambda: ladd(F, X, Y, Z, q, q))):
+        pt, line = fn()
+        for c in pt:
+            assert fits(c, vm), ("lines", op, vmax_of(c) / P)
+        for c in line:
+            assert fits(c, 2 * P)
+        out[op] = max(vmax_of(c) for c in pt) / P
+    return out
+
+
+def check_pair():
+    """the three-lane Fp12 value: lane values normalised below 2p (reduced after every step), the
+    lines' coefficients below 2p"""
+    A = (Fp2Ops.nrm(2 * P), Fp2Ops.nrm(2 * P))
+    ln = Fp2Ops.nrm(2 * P)
+    out = {}
+    for op, fn in (("sqr", lambda: g4_sqr(A)), ("line", lambda: g4_mul_line(A, ln, ln, ln))):
+        r = fn()
+        assert all(fits(c, 2 * P) for c in r), op
+        out[op] = max(vmax_of(c) for c in r) / P
+    return out
+
+
 def fits(x, vmax):
     return vmax_of(x) <= vmax and all(
         all(l <= M28 for l in b.lb[:13]) and b.lb[13] <= (vmax >> 364) for b in ([x] if isinstance(x, Bound) else x))
@@ -352,6 +536,8 @@ def search(vmax, fields=("Fp", "Fp2")):
     need = {}
 
     def auto(a, b, site):
+        if site == "2N" and ("lines" in fields or "pair" in fields):
+            return plain(a, b, site)  # the f2l_mul leaf's constant is shared: fixed
         t = max(1, -(-max(b.lb[:13]) // M28))
         s = 1
         while not all(k >= x for k, x in zip(kconst(s, t), b.lb)):
@@ -364,7 +550,12 @@ def search(vmax, fields=("Fp", "Fp2")):
     sub = auto
     try:
         for _ in range(4):  # the sites feed each other: iterate to the fixed point
-            check(vmax, fields)
+            if "lines" in fields:
+                check_lines(vmax)
+            elif "pair" in fields:
+                check_pair()
+            else:
+                check(vmax, fields)
     finally:
         sub = plain
     return dict(sorted(need.items()))

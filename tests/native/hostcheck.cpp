@@ -7,6 +7,7 @@
 #include "../../charon_amd/csrc/ops.h"
 #include "../../charon_amd/csrc/rlc.h"
 #include "../../charon_amd/csrc/ta_small.h"
+#include "../../charon_amd/csrc/pair28.h"
 #include <string.h>
 
 namespace hb {
@@ -601,5 +602,92 @@ extern "C" int hc_rlc_sum_g2_lazy(int k, const uint8_t* sigs, const uint32_t* ab
     coef[i] = {ab[2 * i], ab[2 * i + 1]};
   }
   g2_compress(out96, jac_to_aff(g2l_msm_ladder(tab, coef, 0, (uint32_t)k)));
+  return 0;
+}
+
+// ---- round 4: the Miller-loop arithmetic in lazy limbs (pair28.h) against the stored-word code
+static Fp hc_fp_in(const uint8_t* b) {
+  Fp r;
+  fp_from_be_raw(r, b);
+  return fp_to_mont(r);
+}
+static void hc_fp_out(uint8_t* b, const Fp& a) { fp_to_be_raw(b, fp_from_mont(a)); }
+static void hc_f2_out(uint8_t* b, const Fp2& a) {
+  hc_fp_out(b, a.c0);
+  hc_fp_out(b + 48, a.c1);
+}
+
+// The 68 lines of Q (x0 x1 y0 y1, canonical big-endian) by lines.h's stored-word chain and by
+// pair28.h line_chain28, canonical bytes (68 x 288 each); cnt: Fp products of each chain.
+extern "C" int hc_line_chain28(const uint8_t* q192, int eval, uint8_t* out_stored, uint8_t* out_lazy,
+                               unsigned long long* cnt) {
+  const G2A Q = {{hc_fp_in(q192), hc_fp_in(q192 + 48)}, {hc_fp_in(q192 + 96), hc_fp_in(q192 + 144)}, false};
+  LineEntryHost ls[N_LINES];
+  g_cnt_fp_mul = 0;
+  hc_line_chain(Q, ls, eval != 0);
+  cnt[0] = g_cnt_fp_mul;
+  for (int j = 0; j < N_LINES; j++) {
+    hc_f2_out(out_stored + 288 * j, ls[j].a0);
+    hc_f2_out(out_stored + 288 * j + 96, ls[j].a1);
+    hc_f2_out(out_stored + 288 * j + 192, ls[j].b1);
+  }
+  g_cnt_fp_mul = 0;
+  LineCoeffs ll[N_LINES];
+  auto put = [&](int j, const LineCoeffs& l) { ll[j] = l; };
+  if (eval) line_chain28<true>([&]() { return Q; }, put);
+  else line_chain28<false>([&]() { return Q; }, put);
+  cnt[1] = g_cnt_fp_mul;
+  int bad = 0;
+  for (int j = 0; j < N_LINES; j++) {
+    // reduced values join to stored words below 2p: check the stored-word invariant too
+    const Fp* v[6] = {&ll[j].a0.c0, &ll[j].a0.c1, &ll[j].a1.c0, &ll[j].a1.c1, &ll[j].b1.c0, &ll[j].b1.c1};
+    for (int k = 0; k < 6; k++) {
+      Fp d;
+      if (raw_sub_const(d, *v[k], P2_RAW) == 0) bad = 1;  // >= 2p
+      hc_fp_out(out_lazy + 288 * j + 48 * k, *v[k]);
+    }
+  }
+  return bad;
+}
+
+// The three-lane Fp12 operations of pair28.h (g4_sqr / g4_mul_line, the roles run one after the
+// other with the exchanges of pair3.h's Grp) against tower.h's f12_sqr / f12_mul_line.  f: 12 Fp in
+// tower order (c0.c0, c0.c1, c0.c2, c1.c0, c1.c1, c1.c2; Fp2 as c0, c1); line: a0, a1, b1.  out:
+// four Fp12 values, 576 B each: lanes' square, tower square, lanes' line product, tower line product.
+extern "C" int hc_g4_ops(const uint8_t* f576, const uint8_t* line288, uint8_t* out) {
+  Fp12 f;
+  Fp2* c[6] = {&f.c0.c0, &f.c0.c1, &f.c0.c2, &f.c1.c0, &f.c1.c1, &f.c1.c2};
+  for (int i = 0; i < 6; i++) *c[i] = {hc_fp_in(f576 + 96 * i), hc_fp_in(f576 + 96 * i + 48)};
+  const Fp2 a0 = {hc_fp_in(line288), hc_fp_in(line288 + 48)}, a1 = {hc_fp_in(line288 + 96), hc_fp_in(line288 + 144)},
+            b1 = {hc_fp_in(line288 + 192), hc_fp_in(line288 + 240)};
+  // lane k = (z_k, z_{k+3}) with z = (c0.c0, c1.c0, c0.c1, c1.c1, c0.c2, c1.c2); pair3.h g_from_f12
+  const Fp2 z[6] = {f.c0.c0, f.c1.c0, f.c0.c1, f.c1.c1, f.c0.c2, f.c1.c2};
+  F4L A[3];
+  for (int k = 0; k < 3; k++) A[k] = f4l_red(f4l_from(z[k], z[k + 3]));
+  const int P_[3] = {1, 0, 0}, Q_[3] = {2, 1, 2}, E_[3] = {0, 2, 1};
+  auto out12 = [](uint8_t* b, const F4L* L) {
+    Fp2 zz[6];
+    for (int k = 0; k < 3; k++) {
+      zz[k] = f2l_join(L[k].x);
+      zz[k + 3] = f2l_join(L[k].y);
+    }
+    const Fp2 t[6] = {zz[0], zz[2], zz[4], zz[1], zz[3], zz[5]};  // back to tower order
+    for (int i = 0; i < 6; i++) hc_f2_out(b + 96 * i, t[i]);
+  };
+  auto out12t = [](uint8_t* b, const Fp12& g) {
+    const Fp2 t[6] = {g.c0.c0, g.c0.c1, g.c0.c2, g.c1.c0, g.c1.c1, g.c1.c2};
+    for (int i = 0; i < 6; i++) hc_f2_out(b + 96 * i, t[i]);
+  };
+  F4L v[3], w[3], C[3];
+  for (int k = 0; k < 3; k++) g4_sqr_p1(A[k], A[P_[k]], A[Q_[k]], v[k], w[k]);
+  for (int k = 0; k < 3; k++) C[k] = g4_sqr_p2(k, w[k], v[P_[k]], v[Q_[k]], v[E_[k]]);
+  out12(out, C);
+  out12t(out + 576, f12_sqr(f));
+  const F2L la0 = f2l_from(a0), la1 = f2l_from(a1), lb1 = f2l_from(b1);
+  F4L Qn[3];
+  for (int k = 0; k < 3; k++) Qn[k] = g4_line_p1(A[k], la1);
+  for (int k = 0; k < 3; k++) C[k] = g4_line_p2(k, A[k], la0, lb1, Qn[(k + 1) % 3]);
+  out12(out + 1152, C);
+  out12t(out + 1728, f12_mul_line(f, a0, a1, b1));
   return 0;
 }

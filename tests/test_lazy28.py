@@ -232,3 +232,103 @@ def test_rlc_chunk_ladder_g2_lazy(lib):
         for p, (a, b) in zip(pts, ab):
             want = B.g2_add(want, B.g2_mul(p, (a + b * lam) % B.R))
         assert out.raw == B.g2_compress(want)
+
+
+# ---- round 4: the Miller-loop arithmetic in lazy limbs (charon_amd/csrc/pair28.h)
+
+def test_line_and_pair_bounds():
+    """the chain's point and lines, and the three-lane Fp12 steps, stay reduced below 2p"""
+    assert lazy28.check_lines(2) == {"dbl": 2.0, "add": 2.0}
+    assert lazy28.check_pair() == {"sqr": 2.0, "line": 2.0}
+
+
+@pytest.mark.parametrize("group,prefix", [("lines", "3"), ("pair", "4")])
+def test_line_pair_constants_are_minimal(group, prefix):
+    saved = dict(lazy28.KSITE)
+    try:
+        found = lazy28.search(2, (group,))
+    finally:
+        lazy28.KSITE.clear()
+        lazy28.KSITE.update(saved)
+    assert found == {k: v for k, v in saved.items() if k.startswith(prefix)}
+
+
+def test_constants_match_pair28():
+    src = open(os.path.join(ROOT, "charon_amd", "csrc", "pair28.h")).read()
+    k = lazy28.KSITE
+
+    def used(name, pat):
+        return sorted(tuple(map(int, m)) for m in re.findall(pat, _fn(src, name)))
+
+    sub = r"f2l_sub<(\d+), (\d+)>"
+    assert used("HD void l2_dbl_line", sub) == sorted([k["3D_a0"], k["3D_a1"], k["3D_AE"], k["3D_Y"]])
+    assert used("HD void l2_dbl_line", r"f2l_xi<(\d+), (\d+)>") == [k["3D_xi"]]
+    assert used("HD void l2_add_line", sub) == sorted(
+        [k["3A_th"], k["3A_la"], k["3A_H"], k["3A_a0"], k["3A_a1"], k["3A_Y"], k["3A_GH"]])
+    sq = {tuple(map(int, m)) for n in ("HD void l2_dbl_line", "HD void l2_add_line")
+          for m in re.findall(r"f2l_sqr_k<(\d+), (\d+)>", _fn(src, n))}
+    assert sq == {k["3Q"]}
+    # the Fp4 lane values: f4l_mul / f4l_sqr instantiations and the lane steps
+    assert re.findall(r"f4l_sqr<(\d+), (\d+), (\d+), (\d+)>", _fn(src, "HD void g4_sqr_p1")) == [
+        tuple(map(str, k["4Svxi"] + k["4Svy"]))] * 2
+    assert k["4Swxi"] == k["4Svxi"] and k["4Swy"] == k["4Svy"]
+    assert re.findall(r"f4l_sub<(\d+), (\d+)>", _fn(src, "HD F4L g4_sqr_p2")) == [tuple(map(str, k["4SD"]))]
+    assert re.findall(r"f4l_mul_s<(\d+), (\d+)>", _fn(src, "HD F4L g4_sqr_p2")) == [tuple(map(str, k["4Ss"]))]
+    assert re.findall(r"f4l_mul_s<(\d+), (\d+)>", _fn(src, "HD F4L g4_line_p2")) == [tuple(map(str, k["4Ls"]))]
+    assert re.findall(r"f4l_mul<(\d+), (\d+), (\d+), (\d+)>", _fn(src, "HD F4L g4_line_p2")) == [
+        tuple(map(str, k["4Lmxi"] + k["4Lmy"]))]
+    assert re.findall(r"f2l_sqr_k<(\d+), (\d+)>", _fn(src, "HD F4L f4l_sqr")) == [tuple(map(str, k["4Q"]))] * 3
+
+
+def _f2(b):
+    return (int.from_bytes(b[:48], "big"), int.from_bytes(b[48:96], "big"))
+
+
+def test_line_chain28_matches(lib):
+    """pair28.h line_chain28 (lazy limbs, lines reduced and joined) gives the stored-word chain's
+    68 lines (lines.h line_chain), unevaluated and at -g1, below 2p, with the same product count, on
+    subgroup points and random twist points.  Its doubling keeps T scaled by 4 (no halving: the same
+    projective point), so line j comes out multiplied by a nonzero Fp2 factor c_j -- the same for its
+    three coefficients, and killed by the final exponentiation (c_j^(p^2 - 1) = 1): checked as
+    proportionality, and exact equality for the first line (T not yet scaled)."""
+    lib.hc_line_chain28.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p,
+                                    ctypes.POINTER(ctypes.c_ulonglong)]
+    rng = random.Random(2840)
+    pts = [B.G2_GEN, B.g2_mul(B.G2_GEN, rng.randrange(1, B.R))] + [_random_twist_point(rng) for _ in range(3)]
+    for pt in pts:
+        (x0, x1), (y0, y1) = pt
+        raw = b"".join(v.to_bytes(48, "big") for v in (x0, x1, y0, y1))
+        for ev in (0, 1):
+            a = ctypes.create_string_buffer(68 * 288)
+            b = ctypes.create_string_buffer(68 * 288)
+            cnt = (ctypes.c_ulonglong * 2)()
+            assert lib.hc_line_chain28(raw, ev, a, b, cnt) == 0, "a lazy line at or above 2p"
+            assert a.raw[:288] == b.raw[:288]
+            for j in range(68):
+                s_ = [_f2(a.raw[288 * j + 96 * i:288 * j + 96 * i + 96]) for i in range(3)]
+                l_ = [_f2(b.raw[288 * j + 96 * i:288 * j + 96 * i + 96]) for i in range(3)]
+                k = next(i for i in range(3) if s_[i] != (0, 0))
+                c = B.f2_mul(l_[k], B.f2_inv(s_[k]))  # the line's factor
+                assert c != (0, 0) and all(B.f2_mul(c, s_[i]) == l_[i] for i in range(3)), j
+            assert cnt[0] == cnt[1] == 1571 + (68 * 4 if ev else 0)
+
+
+def _rand_f12(rng):
+    return b"".join(rng.randrange(B.P).to_bytes(48, "big") for _ in range(12))
+
+
+def test_g4_lane_ops_match_tower(lib):
+    """the three-lane Fp12 square and sparse-line product of pair28.h (the roles run in turn with
+    pair3.h's exchanges) equal tower.h's f12_sqr / f12_mul_line, on random values and edge values
+    (zero, one, p - 1 coordinates)"""
+    lib.hc_g4_ops.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p]
+    rng = random.Random(2841)
+    cases = [(_rand_f12(rng), b"".join(rng.randrange(B.P).to_bytes(48, "big") for _ in range(6))) for _ in range(8)]
+    pm1 = (B.P - 1).to_bytes(48, "big")
+    cases.append((pm1 * 12, pm1 * 6))
+    cases.append(((1).to_bytes(48, "big") + bytes(48 * 11), bytes(48 * 6)))
+    for f, ln in cases:
+        out = ctypes.create_string_buffer(4 * 576)
+        assert lib.hc_g4_ops(f, ln, out) == 0
+        assert out.raw[0:576] == out.raw[576:1152], "g4_sqr"
+        assert out.raw[1152:1728] == out.raw[1728:2304], "g4_mul_line"

@@ -50,6 +50,20 @@ pmc() {
    timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d "$P/write" -o run --output-format csv -- python3 "$B" $A > "$P.write.log" 2>&1)
 }
 
+# A/B of library builds on one box (HBLS_LIBRARY): ab TAG WORKLOAD label=path ... ; alternates
+# through the list twice, one bench line each (bench args from $AB_ARGS)
+ab() {
+  local wl=$1
+  shift
+  for rep in 1 2; do
+    for spec in "$@"; do
+      local lab=${spec%%=*} lib=${spec#*=}
+      HBLS_LIBRARY="$lib" timeout -k 10 400 python -u bench.py --workload "$wl" ${AB_ARGS:-$QUIET --key-tables 0} \
+        > "$O/ab_${TAG}_${wl}_${lab}_$rep.json" 2> "$O/ab_${TAG}_${wl}_${lab}_$rep.err" || return 1
+    done
+  done
+}
+
 case "$WHAT" in
   tests) tests "$@" ;;
   bench) bench "$@" ;;
@@ -57,5 +71,6 @@ case "$WHAT" in
   trace) trace "$@" ;;
   pmc) pmc ;;
   final) tests && smoke && lines && trace --steps 5 --warmup 2 --cpu-seconds 0 --callers 0 --aggregate-verify 0 --host-api 0 && pmc ;;
-  *) echo "usage: bash tools/gpu.sh tests|bench|lines|trace|pmc|final TAG [args]" >&2; exit 2 ;;
+  ab) ab "$@" ;;
+  *) echo "usage: bash tools/gpu.sh tests|bench|lines|trace|pmc|final|ab TAG [args]" >&2; exit 2 ;;
 esac
