@@ -691,3 +691,12 @@ extern "C" int hc_g4_ops(const uint8_t* f576, const uint8_t* line288, uint8_t* o
   out12t(out + 1728, f12_mul_line(f, a0, a1, b1));
   return 0;
 }
+
+// fp.h fp_inv (divsteps) against fp_inv_pow (a^(p-2)): x canonical big-endian; out: both inverses
+// (canonical), batches run
+extern "C" int hc_fp_inv(const uint8_t* x48, uint8_t* out96, int* batches) {
+  const Fp a = hc_fp_in(x48);
+  hc_fp_out(out96, fp_inv(a, batches));
+  hc_fp_out(out96 + 48, fp_inv_pow(a));
+  return 0;
+}
