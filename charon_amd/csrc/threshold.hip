@@ -649,6 +649,13 @@ __device__ __forceinline__ bool ta_small_uniform(const int64_t* __restrict__ csm
 }
 #endif
 
+#ifndef HB_TA_LAZY
+#define HB_TA_LAZY 1  // k_ta_sladder's ladder in ec28.h lazy limbs (0: stored words, A/B runs)
+#endif
+#ifndef HB_TA_SMALL_LAZY
+#define HB_TA_SMALL_LAZY 1  // k_ta_small's joint ladder likewise (round 4)
+#endif
+
 // One lane per validator: Q = sum_j [c_j] sigma_j (joint signed-binary NAF, the doublings shared by
 // the t members) into out[v t]; done[v] = 1, or 0 when the wave is not uniform.
 __global__ KB_OCC(HB_OCC_STRAUS) void k_ta_small(const HmEntry* __restrict__ pts, const uint32_t* __restrict__ src,
@@ -687,8 +694,26 @@ __global__ KB_OCC(HB_OCC_STRAUS) void k_ta_small(const HmEntry* __restrict__ pts
   }
   __syncthreads();
   const uint32_t m0 = vc * t;
-  G2J R = jac_infinity<Fp2>();
   const int top = naf_top;
+#if HB_TA_SMALL_LAZY
+  // the joint ladder in lazily reduced 28-bit limbs (ec28.h g2l_dbl / g2l_madd, as k_ta_sladder);
+  // a member at infinity (an undecodable partial, replaced by infinity in k_dec_sig_pt; its group's
+  // status comes from the member flags) is skipped, as jac_add_aff's infinity operand
+  G2L RL = g2l_infinity();
+  HB_NOUNROLL for (int i = top; i >= 0; i--) {
+    RL = g2l_dbl(RL);
+    HB_NOUNROLL for (uint32_t k = 0; k < t; k++) {
+      const int dg = naf[k][i];
+      if (dg != 0) {  // wave-uniform
+        const HmEntry e = pts[src ? src[m0 + k] : m0 + k];
+        const G2L S = g2l_madd(RL, f2l_from(e.x), f2l_from(dg < 0 ? f2_neg(e.y) : e.y));
+        if (!e.inf) RL = S;
+      }
+    }
+  }
+  const G2J R = g2l_to_jac(RL);
+#else
+  G2J R = jac_infinity<Fp2>();
   HB_NOUNROLL for (int i = top; i >= 0; i--) {
     R = jac_dbl(R);
     HB_NOUNROLL for (uint32_t k = 0; k < t; k++) {
@@ -700,6 +725,7 @@ __global__ KB_OCC(HB_OCC_STRAUS) void k_ta_small(const HmEntry* __restrict__ pts
       }
     }
   }
+#endif
   if (valid) {
     out[(size_t)v * t] = {R.X, R.Y, R.Z};
     done[v] = 1;
@@ -726,9 +752,6 @@ __global__ KB_OCC(HB_OCC_STRAUS) void k_ta_stab(const G2JEntry* __restrict__ q, 
 
 // One lane per validator of a wave k_ta_small took: [s] Q over Q's tables (k_ta_jladder's schedule
 // for one member), into the validator's first member slot of `out`, infinity into the others.
-#ifndef HB_TA_LAZY
-#define HB_TA_LAZY 1  // k_ta_sladder's ladder in ec28.h lazy limbs (0: stored words, A/B runs)
-#endif
 __global__ KB_OCC(HB_OCC_STRAUS) void k_ta_sladder(const TaDigits* __restrict__ sdig, const uint8_t* __restrict__ done,
                                                       uint32_t n_groups, uint32_t t, uint4* __restrict__ tab,
                                                       G2JEntry* __restrict__ out) {
