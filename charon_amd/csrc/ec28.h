@@ -360,6 +360,92 @@ HD F2L f2l_mul(const F2L& a, const F2L& b) {
 HD F2L f2l_sqr(const F2L& a) {
   return {l_mul(l_add(a.c0, a.c1), l_sub<36, 1>(a.c0, a.c1)), l_mul(l_shl(a.c0, 1), a.c1)};
 }
+// f2l_sqr with the site's constant K = S p
+template <uint32_t S, uint32_t T>
+HD F2L f2l_sqr_k(const F2L& a) {
+  return {l_mul(l_add(a.c0, a.c1), l_sub<S, T>(a.c0, a.c1)), l_mul(l_shl(a.c0, 1), a.c1)};
+}
+
+// Who computes a formula's Fp2 products.  F2One: this lane alone (f2l_mul / f2l_sqr_k).  F2Half
+// (device, below): the two lanes of a pair, both holding the operands, each computing one output
+// coefficient and taking the other from its partner -- half the multiply-adds on each lane's
+// dependent path, for the latency-bound calls.  The formulas below take the policy as their last
+// argument and multiply through fm / fs; the values are the same either way.
+struct F2One {};
+HD F2L fm(F2One, const F2L& a, const F2L& b) { return f2l_mul(a, b); }
+template <uint32_t S, uint32_t T>
+HD F2L fs(F2One, const F2L& a) { return f2l_sqr_k<S, T>(a); }
+
+#if defined(__HIP_DEVICE_COMPILE__)
+// x0 y0 + x1 y1 (one Montgomery pass, f2l_dot_core): x0 | x1 in the argument VGPRs, y0, y1 through
+// the per-lane LDS slot as f2l_mul_leaf's
+__device__ __noinline__ static u32x16 l_dot_leaf(u32x32 a) {
+  uint32_t x0[14], x1[14], y0[14], y1[14], r[14];
+  const uint32_t lane = threadIdx.x & (HB_ARG_LANES - 1u);
+  HB_UNROLL for (int k = 0; k < 14; k++) {
+    const uint2 v = hb_fp2_arg[k * HB_ARG_LANES + lane];
+    y0[k] = v.x;
+    y1[k] = v.y;
+    x0[k] = a[k];
+    x1[k] = a[16 + k];
+  }
+  f2l_dot_core(r, x0, x1, y0, y1);
+  u32x16 o;
+  HB_UNROLL for (int k = 0; k < 14; k++) o[k] = r[k];
+  return o;
+}
+__device__ __forceinline__ L28 l_dot(const L28& x0, const L28& x1, const L28& y0, const L28& y1) {
+  HB_COUNT_FP_MUL();
+  HB_COUNT_FP_MUL();
+  u32x32 av;
+  const uint32_t lane = threadIdx.x & (HB_ARG_LANES - 1u);
+  HB_UNROLL for (int k = 0; k < 14; k++) {
+    av[k] = x0.l[k];
+    av[16 + k] = x1.l[k];
+    hb_fp2_arg[k * HB_ARG_LANES + lane] = make_uint2(y0.l[k], y1.l[k]);
+  }
+  const u32x16 o = l_dot_leaf(av);
+  L28 r;
+  HB_UNROLL for (int k = 0; k < 14; k++) r.l[k] = o[k];
+  return r;
+}
+__device__ __forceinline__ L28 l_pick(bool take_b, const L28& a, const L28& b) {
+  L28 r;
+  HB_UNROLL for (int i = 0; i < 14; i++) r.l[i] = take_b ? b.l[i] : a.l[i];
+  return r;
+}
+__device__ __forceinline__ L28 l_xch(const L28& a, int addr) {  // the limbs of lane addr / 4
+  L28 r;
+  HB_UNROLL for (int i = 0; i < 14; i++) r.l[i] = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)a.l[i]);
+  return r;
+}
+// h: the coefficient this lane computes; partner: the other lane of the pair (ds_bpermute address).
+// Both lanes run the same instruction stream (operands chosen by select) and hold the same values.
+struct F2Half {
+  int h, partner;
+};
+__device__ __forceinline__ F2Half f2half_make() {  // pairs (2i, 2i + 1) of the wavefront
+  const int lane = (int)(threadIdx.x & 63u);
+  return {lane & 1, (lane ^ 1) << 2};
+}
+__device__ __forceinline__ F2L f2h_join(F2Half m, const L28& mine) {
+  const L28 other = l_xch(mine, m.partner);
+  return {l_pick(m.h != 0, mine, other), l_pick(m.h != 0, other, mine)};
+}
+// coefficient 0: a0 b0 + (K - a1) b1 (K = kF2N, as f2l_mul_core), coefficient 1: a0 b1 + a1 b0
+__device__ __forceinline__ F2L fm(F2Half m, const F2L& a, const F2L& b) {
+  L28 na1;
+  HB_UNROLL for (int j = 0; j < 14; j++) na1.l[j] = kF2N.l[j] - a.c1.l[j];
+  const bool h = m.h != 0;
+  return f2h_join(m, l_dot(a.c0, l_pick(h, na1, a.c1), l_pick(h, b.c0, b.c1), l_pick(h, b.c1, b.c0)));
+}
+// coefficient 0: (a0 + a1)(a0 + K - a1), coefficient 1: (2 a0) a1 (f2l_sqr_k's two products)
+template <uint32_t S, uint32_t T>
+__device__ __forceinline__ F2L fs(F2Half m, const F2L& a) {
+  const bool h = m.h != 0;
+  return f2h_join(m, l_mul(l_pick(h, l_add(a.c0, a.c1), l_shl(a.c0, 1)), l_pick(h, l_sub<S, T>(a.c0, a.c1), a.c1)));
+}
+#endif
 
 // ---- G2 Jacobian points in lazy limbs (E'(Fp2) has no 2-torsion either: h2 and r are odd)
 struct G2L {
@@ -370,16 +456,17 @@ struct G2L {
 // lazy28.py dbl2: D = 4 X B from one product, E = 3A normalised before its square, E W = 3 (A W);
 // the products in the order that ends the inputs' live ranges first (Z3 before B = Y^2, D1 right
 // after A) so that fewer values are held across the product calls
-HDNI G2L g2l_dbl(const G2L& p) {
+template <class M = F2One>
+HDNI G2L g2l_dbl(const G2L& p, M m = M()) {
   G2L r;
-  r.Z = f2l_mul(f2l_shl(p.Y, 1), p.Z);
-  const F2L B = f2l_sqr(p.Y);
-  const F2L A = f2l_sqr(p.X);
-  const F2L D1 = f2l_mul(p.X, B);
-  const F2L C = f2l_sqr(B);
-  const F2L F = f2l_sqr(f2l_norm(f2l_add(f2l_shl(A, 1), A)));
+  r.Z = fm(m, f2l_shl(p.Y, 1), p.Z);
+  const F2L B = fs<36, 1>(m, p.Y);
+  const F2L A = fs<36, 1>(m, p.X);
+  const F2L D1 = fm(m, p.X, B);
+  const F2L C = fs<36, 1>(m, B);
+  const F2L F = fs<36, 1>(m, f2l_norm(f2l_add(f2l_shl(A, 1), A)));
   r.X = f2l_norm(f2l_sub<9, 8>(F, f2l_shl(D1, 3)));
-  const F2L AW = f2l_mul(f2l_sub<11, 1>(f2l_shl(D1, 2), r.X), A);
+  const F2L AW = fm(m, f2l_sub<11, 1>(f2l_shl(D1, 2), r.X), A);
   r.Y = f2l_norm(f2l_sub<9, 8>(f2l_add(f2l_shl(AW, 1), AW), f2l_shl(C, 3)));
   r.inf = p.inf;
   return r;
@@ -394,24 +481,25 @@ HD G2L g2l_infinity() {
 }
 
 // lazy28.py madd2: madd-2007-bl with H normalised (its square is an Fp2 square)
-HDNI G2L g2l_madd(const G2L& p, const F2L& x2, const F2L& y2) {
+template <class M = F2One>
+HDNI G2L g2l_madd(const G2L& p, const F2L& x2, const F2L& y2, M m = M()) {
   if (p.inf) return {x2, y2, {l_from(fp_one()), l_from(fp_zero())}, false};
-  const F2L Z1Z1 = f2l_sqr(p.Z);
-  const F2L U2 = f2l_mul(x2, Z1Z1);
-  const F2L S2 = f2l_mul(f2l_mul(y2, p.Z), Z1Z1);
+  const F2L Z1Z1 = fs<36, 1>(m, p.Z);
+  const F2L U2 = fm(m, x2, Z1Z1);
+  const F2L S2 = fm(m, fm(m, y2, p.Z), Z1Z1);
   const F2L H = f2l_norm(f2l_sub<17, 1>(U2, p.X));
   const F2L rr = f2l_norm(f2l_sub<33, 2>(f2l_shl(S2, 1), f2l_shl(p.Y, 1)));
   if (f2l_is_zero(H)) {
-    if (f2l_is_zero(rr)) return g2l_dbl(p);
+    if (f2l_is_zero(rr)) return g2l_dbl(p, m);
     return g2l_infinity();
   }
-  const F2L HH = f2l_sqr(H);
-  const F2L J1 = f2l_mul(H, HH), V1 = f2l_mul(p.X, HH);
+  const F2L HH = fs<36, 1>(m, H);
+  const F2L J1 = fm(m, H, HH), V1 = fm(m, p.X, HH);
   G2L r;
-  r.X = f2l_norm(f2l_sub<13, 12>(f2l_sqr(rr), f2l_add(f2l_shl(J1, 2), f2l_shl(V1, 3))));
+  r.X = f2l_norm(f2l_sub<13, 12>(fs<36, 1>(m, rr), f2l_add(f2l_shl(J1, 2), f2l_shl(V1, 3))));
   r.Y = f2l_norm(
-      f2l_sub<9, 8>(f2l_mul(f2l_sub<16, 1>(f2l_shl(V1, 2), r.X), rr), f2l_shl(f2l_mul(p.Y, J1), 3)));
-  r.Z = f2l_mul(f2l_shl(p.Z, 1), H);
+      f2l_sub<9, 8>(fm(m, f2l_sub<16, 1>(f2l_shl(V1, 2), r.X), rr), f2l_shl(fm(m, p.Y, J1), 3)));
+  r.Z = fm(m, f2l_shl(p.Z, 1), H);
   r.inf = false;
   return r;
 }
@@ -437,26 +525,27 @@ HD G1J g1l_msm_ladder(const G1J* __restrict__ tab, const Pair* __restrict__ coef
 }
 
 // lazy28.py jadd2: add-2007-bl as g1l_add with H normalised (its square is an Fp2 square)
-HDNI G2L g2l_add(const G2L& p, const G2L& q) {
+template <class M = F2One>
+HDNI G2L g2l_add(const G2L& p, const G2L& q, M m = M()) {
   if (p.inf) return q;
   if (q.inf) return p;
-  const F2L Z1Z1 = f2l_sqr(p.Z), Z2Z2 = f2l_sqr(q.Z);
-  const F2L U1 = f2l_mul(p.X, Z2Z2), U2 = f2l_mul(q.X, Z1Z1);
-  const F2L S1 = f2l_mul(f2l_mul(p.Y, q.Z), Z2Z2);
-  const F2L S2 = f2l_mul(f2l_mul(q.Y, p.Z), Z1Z1);
+  const F2L Z1Z1 = fs<36, 1>(m, p.Z), Z2Z2 = fs<36, 1>(m, q.Z);
+  const F2L U1 = fm(m, p.X, Z2Z2), U2 = fm(m, q.X, Z1Z1);
+  const F2L S1 = fm(m, fm(m, p.Y, q.Z), Z2Z2);
+  const F2L S2 = fm(m, fm(m, q.Y, p.Z), Z1Z1);
   const F2L H = f2l_norm(f2l_sub<2, 1>(U2, U1));
   const F2L rr = f2l_norm(f2l_sub<3, 2>(f2l_shl(S2, 1), f2l_shl(S1, 1)));
   if (f2l_is_zero(H)) {
-    if (f2l_is_zero(rr)) return g2l_dbl(p);
+    if (f2l_is_zero(rr)) return g2l_dbl(p, m);
     return g2l_infinity();
   }
-  const F2L HH = f2l_sqr(H);
-  const F2L J1 = f2l_mul(H, HH), V1 = f2l_mul(U1, HH);
+  const F2L HH = fs<36, 1>(m, H);
+  const F2L J1 = fm(m, H, HH), V1 = fm(m, U1, HH);
   G2L r;
-  r.X = f2l_norm(f2l_sub<13, 12>(f2l_sqr(rr), f2l_add(f2l_shl(J1, 2), f2l_shl(V1, 3))));
+  r.X = f2l_norm(f2l_sub<13, 12>(fs<36, 1>(m, rr), f2l_add(f2l_shl(J1, 2), f2l_shl(V1, 3))));
   r.Y = f2l_norm(
-      f2l_sub<9, 8>(f2l_mul(f2l_sub<15, 1>(f2l_shl(V1, 2), r.X), rr), f2l_shl(f2l_mul(S1, J1), 3)));
-  r.Z = f2l_mul(f2l_mul(f2l_shl(p.Z, 1), q.Z), H);
+      f2l_sub<9, 8>(fm(m, f2l_sub<15, 1>(f2l_shl(V1, 2), r.X), rr), f2l_shl(fm(m, S1, J1), 3)));
+  r.Z = fm(m, fm(m, f2l_shl(p.Z, 1), q.Z), H);
   r.inf = false;
   return r;
 }
@@ -471,16 +560,16 @@ HD G2J g2l_to_jac(const G2L& p) {
 
 // [|x|] P for a Jacobian P in stored words (ec.h jac_mul_by_xabs), the ladder in lazy limbs;
 // `load` returns P again at each of the five additions (not held across the product calls)
-template <class LoadP>
-HDNI G2J g2l_mul_by_xabs_l(const LoadP& load) {
+template <class LoadP, class M = F2One>
+HDNI G2J g2l_mul_by_xabs_l(const LoadP& load, M m = M()) {
   G2L t = g2l_from_jac(load());
   HB_NOUNROLL for (int i = 62; i >= 0; i--) {
-    t = g2l_dbl(t);
+    t = g2l_dbl(t, m);
     if ((HB_X_ABS >> i) & 1) {
 #if defined(__HIP_DEVICE_COMPILE__)
       __asm__ volatile("" ::: "memory");
 #endif
-      t = g2l_add(t, g2l_from_jac(load()));
+      t = g2l_add(t, g2l_from_jac(load()), m);
     }
   }
   return g2l_to_jac(t);

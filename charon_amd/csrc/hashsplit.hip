@@ -14,6 +14,8 @@
 #define HB_FAST_FPMUL 1
 #include "layout.h"
 
+#include <stdlib.h>
+
 namespace hb {
 
 constexpr int HBLOCK = 64;
@@ -116,6 +118,43 @@ __global__ KB_OCC(HB_OCC_HASH) void k_h2c_clear2(uint32_t n, MsgEntry* __restric
 #endif
 }
 
+// The two ladder kernels with each message's G2 arithmetic split over a lane pair (ec28.h F2Half:
+// each lane computes one coefficient of every Fp2 product, ~60 % of the one-lane instruction
+// stream per lane): for calls with too few messages to fill the chip, where the ladders' latency,
+// not their lane-cycles, is what the caller waits for.  Same outputs as k_h2c_clear1 / 2.
+__global__ KB_OCC(HB_OCC_HASH) void k_h2c_clear1h(uint32_t n, MsgEntry* __restrict__ hm) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;
+  if (i >= n) return;  // both lanes of a pair
+  const F2Half m = f2half_make();
+  G2JEntry* q = h2c_q(hm + i);
+  G2J P;
+  {
+    const G2JEntry a = q[0], b = q[1];
+    P = jac_add(G2J{a.X, a.Y, a.Z}, G2J{b.X, b.Y, b.Z});
+  }
+  q[0] = {P.X, P.Y, P.Z};  // the same words from both lanes
+  const G2JEntry* src = q;
+  const G2J t1 = jac_neg(g2l_mul_by_xabs_l([src]() { return G2J{src->X, src->Y, src->Z}; }, m));
+  if (m.h == 0) q[1] = {t1.X, t1.Y, t1.Z};
+#endif
+}
+
+__global__ KB_OCC(HB_OCC_HASH) void k_h2c_clear2h(uint32_t n, MsgEntry* __restrict__ hm) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;
+  if (i >= n) return;
+  const F2Half m = f2half_make();
+  G2JEntry* q = h2c_q(hm + i);
+  const G2JEntry* src = q + 1;
+  const G2J t2 = jac_neg(g2l_mul_by_xabs_l([src]() { return G2J{src->X, src->Y, src->Z}; }, m));
+  if (m.h) return;
+  const G2JEntry ve = q[2];
+  const G2J h = jac_add(t2, G2J{ve.X, ve.Y, ve.Z});
+  q[0] = {h.X, h.Y, h.Z};
+#endif
+}
+
 __global__ KB_OCC(HB_OCC_HASH) void k_h2c_clear3(uint32_t n, MsgEntry* __restrict__ hm) {
 #if defined(__HIP_DEVICE_COMPILE__)
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -131,15 +170,32 @@ __global__ KB_OCC(HB_OCC_HASH) void k_h2c_clear3(uint32_t n, MsgEntry* __restric
 #endif
 }
 
+// messages up to which the ladders run on lane pairs (HBLS_HASH_PAIR_MAX, default 16384: 512
+// wavefronts, half a wave per SIMD -- below it the one-lane ladders leave the chip idle)
+static size_t hash_pair_max() {
+  static const size_t v = [] {
+    const char* e = getenv("HBLS_HASH_PAIR_MAX");
+    return e ? (size_t)strtoull(e, nullptr, 0) : (size_t)16384;
+  }();
+  return v;
+}
+
 void launch_hash_to_g2_split(const uint8_t* msgs, const uint64_t* off, const uint32_t* len, uint32_t n, MsgEntry* hm,
                              hipStream_t s) {
   if (!n) return;
   const unsigned g1 = (unsigned)(((size_t)n + HBLOCK - 1) / HBLOCK), g2 = (unsigned)((2 * (size_t)n + HBLOCK - 1) / HBLOCK);
+  const bool pair = n <= hash_pair_max();
   hipLaunchKernelGGL(k_h2c_field, dim3(g1), dim3(HBLOCK), 0, s, msgs, off, len, n, hm);
   hipLaunchKernelGGL(k_h2c_map, dim3(g2), dim3(HBLOCK), 0, s, n, hm);
-  hipLaunchKernelGGL(k_h2c_clear1, dim3(g1), dim3(HBLOCK), 0, s, n, hm);
+  if (pair)
+    hipLaunchKernelGGL(k_h2c_clear1h, dim3(g2), dim3(HBLOCK), 0, s, n, hm);
+  else
+    hipLaunchKernelGGL(k_h2c_clear1, dim3(g1), dim3(HBLOCK), 0, s, n, hm);
   hipLaunchKernelGGL(k_h2c_clear1b, dim3(g1), dim3(HBLOCK), 0, s, n, hm);
-  hipLaunchKernelGGL(k_h2c_clear2, dim3(g1), dim3(HBLOCK), 0, s, n, hm);
+  if (pair)
+    hipLaunchKernelGGL(k_h2c_clear2h, dim3(g2), dim3(HBLOCK), 0, s, n, hm);
+  else
+    hipLaunchKernelGGL(k_h2c_clear2, dim3(g1), dim3(HBLOCK), 0, s, n, hm);
   hipLaunchKernelGGL(k_h2c_clear3, dim3(g1), dim3(HBLOCK), 0, s, n, hm);
 }
 

@@ -19,6 +19,7 @@
 // tests/test_lazy28.py compares them.
 #pragma once
 #include "pair3.h"
+#include "pair6.h"
 
 namespace hb {
 
@@ -71,11 +72,6 @@ template <uint32_t S, uint32_t T>
 HD F2L f2l_xi(const F2L& a) {
   return {l_sub<S, T>(a.c0, a.c1), l_add(a.c0, a.c1)};
 }
-// ec28.h f2l_sqr with the site's constant: (a0 + a1)(a0 + K - a1) + 2 a0 a1 u
-template <uint32_t S, uint32_t T>
-HD F2L f2l_sqr_k(const F2L& a) {
-  return {l_mul(l_add(a.c0, a.c1), l_sub<S, T>(a.c0, a.c1)), l_mul(l_shl(a.c0, 1), a.c1)};
-}
 
 // ---- the Miller chain: T in homogeneous projective coordinates on the twist (pairing.h
 // miller_dbl_c / miller_add_c), the line as (a0, c1, c2) -- evaluated at P it is
@@ -91,39 +87,39 @@ struct Line28 {
 // Z3 = 8 A D -- the same projective point as miller_dbl_c's, no halving), A = Y^2, B = Z^2,
 // C = 3 b' B = 12 xi B, E = 3 C, D = Y Z; line (A - C, -3 X^2, 2 D), handed to put(Line28) as
 // soon as it exists.  The products run in the order that ends their inputs' live ranges first.
-template <class Put>
-HD void l2_dbl_line(G2P28& T, const Put& put) {
-  const F2L XX = f2l_sqr_k<78, 1>(T.X);
-  const F2L XY = f2l_mul(f2l_shl(T.X, 1), T.Y);
-  const F2L D = f2l_mul(T.Y, T.Z);
-  const F2L A = f2l_sqr_k<78, 1>(T.Y);
-  const F2L B = f2l_sqr_k<78, 1>(T.Z);
+template <class Put, class M = F2One>
+HD void l2_dbl_line(G2P28& T, const Put& put, M m = M()) {
+  const F2L XX = fs<78, 1>(m, T.X);
+  const F2L XY = fm(m, f2l_shl(T.X, 1), T.Y);
+  const F2L D = fm(m, T.Y, T.Z);
+  const F2L A = fs<78, 1>(m, T.Y);
+  const F2L B = fs<78, 1>(m, T.Z);
   const F2L xb = f2l_norm(f2l_xi<2, 1>(B));
   const F2L C = f2l_norm(f2l_add(f2l_shl(xb, 3), f2l_shl(xb, 2)));
   put(Line28{f2l_red(f2l_sub<38, 1>(A, C)), f2l_red(f2l_sub<4, 3>(f2l_zero(), f2l_add(f2l_shl(XX, 1), XX))),
              f2l_red(f2l_shl(D, 1))});
-  T.Z = f2l_red(f2l_shl(f2l_mul(A, D), 3));
+  T.Z = f2l_red(f2l_shl(fm(m, A, D), 3));
   const F2L E = f2l_add(f2l_shl(C, 1), C);
-  T.X = f2l_red(f2l_mul(XY, f2l_norm(f2l_sub<113, 3>(A, E))));
-  const F2L C2 = f2l_sqr_k<78, 1>(C);
-  T.Y = f2l_red(f2l_sub<47, 12>(f2l_sqr_k<78, 1>(f2l_norm(f2l_add(A, E))), f2l_add(f2l_shl(C2, 3), f2l_shl(C2, 2))));
+  T.X = f2l_red(fm(m, XY, f2l_norm(f2l_sub<113, 3>(A, E))));
+  const F2L C2 = fs<78, 1>(m, C);
+  T.Y = f2l_red(f2l_sub<47, 12>(fs<78, 1>(m, f2l_norm(f2l_add(A, E))), f2l_add(f2l_shl(C2, 3), f2l_shl(C2, 2))));
 }
 
 // lazy28.py ladd: T + Q (Q affine, reduced), the chord through T and Q, put(Line28) as above
-template <class Put>
-HD void l2_add_line(G2P28& T, const F2L& xq, const F2L& yq, const Put& put) {
-  const F2L th = f2l_norm(f2l_sub<2, 1>(T.Y, f2l_mul(yq, T.Z)));
-  const F2L la = f2l_norm(f2l_sub<2, 1>(T.X, f2l_mul(xq, T.Z)));
-  put(Line28{f2l_red(f2l_sub<2, 1>(f2l_mul(th, xq), f2l_mul(la, yq))), f2l_red(f2l_sub<5, 1>(f2l_zero(), th)),
+template <class Put, class M = F2One>
+HD void l2_add_line(G2P28& T, const F2L& xq, const F2L& yq, const Put& put, M m = M()) {
+  const F2L th = f2l_norm(f2l_sub<2, 1>(T.Y, fm(m, yq, T.Z)));
+  const F2L la = f2l_norm(f2l_sub<2, 1>(T.X, fm(m, xq, T.Z)));
+  put(Line28{f2l_red(f2l_sub<2, 1>(fm(m, th, xq), fm(m, la, yq))), f2l_red(f2l_sub<5, 1>(f2l_zero(), th)),
              f2l_red(la)});
-  const F2L C = f2l_sqr_k<78, 1>(th);
-  const F2L D = f2l_sqr_k<78, 1>(la);
-  const F2L E = f2l_mul(la, D);
-  const F2L G = f2l_mul(T.X, D);
-  const F2L H = f2l_norm(f2l_sub<3, 2>(f2l_add(E, f2l_mul(T.Z, C)), f2l_shl(G, 1)));
-  T.Z = f2l_red(f2l_mul(T.Z, E));
-  T.Y = f2l_red(f2l_sub<2, 1>(f2l_mul(th, f2l_norm(f2l_sub<6, 1>(G, H))), f2l_mul(T.Y, E)));
-  T.X = f2l_red(f2l_mul(la, H));
+  const F2L C = fs<78, 1>(m, th);
+  const F2L D = fs<78, 1>(m, la);
+  const F2L E = fm(m, la, D);
+  const F2L G = fm(m, T.X, D);
+  const F2L H = f2l_norm(f2l_sub<3, 2>(f2l_add(E, fm(m, T.Z, C)), f2l_shl(G, 1)));
+  T.Z = f2l_red(fm(m, T.Z, E));
+  T.Y = f2l_red(f2l_sub<2, 1>(fm(m, th, f2l_norm(f2l_sub<6, 1>(G, H))), fm(m, T.Y, E)));
+  T.X = f2l_red(fm(m, la, H));
 }
 
 // a chain line as stored words; EVAL: evaluated at -g1 (c1 xP, c2 yP: products of reduced values
@@ -180,18 +176,18 @@ HD F4L f4l_mul_s(const F4L& a) {
   return {f2l_xi<S, T>(a.y), a.x};
 }
 // lazy28.py f4_mul (Karatsuba, normalised): (t0 + xi t1, t2 - t0 - t1)
-template <uint32_t XS, uint32_t XT, uint32_t YS, uint32_t YT>
-HD F4L f4l_mul(const F4L& a, const F4L& b) {
-  const F2L t0 = f2l_mul(a.x, b.x), t1 = f2l_mul(a.y, b.y);
-  const F2L t2 = f2l_mul(f2l_add(a.x, a.y), f2l_add(b.x, b.y));
+template <uint32_t XS, uint32_t XT, uint32_t YS, uint32_t YT, class M = F2One>
+HD F4L f4l_mul(const F4L& a, const F4L& b, M m = M()) {
+  const F2L t0 = fm(m, a.x, b.x), t1 = fm(m, a.y, b.y);
+  const F2L t2 = fm(m, f2l_add(a.x, a.y), f2l_add(b.x, b.y));
   return f4l_norm({f2l_add(t0, f2l_xi<XS, XT>(t1)), f2l_sub<YS, YT>(t2, f2l_add(t0, t1))});
 }
 // lazy28.py f4_sqr: (x^2 + xi y^2, (x + y)^2 - x^2 - y^2), normalised
-template <uint32_t XS, uint32_t XT, uint32_t YS, uint32_t YT>
-HD F4L f4l_sqr(const F4L& a) {
-  const F2L t0 = f2l_sqr_k<9, 2>(a.x), t1 = f2l_sqr_k<9, 2>(a.y);
+template <uint32_t XS, uint32_t XT, uint32_t YS, uint32_t YT, class M = F2One>
+HD F4L f4l_sqr(const F4L& a, M m = M()) {
+  const F2L t0 = fs<9, 2>(m, a.x), t1 = fs<9, 2>(m, a.y);
   return f4l_norm({f2l_add(f2l_xi<XS, XT>(t1), t0),
-                   f2l_sub<YS, YT>(f2l_sqr_k<9, 2>(f2l_norm(f2l_add(a.x, a.y))), f2l_add(t0, t1))});
+                   f2l_sub<YS, YT>(fs<9, 2>(m, f2l_norm(f2l_add(a.x, a.y))), f2l_add(t0, t1))});
 }
 
 // The lane operations of pair3.h in two phases around their lane exchanges, so that the host
@@ -200,9 +196,10 @@ HD F4L f4l_sqr(const F4L& a) {
 // square (pair3.h g_sqr): phase 1 -- v = A^2, w = (A_p + A_q)^2 from the two roles != e(k);
 // phase 2 -- D = w - v_p - v_q, C = Y + [k != 2] s X with (X, Y) = (D, v_e) for k = 0, else
 // (v_e, D); reduced
-HD void g4_sqr_p1(const F4L& A, const F4L& Ap, const F4L& Aq, F4L& v, F4L& w) {
-  v = f4l_sqr<2, 1, 3, 2>(A);
-  w = f4l_sqr<2, 1, 3, 2>(f4l_add(Ap, Aq));
+template <class M = F2One>
+HD void g4_sqr_p1(const F4L& A, const F4L& Ap, const F4L& Aq, F4L& v, F4L& w, M m = M()) {
+  v = f4l_sqr<2, 1, 3, 2>(A, m);
+  w = f4l_sqr<2, 1, 3, 2>(f4l_add(Ap, Aq), m);
 }
 HD F4L g4_sqr_p2(int k, const F4L& w, const F4L& vp, const F4L& vq, const F4L& ve) {
   const F4L D = f4l_sub<9, 2>(w, f4l_add(vp, vq));
@@ -212,11 +209,56 @@ HD F4L g4_sqr_p2(int k, const F4L& w, const F4L& vp, const F4L& vq, const F4L& v
 }
 // product by a sparse line a0 + a1 v + b1 v w (pair3.h g_mul_line): phase 1 -- F a1, sent to the
 // role before; phase 2 -- C = F (a0 + b1 s) + [k == 2 ? s : 1] (F_{k+1} a1); reduced
-HD F4L g4_line_p1(const F4L& F, const F2L& a1) { return {f2l_mul(F.x, a1), f2l_mul(F.y, a1)}; }
-HD F4L g4_line_p2(int k, const F4L& F, const F2L& a0, const F2L& b1, const F4L& Qn) {
+template <class M = F2One>
+HD F4L g4_line_p1(const F4L& F, const F2L& a1, M m = M()) { return {fm(m, F.x, a1), fm(m, F.y, a1)}; }
+template <class M = F2One>
+HD F4L g4_line_p2(int k, const F4L& F, const F2L& a0, const F2L& b1, const F4L& Qn, M m = M()) {
   const F4L Qs = f4l_select(k == 2, f4l_mul_s<2, 1>(Qn), Qn);  // k == 2 ? Qn : s Qn
-  return f4l_red(f4l_add(f4l_mul<2, 1, 3, 2>(F, F4L{a0, b1}), Qs));
+  return f4l_red(f4l_add(f4l_mul<2, 1, 3, 2>(F, F4L{a0, b1}, m), Qs));
 }
+// ---- the final exponentiation's lane operations (pair3.h g_cyclo_sqr / g_mul / g_conj / g_frob)
+// in lazy limbs: lane values reduced (< 2p) in and out (lazy28.py g4_cyc / g4_mul / g4_conj /
+// g4_frob, sites "4C*", "4M*", "4J*", "4F*").
+// cyclotomic square: phase 1 -- t = A^2, sent to role e(k); phase 2 -- from the received te,
+// ts = s te for k = 1, else te; (3 ts.x - 2 A.x, 3 ts.y + 2 A.y), for k = 1 (3 ts.x + 2 A.x,
+// 3 ts.y - 2 A.y), the negated terms as K - 2A
+template <class M = F2One>
+HD F4L g4_cyc_p1(const F4L& A, M m = M()) { return f4l_sqr<2, 1, 3, 2>(A, m); }
+HD F4L g4_cyc_p2(int k, const F4L& te, const F4L& A) {
+  const F4L ts = f4l_select(k == 1, te, f4l_mul_s<5, 1>(te));
+  const F2L x3 = f2l_add(f2l_shl(ts.x, 1), ts.x), y3 = f2l_add(f2l_shl(ts.y, 1), ts.y);
+  const F2L ax2 = f2l_shl(A.x, 1), ay2 = f2l_shl(A.y, 1);
+  const F2L nx = f2l_sub<5, 2>(f2l_zero(), ax2), ny = f2l_sub<5, 2>(f2l_zero(), ay2);
+  return f4l_red({f2l_add(x3, f2l_select(k == 1, nx, ax2)), f2l_add(y3, f2l_select(k == 1, ay2, ny))});
+}
+// product (Karatsuba over the roles): phase 1 -- v = A B, w = (A_p + A_q)(B_p + B_q), the sums
+// normalised; phase 2 -- g4_sqr_p2's recombination (the same constants suffice, lazy28.py g4_mul)
+// (sa = A_p + A_q, sb = B_p + B_q: formed by the caller as the exchanged values arrive)
+template <class M = F2One>
+HD void g4_mul_p1(const F4L& A, const F4L& B, const F4L& sa, const F4L& sb, F4L& v, F4L& w, M m = M()) {
+  v = f4l_mul<2, 1, 3, 2>(A, B, m);
+  w = f4l_mul<2, 1, 3, 2>(f4l_norm(sa), f4l_norm(sb), m);
+}
+// f -> f^(p^6): (-x, y) for k = 1, else (x, -y); reduced
+HD F4L g4_conj(int k, const F4L& A) {
+  const F2L nx = f2l_sub<3, 1>(f2l_zero(), A.x), ny = f2l_sub<3, 1>(f2l_zero(), A.y);
+  return f4l_red({f2l_select(k == 1, A.x, nx), f2l_select(k == 1, ny, A.y)});
+}
+// f -> f^(p^J): the Fp2 coefficients conjugated for odd J, times FROBJ[k], FROBJ[k + 3] (products
+// of reduced values: below 2p as they come)
+template <int J, class M = F2One>
+HD F4L g4_frob(int k, const F4L& A, M m = M()) {
+  const uint32_t(*tab)[2][12] = (J == 1) ? FROB1 : (J == 2) ? FROB2 : FROB3;
+  const F2L cx = f2l_from(f2_from_const(tab[k])), cy = f2l_from(f2_from_const(tab[k + 3]));
+  F2L x = A.x, y = A.y;
+  if (J & 1) {
+    x.c1 = l_sub<3, 1>(l_zero(), x.c1);
+    y.c1 = l_sub<3, 1>(l_zero(), y.c1);
+  }
+  return {fm(m, x, cx), fm(m, y, cy)};
+}
+HD Fp4 f4l_join(const F4L& a) { return {f2l_join(a.x), f2l_join(a.y)}; }
+
 HD F4L g4_one_role(int k) {
   F4L r = {f2l_zero(), f2l_zero()};
   if (k == 0) r.x = f2l_one();
@@ -233,15 +275,70 @@ __device__ __forceinline__ L28 xch(const L28& a, int addr) {
 __device__ __forceinline__ F2L xch(const F2L& a, int addr) { return {xch(a.c0, addr), xch(a.c1, addr)}; }
 __device__ __forceinline__ F4L xch(const F4L& a, int addr) { return {xch(a.x, addr), xch(a.y, addr)}; }
 
-__device__ __forceinline__ F4L g4_one(const Grp& g) { return g4_one_role(g.k); }
-__device__ __forceinline__ F4L g4_sqr(const Grp& g, const F4L& A) {
+// Over a lane group G: Grp (three lanes, pair3.h; each lane its products alone) or Grp6 (six
+// lanes, pair6.h; each Fp2 product split over the role's two lanes, ec28.h F2Half)
+__device__ __forceinline__ F2One fe_m(const Grp&) { return {}; }
+__device__ __forceinline__ F2Half fe_m(const Grp6& g) { return {g.h, g.partner}; }
+template <class G>
+__device__ __forceinline__ F4L g4_one(const G& g) { return g4_one_role(g.k); }
+template <class G>
+__device__ __forceinline__ F4L g4_sqr(const G& g, const F4L& A) {
   F4L v, w;
-  g4_sqr_p1(A, xch(A, g.p), xch(A, g.q), v, w);
+  g4_sqr_p1(A, xch(A, g.p), xch(A, g.q), v, w, fe_m(g));
   return g4_sqr_p2(g.k, w, xch(v, g.p), xch(v, g.q), xch(v, g.e));
 }
-__device__ __forceinline__ F4L g4_mul_line(const Grp& g, const F4L& F, const F2L& a0, const F2L& a1, const F2L& b1) {
-  return g4_line_p2(g.k, F, a0, b1, xch(g4_line_p1(F, a1), g.n1));
+template <class G>
+__device__ __forceinline__ F4L g4_mul_line(const G& g, const F4L& F, const F2L& a0, const F2L& a1, const F2L& b1) {
+  return g4_line_p2(g.k, F, a0, b1, xch(g4_line_p1(F, a1, fe_m(g)), g.n1), fe_m(g));
 }
+
+// The final exponentiation in lazy limbs over G.  The one inversion runs in stored words (pair3.h
+// g_inv / pair6.h g6_inv).
+__device__ __forceinline__ Fp4 fe_inv(const Grp& g, const Fp4& A) { return g_inv(g, A); }
+__device__ __forceinline__ Fp4 fe_inv(const Grp6& g, const Fp4& A) { return g6_inv(g, A); }
+__device__ __forceinline__ bool fe_is_one(const Grp& g, const Fp4& A) { return g_is_one(g, A); }
+__device__ __forceinline__ bool fe_is_one(const Grp6& g, const Fp4& A) { return g6_is_one(g, A); }
+
+template <class G>
+__device__ __forceinline__ F4L g4_cyc(const G& g, const F4L& A) {
+  return g4_cyc_p2(g.k, xch(g4_cyc_p1(A, fe_m(g)), g.e), A);
+}
+template <class G>
+__device__ __forceinline__ F4L g4_mul(const G& g, const F4L& A, const F4L& B) {
+  F4L v, w;
+  const F4L sa = f4l_add(xch(A, g.p), xch(A, g.q));
+  const F4L sb = f4l_add(xch(B, g.p), xch(B, g.q));
+  g4_mul_p1(A, B, sa, sb, v, w, fe_m(g));
+  return g4_sqr_p2(g.k, w, xch(v, g.p), xch(v, g.q), xch(v, g.e));
+}
+template <class G>
+__device__ __forceinline__ F4L g4_pow_x(const G& g, const F4L& f) {
+  F4L r = f;
+  HB_NOUNROLL for (int i = 62; i >= 0; i--) {
+    r = g4_cyc(g, r);
+    if ((HB_X_ABS >> i) & 1) r = g4_mul(g, r, f);
+  }
+  return g4_conj(g.k, r);
+}
+// pair3.h g_final_exp's chain
+template <class G>
+__device__ __forceinline__ F4L g4_final_exp(const G& g, const F4L& f) {
+  const Fp4 fi = fe_inv(g, f4l_join(f));
+  F4L t = g4_mul(g, g4_conj(g.k, f), f4l_from(fi.x, fi.y));
+  t = g4_mul(g, g4_frob<2>(g.k, t, fe_m(g)), t);
+  F4L x = t, b = t;
+  HB_NOUNROLL for (int s = 0; s < 5; s++) {
+    const F4L px = g4_pow_x(g, x);
+    if (s == 3) b = x;
+    if (s < 2) x = g4_mul(g, px, g4_conj(g.k, x));
+    else if (s == 2) x = g4_mul(g, px, g4_frob<1>(g.k, x, fe_m(g)));
+    else x = px;
+  }
+  const F4L c = g4_mul(g, g4_mul(g, x, g4_frob<2>(g.k, b, fe_m(g))), g4_conj(g.k, b));
+  return g4_mul(g, c, g4_mul(g, g4_cyc(g, t), t));
+}
+template <class G>
+__device__ __forceinline__ bool g4_is_one(const G& g, const F4L& A) { return fe_is_one(g, f4l_join(A)); }
 #endif
 
 }  // namespace hb

@@ -13,13 +13,10 @@ namespace hb {
 
 constexpr int BLOCK = 64;
 
-// HB_MML28 / HB_LML28 = 0: the stored-word multi-Miller loop / fused lines+loop (A/B runs); default:
-// the lazy-limb arithmetic of pair28.h
+// HB_MML28 = 0: the stored-word multi-Miller loop (A/B runs); default: the lazy-limb arithmetic of
+// pair28.h
 #ifndef HB_MML28
 #define HB_MML28 1
-#endif
-#ifndef HB_LML28
-#define HB_LML28 1
 #endif
 
 // One lane per distinct message: the unevaluated line chain of H(m).
@@ -47,7 +44,7 @@ __device__ __forceinline__ size_t f_out_index(const Pair3Args& a, uint32_t e) {
   return (size_t)e * (a.f_out_stride ? a.f_out_stride : 1u) + a.f_out_off;
 }
 
-__device__ __forceinline__ Fp4 f4_load(const Fp4Entry& e) { return {e.x, e.y}; }
+__device__ __forceinline__ F4L f4l_load(const Fp4Entry& e) { return f4l_from(e.x, e.y); }
 
 template <int MODE>
 __global__ KB_OCC(HB_OCC_PAIR3) void k_pair3(Pair3Args a) {
@@ -71,13 +68,16 @@ __global__ KB_OCC(HB_OCC_PAIR3) void k_pair3(Pair3Args a) {
   uint32_t m = 0;
   const LineEntry* ml = nullptr;
   if (MODE == P3_PROD) {  // wave-uniform trip count; idle lanes multiply by one
+    // (stored words: a chain of products alone, where pair28.h's per-step reductions cost more than
+    // its lazy additions save -- 1.02 vs 1.13 ms per C3 slot, profiles/r04d_ab_summary.txt)
     const uint32_t first = e * a.f_range;
     const uint32_t cnt = first < a.f_n ? min(a.f_range, a.f_n - first) : 0u;
     Fp4 f = g_one(g);
     HB_NOUNROLL for (uint32_t j = 0; j < a.f_range; j++) {
       const uint32_t idx = j < cnt ? first + j : 0u;
+      const Fp4Entry& v = a.f_in[3ull * idx + g.k];
       Fp4 t;
-      f4_select(t, j >= cnt, f4_load(a.f_in[3ull * idx + g.k]), g_one(g));
+      f4_select(t, j >= cnt, Fp4{v.x, v.y}, g_one(g));
       f = g_mul(g, f, t);
     }
     if (valid) a.f_out[3 * f_out_index(a, e) + g.k] = Fp4Entry{f.x, f.y};
@@ -147,21 +147,26 @@ __global__ KB_OCC(HB_OCC_PAIR3) void k_pair3(Pair3Args a) {
   const LineEntry* sl = a.sig_lines + u;
   // Lines in loop order: for each bit i = 62..0 of |x| a doubling line (preceded by f^2 except
   // at the top) and, if bit i is set, an addition line.  One copy of the line products.  FIN without
-  // sig_lines: no loop (its factors come stored, the signature side's from MLS).
-  Fp4 f = g_one(g);
+  // sig_lines: no loop (its factors come stored, the signature side's from MLS).  The accumulator
+  // and the final exponentiation in lazy limbs (pair28.h), reduced below 2p after every step.
+  F4L f = g4_one(g);
+  const L28 px = l_from(P.x), py = l_from(P.y);
   int bit = 62;
   bool pending_add = false;
   const int n_lines = (MODE == P3_FIN && !a.sig_lines) ? 0 : N_LINES;
   HB_NOUNROLL for (int j = 0; j < n_lines; j++) {
     const bool dbl = !pending_add;
-    if (dbl && j > 0) f = g_sqr(g, f);
+    if (dbl && j > 0) f = g4_sqr(g, f);
     if (MODE != P3_FIN && MODE != P3_MLS) {
-      LineEntry L = ml[j];
-      f = g_mul_line(g, f, L.a0, f2_mul_fp(L.a1, P.x), f2_mul_fp(L.b1, P.y));
+      F2L l0, l1, l2;
+      line_split(ml[j], l0, l1, l2);
+      // evaluated at P: c1 xP, c2 yP (products of reduced values: below 2p)
+      f = g4_mul_line(g, f, l0, F2L{l_mul(l1.c0, px), l_mul(l1.c1, px)}, F2L{l_mul(l2.c0, py), l_mul(l2.c1, py)});
     }
     if (MODE != P3_ML) {
-      LineEntry S = sl[(size_t)j * a.stride];
-      f = g_mul_line(g, f, S.a0, S.a1, S.b1);
+      F2L s0, s1, s2;
+      line_split(sl[(size_t)j * a.stride], s0, s1, s2);
+      f = g4_mul_line(g, f, s0, s1, s2);
     }
     if (dbl) {
       pending_add = ((HB_X_ABS >> bit) & 1) != 0;
@@ -171,15 +176,14 @@ __global__ KB_OCC(HB_OCC_PAIR3) void k_pair3(Pair3Args a) {
     }
   }
   if (MODE == P3_ML) {
-    Fp4 r;
-    f4_select(r, a.pk_st && a.pk_st[e], f, g_one(g));
-    if (valid) a.f_out[3 * f_out_index(a, e) + g.k] = Fp4Entry{r.x, r.y};
+    const F4L r = f4l_select(a.pk_st && a.pk_st[e], f, g4_one(g));
+    if (valid) a.f_out[3 * f_out_index(a, e) + g.k] = f4l_store(r);
     // groups of the small calls: the byte P3_FULL's verdict rules would fail without a pairing
     if (a.f_bad && valid && g.k == 0) a.f_bad[e] = ((a.pk_st && a.pk_st[e]) || P.inf || a.hm[m].h.inf) ? 1 : 0;
     return;
   }
   if (MODE == P3_MLS) {
-    if (valid) a.f_out[3 * f_out_index(a, e) + g.k] = Fp4Entry{f.x, f.y};
+    if (valid) a.f_out[3 * f_out_index(a, e) + g.k] = f4l_store(f);
     return;
   }
   if (MODE == P3_FIN) {  // times the stored Miller loops of entries [e f_range, ...) (wave-uniform trip count)
@@ -187,13 +191,11 @@ __global__ KB_OCC(HB_OCC_PAIR3) void k_pair3(Pair3Args a) {
     const uint32_t cnt = first < a.f_n ? min(a.f_range, a.f_n - first) : 0u;
     HB_NOUNROLL for (uint32_t j = 0; j < a.f_range; j++) {
       const uint32_t idx = j < cnt ? first + j : 0u;
-      Fp4 t;
-      f4_select(t, j >= cnt, f4_load(a.f_in[3ull * idx + g.k]), g_one(g));
-      f = g_mul(g, f, t);
+      f = g4_mul(g, f, f4l_select(j >= cnt, f4l_load(a.f_in[3ull * idx + g.k]), g4_one(g)));
     }
   }
-  f = g_final_exp(g, f);
-  const bool one = g_is_one(g, f);
+  f = g4_final_exp(g, f);
+  const bool one = g4_is_one(g, f);
   if (valid && g.k == 0) {
     uint8_t s;
     if (MODE == P3_FIN) s = (a.pk_st && a.pk_st[e]) ? (uint8_t)1 : (one ? ST_OK : ST_NOT_VERIFIED);
@@ -222,15 +224,14 @@ __global__ KB_OCC(HB_OCC_PAIR3) void k_pair6_fin(Pair3Args a) {
   const uint32_t e = valid ? unit : a.n - 1;
   const uint32_t first = e * a.f_range;
   const uint32_t cnt = first < a.f_n ? min(a.f_range, a.f_n - first) : 0u;
-  Fp4 f = g6_one(g);
+  F4L f = g4_one(g);
   HB_NOUNROLL for (uint32_t j = 0; j < a.f_range; j++) {
     const uint32_t idx = j < cnt ? first + j : 0u;
-    Fp4 t;
-    f4_select(t, j >= cnt, f4_load(a.f_in[3ull * idx + g.k]), g6_one(g));
-    f = j == 0 ? t : g6_mul(g, f, t);
+    const F4L t = f4l_select(j >= cnt, f4l_load(a.f_in[3ull * idx + g.k]), g4_one(g));
+    f = j == 0 ? t : g4_mul(g, f, t);
   }
-  f = g6_final_exp(g, f);
-  const bool one = g6_is_one(g, f);
+  f = g4_final_exp(g, f);  // pair28.h, each Fp2 product split over the role's two lanes
+  const bool one = g4_is_one(g, f);
   if (valid && g.k == 0 && g.h == 0)
     a.status[e] = (a.pk_st && a.pk_st[e]) ? (uint8_t)1 : (one ? ST_OK : ST_NOT_VERIFIED);
 #endif
@@ -276,14 +277,29 @@ void launch_mml_eval(const Pair3Args& a, LineEntry* ev, hipStream_t s) {
 
 // The (-g1, S) Miller loop of ONE point S (Jacobian), its lines produced and consumed at once: a
 // two-wave workgroup per point -- wave 0 steps T through the chain of S (affine first) and hands
-// each line, evaluated at -g1, over through LDS; wave 1 (three lanes, pair3.h) squares and
-// multiplies it into f while wave 0 already computes the next.  The chain's latency is then about
-// one of the two halves instead of k_slines followed by k_pair3<MLS> (the slot-wide check's signature
-// side: a tail of every slot, on the critical path of small slots).  bad[e] = 1 for S at infinity.
+// each line, evaluated at -g1, over through LDS; wave 1 squares and multiplies it into f while wave
+// 0 already computes the next.  The chain's latency is then about one of the two halves instead of
+// k_slines followed by k_pair3<MLS> (the slot-wide check's signature side: a tail of every slot, on
+// the critical path of small slots).  bad[e] = 1 for S at infinity.
+// Both halves in lazy limbs (pair28.h) with every Fp2 product split over two lanes (ec28.h
+// F2Half): the producer's chain on lanes (0, 1), the consumer's Fp12 over six lanes (pair6.h Grp6),
+// each lane's instruction stream ~60 % of the one-lane / three-lane one -- this kernel is
+// latency-bound (one workgroup per point, few points).
 // SIDE 1 (the small calls' group checks): the (P_g, H(m_g)) loop instead, H(m_g) affine from the
 // message table (its lines need not exist yet: only the hashing is waited for), the lines
 // evaluated at P_g by the consumer; bad[e] = the group fails without a pairing (state, P or H(m)
 // at infinity), as k_pair3<ML>'s f_bad.
+// (c1 x, c2 y) for a line's c1, c2 and a point's x, y (reduced), the four Fp products split over the
+// pair: lane h computes the coefficient-h halves
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ void line_eval_h(F2Half m, F2L& c1, F2L& c2, const L28& x, const L28& y) {
+  const bool h = m.h != 0;
+  const L28 e1 = l_mul(l_pick(h, c1.c0, c1.c1), x), e2 = l_mul(l_pick(h, c2.c0, c2.c1), y);
+  c1 = f2h_join(m, e1);
+  c2 = f2h_join(m, e2);
+}
+#endif
+
 template <int SIDE>
 __global__ __launch_bounds__(128, 1) void k_lml(LmlArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -292,93 +308,59 @@ __global__ __launch_bounds__(128, 1) void k_lml(LmlArgs a) {
   if (e >= a.n) return;  // workgroup-uniform
   __shared__ LineEntry buf[2];
   __shared__ uint32_t sinf;
-  const bool producer = threadIdx.x < 64;
-#if HB_LML28
-  G2P28 T;
   __shared__ HmEntry qsh;  // the producer's affine point, re-read at the chain's additions
-#else
-  G2Proj T;
-#endif
-  G2A Q;
+  const bool producer = threadIdx.x < 64;
+  const F2Half hm2 = f2half_make();
+  G2P28 T;
   if (producer) {
+    G2A Q;
     if (SIDE == 0) {
       const G2JEntry pe = a.pts[e];
       Q = jac_to_aff(G2J{pe.X, pe.Y, pe.Z});
     } else {
       Q = hm_load(a.hm[a.msg_idx[e]].h);
     }
-#if HB_LML28
     T = {f2l_from(Q.x), f2l_from(Q.y), f2l_one()};
-    if (threadIdx.x == 0) qsh = HmEntry{Q.x, Q.y, 0u, {0u, 0u, 0u}};
-#else
-    T = {Q.x, Q.y, f2_one()};
-#endif
-    if (threadIdx.x == 0) sinf = Q.inf ? 1u : 0u;
+    if (threadIdx.x == 0) {
+      qsh = HmEntry{Q.x, Q.y, 0u, {0u, 0u, 0u}};
+      sinf = Q.inf ? 1u : 0u;
+    }
   }
   G1AEntry P{};
   if (SIDE == 1 && !producer) P = a.pk[e];
-  Grp g = grp_make();
-#if HB_LML28
+  const Grp6 g = grp6_make();
   F4L f = g4_one(g);
-  F2L px, py;  // SIDE 1: P's coordinates, the consumer evaluates at P
-  if (SIDE == 1) {
-    px = {l_from(P.x), l_zero()};
-    py = {l_from(P.y), l_zero()};
-  }
-#else
-  Fp4 f = g_one(g);
-#endif
-  int bit = 62;        // consumer: the loop schedule of k_pair3
+  const L28 px = l_from(P.x), py = l_from(P.y);  // SIDE 1: the consumer evaluates at P
+  int bit = 62;  // consumer: the loop schedule of k_pair3
   bool pending_add = false;
-  int pbit = 62;       // producer: the chain schedule of line_chain
+  int pbit = 62;  // producer: the chain schedule of line_chain
   bool padd = false;
   HB_NOUNROLL for (int j = 0; j <= N_LINES; j++) {
     if (producer && j < N_LINES) {
-#if HB_LML28
       auto put = [&](const Line28& l28) {
-        const LineCoeffs l = SIDE == 0 ? line28_store<true>(l28) : line28_store<false>(l28);
-        if (threadIdx.x == 0) buf[j & 1] = {l.a0, l.a1, l.b1};
+        F2L c1 = l28.a1, c2 = l28.b1;
+        if (SIDE == 0)  // at -g1
+          line_eval_h(hm2, c1, c2, l_from(fp_from_const(G1_GEN_X)), l_from(fp_from_const(G1_GEN_NEG_Y)));
+        if (threadIdx.x == 0) buf[j & 1] = {f2l_join(l28.a0), f2l_join(c1), f2l_join(c2)};
       };
       if (!padd) {
-        l2_dbl_line(T, put);
+        l2_dbl_line(T, put, hm2);
         padd = ((HB_X_ABS >> pbit) & 1) != 0;
         pbit--;
       } else {
         const HmEntry qe = qsh;
-        l2_add_line(T, f2l_from(qe.x), f2l_from(qe.y), put);
+        l2_add_line(T, f2l_from(qe.x), f2l_from(qe.y), put, hm2);
         padd = false;
       }
-#else
-      LineCoeffs l;
-      if (!padd) {
-        l = miller_dbl_c(T);
-        padd = ((HB_X_ABS >> pbit) & 1) != 0;
-        pbit--;
-      } else {
-        l = miller_add_c(T, Q.x, Q.y);
-        padd = false;
-      }
-      if (SIDE == 0) line_eval(l, fp_from_const(G1_GEN_X), fp_from_const(G1_GEN_NEG_Y));
-      if (threadIdx.x == 0) buf[j & 1] = {l.a0, l.a1, l.b1};
-#endif
     }
     if (!producer && j > 0) {
       const LineEntry L = buf[(j - 1) & 1];
       const bool dbl = !pending_add;
-#if HB_LML28
       if (dbl && j > 1) f = g4_sqr(g, f);
       F2L l0, l1, l2;
       line_split(L, l0, l1, l2);
-      if (SIDE == 1) {  // c1 xP, c2 yP (products of reduced values: below 2p)
-        l1 = {l_mul(l1.c0, px.c0), l_mul(l1.c1, px.c0)};
-        l2 = {l_mul(l2.c0, py.c0), l_mul(l2.c1, py.c0)};
-      }
+      if (SIDE == 1) line_eval_h(hm2, l1, l2, px, py);  // c1 xP, c2 yP (products of reduced values: below 2p)
       f = g4_mul_line(g, f, l0, l1, l2);
-#else
-      if (dbl && j > 1) f = g_sqr(g, f);
-      if (SIDE == 0) f = g_mul_line(g, f, L.a0, L.a1, L.b1);
-      else f = g_mul_line(g, f, L.a0, f2_mul_fp(L.a1, P.x), f2_mul_fp(L.b1, P.y));
-#endif
       if (dbl) {
         pending_add = ((HB_X_ABS >> bit) & 1) != 0;
         bit--;
@@ -388,13 +370,9 @@ __global__ __launch_bounds__(128, 1) void k_lml(LmlArgs a) {
     }
     __syncthreads();
   }
-  if (!producer && threadIdx.x < 64 + 3) {
+  if (!producer && threadIdx.x < 64 + 6 && g.h == 0) {
     const size_t o = (size_t)e * (a.f_stride ? a.f_stride : 1u) + a.f_off;
-#if HB_LML28
     a.f_out[3 * o + g.k] = f4l_store(f);
-#else
-    a.f_out[3 * o + g.k] = Fp4Entry{f.x, f.y};
-#endif
     if (threadIdx.x == 64 && a.bad)
       a.bad[e] = SIDE == 0 ? (uint8_t)sinf : (uint8_t)((a.pk_st && a.pk_st[e]) || P.inf || sinf ? 1 : 0);
   }

@@ -210,6 +210,10 @@ KSITE = {
     "3Q": (78, 1),
     "4Lmxi": (2, 1), "4Lmy": (3, 2), "4Ls": (2, 1), "4Q": (9, 2), "4SD": (9, 2), "4Ss": (14, 4),
     "4Svxi": (2, 1), "4Svy": (3, 2), "4Swxi": (2, 1), "4Swy": (3, 2),
+    # the final exponentiation's lane operations (cyclotomic square "C", product "M", conjugate "J",
+    # Frobenius "F"); they share 4Q with the Miller loop's squares
+    "4Cn": (5, 2), "4Cs": (5, 1), "4Cvxi": (2, 1), "4Cvy": (3, 2), "4Fn": (3, 1), "4Jn": (3, 1),
+    "4MD": (9, 2), "4Ms": (14, 4), "4Mvxi": (2, 1), "4Mvy": (3, 2), "4Mwxi": (2, 1), "4Mwy": (3, 2),
 }
 
 
@@ -501,6 +505,58 @@ def check_pair():
     return out
 
 
+# the final exponentiation's lane operations (pair28.h g4_cyc / g4_mul / g4_conj / g4_frob)
+def g4_cyc(A):
+    """pair28.h g4_cyc_p1 / g4_cyc_p2 (pair3.h g_cyclo_sqr): t = A^2 (sent to role e(k)); from the
+    received te: ts = s te for k = 1, else te; (3 ts.x - 2 A.x, 3 ts.y + 2 A.y), for k = 1
+    (3 ts.x + 2 A.x, 3 ts.y - 2 A.y), the negated terms as K - 2A; reduced"""
+    t = f4_sqr(A, "Cv")
+    ts = bmax(f4_mul_s(t, "Cs"), t)
+    x3 = f2_add(f2_shl(ts[0], 1), ts[0])
+    y3 = f2_add(f2_shl(ts[1], 1), ts[1])
+    ax2, ay2 = f2_shl(A[0], 1), f2_shl(A[1], 1)
+    nx, ny = f2_sub(ZERO2, ax2, "4Cn"), f2_sub(ZERO2, ay2, "4Cn")
+    return f4_red((f2_add(x3, bmax(ax2, nx)), f2_add(y3, bmax(ay2, ny))))
+
+
+def g4_mul(A, B):
+    """pair28.h g4_mul_p1 / g4_mul_p2 (pair3.h g_mul): v = A B, w = (A_p + A_q)(B_p + B_q) with the
+    sums normalised, the recombination of g4_sqr with its own constants; reduced"""
+    v = f4_mul(A, B, "Mv")
+    w = f4_mul(f4_norm(f4_add(A, A)), f4_norm(f4_add(B, B)), "Mw")
+    D = f4_sub(w, f4_add(v, v), "MD")
+    X = bmax(D, v)
+    Y = bmax(v, D)
+    sx = bmax(f4_mul_s(X, "Ms"), X)
+    return f4_red(f4_add(Y, sx))
+
+
+def g4_conj(A):
+    """pair28.h g4_conj: (K - x, y) for k = 1, else (x, K - y); reduced"""
+    return f4_red((bmax(A[0], f2_sub(ZERO2, A[0], "4Jn")), bmax(A[1], f2_sub(ZERO2, A[1], "4Jn"))))
+
+
+def g4_frob(A, c):
+    """pair28.h g4_frob: the Fp2 coefficients conjugated (odd J: c1 -> K - c1), times the reduced
+    constants -- products of reduced values, below 2p without a reduction"""
+    def cj(a):
+        return (a[0], bmax(a[1], sub(ZERO2[0], a[1], "4Fn")))
+    return (f2_mul(cj(A[0]), c, "2N"), f2_mul(cj(A[1]), c, "2N"))
+
+
+def check_fe():
+    """the final exponentiation's lane values: reduced (< 2p) in, reduced out, every operation"""
+    A = (Fp2Ops.nrm(2 * P), Fp2Ops.nrm(2 * P))
+    c = Fp2Ops.nrm(2 * P)
+    out = {}
+    for op, fn in (("cyc", lambda: g4_cyc(A)), ("mul", lambda: g4_mul(A, A)), ("conj", lambda: g4_conj(A)),
+                   ("frob", lambda: g4_frob(A, c))):
+        r = fn()
+        assert all(fits(x, 2 * P) for x in r), op
+        out[op] = max(vmax_of(x) for x in r) / P
+    return out
+
+
 def fits(x, vmax):
     return vmax_of(x) <= vmax and all(
         all(l <= M28 for l in b.lb[:13]) and b.lb[13] <= (vmax >> 364) for b in ([x] if isinstance(x, Bound) else x))
@@ -536,7 +592,7 @@ def search(vmax, fields=("Fp", "Fp2")):
     need = {}
 
     def auto(a, b, site):
-        if site == "2N" and ("lines" in fields or "pair" in fields):
+        if site == "2N" and ("lines" in fields or "pair" in fields or "fe" in fields):
             return plain(a, b, site)  # the f2l_mul leaf's constant is shared: fixed
         t = max(1, -(-max(b.lb[:13]) // M28))
         s = 1
@@ -554,6 +610,8 @@ def search(vmax, fields=("Fp", "Fp2")):
                 check_lines(vmax)
             elif "pair" in fields:
                 check_pair()
+            elif "fe" in fields:
+                check_fe()
             else:
                 check(vmax, fields)
     finally:

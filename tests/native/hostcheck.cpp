@@ -692,6 +692,93 @@ extern "C" int hc_g4_ops(const uint8_t* f576, const uint8_t* line288, uint8_t* o
   return 0;
 }
 
+// pair28.h's final exponentiation in lazy limbs, the three roles emulated (F2One), against
+// pairing.h final_exponentiation: f576 tower order (as hc_g4_ops); out: both results (576 + 576)
+extern "C" int hc_fe28(const uint8_t* f576, uint8_t* out) {
+  Fp12 f;
+  Fp2* c[6] = {&f.c0.c0, &f.c0.c1, &f.c0.c2, &f.c1.c0, &f.c1.c1, &f.c1.c2};
+  for (int i = 0; i < 6; i++) *c[i] = {hc_fp_in(f576 + 96 * i), hc_fp_in(f576 + 96 * i + 48)};
+  auto lanes = [](const Fp12& g, F4L* A) {
+    const Fp2 z[6] = {g.c0.c0, g.c1.c0, g.c0.c1, g.c1.c1, g.c0.c2, g.c1.c2};
+    for (int k = 0; k < 3; k++) A[k] = f4l_red(f4l_from(z[k], z[k + 3]));
+  };
+  auto tower = [](const F4L* L) {
+    Fp2 z[6];
+    for (int k = 0; k < 3; k++) {
+      z[k] = f2l_join(L[k].x);
+      z[k + 3] = f2l_join(L[k].y);
+    }
+    Fp12 g;
+    g.c0 = {z[0], z[2], z[4]};
+    g.c1 = {z[1], z[3], z[5]};
+    return g;
+  };
+  const int P_[3] = {1, 0, 0}, Q_[3] = {2, 1, 2}, E_[3] = {0, 2, 1};
+  struct L3 {
+    F4L v[3];
+  };
+  auto cyc = [&](const L3& A) {
+    L3 t, r;
+    for (int k = 0; k < 3; k++) t.v[k] = g4_cyc_p1(A.v[k]);
+    for (int k = 0; k < 3; k++) r.v[k] = g4_cyc_p2(k, t.v[E_[k]], A.v[k]);
+    return r;
+  };
+  auto mul = [&](const L3& A, const L3& B) {
+    L3 v, w, r;
+    for (int k = 0; k < 3; k++)
+      g4_mul_p1(A.v[k], B.v[k], f4l_add(A.v[P_[k]], A.v[Q_[k]]), f4l_add(B.v[P_[k]], B.v[Q_[k]]), v.v[k], w.v[k]);
+    for (int k = 0; k < 3; k++) r.v[k] = g4_sqr_p2(k, w.v[k], v.v[P_[k]], v.v[Q_[k]], v.v[E_[k]]);
+    return r;
+  };
+  auto conj = [&](const L3& A) {
+    L3 r;
+    for (int k = 0; k < 3; k++) r.v[k] = g4_conj(k, A.v[k]);
+    return r;
+  };
+  auto frob1 = [&](const L3& A) {
+    L3 r;
+    for (int k = 0; k < 3; k++) r.v[k] = g4_frob<1>(k, A.v[k]);
+    return r;
+  };
+  auto frob2 = [&](const L3& A) {
+    L3 r;
+    for (int k = 0; k < 3; k++) r.v[k] = g4_frob<2>(k, A.v[k]);
+    return r;
+  };
+  auto pow_x = [&](const L3& F) {
+    L3 r = F;
+    for (int i = 62; i >= 0; i--) {
+      r = cyc(r);
+      if ((HB_X_ABS >> i) & 1) r = mul(r, F);
+    }
+    return conj(r);
+  };
+  L3 F, I;
+  lanes(f, F.v);
+  // the inversion in stored words (pair3.h g_inv's result is the group's f^-1; the tower's here)
+  lanes(f12_inv(tower(F.v)), I.v);
+  L3 t = mul(conj(F), I);
+  t = mul(frob2(t), t);
+  L3 x = t, b = t;
+  for (int st = 0; st < 5; st++) {
+    const L3 px = pow_x(x);
+    if (st == 3) b = x;
+    if (st < 2) x = mul(px, conj(x));
+    else if (st == 2) x = mul(px, frob1(x));
+    else x = px;
+  }
+  const L3 cc = mul(mul(x, frob2(b)), conj(b));
+  const L3 res = mul(cc, mul(cyc(t), t));
+  const Fp12 got = tower(res.v), want = final_exponentiation(f);
+  const Fp2 g6[6] = {got.c0.c0, got.c0.c1, got.c0.c2, got.c1.c0, got.c1.c1, got.c1.c2};
+  const Fp2 w6[6] = {want.c0.c0, want.c0.c1, want.c0.c2, want.c1.c0, want.c1.c1, want.c1.c2};
+  for (int i = 0; i < 6; i++) {
+    hc_f2_out(out + 96 * i, g6[i]);
+    hc_f2_out(out + 576 + 96 * i, w6[i]);
+  }
+  return 0;
+}
+
 // fp.h fp_inv (divsteps) against fp_inv_pow (a^(p-2)): x canonical big-endian; out: both inverses
 // (canonical), batches run
 extern "C" int hc_fp_inv(const uint8_t* x48, uint8_t* out96, int* batches) {

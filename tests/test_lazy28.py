@@ -62,6 +62,8 @@ def test_constants_match_ec28():
     assert used("HDNI G2L g2l_add", pat=r"f2l_sub<(\d+), (\d+)>") == sorted(
         [k["2J_H"], k["2J_R"], k["2J_X"], k["2J_W"], k["2J_Y"]])
     assert used("HD F2L f2l_sqr") == [k["2Q"]]
+    # the G2 formulas square through the product policy (fs<S, T>) with the same constant
+    assert set(used("HDNI G2L g2l_dbl", "HDNI G2L g2l_madd", "HDNI G2L g2l_add", pat=r"fs<(\d+), (\d+)>")) == {k["2Q"]}
     assert re.search(r"kF2N = k28_make\((\d+), (\d+)\)", src).groups() == tuple(map(str, k["2N"]))
     kp = [int(x, 16) for x in re.search(r"kP28_\[14\] = \{([^}]*)\}", src).group(1).replace("u", "").split(",")]
     assert kp == lazy28.P28
@@ -242,15 +244,29 @@ def test_line_and_pair_bounds():
     assert lazy28.check_pair() == {"sqr": 2.0, "line": 2.0}
 
 
-@pytest.mark.parametrize("group,prefix", [("lines", "3"), ("pair", "4")])
-def test_line_pair_constants_are_minimal(group, prefix):
+FE_SITES = "CMFJ"  # the final exponentiation's sites among the "4" ones
+
+
+@pytest.mark.parametrize("group,keep", [("lines", lambda k: k[0] == "3"),
+                                        ("pair", lambda k: k[0] == "4" and k[1] not in FE_SITES),
+                                        ("fe", lambda k: k[0] == "4" and k[1] in FE_SITES)])
+def test_line_pair_constants_are_minimal(group, keep):
     saved = dict(lazy28.KSITE)
     try:
         found = lazy28.search(2, (group,))
     finally:
         lazy28.KSITE.clear()
         lazy28.KSITE.update(saved)
-    assert found == {k: v for k, v in saved.items() if k.startswith(prefix)}
+    if group == "fe":  # the squares' constant is the Miller loop's (larger than the FE alone needs)
+        need = found.pop("4Q")
+        assert need[0] <= saved["4Q"][0] and need[1] <= saved["4Q"][1]
+    assert found == {k: v for k, v in saved.items() if keep(k)}
+
+
+def test_fe_bounds():
+    """the final exponentiation's lane operations keep the lane values reduced below 2p"""
+    r = lazy28.check_fe()
+    assert r["cyc"] == r["mul"] == r["conj"] == 2.0 and r["frob"] < 1.1
 
 
 def test_constants_match_pair28():
@@ -266,7 +282,7 @@ def test_constants_match_pair28():
     assert used("HD void l2_add_line", sub) == sorted(
         [k["3A_th"], k["3A_la"], k["3A_H"], k["3A_a0"], k["3A_a1"], k["3A_Y"], k["3A_GH"]])
     sq = {tuple(map(int, m)) for n in ("HD void l2_dbl_line", "HD void l2_add_line")
-          for m in re.findall(r"f2l_sqr_k<(\d+), (\d+)>", _fn(src, n))}
+          for m in re.findall(r"fs<(\d+), (\d+)>", _fn(src, n))}
     assert sq == {k["3Q"]}
     # the Fp4 lane values: f4l_mul / f4l_sqr instantiations and the lane steps
     assert re.findall(r"f4l_sqr<(\d+), (\d+), (\d+), (\d+)>", _fn(src, "HD void g4_sqr_p1")) == [
@@ -277,7 +293,18 @@ def test_constants_match_pair28():
     assert re.findall(r"f4l_mul_s<(\d+), (\d+)>", _fn(src, "HD F4L g4_line_p2")) == [tuple(map(str, k["4Ls"]))]
     assert re.findall(r"f4l_mul<(\d+), (\d+), (\d+), (\d+)>", _fn(src, "HD F4L g4_line_p2")) == [
         tuple(map(str, k["4Lmxi"] + k["4Lmy"]))]
-    assert re.findall(r"f2l_sqr_k<(\d+), (\d+)>", _fn(src, "HD F4L f4l_sqr")) == [tuple(map(str, k["4Q"]))] * 3
+    assert re.findall(r"fs<(\d+), (\d+)>", _fn(src, "HD F4L f4l_sqr")) == [tuple(map(str, k["4Q"]))] * 3
+    # the final exponentiation's lane operations
+    assert k["4Cvxi"] + k["4Cvy"] == k["4Svxi"] + k["4Svy"]  # g4_cyc_p1 squares as g4_sqr_p1
+    assert re.findall(r"f4l_sqr<(\d+), (\d+), (\d+), (\d+)>", _fn(src, "HD F4L g4_cyc_p1")) == [
+        tuple(map(str, k["4Cvxi"] + k["4Cvy"]))]
+    assert used("HD F4L g4_cyc_p2", r"f4l_mul_s<(\d+), (\d+)>") == [k["4Cs"]]
+    assert used("HD F4L g4_cyc_p2", sub) == [k["4Cn"]] * 2
+    assert re.findall(r"f4l_mul<(\d+), (\d+), (\d+), (\d+)>", _fn(src, "HD void g4_mul_p1")) == [
+        tuple(map(str, k["4Mvxi"] + k["4Mvy"])), tuple(map(str, k["4Mwxi"] + k["4Mwy"]))]
+    assert (k["4MD"], k["4Ms"]) == (k["4SD"], k["4Ss"])  # g4_mul recombines through g4_sqr_p2
+    assert used("HD F4L g4_conj", sub) == [k["4Jn"]] * 2
+    assert used("HD F4L g4_frob", r"l_sub<(\d+), (\d+)>") == [k["4Fn"]] * 2
 
 
 def _f2(b):
@@ -332,3 +359,18 @@ def test_g4_lane_ops_match_tower(lib):
         assert lib.hc_g4_ops(f, ln, out) == 0
         assert out.raw[0:576] == out.raw[576:1152], "g4_sqr"
         assert out.raw[1152:1728] == out.raw[1728:2304], "g4_mul_line"
+
+
+def test_fe28_matches_tower(lib):
+    """pair28.h's final exponentiation in lazy limbs (g4_cyc / g4_mul / g4_conj / g4_frob, the
+    three roles run in turn with pair3.h's exchanges) equals pairing.h final_exponentiation, on
+    random values and edge values (p - 1 coordinates, one)"""
+    lib.hc_fe28.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+    rng = random.Random(7741)
+    cases = [_rand_f12(rng) for _ in range(3)]
+    cases.append((B.P - 1).to_bytes(48, "big") * 12)
+    cases.append((1).to_bytes(48, "big") + bytes(48 * 11))
+    for f in cases:
+        out = ctypes.create_string_buffer(2 * 576)
+        assert lib.hc_fe28(f, out) == 0
+        assert out.raw[:576] == out.raw[576:]

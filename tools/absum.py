@@ -1,26 +1,21 @@
 #!/usr/bin/env python3
-"""Summary of A/B bench results (bench_<variant>_<k>.json): per variant the value, ms/step, parity, selected kernel
-times and the single-call latency.  Usage: absum.py TAG"""
+"""Summary of tools/gpu.sh ab results: gpurun_out/ab_TAG_WORKLOAD_LABEL_REP.json -> per run the value,
+ms/step, single-call latency and the kernels' alone times.  Usage: absum.py TAG [kernel substrings]"""
+import glob
 import json
-import os
 import sys
 
 tag = sys.argv[1]
-k = 1
-while os.path.exists(f"gpurun_out/ab_{tag}_{k}.json"):
-    env = open(f"gpurun_out/ab_{tag}_{k}.env").read().strip() if os.path.exists(f"gpurun_out/ab_{tag}_{k}.env") else "?"
+keys = sys.argv[2:] or ["hash", "lines", "pair3", "lml", "fin", "dec", "rlc", "ta_small", "slines", "fb"]
+for f in sorted(glob.glob(f"gpurun_out/ab_{tag}_*.json")):
     try:
-        d = json.loads(open(f"gpurun_out/ab_{tag}_{k}.json").read().strip().splitlines()[-1])
+        d = json.loads(open(f).read().strip().splitlines()[-1])
     except Exception as e:  # noqa: BLE001
-        print(k, env, "unreadable", e)
-        k += 1
+        print(f, "unreadable", e)
         continue
-    ks = d.get("kernels", {})
-    cc = d.get("concurrent_callers") or {}
-    sel = {n: ks[n]["ms_per_step"] for n in ("k_pair3_mml", "k_pair3_fin", "k_pair3_ml", "k_pair3_mls", "k_slines",
-                                            "k_dec_sig_pt", "k_hash_to_g2", "k_rlc", "k_ta_small") if n in ks}
-    print(k, env.replace("HBLS_LIBRARY=charon_amd/lib/variants/", "")[:60], d["value"], d["ms_per_step"],
-          all(d["parity"].values()), sel, cc.get("single_call_latency_ms"), cc.get("calls_per_s"))
-    if cc.get("single_call_kernels_ms"):
-        print("   single call:", cc["single_call_kernels_ms"])
-    k += 1
+    ks = {n: round(v["ms_per_step"], 2) for n, v in d.get("kernels", {}).items()
+          if isinstance(v, dict) and "ms_per_step" in v and any(k in n for k in keys)}
+    lat = d.get("single_call_latency_ms")
+    cc = (d.get("concurrent_callers") or {}).get("calls_per_s")
+    print(f.split("/")[-1][len("ab_"):-5], f"{d['value'] / 1e6:.3f} M/s", f"{d['ms_per_step']:.2f} ms",
+          f"lat {lat}" if lat else "", f"callers {cc}" if cc else "", ks)
