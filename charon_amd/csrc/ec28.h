@@ -375,6 +375,26 @@ struct F2One {};
 HD F2L fm(F2One, const F2L& a, const F2L& b) { return f2l_mul(a, b); }
 template <uint32_t S, uint32_t T>
 HD F2L fs(F2One, const F2L& a) { return f2l_sqr_k<S, T>(a); }
+// Independent products in one call, so that a policy spreading them over more lanes (pair28.h
+// F2Hex: six lanes, one coefficient each) can run them side by side; the default runs them in turn.
+template <class M>
+HD void fm2(M m, const F2L& a0, const F2L& b0, const F2L& a1, const F2L& b1, F2L& t0, F2L& t1) {
+  t0 = fm(m, a0, b0);
+  t1 = fm(m, a1, b1);
+}
+template <class M>
+HD void fm3(M m, const F2L& a0, const F2L& b0, const F2L& a1, const F2L& b1, const F2L& a2, const F2L& b2, F2L& t0,
+            F2L& t1, F2L& t2) {
+  t0 = fm(m, a0, b0);
+  t1 = fm(m, a1, b1);
+  t2 = fm(m, a2, b2);
+}
+template <uint32_t S, uint32_t T, class M>
+HD void fs3(M m, const F2L& a0, const F2L& a1, const F2L& a2, F2L& t0, F2L& t1, F2L& t2) {
+  t0 = fs<S, T>(m, a0);
+  t1 = fs<S, T>(m, a1);
+  t2 = fs<S, T>(m, a2);
+}
 
 #if defined(__HIP_DEVICE_COMPILE__)
 // x0 y0 + x1 y1 (one Montgomery pass, f2l_dot_core): x0 | x1 in the argument VGPRs, y0, y1 through

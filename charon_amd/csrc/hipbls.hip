@@ -1240,14 +1240,18 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
     ga.skip_hm = 1;
     // these calls are single Verifies and small batches, latency-bound: each group's sums (S kept
     // Jacobian, no lines), then its signature side's Miller loop -- lines produced and consumed in
-    // one kernel (k_lml) -- while the messages still hash; after the hashing (not its lines) the
-    // (P, H(m)) loop the same way, then ONE six-lane final exponentiation of the two stored loops
-    // (f1[2g], f1[2g + 1])
+    // one kernel (k_lml) -- on side stream 0 while the messages still hash; after the hashing (not
+    // its lines) the (P, H(m)) loop the same way on s, beside it; then ONE six-lane final
+    // exponentiation of the two stored loops (f1[2g], f1[2g + 1])
     ga.gS = f1S;
     ga.bS = nullptr;
     ga.fe_batch = 1;
     TIMED(d, "k_group_prep", s, launch_group_prep(ga, s));
-    TIMED(d, "k_pair3", s, launch_lml(f1S, ng, f1, 2, 1, nullptr, s));
+    hipStream_t sl = w.side[0];
+    HCHK(hipEventRecord(w.ev_msm, s));
+    HCHK(hipStreamWaitEvent(sl, w.ev_msm, 0));
+    TIMED(d, "k_pair3", sl, launch_lml(f1S, ng, f1, 2, 1, nullptr, sl));
+    HCHK(hipEventRecord(w.ev_side[0], sl));
     if (g0 == 0 && (h_ready || hm_ready)) HCHK(hipStreamWaitEvent(s, h_ready ? h_ready : hm_ready, 0));
     LmlArgs pa{};
     pa.pk = gP;
@@ -1259,6 +1263,7 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
     pa.f_stride = 2;
     pa.bad = f1bad;
     TIMED(d, "k_pair3", s, launch_lml_p(pa, s));
+    HCHK(hipStreamWaitEvent(s, w.ev_side[0], 0));
     Pair3Args pf{};
     pf.pk_st = f1bad;
     pf.n = ng;

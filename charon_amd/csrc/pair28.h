@@ -178,16 +178,16 @@ HD F4L f4l_mul_s(const F4L& a) {
 // lazy28.py f4_mul (Karatsuba, normalised): (t0 + xi t1, t2 - t0 - t1)
 template <uint32_t XS, uint32_t XT, uint32_t YS, uint32_t YT, class M = F2One>
 HD F4L f4l_mul(const F4L& a, const F4L& b, M m = M()) {
-  const F2L t0 = fm(m, a.x, b.x), t1 = fm(m, a.y, b.y);
-  const F2L t2 = fm(m, f2l_add(a.x, a.y), f2l_add(b.x, b.y));
+  F2L t0, t1, t2;
+  fm3(m, a.x, b.x, a.y, b.y, f2l_add(a.x, a.y), f2l_add(b.x, b.y), t0, t1, t2);
   return f4l_norm({f2l_add(t0, f2l_xi<XS, XT>(t1)), f2l_sub<YS, YT>(t2, f2l_add(t0, t1))});
 }
 // lazy28.py f4_sqr: (x^2 + xi y^2, (x + y)^2 - x^2 - y^2), normalised
 template <uint32_t XS, uint32_t XT, uint32_t YS, uint32_t YT, class M = F2One>
 HD F4L f4l_sqr(const F4L& a, M m = M()) {
-  const F2L t0 = fs<9, 2>(m, a.x), t1 = fs<9, 2>(m, a.y);
-  return f4l_norm({f2l_add(f2l_xi<XS, XT>(t1), t0),
-                   f2l_sub<YS, YT>(fs<9, 2>(m, f2l_norm(f2l_add(a.x, a.y))), f2l_add(t0, t1))});
+  F2L t0, t1, t2;
+  fs3<9, 2>(m, a.x, a.y, f2l_norm(f2l_add(a.x, a.y)), t0, t1, t2);
+  return f4l_norm({f2l_add(f2l_xi<XS, XT>(t1), t0), f2l_sub<YS, YT>(t2, f2l_add(t0, t1))});
 }
 
 // The lane operations of pair3.h in two phases around their lane exchanges, so that the host
@@ -210,7 +210,11 @@ HD F4L g4_sqr_p2(int k, const F4L& w, const F4L& vp, const F4L& vq, const F4L& v
 // product by a sparse line a0 + a1 v + b1 v w (pair3.h g_mul_line): phase 1 -- F a1, sent to the
 // role before; phase 2 -- C = F (a0 + b1 s) + [k == 2 ? s : 1] (F_{k+1} a1); reduced
 template <class M = F2One>
-HD F4L g4_line_p1(const F4L& F, const F2L& a1, M m = M()) { return {fm(m, F.x, a1), fm(m, F.y, a1)}; }
+HD F4L g4_line_p1(const F4L& F, const F2L& a1, M m = M()) {
+  F4L r;
+  fm2(m, F.x, a1, F.y, a1, r.x, r.y);
+  return r;
+}
 template <class M = F2One>
 HD F4L g4_line_p2(int k, const F4L& F, const F2L& a0, const F2L& b1, const F4L& Qn, M m = M()) {
   const F4L Qs = f4l_select(k == 2, f4l_mul_s<2, 1>(Qn), Qn);  // k == 2 ? Qn : s Qn
@@ -255,7 +259,9 @@ HD F4L g4_frob(int k, const F4L& A, M m = M()) {
     x.c1 = l_sub<3, 1>(l_zero(), x.c1);
     y.c1 = l_sub<3, 1>(l_zero(), y.c1);
   }
-  return {fm(m, x, cx), fm(m, y, cy)};
+  F4L r;
+  fm2(m, x, cx, y, cy, r.x, r.y);
+  return r;
 }
 HD Fp4 f4l_join(const F4L& a) { return {f2l_join(a.x), f2l_join(a.y)}; }
 
@@ -275,10 +281,84 @@ __device__ __forceinline__ L28 xch(const L28& a, int addr) {
 __device__ __forceinline__ F2L xch(const F2L& a, int addr) { return {xch(a.c0, addr), xch(a.c1, addr)}; }
 __device__ __forceinline__ F4L xch(const F4L& a, int addr) { return {xch(a.x, addr), xch(a.y, addr)}; }
 
-// Over a lane group G: Grp (three lanes, pair3.h; each lane its products alone) or Grp6 (six
-// lanes, pair6.h; each Fp2 product split over the role's two lanes, ec28.h F2Half)
+// Eighteen lanes per Fp12 value: each role k of pair3.h held by SIX lanes j = 0..5 (lane = 18 grp +
+// 6 k + j, three values per wavefront, lanes 54..63 shadow a group), which run a role's independent
+// Fp2 products side by side -- lane j computes coefficient j & 1 of product j >> 1 of a batch of
+// three (fm3 / fs3; fm2 leaves lanes 4, 5 duplicating) and every lane gathers the six results.  The
+// lane values stay duplicated over the six lanes; each lane's stream holds one Fp product per batch
+// instead of the three (Grp6) or six (Grp) -- the final exponentiations of single calls and of the
+// slot-wide check, which nothing else hides.
+struct F2Hex {
+  int j;
+  int at[6];  // the role's six lanes (ds_bpermute addresses)
+};
+struct Grp18 {
+  int k, j;
+  int n1, n2, e, p, q;  // pair3.h Grp's exchanges, between lanes of the same j
+  F2Hex hx;
+};
+__device__ __forceinline__ Grp18 grp18_make() {
+  const int lane = (int)(threadIdx.x & 63u);
+  const int grp = lane / 18, r = lane - 18 * grp;
+  Grp18 g;
+  g.k = r / 6;
+  g.j = r - 6 * g.k;
+  const int base = 18 * grp;
+  auto at = [&](int role, int jj) { return ((base + 6 * role + jj) & 63) << 2; };
+  g.n1 = at((g.k + 1) % 3, g.j);
+  g.n2 = at((g.k + 2) % 3, g.j);
+  g.e = at((3 - g.k) % 3, g.j);
+  g.p = at(g.k == 0 ? 1 : 0, g.j);
+  g.q = at(g.k == 0 ? 2 : g.k, g.j);
+  g.hx.j = g.j;
+  HB_UNROLL for (int jj = 0; jj < 6; jj++) g.hx.at[jj] = at(g.k, jj);
+  return g;
+}
+// the pair3.h lane group seen from one j (the inversion and the final test run duplicated)
+__device__ __forceinline__ Grp grp_of(const Grp18& g) { return {g.k, g.n1, g.n2, g.e, g.p, g.q}; }
+
+__device__ __forceinline__ F2L f2hex_pick3(int w, const F2L& a0, const F2L& a1, const F2L& a2) {
+  return f2l_select(w == 2, f2l_select(w == 1, a0, a1), a2);
+}
+__device__ __forceinline__ void f2hex_gather(const F2Hex& m, const L28& mine, F2L& t0, F2L& t1, F2L& t2) {
+  t0 = {l_xch(mine, m.at[0]), l_xch(mine, m.at[1])};
+  t1 = {l_xch(mine, m.at[2]), l_xch(mine, m.at[3])};
+  t2 = {l_xch(mine, m.at[4]), l_xch(mine, m.at[5])};
+}
+// coefficient j & 1 of a_w b_w, w = j >> 1 (ec28.h fm(F2Half)'s operand choice)
+__device__ __forceinline__ L28 f2hex_dot(const F2Hex& m, const F2L& a, const F2L& b) {
+  L28 na1;
+  HB_UNROLL for (int i = 0; i < 14; i++) na1.l[i] = kF2N.l[i] - a.c1.l[i];
+  const bool h = (m.j & 1) != 0;
+  return l_dot(a.c0, l_pick(h, na1, a.c1), l_pick(h, b.c0, b.c1), l_pick(h, b.c1, b.c0));
+}
+__device__ __forceinline__ void fm3(const F2Hex& m, const F2L& a0, const F2L& b0, const F2L& a1, const F2L& b1,
+                                    const F2L& a2, const F2L& b2, F2L& t0, F2L& t1, F2L& t2) {
+  const int w = m.j >> 1;
+  f2hex_gather(m, f2hex_dot(m, f2hex_pick3(w, a0, a1, a2), f2hex_pick3(w, b0, b1, b2)), t0, t1, t2);
+}
+__device__ __forceinline__ void fm2(const F2Hex& m, const F2L& a0, const F2L& b0, const F2L& a1, const F2L& b1, F2L& t0,
+                                    F2L& t1) {
+  const bool w1 = m.j >= 2;  // lanes 4, 5 repeat product 1
+  F2L u0, u1, u2;
+  f2hex_gather(m, f2hex_dot(m, f2l_select(w1, a0, a1), f2l_select(w1, b0, b1)), u0, u1, u2);
+  t0 = u0;
+  t1 = u1;
+}
+template <uint32_t S, uint32_t T>
+__device__ __forceinline__ void fs3(const F2Hex& m, const F2L& a0, const F2L& a1, const F2L& a2, F2L& t0, F2L& t1,
+                                    F2L& t2) {
+  const F2L u = f2hex_pick3(m.j >> 1, a0, a1, a2);
+  const bool h = (m.j & 1) != 0;
+  f2hex_gather(m, l_mul(l_pick(h, l_add(u.c0, u.c1), l_shl(u.c0, 1)), l_pick(h, l_sub<S, T>(u.c0, u.c1), u.c1)), t0,
+               t1, t2);
+}
+
+// Over a lane group G: Grp (three lanes, pair3.h; each lane its products alone), Grp6 (six lanes,
+// pair6.h; each Fp2 product split over the role's two lanes, ec28.h F2Half) or Grp18 (above)
 __device__ __forceinline__ F2One fe_m(const Grp&) { return {}; }
 __device__ __forceinline__ F2Half fe_m(const Grp6& g) { return {g.h, g.partner}; }
+__device__ __forceinline__ const F2Hex& fe_m(const Grp18& g) { return g.hx; }
 template <class G>
 __device__ __forceinline__ F4L g4_one(const G& g) { return g4_one_role(g.k); }
 template <class G>
@@ -298,6 +378,8 @@ __device__ __forceinline__ Fp4 fe_inv(const Grp& g, const Fp4& A) { return g_inv
 __device__ __forceinline__ Fp4 fe_inv(const Grp6& g, const Fp4& A) { return g6_inv(g, A); }
 __device__ __forceinline__ bool fe_is_one(const Grp& g, const Fp4& A) { return g_is_one(g, A); }
 __device__ __forceinline__ bool fe_is_one(const Grp6& g, const Fp4& A) { return g6_is_one(g, A); }
+__device__ __forceinline__ Fp4 fe_inv(const Grp18& g, const Fp4& A) { return g_inv(grp_of(g), A); }
+__device__ __forceinline__ bool fe_is_one(const Grp18& g, const Fp4& A) { return g_is_one(grp_of(g), A); }
 
 template <class G>
 __device__ __forceinline__ F4L g4_cyc(const G& g, const F4L& A) {

@@ -9,6 +9,8 @@
 #include "pair3.h"
 #include "pair6.h"
 
+#include <stdlib.h>
+
 namespace hb {
 
 constexpr int BLOCK = 64;
@@ -209,18 +211,27 @@ __global__ KB_OCC(HB_OCC_PAIR3) void k_pair3(Pair3Args a) {
 #endif
 }
 
-// A final exponentiation over SIX lanes per unit (pair6.h: every Fp2 product split between two
+// A final exponentiation over SIX lanes per unit (pair6.h Grp6: every Fp2 product split between two
+// lanes) or EIGHTEEN (pair28.h Grp18: a role's independent Fp2 products side by side over six
 // lanes): the product of the unit's f_range stored values, exponentiated, its verdict -- k_pair3<FIN>
-// with sig_lines == nullptr at about half the latency.  Ten units per wavefront.
-constexpr int FE6_PER_WAVE = 10;
+// with sig_lines == nullptr at a half / a quarter of the latency.  Ten / three units per wavefront.
+#if defined(__HIP_DEVICE_COMPILE__)
+template <int PER_WAVE>
+__device__ __forceinline__ auto fe_group() {
+  if constexpr (PER_WAVE == 3) return grp18_make();
+  else return grp6_make();
+}
+#endif
+template <int PER_WAVE>
 __global__ KB_OCC(HB_OCC_PAIR3) void k_pair6_fin(Pair3Args a) {
 #if defined(__HIP_DEVICE_COMPILE__)
   if (a.guard && *a.guard == 0) return;
-  const Grp6 g = grp6_make();
-  const int grp = (int)(threadIdx.x & 63u) / 6;
-  if (blockIdx.x * FE6_PER_WAVE >= a.n) return;  // wave-uniform
-  const uint32_t unit = blockIdx.x * FE6_PER_WAVE + (uint32_t)grp;
-  const bool valid = grp < FE6_PER_WAVE && unit < a.n;
+  const auto g = fe_group<PER_WAVE>();
+  constexpr int LANES = PER_WAVE == 3 ? 18 : 6;  // lanes per unit
+  const int grp = (int)(threadIdx.x & 63u) / LANES;
+  if (blockIdx.x * PER_WAVE >= a.n) return;  // wave-uniform
+  const uint32_t unit = blockIdx.x * PER_WAVE + (uint32_t)grp;
+  const bool valid = grp < PER_WAVE && unit < a.n;
   const uint32_t e = valid ? unit : a.n - 1;
   const uint32_t first = e * a.f_range;
   const uint32_t cnt = first < a.f_n ? min(a.f_range, a.f_n - first) : 0u;
@@ -230,16 +241,32 @@ __global__ KB_OCC(HB_OCC_PAIR3) void k_pair6_fin(Pair3Args a) {
     const F4L t = f4l_select(j >= cnt, f4l_load(a.f_in[3ull * idx + g.k]), g4_one(g));
     f = j == 0 ? t : g4_mul(g, f, t);
   }
-  f = g4_final_exp(g, f);  // pair28.h, each Fp2 product split over the role's two lanes
+  f = g4_final_exp(g, f);  // pair28.h
   const bool one = g4_is_one(g, f);
-  if (valid && g.k == 0 && g.h == 0)
+  int sub;  // the lane of a role that stores
+  if constexpr (PER_WAVE == 3) sub = g.j;
+  else sub = g.h;
+  if (valid && g.k == 0 && sub == 0)
     a.status[e] = (a.pk_st && a.pk_st[e]) ? (uint8_t)1 : (one ? ST_OK : ST_NOT_VERIFIED);
 #endif
 }
 
+// units up to which the eighteen-lane kernel runs (HBLS_FE18_MAX, default 256: a few waves per
+// XCD; beyond, the six-lane one's fewer duplicated additions per unit win)
+static uint32_t fe18_max() {
+  static const uint32_t v = [] {
+    const char* e = getenv("HBLS_FE18_MAX");
+    return e ? (uint32_t)strtoul(e, nullptr, 0) : 256u;
+  }();
+  return v;
+}
+
 void launch_pair6_fin(const Pair3Args& a, hipStream_t s) {
   if (!a.n) return;
-  hipLaunchKernelGGL(k_pair6_fin, dim3((a.n + FE6_PER_WAVE - 1) / FE6_PER_WAVE), dim3(64), 0, s, a);
+  if (a.n <= fe18_max())
+    hipLaunchKernelGGL(k_pair6_fin<3>, dim3((a.n + 2) / 3), dim3(64), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_pair6_fin<10>, dim3((a.n + 9) / 10), dim3(64), 0, s, a);
 }
 
 // The Miller lines of every verification group's (P_g, H(m_g)) evaluated at P_g, for the
@@ -281,10 +308,10 @@ void launch_mml_eval(const Pair3Args& a, LineEntry* ev, hipStream_t s) {
 // 0 already computes the next.  The chain's latency is then about one of the two halves instead of
 // k_slines followed by k_pair3<MLS> (the slot-wide check's signature side: a tail of every slot, on
 // the critical path of small slots).  bad[e] = 1 for S at infinity.
-// Both halves in lazy limbs (pair28.h) with every Fp2 product split over two lanes (ec28.h
-// F2Half): the producer's chain on lanes (0, 1), the consumer's Fp12 over six lanes (pair6.h Grp6),
-// each lane's instruction stream ~60 % of the one-lane / three-lane one -- this kernel is
-// latency-bound (one workgroup per point, few points).
+// Both halves in lazy limbs (pair28.h): the producer's chain with every Fp2 product split over a
+// lane pair (ec28.h F2Half), the consumer's Fp12 over eighteen lanes (pair28.h Grp18: a role's
+// independent Fp2 products side by side over six lanes) -- this kernel is latency-bound (one
+// workgroup per point, few points).
 // SIDE 1 (the small calls' group checks): the (P_g, H(m_g)) loop instead, H(m_g) affine from the
 // message table (its lines need not exist yet: only the hashing is waited for), the lines
 // evaluated at P_g by the consumer; bad[e] = the group fails without a pairing (state, P or H(m)
@@ -328,7 +355,7 @@ __global__ __launch_bounds__(128, 1) void k_lml(LmlArgs a) {
   }
   G1AEntry P{};
   if (SIDE == 1 && !producer) P = a.pk[e];
-  const Grp6 g = grp6_make();
+  const Grp18 g = grp18_make();
   F4L f = g4_one(g);
   const L28 px = l_from(P.x), py = l_from(P.y);  // SIDE 1: the consumer evaluates at P
   int bit = 62;  // consumer: the loop schedule of k_pair3
@@ -370,7 +397,7 @@ __global__ __launch_bounds__(128, 1) void k_lml(LmlArgs a) {
     }
     __syncthreads();
   }
-  if (!producer && threadIdx.x < 64 + 6 && g.h == 0) {
+  if (!producer && threadIdx.x < 64 + 18 && g.j == 0) {
     const size_t o = (size_t)e * (a.f_stride ? a.f_stride : 1u) + a.f_off;
     a.f_out[3 * o + g.k] = f4l_store(f);
     if (threadIdx.x == 64 && a.bad)

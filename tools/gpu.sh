@@ -5,6 +5,7 @@
 #   trace  TAG [bench args]         rocprofv3 kernel trace + stats of a bench run
 #   pmc    TAG                      kernel trace + SQ / FETCH_SIZE / WRITE_SIZE passes over one C3 slot
 #   final  TAG                      tests, smoke, lines, trace of the default C3 line, pmc
+#   single TAG [calls]              kernel trace of single-item Verify calls (tools/diag_single.py)
 # Every GPU step has its own time limit and the steps are chained with &&: the first failure,
 # abort or time-out ends the script.
 set -o pipefail
@@ -49,6 +50,11 @@ pmc() {
    timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d "$P/fetch" -o run --output-format csv -- python3 "$B" $A > "$P.fetch.log" 2>&1 &&
    timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d "$P/write" -o run --output-format csv -- python3 "$B" $A > "$P.write.log" 2>&1)
 }
+single() {
+  (cd /tmp && export TMPDIR=/tmp &&
+   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/single_$TAG" -o run --output-format csv -- python3 \
+     "$GRAFT_REPO_ROOT/tools/diag_single.py" "${1:-8}" > "$O/single_$TAG.log" 2>&1)
+}
 
 # A/B of library builds on one box (HBLS_LIBRARY): ab TAG WORKLOAD label=path ... ; alternates
 # through the list twice, one bench line each (bench args from $AB_ARGS)
@@ -72,5 +78,6 @@ case "$WHAT" in
   pmc) pmc ;;
   final) tests && smoke && lines && trace --steps 5 --warmup 2 --cpu-seconds 0 --callers 0 --aggregate-verify 0 --host-api 0 && pmc ;;
   ab) ab "$@" ;;
-  *) echo "usage: bash tools/gpu.sh tests|bench|lines|trace|pmc|final|ab TAG [args]" >&2; exit 2 ;;
+  single) single "$@" ;;
+  *) echo "usage: bash tools/gpu.sh tests|bench|lines|trace|pmc|final|ab|single TAG [args]" >&2; exit 2 ;;
 esac
