@@ -138,7 +138,7 @@ def ta_share_positions(n, t):
     return list(range(t))
 
 
-def corrupt(L, d, frac, seed):
+def corrupt(L, d, frac, seed, classes=(0, 1, 2, 3, 4)):
     """C5: corrupt `frac` of the partials in equal fifths (core/parsigex/parsigex_test.go:285-289,
     core/sigagg/sigagg_test.go:46-67 classes) and derive every expected status by construction:
       0 random 96 bytes without the compression flag   -> BAD_SIGNATURE (undecodable)
@@ -155,7 +155,7 @@ def corrupt(L, d, frac, seed):
     n, t, V, NP = d["n"], d["t"], d["V"], d["NP"]
     rng = random.Random(seed)
     bad = rng.sample(range(NP), int(NP * frac))
-    cls = {i: k % 5 for k, i in enumerate(bad)}
+    cls = {i: k % 5 for k, i in enumerate(bad) if k % 5 in classes}  # (classes: a subset, diagnosis)
     with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests", "golden", "off_subgroup_g2.json")) as f:
         offsub = [bytes.fromhex(x) for x in json.load(f)["points"]]
     sigs = d["sigs"].reshape(NP, 96)
@@ -203,7 +203,7 @@ def corrupt(L, d, frac, seed):
             exp_ta[v] = exp_agg[v] = 2
         elif any(c is not None for c in mem):
             exp_agg[v] = 3
-    d.update(exp_v=exp_v, exp_ta=exp_ta, exp_agg=exp_agg, n_corrupted=len(bad))
+    d.update(exp_v=exp_v, exp_ta=exp_ta, exp_agg=exp_agg, n_corrupted=len(cls))
 
 
 def setup_inputs(L, wl, V, rank):
@@ -898,6 +898,11 @@ def main(argv=None):
     if rank == 0 and world == 1 and args.key_tables and not staged:
         out["with_key_tables"] = key_table_slots(L, d_pk, d_dvpk, outs, NP, V, args.steps, step_slot, mk, items)
 
+    if os.environ.get("HBLS_STATS") == "1":  # fallback counters over the whole run (diagnosis)
+        st = (ctypes.c_uint64 * 6)()
+        _chk(L, L.hbls_stats(st, 6))
+        out["fallback_stats"] = dict(zip(("items", "groups", "fallback_items", "last_chunk_groups_checked",
+                                          "slot_checks", "slot_checks_failed"), list(st)))
     out["kernels"], out["roofline"] = kernel_roofline()
 
     if rank == 0 and world == 1 and args.aggregate_verify:
