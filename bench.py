@@ -502,7 +502,9 @@ def roofline_from_timing(recs, steps, units):
                      "units_per_step": u, "fpmul_per_unit_alg": alg, "fpmul_per_unit_exec": exe,
                      "achieved_Tops_alg": round(u * alg * opcounts.MAC_PER_FPMUL / t / 1e12, 3) if t > 0 else None,
                      "achieved_Tops_exec": round(u * exe * opcounts.MAC_PER_FPMUL / t / 1e12, 3) if t > 0 else None}
-    dom = max(per, key=lambda k: per[k]["ms_per_step"]) if per else None
+    # the dominant kernel: the most algorithmic work per step (the longest alone time can be a
+    # latency-bound kernel with little work, e.g. the hashing of C2's 64 messages)
+    dom = max(per, key=lambda k: per[k]["units_per_step"] * per[k]["fpmul_per_unit_alg"]) if per else None
     return dom, per
 
 
