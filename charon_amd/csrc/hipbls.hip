@@ -1743,6 +1743,7 @@ struct VReq {
   int rc = 0;
   std::string err;
   bool done = false;
+  bool taken = false;  // in a batch (running or about to)
 };
 
 struct Coalescer {
@@ -1750,16 +1751,21 @@ struct Coalescer {
   std::condition_variable cv;
   std::deque<VReq*> q;
   size_t queued = 0;
-  bool running = false;
+  int active = 0;          // batches running (each on its own host-call context)
+  bool gathering = false;  // a leader is collecting the next batch
   std::chrono::steady_clock::time_point last_end{};  // when the previous batch finished
 };
 Coalescer g_vq;
-size_t g_coalesce_us = (size_t)-1, g_coalesce_max = 0;
+size_t g_coalesce_us = (size_t)-1, g_coalesce_max = 0, g_coalesce_inflight = 0;
 
 void coalesce_params() {
   if (g_coalesce_us == (size_t)-1) {
     g_coalesce_us = env_size("HBLS_COALESCE_US", 200);
     g_coalesce_max = env_size("HBLS_COALESCE_MAX", 1u << 16);
+    // batches in flight at once (HBLS_COALESCE_INFLIGHT, default: the host-call contexts): the
+    // requests that arrive while batches run form the next one, which starts at once instead of
+    // behind them -- a small batch leaves most of the chip idle
+    g_coalesce_inflight = std::max<size_t>(1, env_size("HBLS_COALESCE_INFLIGHT", (size_t)g_ws_sets));
   }
 }
 
@@ -1808,23 +1814,29 @@ int verify_coalesced(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msg
   c.queued += n;
   c.cv.notify_all();
   while (!me.done) {
-    if (!c.running) {
-      c.running = true;
-      // gather more requests only in a busy period (a batch finished within the last few windows):
-      // a lone caller on an idle library runs at once, and under load the requests that queue up
-      // while a batch runs form the next one anyway
+    // a caller whose request is still queued leads the next batch when a context is free
+    if (!me.taken && !c.gathering && (size_t)c.active < g_coalesce_inflight) {
+      c.gathering = true;
+      c.active++;
+      // gather more requests only in a busy period (batches running, or one finished within the
+      // last few windows): a lone caller on an idle library runs at once, and under load the
+      // requests that queue up meanwhile form the next batch
       const auto now = std::chrono::steady_clock::now();
-      const bool busy = now - c.last_end < std::chrono::microseconds(4 * g_coalesce_us) || c.q.size() > 1;
+      const bool busy = c.active > 1 || now - c.last_end < std::chrono::microseconds(4 * g_coalesce_us) ||
+                        c.q.size() > 1;
       auto deadline = now + std::chrono::microseconds(busy ? g_coalesce_us : 0);
       while (c.queued < g_coalesce_max && std::chrono::steady_clock::now() < deadline) c.cv.wait_until(lk, deadline);
       std::vector<VReq*> batch(c.q.begin(), c.q.end());
+      for (VReq* r : batch) r->taken = true;
       c.q.clear();
       c.queued = 0;
+      c.gathering = false;
+      c.cv.notify_all();  // the next leader may start gathering
       lk.unlock();
       run_verify_batch(batch);
       lk.lock();
       for (VReq* r : batch) r->done = true;
-      c.running = false;
+      c.active--;
       c.last_end = std::chrono::steady_clock::now();
       c.cv.notify_all();
     } else {
