@@ -473,21 +473,44 @@ struct G2L {
   bool inf;
 };
 
-// lazy28.py dbl2: D = 4 X B from one product, E = 3A normalised before its square, E W = 3 (A W);
-// the products in the order that ends the inputs' live ranges first (Z3 before B = Y^2, D1 right
-// after A) so that fewer values are held across the product calls
+// v mod p up to a multiple of p: the same residue, normalised, below 2p.  a: limbs below 2^32
+// (not necessarily carried), value below 2^390.  The top estimate l13 2^28 + l12 is within 17 of
+// v / 2^336 (the lower limbs carry at most 16 into limb 12), so top / (p >> 336) is within 2^-40
+// of v / p; minus 2^-20 and truncated it gives floor(v / p) or one less.  The subtraction runs
+// with a signed carry (q < 2^10, so q p_i < 2^38).  (pair28.h's steps end with it.)
+HD L28 l_red(const L28& a) {
+  const double top = (double)a.l[13] * 268435456.0 + (double)a.l[12];
+  const double qd = top * kInvPTop - 0x1p-20;
+  const int32_t q = qd > 0.0 ? (int32_t)qd : 0;
+  L28 r;
+  int64_t c = 0;
+  HB_UNROLL for (int i = 0; i < 13; i++) {
+    c += (int64_t)a.l[i] - (int64_t)q * (int64_t)kP28_[i];
+    r.l[i] = (uint32_t)c & 0x0FFFFFFFu;
+    c >>= 28;
+  }
+  r.l[13] = (uint32_t)(c + (int64_t)a.l[13] - (int64_t)q * (int64_t)kP28_[13]);
+  return r;
+}
+HD F2L f2l_red(const F2L& a) { return {l_red(a.c0), l_red(a.c1)}; }
+
+// lazy28.py dbl2: dbl-2009-l (2M + 5S) with D = 2((X + B)^2 - A - C) partially reduced (l_red, no
+// product -- unreduced, its subtraction constant grows the point past the invariant), X + B and
+// E = 3A normalised before their squares, W first in E W (33p - W.c1 dominates it); the products
+// in the order that ends the inputs' live ranges first (Z3 before B = Y^2, T right after A)
 template <class M = F2One>
 HDNI G2L g2l_dbl(const G2L& p, M m = M()) {
   G2L r;
   r.Z = fm(m, f2l_shl(p.Y, 1), p.Z);
   const F2L B = fs<36, 1>(m, p.Y);
   const F2L A = fs<36, 1>(m, p.X);
-  const F2L D1 = fm(m, p.X, B);
+  const F2L T = fs<36, 1>(m, f2l_norm(f2l_add(p.X, B)));
   const F2L C = fs<36, 1>(m, B);
-  const F2L F = fs<36, 1>(m, f2l_norm(f2l_add(f2l_shl(A, 1), A)));
-  r.X = f2l_norm(f2l_sub<9, 8>(F, f2l_shl(D1, 3)));
-  const F2L AW = fm(m, f2l_sub<11, 1>(f2l_shl(D1, 2), r.X), A);
-  r.Y = f2l_norm(f2l_sub<9, 8>(f2l_add(f2l_shl(AW, 1), AW), f2l_shl(C, 3)));
+  const F2L E = f2l_norm(f2l_add(f2l_shl(A, 1), A));
+  const F2L D = f2l_red(f2l_shl(f2l_sub<3, 2>(T, f2l_add(A, C)), 1));
+  r.X = f2l_norm(f2l_sub<5, 2>(fs<36, 1>(m, E), f2l_shl(D, 1)));
+  const F2L W = f2l_sub<7, 1>(D, r.X);
+  r.Y = f2l_norm(f2l_sub<9, 8>(fm(m, W, E), f2l_shl(C, 3)));
   r.inf = p.inf;
   return r;
 }

@@ -23,26 +23,6 @@
 
 namespace hb {
 
-// v mod p up to a multiple of p: the same residue, normalised, below 2p.  a: limbs below 2^32
-// (not necessarily carried), value below 2^390.  The top estimate l13 2^28 + l12 is within 17 of
-// v / 2^336 (the lower limbs carry at most 16 into limb 12), so top / (p >> 336) is within 2^-40
-// of v / p; minus 2^-20 and truncated it gives floor(v / p) or one less.  The subtraction runs
-// with a signed carry (q < 2^10, so q p_i < 2^38).
-HD L28 l_red(const L28& a) {
-  const double top = (double)a.l[13] * 268435456.0 + (double)a.l[12];
-  const double qd = top * kInvPTop - 0x1p-20;
-  const int32_t q = qd > 0.0 ? (int32_t)qd : 0;
-  L28 r;
-  int64_t c = 0;
-  HB_UNROLL for (int i = 0; i < 13; i++) {
-    c += (int64_t)a.l[i] - (int64_t)q * (int64_t)kP28_[i];
-    r.l[i] = (uint32_t)c & 0x0FFFFFFFu;
-    c >>= 28;
-  }
-  r.l[13] = (uint32_t)(c + (int64_t)a.l[13] - (int64_t)q * (int64_t)kP28_[13]);
-  return r;
-}
-
 HD L28 l_zero() {
   L28 r;
   HB_UNROLL for (int i = 0; i < 14; i++) r.l[i] = 0;
@@ -60,7 +40,6 @@ HD Fp l_join(const L28& a) {
   return r;
 }
 
-HD F2L f2l_red(const F2L& a) { return {l_red(a.c0), l_red(a.c1)}; }
 HD F2L f2l_zero() { return {l_zero(), l_zero()}; }
 HD F2L f2l_one() { return {l_from(fp_one()), l_zero()}; }
 HD F2L f2l_select(bool take_b, const F2L& a, const F2L& b) {

@@ -26,10 +26,10 @@ BLOCK_NAMES = ("f12_sqr", "f12_mul_line", "final_exp", "fp_inv", "g1_dec", "g2_d
 # fp_inv: the inversion by divsteps (fp.h, round 4) runs no Montgomery product but its final
 # conversion to Montgomery form (463 as a^(p-2) before); its ~20 000 32-bit operations per inversion
 # count as overhead, not as algorithmic work
-BLOCKS = dict(zip(BLOCK_NAMES, (36, 39, 7679, 1, 1492, 2190, 732, 1880, 16, 43, 5, 16, 1843, 1571, 16, 29, 18,
+BLOCKS = dict(zip(BLOCK_NAMES, (36, 39, 7679, 1, 1492, 2127, 732, 1880, 16, 43, 5, 16, 1843, 1571, 16, 29, 18,
                                 54, 4, 11, 7)))
 
-G2_DEC_LAZY_EXTRA = 68  # ec28.h g2l_dbl / g2l_madd against ec.h jac_dbl / jac_add_aff (63 x 1 + 5 x 1)
+G2_DEC_LAZY_EXTRA = 5  # ec28.h g2l_madd / g2l_add against ec.h jac_add_aff / jac_add (5 x 1; g2l_dbl is the textbook 2M + 5S since round 4)
 N_LINES = 68      # Miller-loop lines (63 doublings + 5 additions)
 N_SQR = 62        # Fp12 squarings of the Miller loop
 LINE_PRODUCTS = 2 * N_LINES  # two pairs per check

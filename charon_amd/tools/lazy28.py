@@ -200,7 +200,7 @@ VMAX = {"Fp": 20, "Fp2": 16}  # coordinates stay below VMAX p between the ladder
 KSITE = {
     "1D_D": (3, 2), "1D_X": (17, 2), "1D_W": (19, 1), "1D_Y": (9, 8),
     "1A_H": (21, 1), "1A_R": (41, 2), "1A_X": (13, 12), "1A_W": (15, 1), "1A_Y": (9, 8),
-    "2D_X": (9, 8), "2D_W": (11, 1), "2D_Y": (9, 8),
+    "2D_D": (3, 2), "2D_X": (5, 2), "2D_W": (7, 1), "2D_Y": (9, 8),
     "2A_H": (17, 1), "2A_R": (33, 2), "2A_X": (13, 12), "2A_W": (16, 1), "2A_Y": (9, 8),
     "2J_H": (2, 1), "2J_R": (3, 2), "2J_X": (13, 12), "2J_W": (15, 1), "2J_Y": (9, 8),
     "2N": (33, 6), "2Q": (36, 1),
@@ -276,18 +276,19 @@ def jadd(F, X1, Y1, Z1, X2, Y2, Z2):
 
 
 def dbl2(F, X, Y, Z):
-    """g2l_dbl: dbl-2009-l rearranged for the Fp2 products' bounds -- D = 4 X B from one product
-    (the (X + B)^2 - A - C form grows D by its subtraction constant), E = 3A normalised before
-    its square, E W = 3 (A W)"""
+    """g2l_dbl: dbl-2009-l (2M + 5S) with D = 2((X + B)^2 - A - C) partially reduced (red, no
+    product): unreduced, D's subtraction constant grows the point past VMAX; X + B and E = 3A
+    normalised before their squares"""
     A = F.sqr(X)
     B = F.sqr(Y)
     C = F.sqr(B)
-    D1 = F.mul(X, B)                                  # D = 4 D1
-    Fv = F.sqr(F.norm(F.add(F.shl(A, 1), A)))
-    X3 = F.norm(F.sub(Fv, F.shl(D1, 3), "D_X"))
-    W = F.sub(F.shl(D1, 2), X3, "D_W")
-    AW = F.mul(W, A)
-    Y3 = F.norm(F.sub(F.add(F.shl(AW, 1), AW), F.shl(C, 3), "D_Y"))
+    T = F.sqr(F.norm(F.add(X, B)))
+    E = F.norm(F.add(F.shl(A, 1), A))
+    Fv = F.sqr(E)
+    D = f2_red(F.shl(F.sub(T, F.add(A, C), "D_D"), 1))
+    X3 = F.norm(F.sub(Fv, F.shl(D, 1), "D_X"))
+    W = F.sub(D, X3, "D_W")
+    Y3 = F.norm(F.sub(F.mul(W, E), F.shl(C, 3), "D_Y"))  # W first: 33p - W.c1 (2N) dominates
     Z3 = F.mul(F.shl(Y, 1), Z)
     return X3, Y3, Z3
 

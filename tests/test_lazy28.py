@@ -56,7 +56,7 @@ def test_constants_match_ec28():
     assert used("HDNI G1L g1l_dbl") == sorted([k["1D_D"], k["1D_X"], k["1D_W"], k["1D_Y"]])
     assert used("HD G1L g1l_add_tail") == sorted([k["1A_X"], k["1A_Y"], k["1A_W"]])
     assert used("HDNI G1L g1l_madd") == used("HDNI G1L g1l_add") == sorted([k["1A_H"], k["1A_R"]])
-    assert used("HDNI G2L g2l_dbl", pat=r"f2l_sub<(\d+), (\d+)>") == sorted([k["2D_X"], k["2D_W"], k["2D_Y"]])
+    assert used("HDNI G2L g2l_dbl", pat=r"f2l_sub<(\d+), (\d+)>") == sorted([k["2D_D"], k["2D_X"], k["2D_W"], k["2D_Y"]])
     assert used("HDNI G2L g2l_madd", pat=r"f2l_sub<(\d+), (\d+)>") == sorted(
         [k["2A_H"], k["2A_R"], k["2A_X"], k["2A_W"], k["2A_Y"]])
     assert used("HDNI G2L g2l_add", pat=r"f2l_sub<(\d+), (\d+)>") == sorted(
