@@ -170,14 +170,11 @@ __global__ KB_OCC(HB_OCC_HASH) void k_h2c_clear3(uint32_t n, MsgEntry* __restric
 #endif
 }
 
-// messages up to which the ladders run on lane pairs (HBLS_HASH_PAIR_MAX, default 16384: 512
-// wavefronts, half a wave per SIMD -- below it the one-lane ladders leave the chip idle)
+// messages up to which the ladders run on lane pairs (HBLS_HASH_PAIR_MAX, read per call; default
+// 16384: 512 wavefronts, half a wave per SIMD -- below it the one-lane ladders leave the chip idle)
 static size_t hash_pair_max() {
-  static const size_t v = [] {
-    const char* e = getenv("HBLS_HASH_PAIR_MAX");
-    return e ? (size_t)strtoull(e, nullptr, 0) : (size_t)16384;
-  }();
-  return v;
+  const char* e = getenv("HBLS_HASH_PAIR_MAX");
+  return e ? (size_t)strtoull(e, nullptr, 0) : (size_t)16384;
 }
 
 void launch_hash_to_g2_split(const uint8_t* msgs, const uint64_t* off, const uint32_t* len, uint32_t n, MsgEntry* hm,

@@ -1286,6 +1286,7 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
   sa.sig = vsig;
   sa.sig_st = vsigst;
   sa.gverdict = gver;
+  sa.grp_off = dgoff;
   sa.n_agg = (uint32_t)n_agg;
   if (n_agg) {
     sa.ta_status = fold->ta_status;
@@ -1590,9 +1591,18 @@ int verify_host(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msgs, co
   for (size_t k = 0; k < n; k++) mstart[all.idx[k] + 1]++;
   for (size_t j = 0; j < all.len.size(); j++) mstart[j + 1] += mstart[j];
   for (size_t k = 0; k < n; k++) order[mstart[all.idx[k]]++] = k;
+  // a call below the batched final exponentiation's size (the latency-bound small calls, e.g. the
+  // coalesced single-item callers) checks every item alone: a group of several items needs random
+  // coefficients, i.e. a 64-bit scalar ladder per item on the call's critical path (~3.7 ms for a
+  // lone lane), where separate checks only add lanes to kernels that have them to spare
+  // (HBLS_SINGLE_MAX, read per call: items below which every item is its own group; default the
+  // batched final exponentiation's group threshold)
+  const char* sm = getenv("HBLS_SINGLE_MAX");
+  const size_t single_max = sm ? (size_t)strtoull(sm, nullptr, 0) : g_fe_batch_min.load();
+  const size_t gmax = n < single_max ? 1 : g_gmax;
   std::vector<size_t> gstart;  // group starts in `order`
   for (size_t k = 0; k < n; k++)
-    if (k == 0 || all.idx[order[k]] != all.idx[order[k - 1]] || k - gstart.back() >= g_gmax) gstart.push_back(k);
+    if (k == 0 || all.idx[order[k]] != all.idx[order[k - 1]] || k - gstart.back() >= gmax) gstart.push_back(k);
   const size_t n_groups = gstart.size();
   gstart.push_back(n);
   if (n >= 0xffffffffull) return set_err("verify batch: too many items");

@@ -351,6 +351,10 @@ struct ScatterArgs {
   const HmEntry* sig;
   const uint8_t* sig_st;
   const uint8_t* gverdict;  // [n_groups], 0 = the group's combined check passed
+  // [n_groups + 1] group offsets (nullable: every item its own group).  A failing group of one
+  // item is that item's verdict (its check is the item's own up to a nonzero exponent r): no
+  // re-check alone
+  const uint32_t* grp_off;
   // folded aggregates (nullable)
   uint32_t n_agg;
   const uint8_t* ta_status;

@@ -251,14 +251,11 @@ __global__ KB_OCC(HB_OCC_PAIR3) void k_pair6_fin(Pair3Args a) {
 #endif
 }
 
-// units up to which the eighteen-lane kernel runs (HBLS_FE18_MAX, default 256: a few waves per
-// XCD; beyond, the six-lane one's fewer duplicated additions per unit win)
+// units up to which the eighteen-lane kernel runs (HBLS_FE18_MAX, read per call; default 256: a
+// few waves per XCD; beyond, the six-lane one's fewer duplicated additions per unit win)
 static uint32_t fe18_max() {
-  static const uint32_t v = [] {
-    const char* e = getenv("HBLS_FE18_MAX");
-    return e ? (uint32_t)strtoul(e, nullptr, 0) : 256u;
-  }();
-  return v;
+  const char* e = getenv("HBLS_FE18_MAX");
+  return e ? (uint32_t)strtoul(e, nullptr, 0) : 256u;
 }
 
 void launch_pair6_fin(const Pair3Args& a, hipStream_t s) {

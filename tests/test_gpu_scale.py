@@ -413,13 +413,15 @@ def test_batched_fe_rejects_cancelling_errors(L, hipbls, monkeypatch):
     st = hipbls.verify_batch(pks, msgs, bad)
     assert st == [NOT_VERIFIED if i < 2 else OK for i in range(n)]
     d = [b - a for a, b in zip(s0, _stats(L))]
-    assert d[3] >= 1 and d[2] == 2, d  # the failing batch's groups checked alone, then the two items
+    # the failing batch's groups checked alone; those are the two items' own checks (groups of one):
+    # no item is re-checked
+    assert d[3] >= 1 and d[2] == 0, d
 
 
 def test_slot_msm_clean_and_cancelling_errors(L, hipbls, monkeypatch):
     """The slot-wide check (HBLS_SLOT_MSM) on 300 groups of one: a clean call passes it with no
     per-batch or per-item check; two signatures with opposite errors (sig0 + D, sig1 - D) make it
-    fail, and the per-batch check then rejects exactly those two.  Then the adaptive choice: the
+    fail, and the per-batch check then rejects exactly those two (their groups' checks, no re-check alone).  Then the adaptive choice: the
     next calls skip the slot-wide check (same verdicts) until one passes every batch."""
     from oracle import bls12381 as B
     monkeypatch.setenv("HBLS_STATS", "1")
@@ -442,13 +444,13 @@ def test_slot_msm_clean_and_cancelling_errors(L, hipbls, monkeypatch):
         st = hipbls.verify_batch(pks, msgs, bad)
         assert st == [NOT_VERIFIED if i < 2 else OK for i in range(n)]
         d = [b - a for a, b in zip(s0, _stats(L))]
-        assert d[4] == 1 and d[5] == 1 and d[3] >= 1 and d[2] == 2, d
+        assert d[4] == 1 and d[5] == 1 and d[3] >= 1 and d[2] == 0, d
         # adaptive (HBLS_ADAPTIVE, default on): after a failed slot-wide check the next calls skip it
         # and run the per-batch check directly -- same verdicts -- until one passes every batch
         s0 = _stats(L)
         assert hipbls.verify_batch(pks, msgs, bad) == st
         d = [b - a for a, b in zip(s0, _stats(L))]
-        assert d[4] == 0 and d[3] >= 1 and d[2] == 2, d
+        assert d[4] == 0 and d[3] >= 1 and d[2] == 0, d
         s0 = _stats(L)
         assert hipbls.verify_batch(pks, msgs, sigs) == [OK] * n  # clean: skipped, every batch passes
         d = [b - a for a, b in zip(s0, _stats(L))]
@@ -464,8 +466,10 @@ def test_slot_msm_clean_and_cancelling_errors(L, hipbls, monkeypatch):
 
 def test_batched_groups_pass_without_fallback(L, hipbls, monkeypatch):
     """Clean partials over a few messages: every verification group passes its combined check,
-    no item is re-checked alone (the random linear combination is effective, not just correct)."""
+    no item is re-checked alone (the random linear combination is effective, not just correct).
+    (HBLS_SINGLE_MAX=0: a call this small would otherwise check every item alone.)"""
     monkeypatch.setenv("HBLS_STATS", "1")
+    monkeypatch.setenv("HBLS_SINGLE_MAX", "0")
     keys = [hipbls.generate_secret_key() for _ in range(48)]
     msgs = [hashlib.sha256(b"committee %d" % (k % 3)).digest() for k in range(48)]
     sigs = hipbls.sign_batch(keys, msgs)
@@ -482,6 +486,14 @@ def test_batched_groups_pass_without_fallback(L, hipbls, monkeypatch):
     assert st == [NOT_VERIFIED if i == 5 else OK for i in range(48)]
     d = [b - a for a, b in zip(s0, _stats(L))]
     assert d[2] == 16, d
+    # the default for so small a call: every item its own group (its check the item's verdict),
+    # no combination, no re-check
+    monkeypatch.delenv("HBLS_SINGLE_MAX")
+    s0 = _stats(L)
+    st = hipbls.verify_batch(pks, msgs, bad)
+    assert st == [NOT_VERIFIED if i == 5 else OK for i in range(48)]
+    d = [b - a for a, b in zip(s0, _stats(L))]
+    assert d[0] == 48 and d[1] == 48 and d[2] == 0, d
 
 
 R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
@@ -693,6 +705,49 @@ def test_hash_paths_agree(L, monkeypatch):
 
     hs = hm_s.cpu().numpy().reshape(n, E)[:, :208]
     assert canon(hs) == canon(a)
+
+    # the staged kernels for a call below HBLS_HASH_PAIR_MAX: the cofactor ladders on lane pairs
+    # (ec28.h F2Half, the default for 512 messages) and on one lane each give the same points
+    hm_p = torch.zeros(k * E, dtype=torch.uint8, device=dev)
+    hm_1 = torch.zeros(k * E, dtype=torch.uint8, device=dev)
+    _chk(L, L.hbls_hash_to_g2_device(_p(dm), _p(off), _p(ln), k, _p(hm_p), sp))
+    monkeypatch.setenv("HBLS_HASH_PAIR_MAX", "0")
+    _chk(L, L.hbls_hash_to_g2_device(_p(dm), _p(off), _p(ln), k, _p(hm_1), sp))
+    s.synchronize()
+    monkeypatch.delenv("HBLS_HASH_PAIR_MAX")
+    hp = hm_p.cpu().numpy().reshape(k, E)[:, :208]
+    h1 = hm_1.cpu().numpy().reshape(k, E)[:, :208]
+    assert np.array_equal(hp, h1)  # the same formulas and values, products split or not
+    assert canon(hp) == canon(a[:k])
+
+
+def test_small_calls_lane_layouts_agree(hipbls, monkeypatch):
+    """A small Verify batch (the latency path: k_lml with its lane-pair chain and eighteen-lane loop,
+    the final exponentiation over eighteen lanes) against the same batch with the six-lane final
+    exponentiation (HBLS_FE18_MAX=0) and one-lane hashing ladders (HBLS_HASH_PAIR_MAX=0): the
+    statuses agree with each other and with construction."""
+    rng = random.Random(77)
+    keys = [hipbls.generate_secret_key() for _ in range(24)]
+    msgs = [hashlib.sha256(b"small %d" % (k % 9)).digest() for k in range(24)]
+    sigs = hipbls.sign_batch(keys, msgs)
+    pks = [hipbls.secret_to_public_key(k) for k in keys]
+    cases = []
+    for j in range(48):
+        k = rng.randrange(24)
+        if j % 5 == 0:
+            cases.append((pks[k], hashlib.sha256(b"wrong %d" % j).digest(), sigs[k], NOT_VERIFIED))
+        else:
+            cases.append((pks[k], msgs[k], sigs[k], OK))
+    pk, m, sg, want = zip(*cases)
+    got = hipbls.verify_batch(list(pk), list(m), list(sg))
+    monkeypatch.setenv("HBLS_FE18_MAX", "0")
+    monkeypatch.setenv("HBLS_HASH_PAIR_MAX", "0")
+    got6 = hipbls.verify_batch(list(pk), list(m), list(sg))
+    one = hipbls.verify_batch([pk[1]], [m[1]], [sg[1]])
+    monkeypatch.delenv("HBLS_FE18_MAX")
+    monkeypatch.delenv("HBLS_HASH_PAIR_MAX")
+    assert list(got) == list(want) == list(got6)
+    assert list(one) == [want[1]]
 
 
 def test_slot_c3_full_size(L):

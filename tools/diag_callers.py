@@ -40,6 +40,22 @@ def worker(w):
         k += threads
 
 
+if len(sys.argv) > 3 and sys.argv[3] == "batch":  # one caller, `threads` items per call (a trace target)
+    m = threads
+    st = np.zeros(m, dtype=np.uint8)
+    idx = [(k * 104729) % NP for k in range(m)]
+    P = np.concatenate([pks[48 * i:48 * i + 48] for i in idx])
+    S = np.concatenate([sigs[96 * i:96 * i + 96] for i in idx])
+    M = np.concatenate([msgs[32 * i:32 * i + 32] for i in idx])
+    off = np.arange(m, dtype=np.uint64) * 32
+    ln = np.full(m, 32, dtype=np.uint32)
+    ts = []
+    for _ in range(12):
+        t1 = time.perf_counter()
+        L.hbls_verify_batch(bench._p(P), bench._p(S), bench._p(M), bench._p(off), bench._p(ln), m, bench._p(st))
+        ts.append((time.perf_counter() - t1) * 1e3)
+    print(f"batch of {m}: ms", [round(x, 2) for x in ts], "all ok", not st.any(), flush=True)
+    sys.exit(0)
 t0 = time.perf_counter()
 ths = [threading.Thread(target=worker, args=(w,)) for w in range(threads)]
 for th in ths:
