@@ -567,6 +567,45 @@ HD G1J g1l_msm_ladder(const G1J* __restrict__ tab, const Pair* __restrict__ coef
   return g1l_to_jac(R);
 }
 
+// The sparse coefficient format of the chunk ladders when no bucket MSM reads the coefficients
+// (vbatch.hip rlc_digits): r = A + B lambda, A = sum_j u_j 4^j and B = sum_j v_j 4^j over
+// RLC_DIGITS = 22 positions, every (u_j, v_j) one of the eight nonzero pairs of {-1, 0, 1}^2 --
+// three random bits d: entry d & 3 of (1, 0), (0, 1), (1, 1), (1, -1), negated when d & 4.  Base 4
+// with digits in {-1, 0, 1} is a unique representation and |A|, |B| < 2^44 are far below the
+// shortest nonzero (a, b) with a + b lambda = 0 mod r (~2^127), so the 8^22 = 2^66 digit strings
+// are 2^66 distinct coefficients mod r; one addition per digit: 22 per item where the dense
+// 32-bit pair takes 32 (and every digit is nonzero, so no lane adds a point it then drops).
+// Digit j of an item's record: bits 3 (j mod 10) .. +2 of word j / 10; word 3 nonzero = usable.
+constexpr int RLC_DIGITS = 22;
+template <class Quad>
+HD uint32_t rlc_digit(const Quad& c, int j) {
+  const uint32_t w = j < 10 ? c.x : (j < 20 ? c.y : c.z);
+  return (w >> (3 * (j % 10))) & 7u;
+}
+
+// sum_i [A_i] T_i1 + [B_i] T_i2 over a chunk in the sparse format: tab[4i + e] the affine points
+// T1, T2, T1 + T2, T1 - T2 (Z = 1 records); the 44 doublings shared by the chunk's items
+template <class Quad>  // uint4 on the device
+HD G1J g1l_msm_ladder_sparse(const G1J* __restrict__ tab, const Quad* __restrict__ coef4, uint32_t first,
+                             uint32_t cnt) {
+  G1L R = g1l_infinity();
+  HB_NOUNROLL for (int j = RLC_DIGITS - 1; j >= 0; j--) {
+    if (j != RLC_DIGITS - 1) {
+      R = g1l_dbl(R);
+      R = g1l_dbl(R);
+    }
+    HB_NOUNROLL for (uint32_t k = 0; k < cnt; k++) {
+      const uint32_t i = first + k;
+      const Quad c = coef4[i];
+      if (!c.w) continue;
+      const uint32_t d = rlc_digit(c, j);
+      const G1J T = tab[4ull * i + (d & 3u)];
+      R = g1l_madd(R, l_from(T.X), l_from((d & 4u) ? fp_neg(T.Y) : T.Y));
+    }
+  }
+  return g1l_to_jac(R);
+}
+
 // lazy28.py jadd2: add-2007-bl as g1l_add with H normalised (its square is an Fp2 square)
 template <class M = F2One>
 HDNI G2L g2l_add(const G2L& p, const G2L& q, M m = M()) {
@@ -632,6 +671,28 @@ HD G2J g2l_msm_ladder(const G2J* __restrict__ tab, const Pair* __restrict__ coef
         const G2J T = tab[3ull * i + sel - 1u];
         R = g2l_madd(R, f2l_from(T.X), f2l_from(T.Y));
       }
+    }
+  }
+  return g2l_to_jac(R);
+}
+
+// the G2 twin of g1l_msm_ladder_sparse: tab[4i + e] affine S, -psi^2(S), their sum and difference
+template <class Quad>
+HD G2J g2l_msm_ladder_sparse(const G2J* __restrict__ tab, const Quad* __restrict__ coef4, uint32_t first,
+                             uint32_t cnt) {
+  G2L R = g2l_infinity();
+  HB_NOUNROLL for (int j = RLC_DIGITS - 1; j >= 0; j--) {
+    if (j != RLC_DIGITS - 1) {
+      R = g2l_dbl(R);
+      R = g2l_dbl(R);
+    }
+    HB_NOUNROLL for (uint32_t k = 0; k < cnt; k++) {
+      const uint32_t i = first + k;
+      const Quad c = coef4[i];
+      if (!c.w) continue;
+      const uint32_t d = rlc_digit(c, j);
+      const G2J T = tab[4ull * i + (d & 3u)];
+      R = g2l_madd(R, f2l_from(T.X), f2l_from((d & 4u) ? f2_neg(T.Y) : T.Y));
     }
   }
   return g2l_to_jac(R);

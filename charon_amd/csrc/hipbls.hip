@@ -311,7 +311,7 @@ enum WsId {
   W_TAPTS, W_TADST, W_TAMST, W_TADIG, W_TATAB, W_TAJ,  // ThresholdAggregate / Aggregate
   W_TACSM, W_TASDIG, W_TASOK, W_TASDONE, W_TASTAB, W_TANONUNI,  // its small-scalar path
   W_SEGA, W_SEGB, W_SEGSTA, W_SEGSTB, W_VAPT, W_VAPV, W_PLAN,  // VerifyAggregate key reduction
-  W_PCNT, W_PCOFF, W_PCFIRST, W_PCCOUNT, W_COEF, W_RT1, W_RT2,  // chunk plan + multi-scalar RLC
+  W_PCNT, W_PCOFF, W_PCFIRST, W_PCCOUNT, W_COEF, W_COEF4, W_RT1, W_RT2,  // chunk plan + multi-scalar RLC
   W_TPCNT, W_TPCOFF, W_TPCFIRST, W_TPCCOUNT,                    // chunk plan of the aggregation
   W_FBUF, W_GS, W_BS, W_BLINES, W_BBAD, W_BVER, W_GLIST, W_GCOUNT,  // batched final exponentiation
   W_MCNT, W_MOFF, W_MCUR, W_MORDER, W_MENT, W_MBUCKET, W_MPART, W_MPART2, W_MTOT, W_PBUF1, W_PBUF2, W_PBUF3, W_SFAIL,  // slot-wide check
@@ -928,11 +928,16 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
     const size_t max_chunks = n / cmax + n_groups;
     uint32_t *pcnt, *pcoff, *pcf, *pcc;
     uint2* coef;
+    uint4* coef4 = nullptr;
     G1J* t1;
     G2J* t2;
+    // the sparse coefficient format (22 additions per item instead of 32) unless the slot-wide
+    // bucket MSM reads the coefficients: under attack (skip_msm) and below the slot-wide size
+    const bool sparse = !(smsm && !skip_msm);
     if (wsbuf(w, W_PCNT, n_groups, &pcnt) || wsbuf(w, W_PCOFF, n_groups + 1, &pcoff) ||
         wsbuf(w, W_PCFIRST, max_chunks, &pcf) || wsbuf(w, W_PCCOUNT, max_chunks, &pcc) ||
-        wsbuf(w, W_COEF, n + n_agg, &coef) || wsbuf(w, W_RT1, 3 * n, &t1) || wsbuf(w, W_RT2, 3 * n, &t2))
+        wsbuf(w, W_COEF, n + n_agg, &coef) || wsbuf(w, W_RT1, 4 * n, &t1) || wsbuf(w, W_RT2, 4 * n, &t2) ||
+        (sparse && wsbuf(w, W_COEF4, n, &coef4)))
       return -1;
     TIMED(d, "k_plan", s, launch_plan(dgoff, (uint32_t)n_groups, cmax, pcnt, pcoff, pcf, pcc, s));
     RlcMsmArgs ra{};
@@ -946,6 +951,8 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
     ra.key_base = 0;
     ra.key = key;
     ra.coef = coef;
+    ra.coef4 = coef4;
+    ra.sparse = sparse ? 1 : 0;
     ra.t1 = t1;
     ra.t2 = t2;
     ra.pout = pr;

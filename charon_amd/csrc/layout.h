@@ -239,9 +239,11 @@ struct RlcMsmArgs {
   const uint32_t* total;  // device: number of chunks
   uint32_t key_base;
   RlcKey key;
-  uint2* coef;    // per item
-  G1J* t1;        // 3 per item
-  G2J* t2;        // 3 per item
+  uint2* coef;    // per item (the dense (a, b) pairs a bucket MSM reads)
+  uint4* coef4;   // per item in the sparse format (ec28.h RLC_DIGITS), when `sparse`
+  int sparse;     // 1: sparse coefficients (sides 1 and 3 only; nothing reads coef)
+  G1J* t1;        // 3 per item (4 when sparse)
+  G2J* t2;        // 3 per item (4 when sparse)
   G1JEntry* pout;
   G2JEntry* sout;
   int always;     // random r for groups of one item too (batched final exponentiation)

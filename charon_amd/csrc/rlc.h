@@ -44,4 +44,40 @@ HD G2J rlc_g2(const G2A& S, uint32_t a, uint32_t b) {
   return joint_mul32(S, S2, a, b);
 }
 
+// The chunk ladders' points in ec28.h's sparse coefficient format: per item T1, T2, T1 + T2,
+// T1 - T2 at t[4i .. 4i + 3], affine with ONE inversion per chunk (Montgomery's trick).  Forward
+// pass (sparse_put, items in order): the four records, entry 0's Z holding the running product of
+// the sums' Z before this item; returns the product through it.  Then inv = 1 / that product and
+// the backward pass (sparse_fix, items in reverse) makes the records affine, returning the inverse
+// of the product before the item.  A sum at infinity (T1 = -+T2: never for points of the prime
+// subgroups) keeps Z = 1 so the product stays invertible; such an item's record is never read.
+template <class F>
+HD F sparse_put(Jac<F>* t, uint64_t i, const Aff<F>& P, const Aff<F>& P2, const F& acc) {
+  const Jac<F> J1 = jac_from_aff(P), J2 = jac_from_aff(P2);
+  Jac<F> J3 = jac_add_aff(J1, P2);
+  Jac<F> J4 = jac_add_aff(J1, Aff<F>{P2.x, f_neg(P2.y), false});
+  if (f_is_zero(J3.Z)) J3.Z = J1.Z;
+  if (f_is_zero(J4.Z)) J4.Z = J1.Z;
+  t[4 * i] = {J1.X, J1.Y, acc};
+  t[4 * i + 1] = J2;
+  t[4 * i + 2] = J3;
+  t[4 * i + 3] = J4;
+  return f_mul(f_mul(acc, J3.Z), J4.Z);
+}
+template <class F>
+HD F sparse_fix(Jac<F>* t, uint64_t i, const F& inv_through) {
+  Jac<F> J1 = t[4 * i];
+  const Jac<F> J3 = t[4 * i + 2], J4 = t[4 * i + 3];
+  const F one = t[4 * i + 1].Z;
+  const F z34 = f_mul(inv_through, J1.Z);  // 1 / (Z3 Z4)
+  const F inv_before = f_mul(f_mul(inv_through, J3.Z), J4.Z);
+  const F z3 = f_mul(z34, J4.Z), z4 = f_mul(z34, J3.Z);
+  const F z3s = f_sqr(z3), z4s = f_sqr(z4);
+  J1.Z = one;
+  t[4 * i] = J1;
+  t[4 * i + 2] = {f_mul(J3.X, z3s), f_mul(J3.Y, f_mul(z3s, z3)), one};
+  t[4 * i + 3] = {f_mul(J4.X, z4s), f_mul(J4.Y, f_mul(z4s, z4)), one};
+  return inv_before;
+}
+
 }  // namespace hb

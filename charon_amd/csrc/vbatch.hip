@@ -172,6 +172,20 @@ __device__ __forceinline__ void rlc_coeffs(const RlcKey& key, uint32_t item, uin
   if ((a | b) == 0) a = 1;  // r != 0
 }
 
+// the sparse-format digits of entry `item` (ec28.h RLC_DIGITS: 66 random bits of the same hash
+// block, 10 three-bit digits per word), word 3 = 1 (usable)
+__device__ __forceinline__ uint4 rlc_digits(const RlcKey& key, uint32_t item) {
+  uint32_t w[16];
+  HB_UNROLL for (int j = 0; j < 8; j++) w[j] = key.w[j];
+  w[8] = item;
+  w[9] = 0x80000000u;
+  HB_UNROLL for (int j = 10; j < 15; j++) w[j] = 0;
+  w[15] = 36 * 8;
+  Sha256State st = sha256_init();
+  sha256_compress(st, w);
+  return make_uint4(st.h[0] & 0x3fffffffu, st.h[1] & 0x3fffffffu, st.h[2] & 0x3fu, 1u);
+}
+
 __device__ __forceinline__ bool item_usable(const G1AEntry& p, uint8_t pst, const HmEntry& s, uint8_t sst) {
   return !pst && !sst && !p.inf && !s.inf;
 }
@@ -300,75 +314,118 @@ __device__ __forceinline__ Jac<F> msm_ladder(const Jac<F>* __restrict__ tab, con
   return R;
 }
 
-// SIDES as RlcMsmArgs::sides, a template argument so that the public-key-only launch of the
-// slot-wide check does not allocate registers for the G2 ladder
-template <int SIDES>
-__global__ KB_OCC(HB_OCC_RLC) void k_rlc_msm(RlcMsmArgs a) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  if (a.guard && *a.guard == 0) return;
-  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= *a.total) return;
-  const uint32_t first = a.cfirst[c], cc = a.ccount[c], cnt = cc & 0x7fffffffu;
-  const bool single = (cc & 0x80000000u) != 0 && !a.always;
-  if (single) {  // r = 1
-    const uint32_t i = first;
-    const bool usable = !a.pk_st[i] && !a.sig_st[i] && !a.pk[i].inf && !a.sig[i].inf;
-    const G1AEntry pe = a.pk[i];
-    if (SIDES & 1) {
-      const G1J rp = usable ? jac_from_aff(G1A{pe.x, pe.y, false}) : jac_infinity<Fp>();
-      a.pout[i] = {rp.X, rp.Y, rp.Z};
-      a.coef[i] = make_uint2(usable ? 1u : 0u, 0u);
+// the stored-word twin of ec28.h g1l/g2l_msm_ladder_sparse (HB_G1_LAZY=0 / HB_G2_LAZY=0 builds)
+template <class F>
+__device__ __forceinline__ Jac<F> msm_ladder_sparse(const Jac<F>* __restrict__ tab, const uint4* __restrict__ coef4,
+                                                    uint32_t first, uint32_t cnt) {
+  Jac<F> R = jac_infinity<F>();
+  HB_NOUNROLL for (int j = RLC_DIGITS - 1; j >= 0; j--) {
+    if (j != RLC_DIGITS - 1) R = jac_dbl(jac_dbl(R));
+    HB_NOUNROLL for (uint32_t k = 0; k < cnt; k++) {
+      const uint32_t i = first + k;
+      const uint4 c = coef4[i];
+      if (!c.w) continue;
+      const uint32_t d = rlc_digit(c, j);
+      const Jac<F> T = tab[4ull * i + (d & 3u)];
+      R = jac_add_aff(R, Aff<F>{T.X, (d & 4u) ? f_neg(T.Y) : T.Y, false});
     }
-    if (SIDES & 2) {
-      const HmEntry se = a.sig[i];
-      const G2J rs = usable ? jac_from_aff(G2A{se.x, se.y, false}) : jac_infinity<Fp2>();
-      a.sout[i] = {rs.X, rs.Y, rs.Z};
-    }
-    return;
   }
+  return R;
+}
+
+// The pieces of the chunk kernels.  Split (HB_RLC_SPLIT, default): one kernel builds the
+// coefficients and ladder tables, then one kernel per side runs the ladder -- each kernel holds
+// only its own phase's state (the fused kernel spilled 1.6 KB per lane: the SHA schedule, the
+// inversion and both ladders in one register allocation).
+#ifndef HB_RLC_SPLIT
+#define HB_RLC_SPLIT 1
+#endif
+
+// a group of ONE item keeps r = 1 (unless `always`): its records written here; true if so
+template <int SIDES>
+__device__ __forceinline__ bool rlc_single(const RlcMsmArgs& a, uint32_t first, uint32_t cc, bool write) {
+  if (!((cc & 0x80000000u) != 0 && !a.always)) return false;
+  if (!write) return true;
+  const uint32_t i = first;
+  const bool usable = !a.pk_st[i] && !a.sig_st[i] && !a.pk[i].inf && !a.sig[i].inf;
+  const G1AEntry pe = a.pk[i];
   if (SIDES & 1) {
-    // coefficients and the G1 ladder points of the chunk's items
-    Fp acc = fp_one();
+    const G1J rp = usable ? jac_from_aff(G1A{pe.x, pe.y, false}) : jac_infinity<Fp>();
+    a.pout[i] = {rp.X, rp.Y, rp.Z};
+    a.coef[i] = make_uint2(usable ? 1u : 0u, 0u);
+  }
+  if (SIDES & 2) {
+    const HmEntry se = a.sig[i];
+    const G2J rs = usable ? jac_from_aff(G2A{se.x, se.y, false}) : jac_infinity<Fp2>();
+    a.sout[i] = {rs.X, rs.Y, rs.Z};
+  }
+  return true;
+}
+
+// coefficients and the G1 ladder points of a chunk's items: P, phi(P), P + phi(P) (dense) or
+// P, phi(P), P + phi(P), P - phi(P) (sparse), affine with ONE inversion per chunk (Montgomery's
+// trick), so the ladder adds affine points (7M + 4S instead of 11M + 5S)
+__device__ __forceinline__ void rlc_tab_g1(const RlcMsmArgs& a, uint32_t first, uint32_t cnt) {
+  Fp acc = fp_one();
+  if (a.sparse) {
     HB_NOUNROLL for (uint32_t k = 0; k < cnt; k++) {
       const uint32_t i = first + k;
       const bool usable = !a.pk_st[i] && !a.sig_st[i] && !a.pk[i].inf && !a.sig[i].inf;
-      uint32_t ca = 0, cb = 0;
-      if (usable) rlc_coeffs(a.key, a.key_base + i, ca, cb);
-      a.coef[i] = make_uint2(ca, cb);
+      a.coef4[i] = usable ? rlc_digits(a.key, a.key_base + i) : make_uint4(0u, 0u, 0u, 0u);
       const G1AEntry pe = a.pk[i];
       const G1A P = {pe.x, pe.y, false};
-      const G1A P2 = {fp_mul(P.x, fp_from_const(G1_BETA)), P.y, false};
-      const G1J J1 = jac_from_aff(P), J2 = jac_from_aff(P2);
-      G1J J3 = jac_add_aff(J1, P2);
-      if (fp_is_zero(J3.Z)) J3.Z = fp_one();  // never for a point of G1; keeps the product invertible
-      a.t1[3ull * i] = {J1.X, J1.Y, acc};     // the running product of the Z before this item
-      a.t1[3ull * i + 1] = J2;
-      a.t1[3ull * i + 2] = J3;
-      acc = fp_mul(acc, J3.Z);
+      acc = sparse_put(a.t1, i, P, G1A{fp_mul(P.x, fp_from_const(G1_BETA)), P.y, false}, acc);
     }
-    // P + phi(P) of every item affine with ONE inversion per chunk (Montgomery's trick), so the
-    // ladder adds affine points (7M + 4S instead of 11M + 5S)
     Fp inv = fp_inv(acc);
-    HB_NOUNROLL for (int k = (int)cnt - 1; k >= 0; k--) {
-      const uint32_t i = first + (uint32_t)k;
-      const G1J J3 = a.t1[3ull * i + 2];
-      G1J J1 = a.t1[3ull * i];
-      const Fp zi = fp_mul(inv, J1.Z);
-      inv = fp_mul(inv, J3.Z);
-      const Fp zi2 = fp_sqr(zi);
-      J1.Z = fp_one();
-      a.t1[3ull * i] = J1;
-      a.t1[3ull * i + 2] = {fp_mul(J3.X, zi2), fp_mul(J3.Y, fp_mul(zi2, zi)), fp_one()};
-    }
-    const G1J rp = HB_G1_LAZY ? g1l_msm_ladder(a.t1, a.coef, first, cnt) : msm_ladder<Fp, true>(a.t1, a.coef, first, cnt);
-    a.pout[first] = {rp.X, rp.Y, rp.Z};
-    const G1J zi = jac_infinity<Fp>();
-    for (uint32_t k = 1; k < cnt; k++) a.pout[first + k] = {zi.X, zi.Y, zi.Z};
+    HB_NOUNROLL for (int k = (int)cnt - 1; k >= 0; k--) inv = sparse_fix(a.t1, first + (uint32_t)k, inv);
+    return;
   }
-  if (!(SIDES & 2)) return;
-  // the G2 ladder points (S + (-psi^2 S) affine like the G1 side: one Fp2 inversion per chunk),
-  // then the G2 ladder (coefficients from the workspace)
+  HB_NOUNROLL for (uint32_t k = 0; k < cnt; k++) {
+    const uint32_t i = first + k;
+    const bool usable = !a.pk_st[i] && !a.sig_st[i] && !a.pk[i].inf && !a.sig[i].inf;
+    uint32_t ca = 0, cb = 0;
+    if (usable) rlc_coeffs(a.key, a.key_base + i, ca, cb);
+    a.coef[i] = make_uint2(ca, cb);
+    const G1AEntry pe = a.pk[i];
+    const G1A P = {pe.x, pe.y, false};
+    const G1A P2 = {fp_mul(P.x, fp_from_const(G1_BETA)), P.y, false};
+    const G1J J1 = jac_from_aff(P), J2 = jac_from_aff(P2);
+    G1J J3 = jac_add_aff(J1, P2);
+    if (fp_is_zero(J3.Z)) J3.Z = fp_one();  // never for a point of G1; keeps the product invertible
+    a.t1[3ull * i] = {J1.X, J1.Y, acc};     // the running product of the Z before this item
+    a.t1[3ull * i + 1] = J2;
+    a.t1[3ull * i + 2] = J3;
+    acc = fp_mul(acc, J3.Z);
+  }
+  Fp inv = fp_inv(acc);
+  HB_NOUNROLL for (int k = (int)cnt - 1; k >= 0; k--) {
+    const uint32_t i = first + (uint32_t)k;
+    const G1J J3 = a.t1[3ull * i + 2];
+    G1J J1 = a.t1[3ull * i];
+    const Fp zi = fp_mul(inv, J1.Z);
+    inv = fp_mul(inv, J3.Z);
+    const Fp zi2 = fp_sqr(zi);
+    J1.Z = fp_one();
+    a.t1[3ull * i] = J1;
+    a.t1[3ull * i + 2] = {fp_mul(J3.X, zi2), fp_mul(J3.Y, fp_mul(zi2, zi)), fp_one()};
+  }
+}
+
+// the G2 ladder points: S, -psi^2(S), their sum (and difference when sparse), affine likewise
+__device__ __forceinline__ void rlc_tab_g2(const RlcMsmArgs& a, uint32_t first, uint32_t cnt) {
   Fp2 acc2 = f2_one();
+  if (a.sparse) {
+    HB_NOUNROLL for (uint32_t k = 0; k < cnt; k++) {
+      const uint32_t i = first + k;
+      const HmEntry se = a.sig[i];
+      const G2A S = {se.x, se.y, false};
+      const G2A S2 = {f2_mul(S.x, f2_from_const(PSI2_CX)), f2_neg(f2_mul(S.y, f2_from_const(PSI2_CY))), false};
+      acc2 = sparse_put(a.t2, i, S, S2, acc2);
+    }
+    Fp2 inv2 = f2_inv(acc2);
+    HB_NOUNROLL for (int k = (int)cnt - 1; k >= 0; k--) inv2 = sparse_fix(a.t2, first + (uint32_t)k, inv2);
+    return;
+  }
   HB_NOUNROLL for (uint32_t k = 0; k < cnt; k++) {
     const uint32_t i = first + k;
     const HmEntry se = a.sig[i];
@@ -394,10 +451,53 @@ __global__ KB_OCC(HB_OCC_RLC) void k_rlc_msm(RlcMsmArgs a) {
     a.t2[3ull * i] = J1;
     a.t2[3ull * i + 2] = {f2_mul(J3.X, zi2), f2_mul(J3.Y, f2_mul(zi2, zi)), f2_one()};
   }
-  const G2J rs = HB_G2_LAZY ? g2l_msm_ladder(a.t2, a.coef, first, cnt) : msm_ladder<Fp2, true>(a.t2, a.coef, first, cnt);
+}
+
+// the chunk's sums (ec28.h ladders; coefficients from the workspace) at its first item, infinity
+// at the others, so k_group_prep sums the items as before
+__device__ __forceinline__ void rlc_lad_g1(const RlcMsmArgs& a, uint32_t first, uint32_t cnt) {
+  const G1J rp = a.sparse ? (HB_G1_LAZY ? g1l_msm_ladder_sparse(a.t1, a.coef4, first, cnt)
+                                        : msm_ladder_sparse<Fp>(a.t1, a.coef4, first, cnt))
+                          : (HB_G1_LAZY ? g1l_msm_ladder(a.t1, a.coef, first, cnt)
+                                        : msm_ladder<Fp, true>(a.t1, a.coef, first, cnt));
+  a.pout[first] = {rp.X, rp.Y, rp.Z};
+  const G1J zi = jac_infinity<Fp>();
+  for (uint32_t k = 1; k < cnt; k++) a.pout[first + k] = {zi.X, zi.Y, zi.Z};
+}
+__device__ __forceinline__ void rlc_lad_g2(const RlcMsmArgs& a, uint32_t first, uint32_t cnt) {
+  const G2J rs = a.sparse ? (HB_G2_LAZY ? g2l_msm_ladder_sparse(a.t2, a.coef4, first, cnt)
+                                        : msm_ladder_sparse<Fp2>(a.t2, a.coef4, first, cnt))
+                          : (HB_G2_LAZY ? g2l_msm_ladder(a.t2, a.coef, first, cnt)
+                                        : msm_ladder<Fp2, true>(a.t2, a.coef, first, cnt));
   a.sout[first] = {rs.X, rs.Y, rs.Z};
   const G2J zs = jac_infinity<Fp2>();
   for (uint32_t k = 1; k < cnt; k++) a.sout[first + k] = {zs.X, zs.Y, zs.Z};
+}
+
+// One lane per chunk.  PHASE 0: everything (fused); 1: coefficients and tables of SIDES; 2: the
+// ladder of side SIDES (1 or 2).  SIDES as RlcMsmArgs::sides, a template argument so that the
+// public-key-only launch of the slot-wide check does not allocate registers for the G2 side.
+template <int SIDES, int PHASE>
+__global__ KB_OCC(HB_OCC_RLC) void k_rlc_msm(RlcMsmArgs a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (a.guard && *a.guard == 0) return;
+  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= *a.total) return;
+  const uint32_t first = a.cfirst[c], cc = a.ccount[c], cnt = cc & 0x7fffffffu;
+  if (rlc_single<SIDES>(a, first, cc, PHASE != 2)) return;
+  if (PHASE == 2) {
+    if (SIDES == 1) rlc_lad_g1(a, first, cnt);
+    else rlc_lad_g2(a, first, cnt);
+    return;
+  }
+  if (SIDES & 1) {
+    rlc_tab_g1(a, first, cnt);
+    if (PHASE == 0) rlc_lad_g1(a, first, cnt);
+  }
+  if (SIDES & 2) {
+    rlc_tab_g2(a, first, cnt);
+    if (PHASE == 0) rlc_lad_g2(a, first, cnt);
+  }
 #endif
 }
 
@@ -415,9 +515,17 @@ void launch_scan(const uint32_t* cnt, uint32_t n, uint32_t* off, hipStream_t s) 
 void launch_rlc_msm(const RlcMsmArgs& a, uint32_t max_chunks, hipStream_t s) {
   if (!max_chunks) return;
   const dim3 grid((max_chunks + BLOCK - 1) / BLOCK);
-  if (a.sides == 1) hipLaunchKernelGGL(k_rlc_msm<1>, grid, dim3(BLOCK), 0, s, a);
-  else if (a.sides == 2) hipLaunchKernelGGL(k_rlc_msm<2>, grid, dim3(BLOCK), 0, s, a);
-  else hipLaunchKernelGGL(k_rlc_msm<3>, grid, dim3(BLOCK), 0, s, a);
+  if (!HB_RLC_SPLIT) {
+    if (a.sides == 1) hipLaunchKernelGGL((k_rlc_msm<1, 0>), grid, dim3(BLOCK), 0, s, a);
+    else if (a.sides == 2) hipLaunchKernelGGL((k_rlc_msm<2, 0>), grid, dim3(BLOCK), 0, s, a);
+    else hipLaunchKernelGGL((k_rlc_msm<3, 0>), grid, dim3(BLOCK), 0, s, a);
+    return;
+  }
+  if (a.sides == 1) hipLaunchKernelGGL((k_rlc_msm<1, 1>), grid, dim3(BLOCK), 0, s, a);
+  else if (a.sides == 2) hipLaunchKernelGGL((k_rlc_msm<2, 1>), grid, dim3(BLOCK), 0, s, a);
+  else hipLaunchKernelGGL((k_rlc_msm<3, 1>), grid, dim3(BLOCK), 0, s, a);
+  if (a.sides & 1) hipLaunchKernelGGL((k_rlc_msm<1, 2>), grid, dim3(BLOCK), 0, s, a);
+  if (a.sides & 2) hipLaunchKernelGGL((k_rlc_msm<2, 2>), grid, dim3(BLOCK), 0, s, a);
 }
 
 // One lane per item (then per folded aggregate): final status, or a place in the fallback list.

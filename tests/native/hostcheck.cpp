@@ -564,6 +564,46 @@ extern "C" int hc_rlc_sum_g1_lazy(int k, const uint8_t* pks, const uint32_t* ab,
   return 0;
 }
 
+// the sparse-format chunk ladders (ec28.h g1l/g2l_msm_ladder_sparse) with the table built as
+// vbatch.hip k_rlc_msm builds it (rlc.h sparse_put / sparse_fix): sum over k items of
+// [A_i + B_i lambda] P_i, dig = 4 words per item (word 3 = 0: the item is skipped), compressed
+struct HcQuad {
+  uint32_t x, y, z, w;
+};
+extern "C" int hc_rlc_sum_g1_sparse(int k, const uint8_t* pks, const uint32_t* dig, uint8_t* out48) {
+  G1J tab[4 * 64];
+  HcQuad coef[64];
+  if (k < 1 || k > 64) return 1;
+  Fp acc = fp_one();
+  for (int i = 0; i < k; i++) {
+    G1A p;
+    if (g1_decompress(p, pks + 48 * i)) return 1;
+    acc = sparse_put(tab, (uint64_t)i, p, G1A{fp_mul(p.x, fp_from_const(G1_BETA)), p.y, false}, acc);
+    coef[i] = {dig[4 * i], dig[4 * i + 1], dig[4 * i + 2], dig[4 * i + 3]};
+  }
+  Fp inv = fp_inv(acc);
+  for (int i = k - 1; i >= 0; i--) inv = sparse_fix(tab, (uint64_t)i, inv);
+  g1_compress(out48, jac_to_aff(g1l_msm_ladder_sparse(tab, coef, 0, (uint32_t)k)));
+  return 0;
+}
+extern "C" int hc_rlc_sum_g2_sparse(int k, const uint8_t* sigs, const uint32_t* dig, uint8_t* out96) {
+  G2J tab[4 * 64];
+  HcQuad coef[64];
+  if (k < 1 || k > 64) return 1;
+  Fp2 acc = f2_one();
+  for (int i = 0; i < k; i++) {
+    G2A p;
+    if (g2_decompress(p, sigs + 96 * i)) return 1;
+    const G2A p2 = {f2_mul(p.x, f2_from_const(PSI2_CX)), f2_neg(f2_mul(p.y, f2_from_const(PSI2_CY))), false};
+    acc = sparse_put(tab, (uint64_t)i, p, p2, acc);
+    coef[i] = {dig[4 * i], dig[4 * i + 1], dig[4 * i + 2], dig[4 * i + 3]};
+  }
+  Fp2 inv = f2_inv(acc);
+  for (int i = k - 1; i >= 0; i--) inv = sparse_fix(tab, (uint64_t)i, inv);
+  g2_compress(out96, jac_to_aff(g2l_msm_ladder_sparse(tab, coef, 0, (uint32_t)k)));
+  return 0;
+}
+
 // [|x|] P both ways for a Jacobian G2 point given as the affine point (x0 x1 y0 y1, big-endian)
 // scaled by z = (z0, z1) (z = 0: infinity): out96x2 = compressed results of ec.h jac_mul_by_xabs
 // and ec28.h g2l_mul_by_xabs_l

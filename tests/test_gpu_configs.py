@@ -158,14 +158,15 @@ def test_slot_c5_shard_adversarial(L, c4):
     assert B.verify(bytes(d["dv_pks"][48 * v:48 * v + 48]), root, agg) == NOT_VERIFIED == ast[v]
 
 
-def test_slot_c3_adversarial(L):
+def test_slot_c3_adversarial(L, monkeypatch):
     """BASELINE configs[2] geometry with the C5 adversarial mix: 100 000 validators of a 10-operator
     threshold-7 cluster over distinct per-validator messages, the non-prefix aggregated share set
     {1, 2, 3, 4, 8, 9, 10}, 1 % of the 1 M partials corrupted in equal fifths (bench.corrupt), the
     aggregated members among them.  This drives the failure paths at 10-item groups: the failing
     slot-wide check, the per-batch check, the per-group and per-item fallbacks, the 10-member chunk
     ladders, and the small-scalar aggregation over groups with a bad member.  The slot runs twice:
-    the second call takes the per-batch check directly (adaptive).  Every status is exact against the
+    the second call takes the per-batch check directly (adaptive), its random combination in the
+    sparse coefficient format (ec28.h RLC_DIGITS).  Every status is exact against the
     construction; the oracle recomputes two partials of every class, 16 clean partials and 8
     aggregates (clean, with an undecodable member, with a decodable wrong member)."""
     import bench
@@ -181,8 +182,16 @@ def test_slot_c3_adversarial(L):
     rng = random.Random(303)
     bad_items = rng.sample(range(NP), int(NP * 0.01))
     assert len(set(bad_items) & set(members.reshape(-1).tolist())) > 0.6 * len(bad_items)  # aggregated members
-    for _ in range(2):
+    monkeypatch.setenv("HBLS_STATS", "1")
+    L.hbls_slot_msm(L.hbls_slot_msm(0))  # a clean adaptive history (an earlier test may leave it under attack)
+    for call in range(2):
+        s0 = (ctypes.c_uint64 * 6)()
+        assert L.hbls_stats(s0, 6) == 0
         vst, tst, ast, tout = _run_slot(L, d, sigs=d["sigs"])
+        s1 = (ctypes.c_uint64 * 6)()
+        assert L.hbls_stats(s1, 6) == 0
+        tried, failed = s1[4] - s0[4], s1[5] - s0[5]
+        assert (tried >= 1 and failed >= 1) if call == 0 else tried == 0, (call, tried, failed)
         bad = np.nonzero(vst != d["exp_v"])[0]
         assert len(bad) == 0, [(int(i), int(vst[i]), int(d["exp_v"][i])) for i in bad[:10]]
         assert np.array_equal(tst, d["exp_ta"])

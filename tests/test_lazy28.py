@@ -198,6 +198,93 @@ def test_rlc_chunk_ladder_lazy(lib):
         assert out.raw == B.g1_compress(want)
 
 
+def _sparse_digits(rng, k, cases):
+    """k items' sparse-format records (ec28.h RLC_DIGITS) and their (A, B): random digits, plus
+    the extreme strings (every digit (1, 1); every digit -(1, -1)) and an unusable item"""
+    recs, ab = [], []
+    for i in range(k):
+        kind = cases[i % len(cases)]
+        if kind == "rand":
+            d = [rng.randrange(8) for _ in range(22)]
+        elif kind == "max":
+            d = [2] * 22
+        else:  # "alt": -(1, -1) = (-1, 1)
+            d = [7] * 22
+        words = [0, 0, 0]
+        for j, v in enumerate(d):
+            words[j // 10] |= v << (3 * (j % 10))
+        usable = kind != "skip"
+        recs.append(words + [1 if usable else 0])
+        A = B_ = 0
+        for j, v in enumerate(d):
+            u, w = [(1, 0), (0, 1), (1, 1), (1, -1)][v & 3]
+            if v & 4:
+                u, w = -u, -w
+            A += u * 4 ** j
+            B_ += w * 4 ** j
+        ab.append((A, B_) if usable else (0, 0))
+    return recs, ab
+
+
+def test_rlc_sparse_chunk_ladders(lib):
+    """ec28.h g1l/g2l_msm_ladder_sparse (k_rlc_msm's chunk ladders in the sparse coefficient
+    format, the table built by rlc.h sparse_put / sparse_fix): sum [A_i + B_i lambda] P_i against
+    the oracle, for chunks of 1, 7 and 16 items, repeated points (the ladder meets +-T), extreme
+    digit strings and a skipped item; and the 8^22 digit strings are distinct coefficients (the
+    base-4 {-1, 0, 1} digits are a unique representation: spot-checked on colliding neighbours)"""
+    lam = (-B.X_PARAM ** 2) % B.R
+    rng = random.Random(2833)
+    for fn, argt in (("hc_rlc_sum_g1_sparse", 48), ("hc_rlc_sum_g2_sparse", 96)):
+        getattr(lib, fn).argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint32), ctypes.c_char_p]
+    g1 = [B.g1_mul(B.G1_GEN, rng.randrange(1, B.R)) for _ in range(5)]
+    g2 = [B.g2_mul(B.G2_GEN, rng.randrange(1, B.R)) for _ in range(3)]
+    plans = [(1, ["rand"]), (7, ["rand", "max", "rand", "skip", "alt"]), (16, ["rand"])]
+    for k, kinds in plans:
+        for side in (1, 2):
+            pool = g1 if side == 1 else g2
+            pts = [pool[rng.randrange(len(pool))] for _ in range(k)]
+            if k == 7:
+                pts[2] = pts[0]  # the same point twice
+            recs, ab = _sparse_digits(rng, k, kinds)
+            flat = (ctypes.c_uint32 * (4 * k))(*[x for r in recs for x in r])
+            if side == 1:
+                buf = b"".join(B.g1_compress(p) for p in pts)
+                out = ctypes.create_string_buffer(48)
+                assert lib.hc_rlc_sum_g1_sparse(k, buf, flat, out) == 0
+                want = None
+                for p, (a, b) in zip(pts, ab):
+                    want = B.g1_add(want, B.g1_mul(p, (a + b * lam) % B.R))
+                assert out.raw == B.g1_compress(want), (k, side)
+            else:
+                buf = b"".join(B.g2_compress(p) for p in pts)
+                out = ctypes.create_string_buffer(96)
+                assert lib.hc_rlc_sum_g2_sparse(k, buf, flat, out) == 0
+                want = None
+                for p, (a, b) in zip(pts, ab):
+                    want = B.g2_add(want, B.g2_mul(p, (a + b * lam) % B.R))
+                assert out.raw == B.g2_compress(want), (k, side)
+    # uniqueness: strings differing in one digit give different (A, B); A + B lambda = A' + B'
+    # lambda mod r with |A - A'|, |B - B'| < 2^45 forces equality (lambda's lattice has no
+    # vector that short: a = b lambda mod r with 0 < |b| < 2^45 means |a| > 2^126)
+    for _ in range(200):
+        recs, ab = _sparse_digits(rng, 1, ["rand"])
+        r0 = recs[0]
+        j = rng.randrange(22)
+        d = (r0[j // 10] >> (3 * (j % 10))) & 7
+        r1 = list(r0)
+        r1[j // 10] ^= ((d ^ ((d + 1 + rng.randrange(7)) % 8)) << (3 * (j % 10)))
+        A0, B0 = ab[0]
+        A1 = B1 = 0
+        for jj in range(22):
+            v = (r1[jj // 10] >> (3 * (jj % 10))) & 7
+            u, w = [(1, 0), (0, 1), (1, 1), (1, -1)][v & 3]
+            if v & 4:
+                u, w = -u, -w
+            A1 += u * 4 ** jj
+            B1 += w * 4 ** jj
+        assert (A0 + B0 * lam - A1 - B1 * lam) % B.R != 0
+
+
 def test_g2_xabs_ladder_lazy(lib):
     """ec28.h g2l_mul_by_xabs_l (the hash's cofactor ladders, general Jacobian additions) against
     ec.h jac_mul_by_xabs and the oracle, on random twist points with random Z, subgroup points and
