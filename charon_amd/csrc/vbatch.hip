@@ -477,8 +477,14 @@ __device__ __forceinline__ void rlc_lad_g2(const RlcMsmArgs& a, uint32_t first, 
 // One lane per chunk.  PHASE 0: everything (fused); 1: coefficients and tables of SIDES; 2: the
 // ladder of side SIDES (1 or 2).  SIDES as RlcMsmArgs::sides, a template argument so that the
 // public-key-only launch of the slot-wide check does not allocate registers for the G2 side.
+#ifndef HB_OCC_RLC_LAD1
+#define HB_OCC_RLC_LAD1 HB_OCC_RLC
+#endif
+#ifndef HB_OCC_RLC_LAD2
+#define HB_OCC_RLC_LAD2 HB_OCC_RLC
+#endif
 template <int SIDES, int PHASE>
-__global__ KB_OCC(HB_OCC_RLC) void k_rlc_msm(RlcMsmArgs a) {
+__global__ KB_OCC(PHASE != 2 ? HB_OCC_RLC : SIDES == 1 ? HB_OCC_RLC_LAD1 : HB_OCC_RLC_LAD2) void k_rlc_msm(RlcMsmArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
   if (a.guard && *a.guard == 0) return;
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
