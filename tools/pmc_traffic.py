@@ -12,7 +12,9 @@ LABELS = {  # bench.py / TIMED label -> kernel symbols of the slot
     "k_dec_pk": ["k_dec_pk", "k_g1_subgroup"], "k_dec_sig_pt": ["k_dec_sig_pt", "k_g2_subgroup"], "k_ta_straus": ["k_ta_jtab", "k_ta_jladder", "k_ta_jgeneral", "k_ta_joint", "k_ta_straus"],
     "k_ta_small": ["k_ta_sprep", "k_ta_small", "k_ta_stab", "k_ta_sladder"], "k_mml_eval": ["k_mml_eval"],
     "k_pair3_mls": ["k_pair3<5>", "k_lml<0>", "k_lml<1>"],
-    "k_group_sum": ["k_group_sum"], "k_rlc": ["k_rlc_msm<1>", "k_rlc<1>", "k_rlc_msm<2>", "k_rlc<2>", "k_rlc_msm<3>", "k_rlc<3>", "k_rlc_msm", "k_rlc"], "k_group_prep": ["k_group_prep_p", "k_group_prep_b"],
+    "k_group_sum": ["k_group_sum"], "k_rlc": ["k_rlc_msm<1>", "k_rlc<1>", "k_rlc_msm<2>", "k_rlc<2>", "k_rlc_msm<3>", "k_rlc<3>", "k_rlc_msm", "k_rlc",
+              "k_rlc_msm<1, 0>", "k_rlc_msm<1, 1>", "k_rlc_msm<1, 2>", "k_rlc_msm<2, 0>", "k_rlc_msm<2, 1>",
+              "k_rlc_msm<2, 2>", "k_rlc_msm<3, 0>", "k_rlc_msm<3, 1>"], "k_group_prep": ["k_group_prep_p", "k_group_prep_b"],
     "k_msm_bucket": ["k_msm_bucket"], "k_msm_reduce": ["k_msm_reduce"], "k_msm_sum": ["k_msm_sum"],
     "k_slines": ["k_slines"], "k_pair3_mml": ["k_pair3<4>"], "k_pair3_prod": ["k_pair3<3>"],
     "k_pair3_fin": ["k_pair3<2>", "k_pair6_fin", "k_pair6_fin<3>", "k_pair6_fin<10>"], "k_pair3_ml": ["k_pair3<1>"], "k_attestation_roots": ["k_attestation_roots"],
