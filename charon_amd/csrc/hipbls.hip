@@ -932,7 +932,8 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
     G1J* t1;
     G2J* t2;
     // the sparse coefficient format (22 additions per item instead of 32) unless the slot-wide
-    // bucket MSM reads the coefficients: under attack (skip_msm) and below the slot-wide size
+    // bucket MSM reads the coefficients: under attack (skip_msm), or a chunked call without the
+    // slot-wide check (HBLS_SLOT_MSM above its size)
     const bool sparse = !(smsm && !skip_msm);
     if (wsbuf(w, W_PCNT, n_groups, &pcnt) || wsbuf(w, W_PCOFF, n_groups + 1, &pcoff) ||
         wsbuf(w, W_PCFIRST, max_chunks, &pcf) || wsbuf(w, W_PCCOUNT, max_chunks, &pcc) ||
