@@ -158,6 +158,49 @@ def test_slot_c5_shard_adversarial(L, c4):
     assert B.verify(bytes(d["dv_pks"][48 * v:48 * v + 48]), root, agg) == NOT_VERIFIED == ast[v]
 
 
+def test_slot_c5_shard_cancelling_errors(L, c4, monkeypatch):
+    """The C5 shard (1 % corrupted) plus, in one clean validator, two partials outside its aggregated
+    members carrying opposite errors (sig_a + D, sig_b - D): the plain sum of the validator's
+    partials is unchanged, so only the random combination's distinct coefficients reject them.  Two
+    calls from a clean adaptive history: the first behind a failing slot-wide check (dense
+    coefficients), the second under attack (sparse coefficients, ec28.h RLC_DIGITS) -- both
+    reject exactly those two, and every other status stays exact."""
+    import bench
+    from oracle import bls12381 as B
+    d = dict(c4)
+    d["sigs"] = c4["sigs"].copy()
+    bench.corrupt(L, d, 0.01, seed=11)
+    V, n, t = d["V"], d["n"], d["t"]
+    exp_v = d["exp_v"].copy()
+    voff = np.asarray(d["vgrp_off"], dtype=np.int64)
+    members = np.asarray(d["ta_src"], dtype=np.int64).reshape(V, t)
+    v = next(v for v in range(V) if d["exp_agg"][v] == OK and
+             all(exp_v[i] == OK for i in range(voff[v], voff[v + 1])))
+    a, b = [i for i in range(voff[v], voff[v + 1]) if i not in set(members[v].tolist())][:2]
+    sig = d["sigs"].reshape(-1, 96)
+    j = next(j for j in range(voff[v + 1], len(exp_v)) if exp_v[j] == OK)
+    D = B.g2_decompress(bytes(sig[j]))  # a valid point: another validator's clean partial
+    sig[a] = np.frombuffer(B.g2_compress(B.g2_add(B.g2_decompress(bytes(sig[a])), D)), dtype=np.uint8)
+    sig[b] = np.frombuffer(B.g2_compress(B.g2_add(B.g2_decompress(bytes(sig[b])), B.g2_neg(D))), dtype=np.uint8)
+    exp_v[a] = exp_v[b] = NOT_VERIFIED
+    for i in (a, b):
+        assert B.verify(bytes(d["pks"][48 * i:48 * i + 48]), bytes(d["item_msgs"][32 * i:32 * i + 32]),
+                        bytes(sig[i])) == NOT_VERIFIED
+    monkeypatch.setenv("HBLS_STATS", "1")
+    L.hbls_slot_msm(L.hbls_slot_msm(0))  # a clean adaptive history
+    for call in range(2):
+        s0 = (ctypes.c_uint64 * 6)()
+        assert L.hbls_stats(s0, 6) == 0
+        vst, tst, ast, tout = _run_slot(L, d, sigs=d["sigs"])
+        s1 = (ctypes.c_uint64 * 6)()
+        assert L.hbls_stats(s1, 6) == 0
+        assert (s1[4] - s0[4] >= 1) if call == 0 else (s1[4] - s0[4] == 0), call  # slot-wide check, then skipped
+        bad = np.nonzero(vst != exp_v)[0]
+        assert len(bad) == 0, (call, [(int(i), int(vst[i]), int(exp_v[i])) for i in bad[:10]])
+        assert np.array_equal(tst, d["exp_ta"]) and np.array_equal(ast, d["exp_agg"]), call
+        assert bytes(tout[v]) == bytes(d["root_sigs"].reshape(V, 96)[v])
+
+
 def test_slot_c3_adversarial(L, monkeypatch):
     """BASELINE configs[2] geometry with the C5 adversarial mix: 100 000 validators of a 10-operator
     threshold-7 cluster over distinct per-validator messages, the non-prefix aggregated share set
