@@ -104,10 +104,14 @@ HD L28 l_sqr(const L28& a) {
   HB_UNROLL for (int i = 0; i < 14; i++) r.l[i] = o[i];
   return r;
 }
-#else
+#else  // host: fp.h's choice of cores (hostmul64.h unless HB_HOST_MUL28)
 HD L28 l_mul_nc(const L28& a, const L28& b) {
   L28 r;
+#if defined(HB_HOST_MUL28)
   fp_mul28_core(r.l, a.l, b.l);
+#else
+  hm64::mul_limbs28(r.l, a.l, b.l);
+#endif
   return r;
 }
 HD L28 l_mul(const L28& a, const L28& b) {
@@ -117,7 +121,11 @@ HD L28 l_mul(const L28& a, const L28& b) {
 HD L28 l_sqr(const L28& a) {
   HB_COUNT_FP_MUL();
   L28 r;
+#if defined(HB_HOST_MUL28)
   fp_sqr28_core(r.l, a.l);
+#else
+  hm64::mul_limbs28(r.l, a.l, a.l);
+#endif
   return r;
 }
 #endif
@@ -352,7 +360,14 @@ HD F2L f2l_mul(const F2L& a, const F2L& b) {
   HB_COUNT_FP_MUL();
   HB_COUNT_FP_MUL();
   F2L r;
+#if defined(HB_HOST_MUL28)
   f2l_mul_core(r.c0.l, r.c1.l, a.c0.l, a.c1.l, b.c0.l, b.c1.l);
+#else
+  uint32_t na1[14];
+  HB_UNROLL for (int j = 0; j < 14; j++) na1[j] = kF2N.l[j] - a.c1.l[j];
+  hm64::dot_limbs28(r.c0.l, a.c0.l, na1, b.c0.l, b.c1.l);
+  hm64::dot_limbs28(r.c1.l, a.c0.l, a.c1.l, b.c1.l, b.c0.l);
+#endif
   return r;
 }
 #endif

@@ -531,20 +531,43 @@ HD Fp fp28_to(const Fp28& a) {
   return r;
 }
 #else
+// Host (test harness, CPU baseline): the same products with 64-bit words (hostmul64.h: identical
+// results); HB_HOST_MUL28 keeps the 28-bit cores
+}  // namespace hb
+#include "hostmul64.h"
+namespace hb {
 HD void fp2_mul_pair(Fp& r0, Fp& r1, const Fp& a0, const Fp& a1, const Fp& b0, const Fp& b1) {
+#if defined(HB_HOST_MUL28)
   fp2_mul_core(r0.v, r1.v, a0.v, a1.v, b0.v, b1.v);
+#else
+  hm64::fp2_mul_words(r0.v, r1.v, a0.v, a1.v, b0.v, b1.v);
+#endif
 }
-HD void fp2_sqr_pair(Fp& r0, Fp& r1, const Fp& a0, const Fp& a1) { fp2_sqr_core(r0.v, r1.v, a0.v, a1.v); }
+HD void fp2_sqr_pair(Fp& r0, Fp& r1, const Fp& a0, const Fp& a1) {
+#if defined(HB_HOST_MUL28)
+  fp2_sqr_core(r0.v, r1.v, a0.v, a1.v);
+#else
+  hm64::fp2_mul_words(r0.v, r1.v, a0.v, a1.v, a0.v, a1.v);
+#endif
+}
 HD Fp fp_mul(const Fp& a, const Fp& b) {
   HB_COUNT_FP_MUL();
   Fp r;
+#if defined(HB_HOST_MUL28)
   fp_mul_core(r.v, a.v, b.v);
+#else
+  hm64::mul_words(r.v, a.v, b.v);
+#endif
   return r;
 }
 HD Fp fp_sqr(const Fp& a) {
   HB_COUNT_FP_MUL();
   Fp r;
+#if defined(HB_HOST_MUL28)
   fp_sqr_core(r.v, a.v);
+#else
+  hm64::mul_words(r.v, a.v, a.v);
+#endif
   return r;
 }
 struct Fp28 {
@@ -553,13 +576,21 @@ struct Fp28 {
 HD Fp28 fp28_mul(const Fp28& a, const Fp28& b) {
   HB_COUNT_FP_MUL();
   Fp28 r;
+#if defined(HB_HOST_MUL28)
   fp_mul28_core(r.l, a.l, b.l);
+#else
+  hm64::mul_limbs28(r.l, a.l, b.l);
+#endif
   return r;
 }
 HD Fp28 fp28_sqr(const Fp28& a) {
   HB_COUNT_FP_MUL();
   Fp28 r;
+#if defined(HB_HOST_MUL28)
   fp_sqr28_core(r.l, a.l);
+#else
+  hm64::mul_limbs28(r.l, a.l, a.l);
+#endif
   return r;
 }
 HD Fp28 fp28_from(const Fp& a) {

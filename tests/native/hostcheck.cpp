@@ -564,6 +564,65 @@ extern "C" int hc_rlc_sum_g1_lazy(int k, const uint8_t* pks, const uint32_t* ab,
   return 0;
 }
 
+// hostmul64.h's 64-bit products against the 28-bit cores they replace on the host, on `iters`
+// random operands each: stored words below 2^381, normalised limbs, lazy limbs (below 2^30; the
+// dot product's below 2^29), and the Fp2 product's signed real part.  Returns the mismatches.
+extern "C" int hc_mul64_selftest(int iters, uint64_t seed) {
+  uint64_t s = seed * 0x9E3779B97F4A7C15ull + 1;
+  auto rnd = [&]() {
+    s ^= s << 13;
+    s ^= s >> 7;
+    s ^= s << 17;
+    return (uint32_t)(s >> 16);
+  };
+  auto words = [&](uint32_t* w) {
+    for (int i = 0; i < 12; i++) w[i] = rnd();
+    w[11] &= 0x1fffffffu;  // < 2^381 < 2p
+  };
+  auto limbs = [&](uint32_t* l, int bits) {
+    for (int i = 0; i < 14; i++) l[i] = rnd() & ((1u << bits) - 1u);
+  };
+  int bad = 0;
+  for (int it = 0; it < iters; it++) {
+    uint32_t a[12], b[12], c[12], d[12], r0[12], r1[12], q0[12], q1[12];
+    words(a), words(b), words(c), words(d);
+    fp_mul_core(r0, a, b);
+    hm64::mul_words(q0, a, b);
+    bad += memcmp(r0, q0, sizeof r0) != 0;
+    fp_sqr_core(r0, a);
+    hm64::mul_words(q0, a, a);
+    bad += memcmp(r0, q0, sizeof r0) != 0;
+    fp2_mul_core(r0, r1, a, b, c, d);
+    hm64::fp2_mul_words(q0, q1, a, b, c, d);
+    bad += memcmp(r0, q0, sizeof r0) != 0 || memcmp(r1, q1, sizeof r1) != 0;
+    fp2_sqr_core(r0, r1, a, b);
+    hm64::fp2_mul_words(q0, q1, a, b, a, b);
+    bad += memcmp(r0, q0, sizeof r0) != 0 || memcmp(r1, q1, sizeof r1) != 0;
+    uint32_t x[14], y[14], z[14], u[14], l0[14], l1[14], m0[14], m1[14];
+    for (int lazy = 0; lazy < 2; lazy++) {
+      limbs(x, lazy ? 30 : 28), limbs(y, lazy ? 30 : 28);
+      fp_mul28_core(l0, x, y);
+      hm64::mul_limbs28(m0, x, y);
+      bad += memcmp(l0, m0, sizeof l0) != 0;
+      fp_sqr28_core(l0, x);
+      hm64::mul_limbs28(m0, x, x);
+      bad += memcmp(l0, m0, sizeof l0) != 0;
+      limbs(x, 29), limbs(y, 29), limbs(z, 29), limbs(u, 29);
+      f2l_dot_core(l0, x, y, z, u);
+      hm64::dot_limbs28(m0, x, y, z, u);
+      bad += memcmp(l0, m0, sizeof l0) != 0;
+    }
+    limbs(x, 28), limbs(y, 28), limbs(z, 28), limbs(u, 28);
+    F2L fa, fb;
+    for (int i = 0; i < 14; i++) fa.c0.l[i] = x[i], fa.c1.l[i] = y[i], fb.c0.l[i] = z[i], fb.c1.l[i] = u[i];
+    f2l_mul_core(l0, l1, x, y, z, u);
+    const F2L fr = f2l_mul(fa, fb);
+    for (int i = 0; i < 14; i++) m0[i] = fr.c0.l[i], m1[i] = fr.c1.l[i];
+    bad += memcmp(l0, m0, sizeof l0) != 0 || memcmp(l1, m1, sizeof l1) != 0;
+  }
+  return bad;
+}
+
 // the sparse-format chunk ladders (ec28.h g1l/g2l_msm_ladder_sparse) with the table built as
 // vbatch.hip k_rlc_msm builds it (rlc.h sparse_put / sparse_fix): sum over k items of
 // [A_i + B_i lambda] P_i, dig = 4 words per item (word 3 = 0: the item is skipped), compressed

@@ -253,3 +253,13 @@ def test_fp_inv_divsteps(hc):
         assert int.from_bytes(out.raw[48:], "big") == want, x
         worst = max(worst, nb.value)
     assert worst <= 34, worst  # FP_INV_BATCHES = 40
+
+
+def test_host_mul64_matches_r28(hc):
+    """hostmul64.h (the host builds' 64-bit Montgomery products: the CPU baseline and this harness)
+    returns bit for bit what the 28-bit cores of fp.h / ec28.h return: stored-word products and
+    squares, the Fp2 product with its signed real part, 28-bit-limb products on normalised and
+    lazy limbs, the lazy Fp2 dot product and f2l_mul"""
+    hc.hc_mul64_selftest.argtypes = [ctypes.c_int, ctypes.c_uint64]
+    assert hc.hc_mul64_selftest(4000, 2834) == 0
+
