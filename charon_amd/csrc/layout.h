@@ -355,7 +355,7 @@ struct ScatterArgs {
   const uint8_t* gverdict;  // [n_groups], 0 = the group's combined check passed
   // [n_groups + 1] group offsets (nullable: every item its own group).  A failing group of one
   // item is that item's verdict (its check is the item's own up to a nonzero exponent r): no
-  // re-check alone
+  // re-check alone -- unless aggregates are folded in (n_agg), which join their group's check
   const uint32_t* grp_off;
   // folded aggregates (nullable)
   uint32_t n_agg;

@@ -544,7 +544,8 @@ __global__ KB void k_scatter(ScatterArgs a) {
     else if (a.sig_st[i]) s = ST_BAD_SIGNATURE;
     else if (a.pk[i].inf || a.sig[i].inf || a.hm[a.msg_idx[i]].h.inf) s = ST_NOT_VERIFIED;  // verify_core
     else if (a.gverdict[a.item_grp[i]] == 0) s = ST_OK;
-    else if (!a.grp_off || a.grp_off[a.item_grp[i] + 1] - a.grp_off[a.item_grp[i]] <= 1) s = ST_NOT_VERIFIED;
+    else if (!a.n_agg && (!a.grp_off || a.grp_off[a.item_grp[i] + 1] - a.grp_off[a.item_grp[i]] <= 1))
+      s = ST_NOT_VERIFIED;  // a group of one item (with a folded aggregate it has a second member)
     else {
       a.list[atomicAdd(a.count, 1u)] = i;
       return;
