@@ -201,6 +201,24 @@ def test_slot_c5_shard_cancelling_errors(L, c4, monkeypatch):
         assert bytes(tout[v]) == bytes(d["root_sigs"].reshape(V, 96)[v])
 
 
+def test_slot_groups_of_one_partial_with_folded_aggregate(L):
+    """Validator groups of ONE partial (a 1-of-1 cluster) with each aggregate's verification folded
+    into its group's check: a wrong DV key fails validator 5's group through its aggregate alone.
+    The partial must still verify (a failing group of one is its item's verdict only without a
+    folded aggregate), the aggregate alone is NOT_VERIFIED, every other status stays OK."""
+    import bench
+    d = dict(bench.setup_inputs(L, dict(validators=64, n=1, t=1, distinct=False, n_msgs=4), 64, 0))
+    V = d["V"]
+    dv = d["dv_pks"].copy().reshape(V, 48)
+    dv[5] = dv[6]
+    d["dv_pks"] = dv.reshape(-1)
+    vst, tst, ast, tout = _run_slot(L, d)
+    assert int((vst != OK).sum()) == 0, [int(x) for x in np.nonzero(vst != OK)[0]]
+    assert int((tst != OK).sum()) == 0
+    assert [int(x) for x in np.nonzero(ast != OK)[0]] == [5] and ast[5] == NOT_VERIFIED
+    assert np.array_equal(tout, d["root_sigs"].reshape(V, 96))
+
+
 def test_slot_c3_adversarial(L, monkeypatch):
     """BASELINE configs[2] geometry with the C5 adversarial mix: 100 000 validators of a 10-operator
     threshold-7 cluster over distinct per-validator messages, the non-prefix aggregated share set
