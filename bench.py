@@ -46,10 +46,11 @@ import numpy as np
 # four side streams) + the library stream.  With HIP's default of four, streams share queues and a
 # latency-bound kernel (one final exponentiation, a hashing stage of 64 messages) holds up
 # whatever else sits in its queue: C3 106.4 -> 101.3 ms, C2 16.7 -> 16.0 ms per slot on one box
-# (profiles/r03j_*).  Set before anything initialises the HIP runtime, over the environment's
+# (profiles/r03j_*) with 16; 32 (the most the pool allows) adds C2 +2.6 %, C3 and C5 unchanged
+# (profiles/r04q32_hw_queues_ab.txt).  Set before anything initialises the HIP runtime, over the environment's
 # value (the GPU pool exports HIP's default of four); HBLS_HW_QUEUES chooses another count (at most
 # 32).  A charon process sets it the same way in its environment.
-os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, max(1, int(os.environ.get("HBLS_HW_QUEUES", "16")))))
+os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, max(1, int(os.environ.get("HBLS_HW_QUEUES", "32")))))
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 if ROOT not in sys.path:
