@@ -529,6 +529,8 @@ def main(argv=None):
                     help="threads calling the host-buffer entry points at once (with --host-api; 1: skip)")
     ap.add_argument("--inflight", type=int, default=3,
                     help="slots in flight (each on its own stream and outputs); 1 = one slot at a time")
+    ap.add_argument("--exchange-rehearsal", type=int, default=0,
+                    help="at one GPU: run the multi-GPU exchange (RCCL world of one) inside the timed region")
     ap.add_argument("--mode", default="slot", choices=["slot", "staged"],
                     help="slot: one hbls_slot_device call per step (stages overlap); staged: stage by stage")
     args = ap.parse_args(argv)
@@ -570,6 +572,7 @@ def main(argv=None):
     n_sets = max(1, args.inflight)
     outs = [{"hm": torch.zeros(M * L.hbls_hm_entry_bytes(), dtype=torch.uint8, device=dev),
              "vst": torch.full((NP,), 255, dtype=torch.uint8, device=dev),
+             "vbits": torch.zeros(((NP + 7) // 8,), dtype=torch.uint8, device=dev),
              "tout": torch.zeros(V * 96, dtype=torch.uint8, device=dev),
              "tst": torch.full((V,), 255, dtype=torch.uint8, device=dev),
              "ast": torch.full((V,), 255, dtype=torch.uint8, device=dev),
@@ -579,12 +582,13 @@ def main(argv=None):
 
     xchg = None
     exch = None
-    if world > 1:
+    xw = world > 1 or bool(args.exchange_rehearsal)  # the exchange runs (a world of one: a rehearsal)
+    if xw:
         # the library's RCCL communicator (rank 0's id over the gloo control plane), then ONE
         # exchange stream for the all-gathers of every in-flight slot (charon_amd/shard.py
         # SlotExchange: the same ordering code tests/test_shard.py runs over gloo)
         init_library_comm(L, world, rank)
-        exch = SlotExchange(world, rank, {"vst": NP, "tout": V * 96, "tst": V, "ast": V}, dev,
+        exch = SlotExchange(world, rank, {"vbits": (NP + 7) // 8, "tout": V * 96, "tst": V, "ast": V}, dev,
                             library_allgather(L), stream=torch.cuda.Stream(device=dev))
         for o in outs:
             o["xchg"] = exch.gather_buffers()
@@ -601,8 +605,9 @@ def main(argv=None):
             grp_off=_p(d_goff).value, n_groups=V, n_ta_partials=V * t, ta_out=_p(o["tout"]).value,
             ta_status=_p(o["tst"]).value, dv_pks=_p(d_dvpk).value, agg_vstatus=_p(o["ast"]).value)
 
-    def exchange(o):  # all-gather verdicts + compressed aggregates to every rank (RCCL)
-        exch.exchange({f: o[f] for f in ("vst", "tout", "tst", "ast")}, o["xchg"], producer=o["stream"])
+    def exchange(o):  # all-gather verify bitmaps + compressed aggregates to every rank (RCCL)
+        _chk(L, L.hbls_status_bitmap(_p(o["vst"]), NP, _p(o["vbits"]), o["sp"]))
+        exch.exchange({f: o[f] for f in ("vbits", "tout", "tst", "ast")}, o["xchg"], producer=o["stream"])
 
     step_no = [0]
 
@@ -617,7 +622,7 @@ def main(argv=None):
         _chk(L, L.hbls_attestation_signing_roots_device(_p(d_att), M, _p(d_dom), 1, None, _p(o["msg"]), o["sp"]))
         _chk(L, L.hbls_slot_device(ctypes.byref(o["slot"]), o["sp"]))
         ev[1].record(st)
-        if world > 1:
+        if xw:
             exchange(o)
         ev[2].record(st)
 
@@ -684,14 +689,18 @@ def main(argv=None):
                                                   for o in used)}
         if not staged:
             parity["aggregate_verify_all_ok"] = all(bool((o["ast"] == 0).all().item()) for o in used)
-    if world > 1 and "exp_v" in d:  # every rank's block equals that rank's construction: check our own
+    if xw and "exp_v" in d:  # every rank's block equals that rank's construction: check our own
+        nb = (NP + 7) // 8
         parity["allgather_ok"] = bool(
-            np.array_equal(xchg["vst"][rank * NP:(rank + 1) * NP].cpu().numpy(), d["exp_v"]) and
+            np.array_equal(xchg["vbits"][rank * nb:(rank + 1) * nb].cpu().numpy(),
+                           np.packbits(d["exp_v"] == 0, bitorder="little")) and
             np.array_equal(xchg["tst"][rank * V:(rank + 1) * V].cpu().numpy(), d["exp_ta"]) and
             np.array_equal(xchg["ast"][rank * V:(rank + 1) * V].cpu().numpy(), d["exp_agg"]))
-    elif world > 1:
-        parity["allgather_ok"] = bool((xchg["vst"] == 0).all().item() and (xchg["tst"] == 0).all().item() and
-                                      (xchg["ast"] == 0).all().item())
+    elif xw:
+        nb = (NP + 7) // 8
+        want = torch.from_numpy(np.packbits(np.ones(NP, dtype=bool), bitorder="little")).to(dev)
+        parity["allgather_ok"] = bool(all(torch.equal(xchg["vbits"][r * nb:(r + 1) * nb], want) for r in range(world))
+                                      and (xchg["tst"] == 0).all().item() and (xchg["ast"] == 0).all().item())
         # rank r's block of the gathered aggregates is rank r's root signatures: check our own block
         clean = d["exp_agg"] == 0 if "exp_v" in d else np.ones(V, dtype=bool)
         parity["allgather_own_block"] = bool(np.array_equal(
@@ -920,8 +929,9 @@ def main(argv=None):
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         out["cpu_baseline"] = cpu_baseline(d, args.cpu_seconds)
 
-    if world > 1:
+    if xw:
         _chk(L, L.hbls_comm_destroy())
+    if world > 1:
         dist.destroy_process_group()
     if rank == 0:
         print(json.dumps(out), flush=True)

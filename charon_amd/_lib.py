@@ -28,7 +28,7 @@ EXPORTS = (
     "hbls_threshold_aggregate_batch", "hbls_aggregate_batch", "hbls_verify_aggregate_batch", "hbls_sign_batch",
     "hbls_secret_to_public_key_batch", "hbls_threshold_split", "hbls_recover_secret", "hbls_hash_to_g2_device",
     "hbls_verify_device", "hbls_threshold_aggregate_device", "hbls_verify_aggregate_device", "hbls_slot_device",
-    "hbls_hm_entry_bytes", "hbls_sync",
+    "hbls_hm_entry_bytes", "hbls_sync", "hbls_status_bitmap",
     "hbls_timing", "hbls_timing_read", "hbls_comm_id_bytes", "hbls_comm_unique_id", "hbls_comm_init",
     "hbls_allgather_device", "hbls_comm_destroy", "hbls_stats", "hbls_fe_batch", "hbls_slot_msm", "hbls_adaptive", "hbls_rlc_lanes", "hbls_ta_joint", "hbls_attestation_signing_roots",
     "hbls_signing_roots", "hbls_attestation_signing_roots_device", "hbls_pk_entry_bytes",
@@ -94,6 +94,7 @@ def _declare(lib):
         "hbls_slot_device": ([ctypes.POINTER(HblsSlot), P], ctypes.c_int),
         "hbls_hm_entry_bytes": ([], SZ),
         "hbls_sync": ([P], ctypes.c_int),
+        "hbls_status_bitmap": ([P, SZ, P, P], ctypes.c_int),
         "hbls_timing": ([ctypes.c_int], ctypes.c_int),
         "hbls_timing_read": ([P, P, SZ, P], ctypes.c_int),
         "hbls_comm_id_bytes": ([], SZ),

@@ -219,6 +219,15 @@ __global__ KERNEL_BOUNDS void k_scatter_status(const uint8_t* __restrict__ st_in
   if (k < n) st_out[order[k]] = st_in[k];
 }
 
+// the verify bitmap of a slot (bit i of byte i / 8, least significant first: status[i] == OK): one
+// ballot per wave, eight bytes per wave -- what the ranks all-gather
+__global__ KERNEL_BOUNDS void k_status_bitmap(const uint8_t* __restrict__ st, uint32_t n, uint8_t* __restrict__ bits) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t m = __ballot(i < n && st[i] == ST_OK);
+  const uint32_t lane = threadIdx.x & 63u, first = i - lane;  // the wave's first item (a multiple of 64)
+  if (lane < 8 && first + 8 * lane < n) bits[first / 8 + lane] = (uint8_t)(m >> (8 * lane));
+}
+
 #define LAUNCH(kern, n, stream, ...)                                                              \
   do {                                                                                            \
     if ((n) > 0) {                                                                                \
@@ -2430,6 +2439,15 @@ size_t hbls_rlc_lanes(size_t lanes) { return g_rlc_lanes.exchange(lanes ? lanes 
 
 int hbls_sync(void* stream) {
   HCHK(hipStreamSynchronize((hipStream_t)stream));
+  return 0;
+}
+
+int hbls_status_bitmap(const uint8_t* status, size_t n, uint8_t* bits, void* stream) {
+  Dev* d;
+  hipStream_t s = (hipStream_t)stream;
+  if (dev_of_stream(s, &d)) return -1;
+  if (n > 0xffffffffull) return set_err("status bitmap: too many items");
+  LAUNCH(k_status_bitmap, n, s, status, (uint32_t)n, bits);
   return 0;
 }
 

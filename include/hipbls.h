@@ -257,6 +257,11 @@ size_t hbls_rlc_lanes(size_t lanes);
 size_t hbls_ta_joint(size_t members);
 /* Wait for all work the library queued on `stream`. */
 int hbls_sync(void* stream);
+/* Device: the verify bitmap of n statuses (bit i of bits[i / 8], least significant bit first, set
+ * when status[i] == HBLS_OK; bits holds ceil(n / 8) bytes), on `stream` -- the compact form of a
+ * slot's verdicts that the ranks all-gather (north_star: "all-gather verify bitmaps"); the
+ * failure classes stay in the owning rank's status bytes. */
+int hbls_status_bitmap(const uint8_t* status, size_t n, uint8_t* bits, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Exchange of slot results between processes that drive one GPU each:

@@ -75,6 +75,24 @@ def test_rccl_world_of_one_slot_exchange(L):
     assert b"no communicator" in L.hbls_last_error()
 
 
+def test_status_bitmap(L):
+    """hbls_status_bitmap (the verify bitmap the ranks all-gather): bit i of byte i / 8, least
+    significant first, set for HBLS_OK -- against numpy's packbits, on lengths around the wave
+    (64 statuses per ballot) and byte boundaries"""
+    import torch
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.Stream(device=dev)
+    rng = np.random.default_rng(9)
+    for n in (1, 7, 8, 63, 64, 65, 1000, 4099):
+        st = rng.integers(0, 4, n, dtype=np.uint8)
+        st[rng.random(n) < 0.5] = OK
+        d_st = torch.from_numpy(st).to(dev)
+        bits = torch.full(((n + 7) // 8,), 0xA5, dtype=torch.uint8, device=dev)
+        assert L.hbls_status_bitmap(_p(d_st), n, _p(bits), ctypes.c_void_p(s.cuda_stream)) == 0
+        s.synchronize()
+        assert np.array_equal(bits.cpu().numpy(), np.packbits(st == OK, bitorder="little")), n
+
+
 def _mixed_inputs(hipbls, rng, n_keys=48, n_items=700):
     keys = [hipbls.generate_secret_key() for _ in range(n_keys)]
     pks = [hipbls.secret_to_public_key(k) for k in keys]

@@ -13,6 +13,7 @@ the slot number); the GPU computes the real ones.
 import os
 import socket
 
+import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
@@ -31,7 +32,9 @@ def _slot_results(cl, slot=0):
     tout = torch.tensor([(b + slot) % 256 for b in b"".join(r * 3 for r in cl.root_sks)], dtype=torch.uint8)
     tst = torch.tensor([(r[-1] + slot) % 3 for r in cl.root_sks], dtype=torch.uint8)
     ast = torch.tensor([(r[-2] + slot) % 4 for r in cl.root_sks], dtype=torch.uint8)
-    return {"vst": vst, "tout": tout, "tst": tst, "ast": ast}
+    # the verify bitmap bench.py exchanges (hbls_status_bitmap: bit i set for status 0)
+    vbits = torch.from_numpy(np.packbits(vst.numpy() == 0, bitorder="little"))
+    return {"vst": vst, "vbits": vbits, "tout": tout, "tst": tst, "ast": ast}
 
 
 def _worker(rank, port, errq):
@@ -47,7 +50,8 @@ def _worker(rank, port, errq):
         assert cl.share_sks == full.share_sks[first * N:(first + V) * N]
         assert [cl.msgs[m] for m in cl.msg_of_validator] == [full.msgs[m] for m in full.msg_of_validator][first:first + V]
         shards = [synth.make_cluster(V, N, T, first_validator=owned_validators(r, V).start) for r in range(WORLD)]
-        exch = SlotExchange(WORLD, rank, {"vst": V * N, "tout": V * 96, "tst": V, "ast": V}, "cpu", gloo_allgather)
+        exch = SlotExchange(WORLD, rank, {"vst": V * N, "vbits": (V * N + 7) // 8, "tout": V * 96, "tst": V, "ast": V},
+                            "cpu", gloo_allgather)
         sets = [exch.gather_buffers() for _ in range(2)]  # two slots in flight, as bench.py --inflight 2
         for slot in range(5):
             recv = sets[slot % 2]
