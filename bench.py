@@ -570,14 +570,26 @@ def main(argv=None):
     d_vgoff, d_dvpk, d_tsig = up(d["vgrp_off"].view(np.int32)), up(d["dv_pks"]), up(d["ta_sigs"])
     # per in-flight slot: its own stream, hashed-message table and outputs (inputs are shared)
     n_sets = max(1, args.inflight)
-    outs = [{"hm": torch.zeros(M * L.hbls_hm_entry_bytes(), dtype=torch.uint8, device=dev),
+    # what the ranks exchange lives in ONE buffer per slot -- [verify bitmap | aggregates | their
+    # statuses | the aggregates' verification statuses] -- that the slot writes in place, so a slot
+    # takes one all-gather (each RCCL call costs ~1 ms of latency however small)
+    NB = (NP + 7) // 8
+    PACK = {"vbits": (0, NB), "tout": (NB, V * 96), "tst": (NB + V * 96, V), "ast": (NB + V * 97, V)}
+    PB = NB + V * 98
+
+    def out_set():
+        o = {"hm": torch.zeros(M * L.hbls_hm_entry_bytes(), dtype=torch.uint8, device=dev),
              "vst": torch.full((NP,), 255, dtype=torch.uint8, device=dev),
-             "vbits": torch.zeros(((NP + 7) // 8,), dtype=torch.uint8, device=dev),
-             "tout": torch.zeros(V * 96, dtype=torch.uint8, device=dev),
-             "tst": torch.full((V,), 255, dtype=torch.uint8, device=dev),
-             "ast": torch.full((V,), 255, dtype=torch.uint8, device=dev),
+             "pack": torch.zeros(PB, dtype=torch.uint8, device=dev),
              "msg": torch.zeros(M * 32, dtype=torch.uint8, device=dev),
-             "stream": torch.cuda.Stream(device=dev)} for _ in range(n_sets)]
+             "stream": torch.cuda.Stream(device=dev)}
+        for f, (a, b) in PACK.items():
+            o[f] = o["pack"][a:a + b]
+        o["tst"].fill_(255)
+        o["ast"].fill_(255)
+        return o
+
+    outs = [out_set() for _ in range(n_sets)]
     d_hm, d_vst, d_tout, d_tst, d_ast = (outs[0][k] for k in ("hm", "vst", "tout", "tst", "ast"))
 
     xchg = None
@@ -588,11 +600,14 @@ def main(argv=None):
         # exchange stream for the all-gathers of every in-flight slot (charon_amd/shard.py
         # SlotExchange: the same ordering code tests/test_shard.py runs over gloo)
         init_library_comm(L, world, rank)
-        exch = SlotExchange(world, rank, {"vbits": (NP + 7) // 8, "tout": V * 96, "tst": V, "ast": V}, dev,
-                            library_allgather(L), stream=torch.cuda.Stream(device=dev))
+        exch = SlotExchange(world, rank, {"pack": PB}, dev, library_allgather(L), stream=torch.cuda.Stream(device=dev))
         for o in outs:
             o["xchg"] = exch.gather_buffers()
         xchg = outs[0]["xchg"]
+
+    def gathered(f):  # field f of every rank, in rank order, from the gathered packs
+        a, b = PACK[f]
+        return torch.cat([xchg["pack"][r * PB + a:r * PB + a + b] for r in range(world)])
 
     stream = outs[0]["stream"]
     sp = ctypes.c_void_p(stream.cuda_stream)
@@ -607,7 +622,7 @@ def main(argv=None):
 
     def exchange(o):  # all-gather verify bitmaps + compressed aggregates to every rank (RCCL)
         _chk(L, L.hbls_status_bitmap(_p(o["vst"]), NP, _p(o["vbits"]), o["sp"]))
-        exch.exchange({f: o[f] for f in ("vbits", "tout", "tst", "ast")}, o["xchg"], producer=o["stream"])
+        exch.exchange({"pack": o["pack"]}, o["xchg"], producer=o["stream"])
 
     step_no = [0]
 
@@ -690,21 +705,20 @@ def main(argv=None):
         if not staged:
             parity["aggregate_verify_all_ok"] = all(bool((o["ast"] == 0).all().item()) for o in used)
     if xw and "exp_v" in d:  # every rank's block equals that rank's construction: check our own
-        nb = (NP + 7) // 8
         parity["allgather_ok"] = bool(
-            np.array_equal(xchg["vbits"][rank * nb:(rank + 1) * nb].cpu().numpy(),
+            np.array_equal(gathered("vbits")[rank * NB:(rank + 1) * NB].cpu().numpy(),
                            np.packbits(d["exp_v"] == 0, bitorder="little")) and
-            np.array_equal(xchg["tst"][rank * V:(rank + 1) * V].cpu().numpy(), d["exp_ta"]) and
-            np.array_equal(xchg["ast"][rank * V:(rank + 1) * V].cpu().numpy(), d["exp_agg"]))
+            np.array_equal(gathered("tst")[rank * V:(rank + 1) * V].cpu().numpy(), d["exp_ta"]) and
+            np.array_equal(gathered("ast")[rank * V:(rank + 1) * V].cpu().numpy(), d["exp_agg"]))
     elif xw:
-        nb = (NP + 7) // 8
         want = torch.from_numpy(np.packbits(np.ones(NP, dtype=bool), bitorder="little")).to(dev)
-        parity["allgather_ok"] = bool(all(torch.equal(xchg["vbits"][r * nb:(r + 1) * nb], want) for r in range(world))
-                                      and (xchg["tst"] == 0).all().item() and (xchg["ast"] == 0).all().item())
+        gv = gathered("vbits")
+        parity["allgather_ok"] = bool(all(torch.equal(gv[r * NB:(r + 1) * NB], want) for r in range(world))
+                                      and (gathered("tst") == 0).all().item() and (gathered("ast") == 0).all().item())
         # rank r's block of the gathered aggregates is rank r's root signatures: check our own block
         clean = d["exp_agg"] == 0 if "exp_v" in d else np.ones(V, dtype=bool)
         parity["allgather_own_block"] = bool(np.array_equal(
-            xchg["tout"][rank * V * 96:(rank + 1) * V * 96].cpu().numpy().reshape(V, 96)[clean],
+            gathered("tout")[rank * V * 96:(rank + 1) * V * 96].cpu().numpy().reshape(V, 96)[clean],
             d["root_sigs"].reshape(V, 96)[clean]))
 
     items = world * (NP + V)

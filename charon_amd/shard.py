@@ -28,7 +28,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-FIELDS = ("vst", "vbits", "tout", "tst", "ast")
+FIELDS = ("vst", "vbits", "tout", "tst", "ast", "pack")
 
 # allgather(send, recv, nbytes, stream): gather `nbytes` of `send` from every rank into `recv`
 # (rank order), ordered on `stream` (a torch.cuda.Stream, or None on the CPU)
@@ -75,7 +75,8 @@ class SlotExchange:
     """All-gather of one slot's results per call, in a fixed issue order.
 
     sizes: bytes per rank of each field (vst = V*n verdict bytes or vbits = their ceil(V*n/8)-byte
-    verify bitmap, tout = V*96 aggregates, tst / ast = V statuses).  `gather_buffers()` makes one set of receive buffers (one per slot in flight);
+    verify bitmap, tout = V*96 aggregates, tst / ast = V statuses; pack = bench.py's one buffer of
+    vbits | tout | tst | ast, one all-gather per slot).  `gather_buffers()` makes one set of receive buffers (one per slot in flight);
     `exchange(outs, recv, producer)` gathers the rank's outputs `outs` into `recv` on the exchange
     stream after `producer` (the slot's stream) has written them, and makes `producer` wait for the
     gather.  `issued` logs (slot sequence number, field) in issue order: identical on every rank.

@@ -56,8 +56,8 @@ def _worker(rank, port, errq):
         for slot in range(5):
             recv = sets[slot % 2]
             assert exch.exchange(_slot_results(cl, slot), recv) == slot
-            want = {f: torch.cat([_slot_results(sh, slot)[f] for sh in shards]) for f in FIELDS}
-            for f in FIELDS:
+            want = {f: torch.cat([_slot_results(sh, slot)[f] for sh in shards]) for f in exch.sizes}
+            for f in exch.sizes:
                 assert torch.equal(recv[f], want[f]), (slot, f)
                 for r in range(WORLD):
                     assert torch.equal(exch.block(recv, f, r), _slot_results(shards[r], slot)[f])
@@ -66,7 +66,8 @@ def _worker(rank, port, errq):
         # every rank issued the same collectives in the same order
         logs = [None] * WORLD
         dist.all_gather_object(logs, exch.issued)
-        assert logs[0] == logs[1] == [(k, f) for k in range(5) for f in FIELDS], logs
+        assert logs[0] == logs[1] == [(k, f) for k in range(5) for f in exch.sizes], logs
+        assert set(exch.sizes) <= set(FIELDS)
         with pytest.raises(ValueError):
             bad = dict(_slot_results(cl))
             bad["vst"] = torch.zeros(1, dtype=torch.uint8)
