@@ -82,6 +82,15 @@ WORKLOADS = {
 }
 
 
+def pack_layout(NP: int, V: int):
+    """The slot's exchanged outputs in one buffer: field -> (offset, bytes), and the total -- the
+    verify bitmap of NP partials, V 96-byte aggregates, their statuses, their verification statuses
+    (one all-gather per slot)."""
+    nb = (NP + 7) // 8
+    layout = {"vbits": (0, nb), "tout": (nb, 96 * V), "tst": (nb + 96 * V, V), "ast": (nb + 97 * V, V)}
+    return layout, nb + 98 * V
+
+
 def _p(x) -> ctypes.c_void_p:
     """Device pointer of a torch tensor or host pointer of a numpy array."""
     if x is None:
@@ -573,9 +582,8 @@ def main(argv=None):
     # what the ranks exchange lives in ONE buffer per slot -- [verify bitmap | aggregates | their
     # statuses | the aggregates' verification statuses] -- that the slot writes in place, so a slot
     # takes one all-gather (each RCCL call costs ~1 ms of latency however small)
-    NB = (NP + 7) // 8
-    PACK = {"vbits": (0, NB), "tout": (NB, V * 96), "tst": (NB + V * 96, V), "ast": (NB + V * 97, V)}
-    PB = NB + V * 98
+    PACK, PB = pack_layout(NP, V)
+    NB = PACK["vbits"][1]
 
     def out_set():
         o = {"hm": torch.zeros(M * L.hbls_hm_entry_bytes(), dtype=torch.uint8, device=dev),

@@ -112,3 +112,20 @@ def test_sharded_slot_exchange_gloo_world2():
             errs.append("rank timed out")
     assert not errs, errs
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+
+
+def test_bench_pack_layout():
+    """bench.py's one exchanged buffer per slot: the fields tile it exactly, in order, with the
+    bitmap rounded up to whole bytes"""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    for NP, V in ((1, 1), (12, 3), (1_000_000, 100_000), (875_001, 125_000)):
+        layout, total = bench.pack_layout(NP, V)
+        pos = 0
+        for f in ("vbits", "tout", "tst", "ast"):
+            off, size = layout[f]
+            assert off == pos, (NP, V, f)
+            pos += size
+        assert pos == total and layout["vbits"][1] == (NP + 7) // 8 and layout["tout"][1] == 96 * V
+
