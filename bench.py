@@ -58,7 +58,7 @@ if ROOT not in sys.path:
 
 from charon_amd import opcounts  # noqa: E402
 from charon_amd.shard import (SlotExchange, init_library_comm, library_allgather, max_over_ranks,  # noqa: E402
-                               owned_validators)
+                               owned_validators, pack_layout, pack_views, unpack_gathered)
 
 METRIC = "verified partial sigs/sec + ThresholdAggregate/sec per node, 1-8 MI355X"
 
@@ -80,15 +80,6 @@ WORKLOADS = {
                     "7-operator threshold-5 cluster, 64 committee signing roots: 875k partial Verify + 125k "
                     "ThresholdAggregate (+125k aggregate Verify) per GPU"),
 }
-
-
-def pack_layout(NP: int, V: int):
-    """The slot's exchanged outputs in one buffer: field -> (offset, bytes), and the total -- the
-    verify bitmap of NP partials, V 96-byte aggregates, their statuses, their verification statuses
-    (one all-gather per slot)."""
-    nb = (NP + 7) // 8
-    layout = {"vbits": (0, nb), "tout": (nb, 96 * V), "tst": (nb + 96 * V, V), "ast": (nb + 97 * V, V)}
-    return layout, nb + 98 * V
 
 
 def _p(x) -> ctypes.c_void_p:
@@ -591,8 +582,7 @@ def main(argv=None):
              "pack": torch.zeros(PB, dtype=torch.uint8, device=dev),
              "msg": torch.zeros(M * 32, dtype=torch.uint8, device=dev),
              "stream": torch.cuda.Stream(device=dev)}
-        for f, (a, b) in PACK.items():
-            o[f] = o["pack"][a:a + b]
+        o.update(pack_views(o["pack"], PACK))
         o["tst"].fill_(255)
         o["ast"].fill_(255)
         return o
@@ -614,8 +604,7 @@ def main(argv=None):
         xchg = outs[0]["xchg"]
 
     def gathered(f):  # field f of every rank, in rank order, from the gathered packs
-        a, b = PACK[f]
-        return torch.cat([xchg["pack"][r * PB + a:r * PB + a + b] for r in range(world)])
+        return unpack_gathered(xchg["pack"], PACK, PB, world, f)
 
     stream = outs[0]["stream"]
     sp = ctypes.c_void_p(stream.cuda_stream)

@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import re
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -33,7 +34,7 @@ EXPORTS = (
     "hbls_allgather_device", "hbls_comm_destroy", "hbls_stats", "hbls_fe_batch", "hbls_slot_msm", "hbls_adaptive", "hbls_rlc_lanes", "hbls_ta_joint", "hbls_attestation_signing_roots",
     "hbls_signing_roots", "hbls_attestation_signing_roots_device", "hbls_pk_entry_bytes",
     "hbls_decompress_pubkeys_device", "hbls_pubkey_cache_add", "hbls_pubkey_cache_clear", "hbls_pubkey_cache_size",
-    "hbls_debug_split",
+    "hbls_debug_split", "hbls_build_id",
 )
 
 ALL_DEVICES = 0xFFFFFFFF
@@ -55,6 +56,45 @@ class HipBlsUnavailable(RuntimeError):
 
 class HipBlsRuntimeError(RuntimeError):
     pass
+
+
+BUILD_ID_PREFIX = "hbls-build:"
+
+
+def source_build_id(root: str = "") -> str:
+    """sha256 (first 16 hex digits) over every file of charon_amd/csrc and include/hipbls.h, names
+    and contents, in sorted order: what charon_amd/build.py embeds as hbls_build_id()."""
+    import hashlib
+
+    root = root or os.path.dirname(_HERE)
+    csrc = os.path.join(root, "charon_amd", "csrc")
+    files = sorted(os.path.join(csrc, f) for f in os.listdir(csrc) if f.endswith((".h", ".hip")))
+    files.append(os.path.join(root, "include", "hipbls.h"))
+    h = hashlib.sha256()
+    for f in files:
+        h.update(os.path.relpath(f, root).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+        h.update(b"\0")
+    return h.hexdigest()[:16]
+
+
+def embedded_build_id(path: str) -> str:
+    """The build id string inside a built library file, read from its bytes (no loading)."""
+    with open(path, "rb") as f:
+        data = f.read()
+    m = re.search(rb"hbls-build:[0-9a-f]{16}(\+[A-Za-z0-9_=,.+-]*)?", data)
+    return m.group(0).decode() if m else ""
+
+
+def check_build_id(lib_id: str, root: str = "") -> None:
+    """Raise HipBlsUnavailable unless lib_id was built from the sources in the tree (tuning
+    variants carry '+defines' after the hash; only the hash is compared)."""
+    want = source_build_id(root)
+    got = lib_id[len(BUILD_ID_PREFIX):].split("+", 1)[0] if lib_id.startswith(BUILD_ID_PREFIX) else ""
+    if got != want:
+        raise HipBlsUnavailable(f"stale libhipbls.so: built from sources {got or '(unknown)'}, the tree is {want}; "
+                                "run `python -m charon_amd.build`")
 
 
 _lock = threading.Lock()
@@ -108,6 +148,7 @@ def _declare(lib):
         "hbls_adaptive": ([ctypes.c_int], ctypes.c_int),
         "hbls_rlc_lanes": ([SZ], SZ),
         "hbls_ta_joint": ([SZ], SZ),
+        "hbls_build_id": ([], ctypes.c_char_p),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)
@@ -117,7 +158,8 @@ def _declare(lib):
 
 def load_library(path: str = ""):
     """Load the shared library without touching the GPU (safe on CPU-only hosts).  HBLS_LIBRARY
-    names a tuning variant built by charon_amd.build (default: the in-tree product library)."""
+    names a tuning variant built by charon_amd.build (default: the in-tree product library).
+    Refuses a library whose embedded build id (hbls_build_id) differs from the tree's sources."""
     path = path or os.environ.get("HBLS_LIBRARY") or LIB_PATH
     global _lib
     with _lock:
@@ -134,6 +176,9 @@ def load_library(path: str = ""):
                 pass
             lib = ctypes.CDLL(path)
             _declare(lib)
+            # provenance: the library must have been built from the sources in this tree
+            if os.path.isdir(os.path.join(os.path.dirname(_HERE), "charon_amd", "csrc")):
+                check_build_id(lib.hbls_build_id().decode())
             _lib = lib
         return _lib
 

@@ -20,7 +20,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 SOURCES = ["hipbls.hip", "pipeline.hip", "threshold.hip", "vbatch.hip", "vgroup.hip", "roots.hip", "hash.hip", "msm.hip",
            "hashsplit.hip"]
 HEADERS = ["hd.h", "consts.h", "fp.h", "fr.h", "tower.h", "ec.h", "ec28.h", "sha256.h", "h2c.h", "pairing.h", "ops.h", "pair3.h",
-           "pair6.h", "layout.h", "lines.h", "rlc.h", "ta_small.h", "pair28.h", "hostmul64.h"]
+           "pair6.h", "layout.h", "lines.h", "rlc.h", "ta_small.h", "pair28.h", "hostmul64.h", "coalesce.h"]
 
 
 def _newer(target, deps):
@@ -30,12 +30,26 @@ def _newer(target, deps):
     return all(os.path.getmtime(d) <= t for d in deps)
 
 
+def build_id(defines=()) -> str:
+    """The id embedded in the library: the source hash (charon_amd._lib.source_build_id) plus the
+    tuning defines of a variant build."""
+    from charon_amd._lib import BUILD_ID_PREFIX, source_build_id
+    bid = BUILD_ID_PREFIX + source_build_id(ROOT)
+    if defines:
+        bid += "+" + ",".join(d.replace(" ", "") for d in defines)
+    return bid
+
+
 def build_library(force: bool = False, verbose: bool = True, defines=(), out: str = LIB) -> str:
     """defines / out: tuning variants (e.g. ("HB_OCC2=2",) -> charon_amd/lib/variants/...), used by
-    tools/ experiments through HBLS_LIBRARY; the product is the default build."""
+    tools/ experiments through HBLS_LIBRARY; the product is the default build.  A library whose
+    embedded build id equals the tree's is reused; any other is rebuilt."""
+    from charon_amd._lib import embedded_build_id
     LIB = out
-    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(ROOT, "include", "hipbls.h")]
-    if not force and _newer(LIB, deps):
+    bid = build_id(defines)
+    if not force and os.path.exists(LIB) and embedded_build_id(LIB) == bid:
+        if verbose:
+            print(f"reused {LIB} ({bid}: built from these sources)")
         return LIB
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
     t = time.time()
@@ -44,8 +58,9 @@ def build_library(force: bool = False, verbose: bool = True, defines=(), out: st
     for src in SOURCES:
         obj = os.path.join(os.path.dirname(LIB), os.path.splitext(src)[0] + ".o")
         objs.append(obj)
+        extra = [f'-DHBLS_BUILD_ID="{bid}"'] if src == "hipbls.hip" else []
         procs.append(subprocess.Popen([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-c"] +
-                                      ["-D" + d for d in defines] + [os.path.join(CSRC, src), "-o", obj]))
+                                      ["-D" + d for d in defines] + extra + [os.path.join(CSRC, src), "-o", obj]))
     for p in procs:
         if p.wait(timeout=3000) != 0:
             raise RuntimeError("hipcc failed")
@@ -53,7 +68,7 @@ def build_library(force: bool = False, verbose: bool = True, defines=(), out: st
                    ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"], check=True, timeout=600)
     os.replace(LIB + ".tmp", LIB)
     if verbose:
-        print(f"built {LIB} in {time.time() - t:.1f}s")
+        print(f"compiled {LIB} in {time.time() - t:.1f}s ({bid})")
     return LIB
 
 

@@ -14,6 +14,7 @@ HD Fp f_sqr(const Fp& a) { return fp_sqr(a); }
 HD Fp f_neg(const Fp& a) { return fp_neg(a); }
 HD Fp f_dbl(const Fp& a) { return fp_dbl(a); }
 HD Fp f_inv(const Fp& a) { return fp_inv(a); }
+HD Fp f_inv_ct(const Fp& a) { return fp_inv_ct(a); }
 HD bool f_is_zero(const Fp& a) { return fp_is_zero(a); }
 HD bool f_eq(const Fp& a, const Fp& b) { return fp_eq(a, b); }
 HD void f_set_zero(Fp& a) { a = fp_zero(); }
@@ -26,6 +27,7 @@ HD Fp2 f_sqr(const Fp2& a) { return f2_sqr(a); }
 HD Fp2 f_neg(const Fp2& a) { return f2_neg(a); }
 HD Fp2 f_dbl(const Fp2& a) { return f2_dbl(a); }
 HD Fp2 f_inv(const Fp2& a) { return f2_inv(a); }
+HD Fp2 f_inv_ct(const Fp2& a) { return f2_inv_ct(a); }
 HD bool f_is_zero(const Fp2& a) { return f2_is_zero(a); }
 HD bool f_eq(const Fp2& a, const Fp2& b) { return f2_eq(a, b); }
 HD void f_set_zero(Fp2& a) { a = f2_zero(); }
@@ -144,7 +146,8 @@ HDNI Jac<F> jac_add(const Jac<F>& p, const Jac<F>& q) {
   return r;
 }
 
-template <class F>
+// kSecret: p depends on a secret key (Sign, SecretToPublicKey): the fixed-trip inversion
+template <class F, bool kSecret = false>
 HDNI Aff<F> jac_to_aff(const Jac<F>& p) {
   Aff<F> r;
   if (jac_is_inf(p)) {
@@ -153,7 +156,7 @@ HDNI Aff<F> jac_to_aff(const Jac<F>& p) {
     r.inf = true;
     return r;
   }
-  F zi = f_inv(p.Z);
+  F zi = kSecret ? f_inv_ct(p.Z) : f_inv(p.Z);
   F zi2 = f_sqr(zi);
   r.x = f_mul(p.X, zi2);
   r.y = f_mul(p.Y, f_mul(zi2, zi));

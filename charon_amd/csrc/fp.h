@@ -241,55 +241,6 @@ HD void fp2_fix_neg(uint32_t* out, const uint32_t* r, bool neg) {  // r (mod 2^3
   HB_UNROLL for (int i = 0; i < 12; i++) out[i] = neg ? s[i] : w[i];
 }
 
-#if defined(HB_FP2_KARA)
-// (Opt-in, measured slower: the leaf needs 248 VGPRs + 14 AGPRs against 145, which drops the G2
-// kernels that call it to one wave per SIMD and adds caller spills -- k_dec_sig_pt + k_g2_subgroup
-// 33.5 -> 40.9 ms, the C3 slot 104.3 -> 109.0 ms, profiles/r03k_*.)
-// Karatsuba over the columns: per column k the three sums
-//   t00 = sum a0_j b0_{k-j},   t11 = sum a1_j b1_{k-j},   t01 = sum (a0 + a1)_j (b0 + b1)_{k-j}
-// give the real column t00 - t11 and the imaginary column t01 - t00 - t11 (= sum a0 b1 + a1 b0):
-// three multiply-add chains per column instead of four (3 x 196 + 2 x 196 = 980 multiply-adds per
-// Fp2 product against 1 176), for five 64-bit additions per column.  The limb sums are < 2^29, so a
-// column of t01 stays < 14 * 2^58; t11 is accumulated negated (signed multiply-adds against -a1),
-// and the imaginary accumulator is exact modulo 2^64 with a true value in [0, 2^63).
-HD void fp2_mul_core(uint32_t* o0, uint32_t* o1, const uint32_t* a0w, const uint32_t* a1w, const uint32_t* b0w,
-                     const uint32_t* b1w) {
-  uint32_t a0[14], a1[14], b0[14], b1[14], sa[14], sb[14], m0[14], m1[14], r0[14], r1[14];
-  int32_t na1[14];
-  fp_split28(a0, a0w);
-  fp_split28(a1, a1w);
-  fp_split28(b0, b0w);
-  fp_split28(b1, b1w);
-  HB_UNROLL for (int j = 0; j < 14; j++) {
-    na1[j] = -(int32_t)a1[j];
-    sa[j] = a0[j] + a1[j];
-    sb[j] = b0[j] + b1[j];
-  }
-  uint64_t ar = 0, ai = 0;
-  HB_UNROLL for (int k = 0; k < 27; k++) {
-    const int lo = k < 14 ? 0 : k - 13, hi = k < 14 ? k : 13;
-    uint64_t t00 = 0, t11n = 0;
-    HB_UNROLL for (int j = lo; j <= hi; j++) {
-      t00 += (uint64_t)a0[j] * b0[k - j];
-      t11n += (uint64_t)((int64_t)na1[j] * (int64_t)(int32_t)b1[k - j]);
-      ai += (uint64_t)sa[j] * sb[k - j];
-    }
-    ar += t00 + t11n;
-    ai += t11n - t00;
-    HB_UNROLL for (int j = lo; j <= hi; j++)
-      if (j < k || k >= 14) {
-        ar += (uint64_t)m0[j] * P28[k - j];
-        ai += (uint64_t)m1[j] * P28[k - j];
-      }
-    HB_MONT28_TAIL_S(ar, m0, k, r0)
-    HB_MONT28_TAIL(ai, m1, k, r1)
-  }
-  r0[13] = (uint32_t)ar;
-  r1[13] = (uint32_t)ai;
-  fp2_fix_neg(o0, r0, (int64_t)ar < 0);
-  fp_join28(o1, r1);
-}
-#else
 HD void fp2_mul_core(uint32_t* o0, uint32_t* o1, const uint32_t* a0w, const uint32_t* a1w, const uint32_t* b0w,
                      const uint32_t* b1w) {
   uint32_t a0[14], a1[14], b0[14], b1[14], m0[14], m1[14], r0[14], r1[14];
@@ -321,7 +272,6 @@ HD void fp2_mul_core(uint32_t* o0, uint32_t* o1, const uint32_t* a0w, const uint
   fp2_fix_neg(o0, r0, (int64_t)ar < 0);
   fp_join28(o1, r1);
 }
-#endif
 
 // (a0 + a1 u)^2 = (a0^2 - a1^2) + 2 a0 a1 u, squares with the doubled-limb cross products
 HD void fp2_sqr_core(uint32_t* o0, uint32_t* o1, const uint32_t* a0w, const uint32_t* a1w) {
@@ -687,7 +637,11 @@ HD Fp fp_inv_pow(const Fp& a) { return fp_pow_win(a, WIN_P_MINUS_2, WIN_P_MINUS_
 // constant-time gcd computation and modular inversion", 2019) in batches of 30 divsteps, on
 // signed 30-bit limbs -- the low 32 bits of f and g decide a batch's 2x2 transition matrix,
 // which is then applied to the full f, g (exactly) and to the cofactors d, e (mod p, with a
-// multiple of p that clears their low 30 bits).  About 15 32-bit operations per divstep and
+// multiple of p that clears their low 30 bits).  The step structure (divsteps_30, update_fg_30,
+// update_de_30, normalize_30 and the branch-free c1/c2/c3 masks with zeta) follows the published
+// safegcd implementation of libsecp256k1's modinv32 (Bernstein & Yang, "Fast constant-time gcd
+// computation and modular inversion", 2019; MIT licence), with BLS12-381's modulus, limb count and
+// constants.  About 15 32-bit operations per divstep and
 // ~300 per batch for the updates; the values are public, so the loop stops once g = 0 (on the
 // device: once every lane of the wave has g = 0).  ~25-35 batches for random 381-bit inputs
 // against the 466 Montgomery products of fp_inv_pow.  The result is the integer inverse z of
@@ -787,12 +741,12 @@ HD void normalize_30(S30& d, int32_t f_sign) {
 
 constexpr int FP_INV_BATCHES = 40;  // 1200 divsteps >= the 1101 that 381-bit inputs can need
 
-// a^-1 (0 -> 0, like a^(p-2)); batches: optional count of the batches run (tests).
-// HB_INV_POW=1: the exponentiation instead (A/B runs)
-#if defined(HB_INV_POW) && HB_INV_POW
-HD Fp fp_inv(const Fp& a, int* batches = nullptr) { return fp_inv_pow(a); }
-#else
-HDNI Fp fp_inv(const Fp& a, int* batches = nullptr) {
+// a^-1 (0 -> 0, like a^(p-2)); batches: optional count of the batches run (tests).  Public data
+// (kEarlyExit): the loop stops once g = 0 in every lane of the wave.  Secret-dependent values
+// (fp_inv_ct: the affine conversion of sk * H(m) and sk * g1 in k_sign / k_sk_to_pk) always run
+// the FP_INV_BATCHES batches, so the trip count does not depend on the input.
+template <bool kEarlyExit>
+HDNI Fp fp_inv_t(const Fp& a, int* batches = nullptr) {
   const Fp c = fp_canon(a);
   S30 f, g, d, e;
   HB_UNROLL for (int i = 0; i < 13; i++) {  // g = c in 30-bit limbs
@@ -812,19 +766,21 @@ HDNI Fp fp_inv(const Fp& a, int* batches = nullptr) {
     zeta = divsteps_30(zeta, (uint32_t)f.v[0], (uint32_t)g.v[0], t);
     update_de_30(d, e, t);
     update_fg_30(f, g, t);
-    int32_t nz = 0;
-    HB_UNROLL for (int i = 0; i < 13; i++) nz |= g.v[i];
+    if (kEarlyExit) {
+      int32_t nz = 0;
+      HB_UNROLL for (int i = 0; i < 13; i++) nz |= g.v[i];
 #if defined(__HIP_DEVICE_COMPILE__)
-    if (!__any(nz != 0)) {  // every lane of the wave is done
-      b++;
-      break;
-    }
+      if (!__any(nz != 0)) {  // every lane of the wave is done
+        b++;
+        break;
+      }
 #else
-    if (nz == 0) {
-      b++;
-      break;
-    }
+      if (nz == 0) {
+        b++;
+        break;
+      }
 #endif
+    }
   }
   if (batches) *batches = b;
   normalize_30(d, f.v[12]);
@@ -838,7 +794,8 @@ HDNI Fp fp_inv(const Fp& a, int* batches = nullptr) {
   }
   return fp_mul(z, fp_from_const(FP_RCUBE));
 }
-#endif
+HD Fp fp_inv(const Fp& a, int* batches = nullptr) { return fp_inv_t<true>(a, batches); }
+HD Fp fp_inv_ct(const Fp& a, int* batches = nullptr) { return fp_inv_t<false>(a, batches); }
 
 // Legendre-style squareness check via a^((p-1)/2) (1: square, 0: zero).
 HD bool fp_is_square(const Fp& a) {

@@ -60,10 +60,7 @@ __global__ KB_OCC(HB_OCC_HASH) void k_h2c_map(uint32_t n, MsgEntry* __restrict__
 //   k_h2c_clear1b u = t1 + psi(P), v = psi^2(2P) - psi(P) - P - t1                          -> (u, v)
 //   k_h2c_clear2  h = [x] u + v                                                          -> h
 //   k_h2c_clear3  h affine                                                               -> hm[i].h
-// the two [x] ladders in lazily reduced 28-bit limbs (ec28.h; HB_H2C_LAZY=0: ec.h, for A/B runs)
-#ifndef HB_H2C_LAZY
-#define HB_H2C_LAZY 1
-#endif
+// the two [x] ladders in lazily reduced 28-bit limbs (ec28.h)
 __global__ KB_OCC(HB_OCC_HASH) void k_h2c_clear1(uint32_t n, MsgEntry* __restrict__ hm) {
 #if defined(__HIP_DEVICE_COMPILE__)
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -75,12 +72,8 @@ __global__ KB_OCC(HB_OCC_HASH) void k_h2c_clear1(uint32_t n, MsgEntry* __restric
     P = jac_add(G2J{a.X, a.Y, a.Z}, G2J{b.X, b.Y, b.Z});
   }
   q[0] = {P.X, P.Y, P.Z};
-#if HB_H2C_LAZY
   const G2JEntry* src = q;
   const G2J t1 = jac_neg(g2l_mul_by_xabs_l([src]() { return G2J{src->X, src->Y, src->Z}; }));  // [x] P (x < 0)
-#else
-  const G2J t1 = jac_neg(jac_mul_by_xabs(P));  // [x] P (x < 0)
-#endif
   q[1] = {t1.X, t1.Y, t1.Z};
 #endif
 }
@@ -105,13 +98,8 @@ __global__ KB_OCC(HB_OCC_HASH) void k_h2c_clear2(uint32_t n, MsgEntry* __restric
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   G2JEntry* q = h2c_q(hm + i);
-#if HB_H2C_LAZY
   const G2JEntry* src = q + 1;
   const G2J t2 = jac_neg(g2l_mul_by_xabs_l([src]() { return G2J{src->X, src->Y, src->Z}; }));
-#else
-  const G2JEntry ue = q[1];
-  const G2J t2 = jac_neg(jac_mul_by_xabs(G2J{ue.X, ue.Y, ue.Z}));
-#endif
   const G2JEntry ve = q[2];
   const G2J h = jac_add(t2, G2J{ve.X, ve.Y, ve.Z});
   q[0] = {h.X, h.Y, h.Z};

@@ -9,6 +9,7 @@
 // p2p/receive.go:52) and the RCCL exchange of slot results between processes.
 #include "layout.h"
 #include "../../include/hipbls.h"
+#include "coalesce.h"
 
 #include <rccl/rccl.h>
 #include <sys/random.h>
@@ -99,7 +100,7 @@ __global__ KERNEL_BOUNDS void k_sign(const uint8_t* __restrict__ sks, const uint
     return;
   }
   G2J sg = jac_mul_aff(hm_load(hm[msg_idx[i]].h), s.v, 255);
-  g2_compress(buf, jac_to_aff(sg));
+  g2_compress(buf, jac_to_aff<Fp2, true>(sg));  // secret-dependent: fixed-trip inversion
   for (int k = 0; k < 96; k++) sigs[96ull * i + k] = buf[k];
   status[i] = ST_OK;
 }
@@ -119,7 +120,7 @@ __global__ KERNEL_BOUNDS void k_sk_to_pk(const uint8_t* __restrict__ sks, uint32
     return;
   }
   G1J p = jac_mul_aff(g1_generator(), s.v, 255);
-  g1_compress(buf, jac_to_aff(p));
+  g1_compress(buf, jac_to_aff<Fp, true>(p));  // secret-dependent: fixed-trip inversion
   for (int k = 0; k < 48; k++) pks[48ull * i + k] = buf[k];
   status[i] = ST_OK;
 }
@@ -263,12 +264,6 @@ std::mutex g_kc_mu;
 std::unordered_map<std::string, uint32_t> g_kc_map;
 size_t g_kc_n = 0;             // published entries (g_kc_mu; written under g_kc_add_mu too)
 std::vector<uint8_t> g_kc_keys;  // their compressed bytes, 48 B each (g_kc_add_mu): fills new devices
-// HBLS_TA_MSM=1: the aggregation as shared-doubling chunks (k_ta_msm) instead of one Straus ladder
-// per member (k_ta_straus).  Off: measured slower at C3 (per-member tables read across lanes
-// uncoalesced; fewer, longer lanes) -- 222.8 ms/slot with per-member ladders vs 224.2-227.8 with
-// chunks of 2, 4 or 8 members.
-bool g_ta_msm = false;
-size_t g_ta_chunk = 4;   // HBLS_TA_CHUNK: members per lane of k_ta_msm (<= TA_CHUNK)
 // HBLS_TA_JOINT: members per lane of the joint aggregation ladders (k_ta_jtab, k_ta_jladder, k_ta_jgeneral) when every group has
 // the same size t; 0 = auto (about TA_JOINT_LANES lanes, at most t and 8), 1 = one ladder per member
 // (k_ta_straus)
@@ -284,10 +279,6 @@ std::atomic<size_t> g_fe_batch_min{2 * FE_BATCH};
 // many (an attack): smaller batches pass more often (group testing; C5, 1 % corrupted partials:
 // 64-group batches nearly all fail and every group then pays its own exponentiation).
 size_t g_fb_batch = 8;
-// HBLS_STAGGER=1: a verification's decompression starts after the previous verification's (slots in
-// flight staggered instead of in lockstep).  Off: with three slots in flight overlapping
-// decompressions measured 131.0-131.5 vs 132.7-133.1 ms per C3 slot (C2 19.9-20.1 vs 20.0-20.4)
-bool g_stagger = false;
 // HBLS_SLOT_MSM: batched verifications of at least this many items (partials + folded aggregates,
 // one chunk of groups) check every group at once -- the signature side as one multi-scalar
 // multiplication (msm.hip), one final exponentiation for the call -- and fall back to the
@@ -321,7 +312,6 @@ enum WsId {
   W_TACSM, W_TASDIG, W_TASOK, W_TASDONE, W_TASTAB, W_TANONUNI,  // its small-scalar path
   W_SEGA, W_SEGB, W_SEGSTA, W_SEGSTB, W_VAPT, W_VAPV, W_PLAN,  // VerifyAggregate key reduction
   W_PCNT, W_PCOFF, W_PCFIRST, W_PCCOUNT, W_COEF, W_COEF4, W_RT1, W_RT2,  // chunk plan + multi-scalar RLC
-  W_TPCNT, W_TPCOFF, W_TPCFIRST, W_TPCCOUNT,                    // chunk plan of the aggregation
   W_FBUF, W_GS, W_BS, W_BLINES, W_BBAD, W_BVER, W_GLIST, W_GCOUNT,  // batched final exponentiation
   W_MCNT, W_MOFF, W_MCUR, W_MORDER, W_MENT, W_MBUCKET, W_MPART, W_MPART2, W_MTOT, W_PBUF1, W_PBUF2, W_PBUF3, W_SFAIL,  // slot-wide check
   W_MLEV,                                                                          // its evaluated Miller lines
@@ -388,11 +378,6 @@ struct Dev {
   Hc hc[N_WS_MAX];
   std::mutex hc_mu;  // hc[].busy
   std::condition_variable hc_cv;
-  // end of the last verification's decompression stage: with HBLS_STAGGER=1 the next verification
-  // starts its own decompression after it, so consecutive slots in flight run staggered (one slot's
-  // decompression beside the previous slot's combinations and pairings) instead of in lockstep
-  hipEvent_t ev_dec = nullptr;
-  bool dec_valid = false;
   // public-key cache (hbls_pubkey_cache_add): decompressed entries + statuses, every device holds
   // all g_kc_n of them
   DevBuf kc_tab, kc_st;
@@ -508,7 +493,6 @@ int dev_create(int ord, Dev** out) {
   int prio_lo = 0, prio_hi = 0;
   HCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
   HCHK(hipStreamCreateWithPriority(&d->stream, hipStreamNonBlocking, prio_lo));
-  HCHK(hipEventCreateWithFlags(&d->ev_dec, hipEventDisableTiming));
   for (int k_ws = 0; k_ws < g_ws_sets; k_ws++) {
     Ws& w = d->ws[k_ws];
     HCHK(hipEventCreateWithFlags(&w.free_ev, hipEventDisableTiming));
@@ -555,15 +539,12 @@ int init_mask(uint32_t mask) {
   g_gmax = std::max<size_t>(1, env_size("HBLS_GROUP_MAX", g_gmax));
   g_rlc_msm = env_size("HBLS_RLC_MSM", 1) != 0;
   g_rlc_lanes = std::max<size_t>(1, env_size("HBLS_RLC_LANES", g_rlc_lanes.load()));
-  g_ta_msm = env_size("HBLS_TA_MSM", 0) != 0;
-  g_ta_chunk = std::min<size_t>(TA_CHUNK, std::max<size_t>(1, env_size("HBLS_TA_CHUNK", g_ta_chunk)));
   g_ta_joint = std::min<size_t>(8, env_size("HBLS_TA_JOINT", g_ta_joint.load()));
   g_ta_small = env_size("HBLS_TA_SMALL", 1) != 0;
   g_fe6 = env_size("HBLS_FE6", 1) != 0;
   g_fe_batch_min = env_size("HBLS_FE_BATCH", g_fe_batch_min.load());
   g_slot_msm_min = env_size("HBLS_SLOT_MSM", g_slot_msm_min.load());
   g_adaptive = env_size("HBLS_ADAPTIVE", 1) != 0;
-  g_stagger = env_size("HBLS_STAGGER", 0) != 0;
   g_ws_sets = (int)std::min<size_t>(N_WS_MAX, std::max<size_t>(1, env_size("HBLS_WS_SETS", 3)));
   {
     size_t fb = std::min<size_t>(FE_BATCH, std::max<size_t>(2, env_size("HBLS_FALLBACK_BATCH", g_fb_batch)));
@@ -702,7 +683,7 @@ int ta_tail(Dev& d, Ws& w, const HmEntry* pts, const uint32_t* src, const uint8_
   // joint ladders over chunks of a validator's members (k_ta_jtab, k_ta_jladder, k_ta_jgeneral) when every group has t members
   const size_t t_u = (n_groups && np % n_groups == 0) ? np / n_groups : 0;
   size_t jc = 0;
-  if (mode == 0 && t_u > 1 && !g_ta_msm) {
+  if (mode == 0 && t_u > 1) {
     const size_t knob = g_ta_joint.load();
     jc = knob ? knob : np / TA_JOINT_LANES;
     jc = std::min<size_t>(std::min<size_t>(jc, t_u), 8);
@@ -728,7 +709,7 @@ int ta_tail(Dev& d, Ws& w, const HmEntry* pts, const uint32_t* src, const uint8_
     // small-scalar path first (groups of exactly t members, wave-uniform index sets); the Lagrange
     // digits and the per-member ladders below skip the groups it aggregated
     uint8_t* sdone = nullptr;
-    if (mode == 0 && !g_ta_msm && g_ta_small && t_u >= 2 && t_u <= (size_t)TA_SMALL_MAX) {
+    if (mode == 0 && g_ta_small && t_u >= 2 && t_u <= (size_t)TA_SMALL_MAX) {
       int64_t* csm;
       TaDigits* sdig;
       uint8_t *sok, *stab;
@@ -742,18 +723,7 @@ int ta_tail(Dev& d, Ws& w, const HmEntry* pts, const uint32_t* src, const uint8_
     TIMED(d, "k_ta_lambda", s,
           launch_ta_lambda(didx, dgoff, (uint32_t)n_groups, (uint32_t)np, mode, dig, mst, s, (uint32_t)t_u, nonuni,
                            sdone));
-    if (g_ta_msm && n_groups) {
-      // chunks of at most TA_CHUNK members share their ladder's doublings (k_ta_msm)
-      const size_t max_chunks = np / g_ta_chunk + n_groups;
-      uint32_t *pcnt, *pcoff, *pcf, *pcc;
-      if (wsbuf(w, W_TPCNT, n_groups, &pcnt) || wsbuf(w, W_TPCOFF, n_groups + 1, &pcoff) ||
-          wsbuf(w, W_TPCFIRST, max_chunks, &pcf) || wsbuf(w, W_TPCCOUNT, max_chunks, &pcc))
-        return -1;
-      TIMED(d, "k_plan", s, launch_plan(dgoff, (uint32_t)n_groups, (uint32_t)g_ta_chunk, pcnt, pcoff, pcf, pcc, s));
-      if (mode == 0) TIMED(d, "k_ta_table", s, launch_ta_table(pts, src, (uint32_t)np, tab, s));
-      TIMED(d, "k_ta_straus", s,
-            launch_ta_msm(pts, src, dig, tab, pcf, pcc, pcoff + n_groups, (uint32_t)max_chunks, mode, pj, s));
-    } else if (jc) {
+    if (jc) {
       TIMED(d, "k_ta_straus", s,
             launch_ta_joint(pts, src, dig, (uint32_t)n_groups, (uint32_t)t_u, (uint32_t)jc, tab, pj, s, sdone, nonuni));
       // groups not all of t_u members: the per-member ladders instead (nothing unless nonuni)
@@ -872,7 +842,6 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
   const int sides1 = smsm && !skip_msm ? 1 : 3;
 
   // fork: decompression on the side streams (after the previous verification's decompression)
-  if (d.dec_valid && g_stagger) HCHK(hipStreamWaitEvent(s, d.ev_dec, 0));
   HCHK(hipEventRecord(w.ev_fork, s));
   for (int k = 0; k < 2; k++) HCHK(hipStreamWaitEvent(w.side[k], w.ev_fork, 0));
   // public keys: from the caller's decompressed-key tables when given (static per cluster lock:
@@ -923,8 +892,6 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
   // random linear combinations per item, then per group
   HCHK(hipStreamWaitEvent(s, w.ev_side[0], 0));
   HCHK(hipStreamWaitEvent(s, w.ev_side[1], 0));
-  HCHK(hipEventRecord(d.ev_dec, s));
-  d.dec_valid = true;
   TIMED(d, "k_item_group", s, launch_item_group(dgoff, (uint32_t)n_groups, (uint32_t)n, igrp, s));
   const uint32_t rlc_cmax = (uint32_t)std::min<size_t>(RLC_CHUNK, std::max<size_t>(1, n / g_rlc_lanes.load()));
   RlcMsmArgs rlc_fallback{};
@@ -1541,10 +1508,18 @@ int for_each_device_hc(size_t n_units, const HcFn& fn) {
 // the entries before `first`).  Caller holds d.mu.
 int kc_fill(Dev& d, const uint8_t* keys, size_t first, size_t m) {
   HCHK(hipSetDevice(d.ord));
-  // launches enqueued earlier (on host-call or caller streams) may still read the table: let them
-  // finish before any entry is rewritten or the table moves.  No new reader can be enqueued
-  // meanwhile (they look indices up under d.mu, held here); cache adds are rare (cluster locks).
-  HCHK(hipDeviceSynchronize());
+  // launches enqueued earlier may still read the table: its only reader, launch_pk_gather of a
+  // host-buffer verification, runs on a workspace side stream, so the library's own streams (the
+  // library stream, the host-call contexts' and the workspaces' side streams) are drained before
+  // any entry is rewritten or the table moves -- not the whole device: caller, torch and RCCL
+  // streams keep running.  No new reader can be enqueued meanwhile (they look indices up under
+  // d.mu, held here); cache adds are rare (cluster locks).
+  HCHK(hipStreamSynchronize(d.stream));
+  for (int k = 0; k < N_WS_MAX; k++) {
+    if (d.hc[k].s) HCHK(hipStreamSynchronize(d.hc[k].s));
+    for (int j = 0; j < N_SIDE; j++)
+      if (d.ws[k].side[j]) HCHK(hipStreamSynchronize(d.ws[k].side[j]));
+  }
   const size_t tot = first + m;
   if (d.kc_tab.cap < tot * sizeof(G1AEntry) || d.kc_st.cap < tot) {  // grow, keeping the old entries
     DevBuf nt, ns;
@@ -1612,10 +1587,10 @@ int verify_host(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msgs, co
   // coalesced single-item callers) checks every item alone: a group of several items needs random
   // coefficients, i.e. a 64-bit scalar ladder per item on the call's critical path (~3.7 ms for a
   // lone lane), where separate checks only add lanes to kernels that have them to spare
-  // (HBLS_SINGLE_MAX, read per call: items below which every item is its own group; default the
+  // (HBLS_SINGLE_MAX, read once: items below which every item is its own group; default the
   // batched final exponentiation's group threshold)
-  const char* sm = getenv("HBLS_SINGLE_MAX");
-  const size_t single_max = sm ? (size_t)strtoull(sm, nullptr, 0) : g_fe_batch_min.load();
+  static const size_t single_max_env = env_size("HBLS_SINGLE_MAX", 0);  // read once
+  const size_t single_max = single_max_env ? single_max_env : g_fe_batch_min.load();
   const size_t gmax = n < single_max ? 1 : g_gmax;
   std::vector<size_t> gstart;  // group starts in `order`
   for (size_t k = 0; k < n; k++)
@@ -1756,44 +1731,27 @@ int group_op_host(const uint8_t* sigs, const int64_t* idx, const uint32_t* grp_o
 }
 
 // ---------------------------------------------------------------------------------------
-// Coalescing of concurrent host calls: the first caller of an idle queue becomes the leader,
-// waits at most HBLS_COALESCE_US for more requests (or until HBLS_COALESCE_MAX items queue up),
-// runs them as one batch and wakes every requester with its own statuses.  Requests that arrive
-// while a batch runs form the next batch.
+// Coalescing of concurrent host calls (coalesce.h): the first caller of an idle queue becomes the
+// leader, waits at most HBLS_COALESCE_US for more requests (or until HBLS_COALESCE_MAX items queue
+// up), runs them as one batch and wakes every requester with its own statuses.  Requests that
+// arrive while a batch runs form the next batch.
 // ---------------------------------------------------------------------------------------
-struct VReq {
-  const uint8_t *pk, *sig, *msg;
-  const uint64_t* off;
-  const uint32_t* len;
-  size_t n;
-  uint8_t* st;
-  int rc = 0;
-  std::string err;
-  bool done = false;
-  bool taken = false;  // in a batch (running or about to)
-};
-
-struct Coalescer {
-  std::mutex mu;
-  std::condition_variable cv;
-  std::deque<VReq*> q;
-  size_t queued = 0;
-  int active = 0;          // batches running (each on its own host-call context)
-  bool gathering = false;  // a leader is collecting the next batch
-  std::chrono::steady_clock::time_point last_end{};  // when the previous batch finished
-};
 Coalescer g_vq;
-size_t g_coalesce_us = (size_t)-1, g_coalesce_max = 0, g_coalesce_inflight = 0;
+CoalesceParams g_cp;
+std::once_flag g_cp_once;
 
-void coalesce_params() {
-  if (g_coalesce_us == (size_t)-1) {
-    g_coalesce_us = env_size("HBLS_COALESCE_US", 200);
-    g_coalesce_max = env_size("HBLS_COALESCE_MAX", 1u << 16);
+// read once, by the first caller, before any request is queued (std::call_once: concurrent first
+// callers all see the three parameters set)
+const CoalesceParams& coalesce_params() {
+  std::call_once(g_cp_once, [] {
+    g_cp.us = env_size("HBLS_COALESCE_US", 200);
+    g_cp.max_items = env_size("HBLS_COALESCE_MAX", 1u << 16);
     // batches in flight at once (HBLS_COALESCE_INFLIGHT, default: the host-call contexts): the
     // requests that arrive while batches run form the next one, which starts at once instead of
     // behind them -- a small batch leaves most of the chip idle
-    g_coalesce_inflight = std::max<size_t>(1, env_size("HBLS_COALESCE_INFLIGHT", (size_t)g_ws_sets));
-  }
+    g_cp.inflight = std::max<size_t>(1, env_size("HBLS_COALESCE_INFLIGHT", (size_t)g_ws_sets));
+  });
+  return g_cp;
 }
 
 void run_verify_batch(std::vector<VReq*>& batch) {
@@ -1825,8 +1783,8 @@ void run_verify_batch(std::vector<VReq*>& batch) {
 
 int verify_coalesced(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msgs, const uint64_t* msg_off,
                      const uint32_t* msg_len, size_t n, uint8_t* status) {
-  coalesce_params();
-  if (g_coalesce_us == 0 || n >= g_coalesce_max) return verify_host(pks, sigs, msgs, msg_off, msg_len, n, status);
+  const CoalesceParams& p = coalesce_params();
+  if (p.us == 0 || n >= p.max_items) return verify_host(pks, sigs, msgs, msg_off, msg_len, n, status);
   VReq me;
   me.pk = pks;
   me.sig = sigs;
@@ -1835,41 +1793,7 @@ int verify_coalesced(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msg
   me.len = msg_len;
   me.n = n;
   me.st = status;
-  Coalescer& c = g_vq;
-  std::unique_lock<std::mutex> lk(c.mu);
-  c.q.push_back(&me);
-  c.queued += n;
-  c.cv.notify_all();
-  while (!me.done) {
-    // a caller whose request is still queued leads the next batch when a context is free
-    if (!me.taken && !c.gathering && (size_t)c.active < g_coalesce_inflight) {
-      c.gathering = true;
-      c.active++;
-      // gather more requests only in a busy period (batches running, or one finished within the
-      // last few windows): a lone caller on an idle library runs at once, and under load the
-      // requests that queue up meanwhile form the next batch
-      const auto now = std::chrono::steady_clock::now();
-      const bool busy = c.active > 1 || now - c.last_end < std::chrono::microseconds(4 * g_coalesce_us) ||
-                        c.q.size() > 1;
-      auto deadline = now + std::chrono::microseconds(busy ? g_coalesce_us : 0);
-      while (c.queued < g_coalesce_max && std::chrono::steady_clock::now() < deadline) c.cv.wait_until(lk, deadline);
-      std::vector<VReq*> batch(c.q.begin(), c.q.end());
-      for (VReq* r : batch) r->taken = true;
-      c.q.clear();
-      c.queued = 0;
-      c.gathering = false;
-      c.cv.notify_all();  // the next leader may start gathering
-      lk.unlock();
-      run_verify_batch(batch);
-      lk.lock();
-      for (VReq* r : batch) r->done = true;
-      c.active--;
-      c.last_end = std::chrono::steady_clock::now();
-      c.cv.notify_all();
-    } else {
-      c.cv.wait(lk);
-    }
-  }
+  coalesce_submit(g_vq, p, me, run_verify_batch);  // coalesce.h
   if (me.rc) g_err = me.err;
   return me.rc;
 }
@@ -1995,6 +1919,11 @@ int hbls_init(uint32_t device_mask) { return init_mask(device_mask); }
 const char* hbls_last_error(void) { return g_err.c_str(); }
 
 int hbls_available(void) { return ensure_init() == 0 ? 1 : 0; }
+
+#ifndef HBLS_BUILD_ID
+#define HBLS_BUILD_ID "hbls-build:unversioned"
+#endif
+const char* hbls_build_id(void) { return HBLS_BUILD_ID; }
 
 int hbls_device_count(void) { return ensure_init() ? -1 : (int)devs().size(); }
 
@@ -2357,7 +2286,6 @@ int hbls_slot_device(const hbls_slot* a, void* stream) {
                    "aggregation group");
   std::lock_guard<std::mutex> lk(d->mu);
   Ws& w = ws_acquire(*d, s);
-  if (d->dec_valid && g_stagger) HCHK(hipStreamWaitEvent(s, d->ev_dec, 0));  // staggered slots (Dev::ev_dec)
   HCHK(hipEventRecord(w.ev_fork, s));
   // messages: hash + Miller lines (side 2)
   hipStream_t sh = w.side[2];

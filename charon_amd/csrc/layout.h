@@ -105,11 +105,6 @@ void launch_ta_layout(const uint32_t* grp_off, uint32_t n_groups, uint32_t t_u, 
 void launch_ta_lambda(const int64_t* idx, const uint32_t* grp_off, uint32_t n_groups, uint32_t n_partials, int mode,
                       TaDigits* dig, uint8_t* mstat, hipStream_t s, uint32_t t_u = 0, uint8_t* nonuni = nullptr,
                       const uint8_t* skip = nullptr);
-constexpr uint32_t TA_CHUNK = 8;  // members per lane of k_ta_msm
-void launch_ta_table(const HmEntry* pts, const uint32_t* src, uint32_t n_partials, void* tab, hipStream_t s);
-void launch_ta_msm(const HmEntry* pts, const uint32_t* src, const TaDigits* dig, void* tab, const uint32_t* cfirst,
-                   const uint32_t* ccount, const uint32_t* total, uint32_t max_chunks, int mode, G2JEntry* out,
-                   hipStream_t s);
 size_t ta_table_bytes(uint32_t n_partials);
 // guard (nullable): nothing unless *guard != 0 (then one lane per member in plain order, skip unused)
 void launch_ta_straus(const HmEntry* pts, const uint32_t* src, const TaDigits* dig, uint32_t n_partials,

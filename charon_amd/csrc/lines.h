@@ -5,47 +5,23 @@
 
 namespace hb {
 
-// HB_LINES28=0: the stored-word chain of pairing.h (A/B runs); default: pair28.h's lazy-limb chain,
-// whose lines equal the stored-word ones up to one nonzero Fp2 factor per line (its doubling keeps
-// T scaled by 4), which the final exponentiation removes (tests/test_lazy28.py)
-#ifndef HB_LINES28
-#define HB_LINES28 1
-#endif
+// pair28.h's lazy-limb chain, whose lines equal pairing.h's stored-word ones up to one nonzero Fp2
+// factor per line (its doubling keeps T scaled by 4), which the final exponentiation removes
+// (tests/test_lazy28.py)
 
 // The Miller chain of an affine G2 point Q: 68 lines, stored at out[j * stride].  EVAL: evaluate
 // each line at -g1 (pair (-g1, S) of the verification equation); otherwise store (a0, c1, c2).
 template <bool EVAL>
 __device__ __forceinline__ void line_chain(const G2A& Q, LineEntry* __restrict__ out, size_t stride) {
-#if HB_LINES28
   line_chain28<EVAL>([&]() { return Q; }, [&](int j, const LineCoeffs& l) { out[(size_t)j * stride] = {l.a0, l.a1, l.b1}; });
-#else
-  G2Proj T = {Q.x, Q.y, f2_one()};
-  int j = 0;
-  HB_NOUNROLL for (int i = 62; i >= 0; i--) {
-    LineCoeffs l = miller_dbl_c(T);
-    if (EVAL) line_eval(l, fp_from_const(G1_GEN_X), fp_from_const(G1_GEN_NEG_Y));
-    out[(size_t)j * stride] = {l.a0, l.a1, l.b1};
-    j++;
-    if ((HB_X_ABS >> i) & 1) {
-      l = miller_add_c(T, Q.x, Q.y);
-      if (EVAL) line_eval(l, fp_from_const(G1_GEN_X), fp_from_const(G1_GEN_NEG_Y));
-      out[(size_t)j * stride] = {l.a0, l.a1, l.b1};
-      j++;
-    }
-  }
-#endif
 }
 
 // line_chain of an affine point read from memory (re-read at the chain's additions instead of
 // held in registers across it)
 template <bool EVAL>
 __device__ __forceinline__ void line_chain_ld(const HmEntry* src, LineEntry* __restrict__ out, size_t stride) {
-#if HB_LINES28
   line_chain28<EVAL>([src]() { return hm_load(*src); },
                      [&](int j, const LineCoeffs& l) { out[(size_t)j * stride] = {l.a0, l.a1, l.b1}; });
-#else
-  line_chain<EVAL>(hm_load(*src), out, stride);
-#endif
 }
 
 #if defined(__HIP_DEVICE_COMPILE__)

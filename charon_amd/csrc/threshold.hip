@@ -649,12 +649,6 @@ __device__ __forceinline__ bool ta_small_uniform(const int64_t* __restrict__ csm
 }
 #endif
 
-#ifndef HB_TA_LAZY
-#define HB_TA_LAZY 1  // k_ta_sladder's ladder in ec28.h lazy limbs (0: stored words, A/B runs)
-#endif
-#ifndef HB_TA_SMALL_LAZY
-#define HB_TA_SMALL_LAZY 1  // k_ta_small's joint ladder likewise (round 4)
-#endif
 
 // One lane per validator: Q = sum_j [c_j] sigma_j (joint signed-binary NAF, the doublings shared by
 // the t members) into out[v t]; done[v] = 1, or 0 when the wave is not uniform.
@@ -695,7 +689,6 @@ __global__ KB_OCC(HB_OCC_STRAUS) void k_ta_small(const HmEntry* __restrict__ pts
   __syncthreads();
   const uint32_t m0 = vc * t;
   const int top = naf_top;
-#if HB_TA_SMALL_LAZY
   // the joint ladder in lazily reduced 28-bit limbs (ec28.h g2l_dbl / g2l_madd, as k_ta_sladder);
   // a member at infinity (an undecodable partial, replaced by infinity in k_dec_sig_pt; its group's
   // status comes from the member flags) is skipped, as jac_add_aff's infinity operand
@@ -712,20 +705,6 @@ __global__ KB_OCC(HB_OCC_STRAUS) void k_ta_small(const HmEntry* __restrict__ pts
     }
   }
   const G2J R = g2l_to_jac(RL);
-#else
-  G2J R = jac_infinity<Fp2>();
-  HB_NOUNROLL for (int i = top; i >= 0; i--) {
-    R = jac_dbl(R);
-    HB_NOUNROLL for (uint32_t k = 0; k < t; k++) {
-      const int dg = naf[k][i];
-      if (dg != 0) {  // wave-uniform
-        const HmEntry e = pts[src ? src[m0 + k] : m0 + k];
-        const G2A P = {e.x, dg < 0 ? f2_neg(e.y) : e.y, e.inf != 0};
-        R = jac_add_aff(R, P);
-      }
-    }
-  }
-#endif
   if (valid) {
     out[(size_t)v * t] = {R.X, R.Y, R.Z};
     done[v] = 1;
@@ -772,36 +751,22 @@ __global__ KB_OCC(HB_OCC_STRAUS) void k_ta_sladder(const TaDigits* __restrict__ 
   }
   __syncthreads();
   const uint4* wt = tab + (size_t)blockIdx.x * 16 * TA_TAB_QUADS * 64 + lane;
-#if HB_TA_LAZY
   G2L RL = g2l_infinity();  // the ladder in lazily reduced 28-bit limbs (ec28.h)
-#else
-  G2J R = jac_infinity<Fp2>();
-#endif
   const int top = naf_top;
   HB_NOUNROLL for (int i = top; i >= 0; i--) {
-#if HB_TA_LAZY
     RL = g2l_dbl(RL);
-#else
-    R = jac_dbl(R);
-#endif
     HB_NOUNROLL for (int b = 0; b < 4; b++) {
       const int dg = naf[b][i];
       if (dg != 0) {  // wave-uniform
         const int e = 4 * b + ((dg < 0 ? -dg : dg) >> 1);
         G2A T = {f2_load_q(wt, e, 0), f2_load_q(wt, e, 6), false};
         if (dg < 0) T.y = f2_neg(T.y);
-#if HB_TA_LAZY
         RL = g2l_madd(RL, f2l_from(T.x), f2l_from(T.y));
-#else
-        R = jac_add_aff(R, T);
-#endif
       }
     }
   }
   if (!valid) return;
-#if HB_TA_LAZY
   G2J R = g2l_to_jac(RL);
-#endif
   if (dn == 2) R = jac_infinity<Fp2>();
   out[(size_t)v * t] = {R.X, R.Y, R.Z};
   const G2J z = jac_infinity<Fp2>();
@@ -820,82 +785,6 @@ void launch_ta_small(const HmEntry* pts, const uint32_t* src, const int64_t* idx
   hipLaunchKernelGGL(k_ta_small, grid, dim3(64), 0, s, pts, src, csm, sdig, sok, n_groups, t, out, done);
   hipLaunchKernelGGL(k_ta_stab, grid, dim3(64), 0, s, (const G2JEntry*)out, n_groups, t, (uint4*)tab, done);
   hipLaunchKernelGGL(k_ta_sladder, grid, dim3(64), 0, s, sdig, done, n_groups, t, (uint4*)tab, out);
-}
-
-// The same aggregation as multi-scalar ladders over chunks of up to TA_CHUNK members of a group
-// (k_plan_* chunk plan, vbatch.hip): k_ta_table builds every member's 15-entry subset table (the
-// first half of k_ta_straus), then one lane per chunk runs ONE 64-step ladder whose doublings the
-// chunk's members share (64 doublings per chunk + 64 additions per member, instead of 64 + 64 per
-// member).  The chunk's sum goes to its first member's slot of `out`, infinity to the others, so
-// k_group_sum adds the members as before.  mode 1 (Aggregate, lambda = 1): a plain sum.
-#if defined(__HIP_DEVICE_COMPILE__)
-__device__ __forceinline__ uint4* member_tab(uint4* tab, uint32_t m) {
-  return tab + (size_t)(m >> 6) * 16 * TA_TAB_QUADS * 64 + (m & 63u);
-}
-#endif
-
-__global__ KB_OCC(HB_OCC_STRAUS) void k_ta_table(const HmEntry* __restrict__ pts, const uint32_t* __restrict__ src,
-                                                    uint32_t n_partials, uint4* __restrict__ tab) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  const uint32_t m = blockIdx.x * 64 + (threadIdx.x & 63u);
-  if (m >= n_partials) return;
-  uint4* wt = member_tab(tab, m);
-  {
-    const HmEntry e = pts[src ? src[m] : m];
-    G2A P0 = {e.x, e.y, e.inf != 0};
-    G2A P1 = {f2_mul(f2_conj(e.x), f2_from_const(PSI_CX)), f2_neg(f2_mul(f2_conj(e.y), f2_from_const(PSI_CY))), P0.inf};
-    G2A P2 = {f2_mul(e.x, f2_from_const(PSI2_CX)), f2_mul(e.y, f2_from_const(PSI2_CY)), P0.inf};
-    G2A P3 = {f2_mul(f2_conj(P2.x), f2_from_const(PSI_CX)), f2_neg(f2_mul(f2_conj(P2.y), f2_from_const(PSI_CY))), P0.inf};
-    tab_store(wt, 0, jac_from_aff(P0));
-    tab_store(wt, 1, jac_from_aff(P1));
-    tab_store(wt, 3, jac_from_aff(P2));
-    tab_store(wt, 7, jac_from_aff(P3));
-  }
-  HB_NOUNROLL for (int sidx = 3; sidx < 16; sidx++) {
-    const int hi = sidx >= 8 ? 8 : (sidx >= 4 ? 4 : 2);
-    if (sidx == hi) continue;
-    const G2J h = tab_load(wt, hi - 1);
-    const G2A ha = {h.X, h.Y, f2_is_zero(h.Z)};
-    tab_store(wt, sidx - 1, jac_add_aff(tab_load(wt, sidx - hi - 1), ha));
-  }
-#endif
-}
-
-__global__ KB_OCC(HB_OCC_STRAUS) void k_ta_msm(const HmEntry* __restrict__ pts, const uint32_t* __restrict__ src,
-                                                  const TaDigits* __restrict__ dig, uint4* __restrict__ tab,
-                                                  const uint32_t* __restrict__ cfirst,
-                                                  const uint32_t* __restrict__ ccount,
-                                                  const uint32_t* __restrict__ total, int mode,
-                                                  G2JEntry* __restrict__ out) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= *total) return;
-  const uint32_t first = cfirst[c], cnt = ccount[c] & 0x7fffffffu;
-  G2J R = jac_infinity<Fp2>();
-  if (mode == 1) {
-    HB_NOUNROLL for (uint32_t k = 0; k < cnt; k++) {
-      const HmEntry e = pts[src ? src[first + k] : first + k];
-      R = jac_add(R, jac_from_aff(G2A{e.x, e.y, e.inf != 0}));
-    }
-  } else {
-    HB_NOUNROLL for (int b = 63; b >= 0; b--) {
-      R = jac_dbl(R);
-      HB_NOUNROLL for (uint32_t k = 0; k < cnt; k++) {
-        const uint32_t m = first + k;
-        const TaDigits d = dig[m];
-        const uint32_t sel = (uint32_t)((d.a[0] >> b) & 1) | ((uint32_t)((d.a[1] >> b) & 1) << 1) |
-                             ((uint32_t)((d.a[2] >> b) & 1) << 2) | ((uint32_t)((d.a[3] >> b) & 1) << 3);
-        const G2J S = jac_add(R, tab_load(member_tab(tab, m), sel == 0 ? 0 : (int)sel - 1));
-        f2_select(R.X, sel != 0, R.X, S.X);
-        f2_select(R.Y, sel != 0, R.Y, S.Y);
-        f2_select(R.Z, sel != 0, R.Z, S.Z);
-      }
-    }
-  }
-  out[first] = {R.X, R.Y, R.Z};
-  const G2J z = jac_infinity<Fp2>();
-  for (uint32_t k = 1; k < cnt; k++) out[first + k] = {z.X, z.Y, z.Z};
-#endif
 }
 
 void launch_ta_lambda(const int64_t* idx, const uint32_t* grp_off, uint32_t n_groups,
@@ -935,18 +824,6 @@ void launch_ta_joint(const HmEntry* pts, const uint32_t* src, const TaDigits* di
   hipLaunchKernelGGL(k_ta_jladder, grid, dim3(64), 0, s, dig, n_groups, t, c, (uint4*)tab, out, skip, nonuni);
   hipLaunchKernelGGL(k_ta_jgeneral, grid, dim3(64), 0, s, pts, src, dig, n_groups, t, c, (uint4*)tab, out, skip,
                      nonuni);
-}
-
-void launch_ta_table(const HmEntry* pts, const uint32_t* src, uint32_t n_partials, void* tab, hipStream_t s) {
-  if (n_partials)
-    hipLaunchKernelGGL(k_ta_table, dim3(blocks_of(n_partials, 64)), dim3(64), 0, s, pts, src, n_partials, (uint4*)tab);
-}
-void launch_ta_msm(const HmEntry* pts, const uint32_t* src, const TaDigits* dig, void* tab, const uint32_t* cfirst,
-                   const uint32_t* ccount, const uint32_t* total, uint32_t max_chunks, int mode, G2JEntry* out,
-                   hipStream_t s) {
-  if (max_chunks)
-    hipLaunchKernelGGL(k_ta_msm, dim3(blocks_of(max_chunks, 64)), dim3(64), 0, s, pts, src, dig, (uint4*)tab, cfirst,
-                       ccount, total, mode, out);
 }
 
 void launch_ta_straus(const HmEntry* pts, const uint32_t* src, const TaDigits* dig, uint32_t n_partials,

@@ -71,13 +71,8 @@ HD Fp2 f2_neg(const Fp2& a) { return f2_sub(f2_zero(), a); }
 HD Fp2 f2_dbl(const Fp2& a) { return f2_add(a, a); }
 HD Fp2 f2_conj(const Fp2& a) { return {a.c0, fp_neg(a.c1)}; }
 
-// Fp2 product and square as single lazily reduced passes (fp.h fp2_mul_core / fp2_sqr_core), or
-// (HB_F2_LAZY=0) as Karatsuba / complex squaring over Fp products.  Counted as 3 and 2 Fp products
-// either way, the unit of the op counts (charon_amd/opcounts.py).
-#ifndef HB_F2_LAZY
-#define HB_F2_LAZY 1
-#endif
-#if HB_F2_LAZY
+// Fp2 product and square as single lazily reduced passes (fp.h fp2_mul_core / fp2_sqr_core).
+// Counted as 3 and 2 Fp products, the unit of the op counts (charon_amd/opcounts.py).
 HD Fp2 f2_mul(const Fp2& a, const Fp2& b) {
   HB_COUNT_FP_MUL();
   HB_COUNT_FP_MUL();
@@ -94,20 +89,6 @@ HD Fp2 f2_sqr(const Fp2& a) {
   fp2_sqr_pair(r.c0, r.c1, a.c0, a.c1);
   return r;
 }
-#else
-HD Fp2 f2_mul(const Fp2& a, const Fp2& b) {
-  Fp t0 = fp_mul(a.c0, b.c0);
-  Fp t1 = fp_mul(a.c1, b.c1);
-  Fp t2 = fp_mul(fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
-  return {fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)};
-}
-
-HD Fp2 f2_sqr(const Fp2& a) {
-  Fp t0 = fp_mul(fp_add(a.c0, a.c1), fp_sub(a.c0, a.c1));
-  Fp t1 = fp_mul(a.c0, a.c1);
-  return {t0, fp_dbl(t1)};
-}
-#endif
 
 HD Fp2 f2_mul_fp(const Fp2& a, const Fp& b) { return {fp_mul(a.c0, b), fp_mul(a.c1, b)}; }
 
@@ -117,11 +98,14 @@ HD Fp2 f2_mul_xi(const Fp2& a) { return {fp_sub(a.c0, a.c1), fp_add(a.c0, a.c1)}
 HD bool f2_is_zero(const Fp2& a) { return fp_is_zero(a.c0) && fp_is_zero(a.c1); }
 HD bool f2_eq(const Fp2& a, const Fp2& b) { return fp_eq(a.c0, b.c0) && fp_eq(a.c1, b.c1); }
 
-HDNI Fp2 f2_inv(const Fp2& a) {
+template <bool kEarlyExit>
+HDNI Fp2 f2_inv_t(const Fp2& a) {
   Fp n = fp_add(fp_sqr(a.c0), fp_sqr(a.c1));
-  Fp ni = fp_inv(n);
+  Fp ni = fp_inv_t<kEarlyExit>(n);
   return {fp_mul(a.c0, ni), fp_neg(fp_mul(a.c1, ni))};
 }
+HD Fp2 f2_inv(const Fp2& a) { return f2_inv_t<true>(a); }
+HD Fp2 f2_inv_ct(const Fp2& a) { return f2_inv_t<false>(a); }
 
 HD Fp2 f2_mul_small(const Fp2& a, int k) { return {fp_mul_small(a.c0, k), fp_mul_small(a.c1, k)}; }
 

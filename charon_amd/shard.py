@@ -121,6 +121,31 @@ class SlotExchange:
         return recv[field][r * n:(r + 1) * n]
 
 
+PACK_FIELDS = ("vbits", "tout", "tst", "ast")
+
+
+def pack_layout(NP: int, V: int):
+    """The slot's exchanged outputs in ONE buffer (one all-gather per slot):
+    field -> (offset, bytes), and the total -- the verify bitmap of NP partials (hbls_status_bitmap,
+    rounded up to whole bytes), V 96-byte aggregates, their statuses, their verification
+    statuses."""
+    nb = (NP + 7) // 8
+    layout = {"vbits": (0, nb), "tout": (nb, 96 * V), "tst": (nb + 96 * V, V), "ast": (nb + 97 * V, V)}
+    return layout, nb + 98 * V
+
+
+def pack_views(pack: torch.Tensor, layout) -> Dict[str, torch.Tensor]:
+    """The fields as views of the slot's pack buffer (the slot writes them in place)."""
+    return {f: pack[a:a + b] for f, (a, b) in layout.items()}
+
+
+def unpack_gathered(gathered_pack: torch.Tensor, layout, total: int, world: int, field: str) -> torch.Tensor:
+    """Field `field` of every rank, in rank order, from the all-gathered packs (world x total
+    bytes): rank r's block is bytes [r n, (r + 1) n) of the result, n = the field's size."""
+    a, b = layout[field]
+    return torch.cat([gathered_pack[r * total + a:r * total + a + b] for r in range(world)])
+
+
 def max_over_ranks(seconds: float, device, group=None) -> float:
     """The slowest rank's time (bench.py reports whole-job throughput against it)."""
     t = torch.tensor([seconds], dtype=torch.float64, device=device)

@@ -49,6 +49,11 @@ const char* hbls_last_error(void);
 int hbls_available(void);
 /* Devices driven by the library (after hbls_init). */
 int hbls_device_count(void);
+/* Build provenance (new, no herumi counterpart): "hbls-build:<sha256 prefix of the charon_amd/csrc files
+ * and this header>[+<compile defines>]", embedded at compile time by charon_amd/build.py.  The
+ * loader (charon_amd/_lib.py) recomputes the source hash from the tree and refuses a library built
+ * from other sources. */
+const char* hbls_build_id(void);
 
 /* ---------------------------------------------------------------------------------------
  * Host-buffer entry points (the drop-in boundary for the Go shim).  Blocking; the library

@@ -19,6 +19,16 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: long-running CPU test")
 
 
+def pytest_report_header(config):
+    """Which library the run tests: its embedded build id against the tree's sources."""
+    from charon_amd import _lib
+    path = os.environ.get("HBLS_LIBRARY") or _lib.LIB_PATH
+    if not os.path.exists(path):
+        return f"libhipbls.so: not built ({path})"
+    lib_id, tree = _lib.embedded_build_id(path), _lib.source_build_id()
+    return f"libhipbls.so: {lib_id} (tree {tree}: {'match' if tree in lib_id else 'STALE'})"
+
+
 @pytest.fixture(scope="session")
 def kats():
     with open(os.path.join(GOLDEN, "kat_reference.json")) as f:

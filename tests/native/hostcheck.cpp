@@ -878,11 +878,71 @@ extern "C" int hc_fe28(const uint8_t* f576, uint8_t* out) {
   return 0;
 }
 
-// fp.h fp_inv (divsteps) against fp_inv_pow (a^(p-2)): x canonical big-endian; out: both inverses
-// (canonical), batches run
-extern "C" int hc_fp_inv(const uint8_t* x48, uint8_t* out96, int* batches) {
+// fp.h fp_inv (divsteps, early exit) and fp_inv_ct (fixed trip count, the secret-key paths)
+// against fp_inv_pow (a^(p-2)): x canonical big-endian; out: the three inverses (canonical), the
+// batches each divstep version ran
+extern "C" int hc_fp_inv(const uint8_t* x48, uint8_t* out144, int* batches, int* batches_ct) {
   const Fp a = hc_fp_in(x48);
-  hc_fp_out(out96, fp_inv(a, batches));
-  hc_fp_out(out96 + 48, fp_inv_pow(a));
+  hc_fp_out(out144, fp_inv(a, batches));
+  hc_fp_out(out144 + 48, fp_inv_pow(a));
+  hc_fp_out(out144 + 96, fp_inv_ct(a, batches_ct));
+  return 0;
+}
+
+// coalesce.h's state machine with a stub batch runner (no GPU): `threads` callers each submit
+// `reqs` requests of 1..3 items; the runner sleeps run_us, checks that none of its requests ran
+// before and writes each item's status (request id & 0xff).  out[0]: most batches running at once
+// (counted by the runner), out[1]: batches, out[2]: requests run twice or never, out[3]: wrong
+// statuses, out[4]: the coalescer's own max_active.
+#include "../../charon_amd/csrc/coalesce.h"
+extern "C" int hc_coalesce_stress(int threads, int reqs, int inflight, int window_us, int run_us, int* out) {
+  Coalescer c;
+  CoalesceParams p;
+  p.us = (size_t)window_us;
+  p.max_items = 1u << 16;
+  p.inflight = (size_t)inflight;
+  const int total = threads * reqs;
+  std::vector<std::atomic<int>> runs(total);
+  for (auto& r : runs) r = 0;
+  std::atomic<int> running{0}, max_running{0}, bad_status{0};
+  auto run = [&](std::vector<VReq*>& batch) {
+    const int now = ++running;
+    int m = max_running.load();
+    while (now > m && !max_running.compare_exchange_weak(m, now)) {
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(run_us));
+    for (VReq* r : batch) {
+      const int id = (int)(intptr_t)r->pk;  // the request id travels in the pk pointer
+      runs[id]++;
+      for (size_t i = 0; i < r->n; i++) r->st[i] = (uint8_t)(id & 0xff);
+      r->rc = 0;
+    }
+    --running;
+  };
+  std::vector<std::thread> th;
+  for (int t = 0; t < threads; t++)
+    th.emplace_back([&, t] {
+      for (int k = 0; k < reqs; k++) {
+        const int id = t * reqs + k;
+        uint8_t st[3] = {0xee, 0xee, 0xee};
+        VReq me;
+        me.pk = (const uint8_t*)(intptr_t)id;
+        me.n = 1 + (size_t)(id % 3);
+        me.st = st;
+        coalesce_submit(c, p, me, run);
+        for (size_t i = 0; i < me.n; i++)
+          if (st[i] != (uint8_t)(id & 0xff)) bad_status++;
+        if (!me.done) bad_status++;
+      }
+    });
+  for (auto& x : th) x.join();
+  int wrong_runs = 0;
+  for (auto& r : runs)
+    if (r.load() != 1) wrong_runs++;
+  out[0] = max_running.load();
+  out[1] = (int)c.batches;
+  out[2] = wrong_runs;
+  out[3] = bad_status.load();
+  out[4] = c.max_active;
   return 0;
 }

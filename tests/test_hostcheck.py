@@ -238,19 +238,23 @@ def test_rlc_endomorphism_ladders(hc, kats):
 def test_fp_inv_divsteps(hc):
     """fp.h fp_inv (Bernstein-Yang divsteps, 30 per batch, stopping once g = 0) equals a^(p-2) and the
     oracle's inverse on 0, 1, p - 1, small values, powers of two, values near 2^380 and 2000 random
-    values, within the FP_INV_BATCHES bound (with room to spare)"""
-    hc.hc_fp_inv.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]
+    values, within the FP_INV_BATCHES bound (with room to spare); the fixed-trip version of the
+    secret-key paths (fp_inv_ct) gives the same inverse after always FP_INV_BATCHES batches"""
+    hc.hc_fp_inv.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int),
+                             ctypes.POINTER(ctypes.c_int)]
     rng = random.Random(30)
     vals = [0, 1, 2, 3, B.P - 1, B.P - 2, (B.P + 1) // 2] + [1 << k for k in range(0, 381, 17)]
     vals += [(1 << 380) + d for d in (-1, 0, 1)] + [rng.randrange(B.P) for _ in range(2000)]
     worst = 0
     for x in vals:
-        out = ctypes.create_string_buffer(96)
-        nb = ctypes.c_int(0)
-        hc.hc_fp_inv(x.to_bytes(48, "big"), out, ctypes.byref(nb))
+        out = ctypes.create_string_buffer(144)
+        nb, nct = ctypes.c_int(0), ctypes.c_int(0)
+        hc.hc_fp_inv(x.to_bytes(48, "big"), out, ctypes.byref(nb), ctypes.byref(nct))
         want = pow(x, B.P - 2, B.P)
         assert int.from_bytes(out.raw[:48], "big") == want, x
-        assert int.from_bytes(out.raw[48:], "big") == want, x
+        assert int.from_bytes(out.raw[48:96], "big") == want, x
+        assert int.from_bytes(out.raw[96:], "big") == want, x
+        assert nct.value == 40, nct.value
         worst = max(worst, nb.value)
     assert worst <= 34, worst  # FP_INV_BATCHES = 40
 

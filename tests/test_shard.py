@@ -20,7 +20,8 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from charon_amd import synth
-from charon_amd.shard import FIELDS, SlotExchange, gloo_allgather, max_over_ranks, owned_validators
+from charon_amd.shard import (FIELDS, PACK_FIELDS, SlotExchange, gloo_allgather, max_over_ranks, owned_validators,
+                               pack_layout, pack_views, unpack_gathered)
 
 V, N, T, WORLD = 3, 4, 3, 2
 
@@ -83,6 +84,55 @@ def _worker(rank, port, errq):
         raise
 
 
+def _packed_worker(rank, port, errq):
+    """bench.py's exchange as it runs on the GPU: ONE packed buffer per slot (pack_layout), the
+    slot's fields written in place into its views, SlotExchange({"pack": PB}) all-gathering it, every
+    rank unpacking every other rank's blocks with unpack_gathered (bench.py's gathered()); two
+    output sets in flight, slot k checked only after slot k + 1 was exchanged into the other set."""
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+        NP = V * N
+        layout, PB = pack_layout(NP, V)
+        cl = synth.make_cluster(V, N, T, first_validator=owned_validators(rank, V).start)
+        shards = [synth.make_cluster(V, N, T, first_validator=owned_validators(r, V).start) for r in range(WORLD)]
+        exch = SlotExchange(WORLD, rank, {"pack": PB}, "cpu", gloo_allgather)
+        outs = []
+        for _ in range(2):
+            o = {"pack": torch.full((PB,), 0xAB, dtype=torch.uint8)}
+            o.update(pack_views(o["pack"], layout))
+            o["xchg"] = exch.gather_buffers()
+            outs.append(o)
+
+        def check(slot, o):
+            for r in range(WORLD):
+                want = _slot_results(shards[r], slot)
+                for f in PACK_FIELDS:
+                    n = layout[f][1]
+                    got = unpack_gathered(o["xchg"]["pack"], layout, PB, WORLD, f)
+                    assert got.numel() == WORLD * n
+                    assert torch.equal(got[r * n:(r + 1) * n], want[f]), (slot, r, f)
+
+        for slot in range(6):
+            o = outs[slot % 2]
+            res = _slot_results(cl, slot)
+            for f in PACK_FIELDS:  # the slot writes its outputs in place
+                o[f].copy_(res[f])
+            assert exch.exchange({"pack": o["pack"]}, o["xchg"]) == slot
+            if slot:
+                check(slot - 1, outs[(slot - 1) % 2])
+        check(5, outs[1])
+        logs = [None] * WORLD
+        dist.all_gather_object(logs, exch.issued)
+        assert logs[0] == logs[1] == [(k, "pack") for k in range(6)], logs
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001 -- reported to the parent
+        errq.put(f"rank {rank}: {type(e).__name__}: {e}")
+        raise
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -94,11 +144,12 @@ def test_owned_validators_partition():
     assert got == list(range(20))
 
 
-def test_sharded_slot_exchange_gloo_world2():
+@pytest.mark.parametrize("worker", [_worker, _packed_worker], ids=["fields", "bench_pack"])
+def test_sharded_slot_exchange_gloo_world2(worker):
     ctx = mp.get_context("spawn")
     errq = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, port, errq)) for r in range(WORLD)]
+    procs = [ctx.Process(target=worker, args=(r, port, errq)) for r in range(WORLD)]
     for p in procs:
         p.start()
     for p in procs:
@@ -115,13 +166,14 @@ def test_sharded_slot_exchange_gloo_world2():
 
 
 def test_bench_pack_layout():
-    """bench.py's one exchanged buffer per slot: the fields tile it exactly, in order, with the
-    bitmap rounded up to whole bytes"""
+    """bench.py's one exchanged buffer per slot (shard.pack_layout): the fields tile it exactly, in
+    order, with the bitmap rounded up to whole bytes"""
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import bench
+    assert bench.pack_layout is pack_layout
     for NP, V in ((1, 1), (12, 3), (1_000_000, 100_000), (875_001, 125_000)):
-        layout, total = bench.pack_layout(NP, V)
+        layout, total = pack_layout(NP, V)
         pos = 0
         for f in ("vbits", "tout", "tst", "ast"):
             off, size = layout[f]
