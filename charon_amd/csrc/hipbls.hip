@@ -308,7 +308,7 @@ enum WsId {
   W_VPK, W_VPKST, W_VSIG, W_VSIGST, W_IGRP, W_PR, W_SR, W_GP, W_GST, W_GMSG, W_GVER, W_GLINES, W_LIST, W_COUNT,
   W_FBLINES,
   W_APK, W_APKST, W_ASIG, W_APR, W_ASR,          // folded aggregates (post-aggregate verification)
-  W_TAPTS, W_TADST, W_TAMST, W_TADIG, W_TATAB, W_TAJ,  // ThresholdAggregate / Aggregate
+  W_TAPTS, W_TADST, W_TAMST, W_TADIG, W_TATAB, W_TAJ, W_TAHIT,  // ThresholdAggregate / Aggregate
   W_TACSM, W_TASDIG, W_TASOK, W_TASDONE, W_TASTAB, W_TANONUNI,  // its small-scalar path
   W_SEGA, W_SEGB, W_SEGSTA, W_SEGSTB, W_VAPT, W_VAPV, W_PLAN,  // VerifyAggregate key reduction
   W_PCNT, W_PCOFF, W_PCFIRST, W_PCCOUNT, W_COEF, W_COEF4, W_RT1, W_RT2,  // chunk plan + multi-scalar RLC
@@ -381,6 +381,14 @@ struct Dev {
   // public-key cache (hbls_pubkey_cache_add): decompressed entries + statuses, every device holds
   // all g_kc_n of them
   DevBuf kc_tab, kc_st;
+  // decompressed-signature cache (vbatch.hip k_sc_put / k_sc_get): filled by host-buffer Verify
+  // batches, read by host-buffer ThresholdAggregate batches.  sc_ev orders every put and get on
+  // the device (recorded after each, waited for before the next: a put rewrites ring entries a get
+  // may read); enqueued under `mu` like everything else.
+  DevBuf sc_key, sc_ent, sc_st, sc_tab;
+  size_t sc_cap = 0, sc_cursor = 0, sc_filled = 0;
+  hipEvent_t sc_ev = nullptr;
+  bool sc_ev_valid = false;
   // adaptive slot-wide check (HBLS_ADAPTIVE): outcomes of recent checked calls, copied to pinned host
   // memory asynchronously and read once their event has completed -- never a synchronisation
   SlotRes* res_host = nullptr;
@@ -393,6 +401,11 @@ struct Dev {
   std::vector<Timed> tev;
   size_t tev_used = 0;
 };
+
+// HBLS_SIG_CACHE / hbls_sig_cache: entries of each device's decompressed-signature cache (a power
+// of two; 0 = off).  2^21 (two C3 slots of partials): 2 M x 305 B = 640 MB per device.
+std::atomic<size_t> g_sc_cap{size_t(1) << 21};
+uint64_t g_sc_k0 = 0x243f6a8885a308d3ull, g_sc_k1 = 0x13198a2e03707344ull;  // keyed hash (getrandom at init)
 
 std::mutex g_init_mu;
 std::vector<Dev*> g_devs;  // in device-mask order (hbls_debug_split: each ordinal repeated); g_devs_mu
@@ -552,6 +565,16 @@ int init_mask(uint32_t mask) {
     g_fb_batch = fb;
   }
   g_mml_pairs = std::min<size_t>(64, env_size("HBLS_MML_PAIRS", g_mml_pairs));
+  {
+    size_t sc = env_size("HBLS_SIG_CACHE", g_sc_cap.load());
+    while (sc & (sc - 1)) sc &= sc - 1;  // a power of two
+    g_sc_cap = std::min<size_t>(sc, size_t(1) << 30);
+    uint64_t k[2];
+    if (getrandom(k, sizeof(k), 0) == (ssize_t)sizeof(k)) {  // otherwise the fixed key (a miss costs time only)
+      g_sc_k0 = k[0];
+      g_sc_k1 = k[1] | 1;
+    }
+  }
   std::vector<Dev*> devs;
   for (int k = 0; k < 32; k++)
     if (mask & (1u << k)) {
@@ -739,10 +762,15 @@ int ta_tail(Dev& d, Ws& w, const HmEntry* pts, const uint32_t* src, const uint8_
   return 0;
 }
 
+// defer_msgs: the caller hashed its defer_msgs messages without their Miller lines (hm[].lines
+// unset; callers whose messages have about one verification group each, batched final
+// exponentiation sizes): the slot-wide check evaluates each group's chain at P directly
+// (k_lines_at_p) and the unevaluated lines are computed only behind a failed check; any other path
+// computes them first.
 int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, const uint32_t* didx,
                     const MsgEntry* hm, size_t n, const uint32_t* dgoff, size_t n_groups, uint8_t* dst,
                     hipStream_t s, hipEvent_t hm_ready, const TaFold* fold, const uint32_t* kc_idx = nullptr,
-                    hipEvent_t h_ready = nullptr) {
+                    hipEvent_t h_ready = nullptr, size_t defer_msgs = 0) {
   if (!dgoff) n_groups = n;
   G1AEntry* vpk;
   HmEntry* vsig;
@@ -963,6 +991,10 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
   // small calls (no batched final exponentiation): the groups' sums and signature lines do not
   // need the hashed messages, so they overlap the hashing; the wait comes before the pairing
   if (hm_ready && bfe) HCHK(hipStreamWaitEvent(s, hm_ready, 0));
+  if (defer_msgs && !bfe) return set_err("verify: deferred Miller lines need the batched final exponentiation");
+  const bool lines_at_p = defer_msgs && smsm && !skip_msm;
+  if (defer_msgs && !lines_at_p)  // the per-batch check reads the unevaluated lines
+    TIMED(d, "k_lines_msg", s, launch_lines_msg(const_cast<MsgEntry*>(hm), (uint32_t)defer_msgs, s));
   Fp4Entry* f1 = nullptr;
   uint8_t* f1bad = nullptr;
   G2JEntry* f1S = nullptr;
@@ -1063,7 +1095,8 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
         pp.f_n = ng;
         pp.f_out = pbuf1;
         pp.sig_lines = mlev;
-        TIMED(d, "k_mml_eval", s, launch_mml_eval(pp, mlev, s));
+        if (lines_at_p) TIMED(d, "k_lines_at_p", s, launch_lines_at_p(pp, mlev, s));
+        else TIMED(d, "k_mml_eval", s, launch_mml_eval(pp, mlev, s));
         TIMED(d, "k_pair3_mml", s, launch_pair3_mml(pp, s));
         Fp4Entry* cur = pbuf1;
         uint32_t cur_n = pp.n;
@@ -1089,6 +1122,9 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
         if (!skip_msm) {
           TIMED(d, "k_pair3_fin", s, g_fe6 ? launch_pair6_fin(pf, s) : launch_pair3_fin(pf, s));
           TIMED(d, "k_slot_verdict", s, launch_slot_verdict(gst, sfail, ng, gver + g0, s));
+          // deferred lines: the per-batch check behind a failed slot-wide check reads them
+          if (lines_at_p)
+            TIMED(d, "k_lines_msg", s, launch_lines_msg(const_cast<MsgEntry*>(hm), (uint32_t)defer_msgs, s, sfail));
           // the slot-wide check failed: the per-batch check (signature sides per item and group;
           // computed in the first pass when the check was skipped)
           if (rlc_fallback_chunks) {
@@ -1332,10 +1368,17 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
 
 // hash every distinct message to G2 (+ its Miller line chain) into hm, on stream s
 int hash_messages(Dev& d, const uint8_t* dmsg, const uint64_t* doff, const uint32_t* dlen, size_t n_msgs,
-                  MsgEntry* hm, hipStream_t s) {
+                  MsgEntry* hm, hipStream_t s, bool lines = true) {
   TIMED(d, "k_hash_to_g2", s, launch_hash_to_g2(dmsg, doff, dlen, (uint32_t)n_msgs, hm, s));
-  TIMED(d, "k_lines_msg", s, launch_lines_msg(hm, (uint32_t)n_msgs, s));
+  if (lines) TIMED(d, "k_lines_msg", s, launch_lines_msg(hm, (uint32_t)n_msgs, s));
   return 0;
+}
+
+// Whether a verification defers its messages' Miller lines (verify_pipeline defer_msgs): messages
+// with about one group each (the chain per group is then no extra work) and the batched sizes.
+bool defer_lines(size_t n_groups, size_t n_msgs) {
+  const size_t fe_min = g_fe_batch_min.load();
+  return fe_min && n_groups >= fe_min && n_groups <= n_msgs;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1559,6 +1602,58 @@ bool kc_lookup(const uint8_t* pks, size_t m, std::vector<uint32_t>& idx, const u
   return any;
 }
 
+// ---- decompressed-signature cache (Dev::sc_*; kernels in vbatch.hip).  Both run under d.mu.
+// sc_ready: the device's cache at the current capacity (allocated on first use; a capacity change
+// drops the old contents), false when the cache is off.
+bool sc_ready(Dev& d, bool alloc) {
+  const size_t cap = g_sc_cap.load();
+  if (cap == 0) return false;
+  if (d.sc_cap == cap) return true;
+  if (!alloc) return false;
+  void* p;
+  if (ensure_buf(d.sc_key, cap * 96, &p) || ensure_buf(d.sc_ent, cap * sizeof(HmEntry), &p) ||
+      ensure_buf(d.sc_st, cap, &p) || ensure_buf(d.sc_tab, 2 * cap * sizeof(uint32_t), &p))
+    return false;
+  if (hipMemset(d.sc_tab.p, 0, 2 * cap * sizeof(uint32_t)) != hipSuccess) return false;
+  if (!d.sc_ev && hipEventCreateWithFlags(&d.sc_ev, hipEventDisableTiming) != hipSuccess) return false;
+  d.sc_cap = cap;
+  d.sc_cursor = d.sc_filled = 0;
+  return true;
+}
+// after a Verify batch: its m signatures (bytes in group order, sig) and their decompressed points
+// and statuses (pts, st, the verification's workspace) enter the ring
+int sc_put(Dev& d, const uint8_t* sig, const HmEntry* pts, const uint8_t* st, size_t m, hipStream_t s) {
+  if (!m || !sc_ready(d, true)) return 0;
+  const size_t cap = d.sc_cap;
+  if (m > cap) {  // only the last cap items fit
+    sig += 96 * (m - cap);
+    pts += m - cap;
+    st += m - cap;
+    m = cap;
+  }
+  if (d.sc_ev_valid) HCHK(hipStreamWaitEvent(s, d.sc_ev, 0));
+  TIMED(d, "k_sc_put", s,
+        launch_sc_put(sig, pts, st, (uint32_t)m, (uint32_t)d.sc_cursor, (uint32_t)cap, d.sc_key.p, (HmEntry*)d.sc_ent.p,
+                      (uint8_t*)d.sc_st.p, (uint32_t*)d.sc_tab.p, (uint32_t)(2 * cap), g_sc_k0, g_sc_k1, s));
+  HCHK(hipEventRecord(d.sc_ev, s));
+  d.sc_ev_valid = true;
+  d.sc_cursor = (d.sc_cursor + m) & (cap - 1);
+  d.sc_filled = std::min(cap, d.sc_filled + m);
+  return 0;
+}
+// before an aggregation's decompression: the cached points of its n members into pts / st, hit[i]
+// set for those (k_dec_sig_pt then skips them).  Returns whether the cache was consulted.
+bool sc_get(Dev& d, const uint8_t* sig, size_t n, HmEntry* pts, uint8_t* st, uint8_t* hit, hipStream_t s) {
+  if (!n || !d.sc_filled || !sc_ready(d, false)) return false;
+  if (d.sc_ev_valid && hipStreamWaitEvent(s, d.sc_ev, 0) != hipSuccess) return false;
+  TIMED(d, "k_sc_get", s,
+        launch_sc_get(sig, (uint32_t)n, d.sc_key.p, (const HmEntry*)d.sc_ent.p, (const uint8_t*)d.sc_st.p,
+                      (const uint32_t*)d.sc_tab.p, (uint32_t)(2 * d.sc_cap), g_sc_k0, g_sc_k1, pts, st, hit, s));
+  if (hipEventRecord(d.sc_ev, s) != hipSuccess) return false;
+  d.sc_ev_valid = true;
+  return true;
+}
+
 // HBLS_HOST_TIMING=1: phases of a host-buffer Verify batch on stderr (diagnosis)
 static bool host_timing() {
   static const bool on = [] {
@@ -1642,7 +1737,8 @@ int verify_host(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msgs, co
     Ws& w = ws_acquire(d, h.s);
     MsgEntry* hm;
     hipEvent_t hm_ready = nullptr, h_ready = nullptr;
-    if (hash_table(d, t, &hm, true, &w, &hm_ready, &h, &h_ready)) return -1;
+    const bool defer = defer_lines(ge - gb, t.len.size());
+    if (hash_table(d, t, &hm, !defer, &w, &hm_ready, &h, &h_ready)) return -1;
     uint8_t *dpk, *dsig, *dst, *dst_out = nullptr;
     uint32_t *didx, *dgoff, *dkc = nullptr, *dord = nullptr;
     if (whole) {  // caller order up, group order on the device
@@ -1668,8 +1764,15 @@ int verify_host(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msgs, co
     if (upload(d, I_MIDX, tidx.data(), m, &didx, &h) || upload(d, I_VGOFF, goff.data(), goff.size(), &dgoff, &h))
       return -1;
     if (use_kc && upload(d, I_KC, kc.data(), m, &dkc, &h)) return -1;
-    if (verify_pipeline(d, w, dpk, dsig, didx, hm, m, dgoff, ge - gb, dst, h.s, hm_ready, nullptr, dkc, h_ready))
+    if (verify_pipeline(d, w, dpk, dsig, didx, hm, m, dgoff, ge - gb, dst, h.s, hm_ready, nullptr, dkc, h_ready,
+                        defer ? t.len.size() : 0))
       return -1;
+    {  // the decompressed partials into the signature cache (the aggregation of these partials reads them)
+      HmEntry* vsig;
+      uint8_t* vsigst;
+      if (wsbuf(w, W_VSIG, m, &vsig) || wsbuf(w, W_VSIGST, m, &vsigst) || sc_put(d, dsig, vsig, vsigst, m, h.s))
+        return -1;
+    }
     if (whole) LAUNCH(k_scatter_status, m, h.s, dst, dord, (uint32_t)m, dst_out);
     if (ws_release(w, h.s)) return -1;
     lk.unlock();  // enqueued: other callers may enqueue while this one waits for its stream
@@ -1716,9 +1819,15 @@ int group_op_host(const uint8_t* sigs, const int64_t* idx, const uint32_t* grp_o
     if (ensure_buf(h.io[I_OUT], ng * 96, &dout) || ensure_buf(h.io[I_STAT], ng, &dst)) return -1;
     Ws& w = ws_acquire(d, h.s);
     HmEntry* pts;
-    uint8_t* mst0;
+    uint8_t *mst0, *hit = nullptr;
     if (wsbuf(w, W_TAPTS, np, &pts) || wsbuf(w, W_TADST, np, &mst0)) return -1;
-    if (np) TIMED(d, "k_dec_sig_pt", h.s, launch_dec_sig_pt(dsig, (uint32_t)np, pts, mst0, h.s));
+    // members verified by an earlier host-buffer Verify batch come from the signature cache; the
+    // rest are decompressed (the same kernels, so the same points and statuses)
+    if (mode == 0 && np && d.sc_filled) {
+      if (wsbuf(w, W_TAHIT, np, &hit)) return -1;
+      if (!sc_get(d, dsig, np, pts, mst0, hit, h.s)) hit = nullptr;
+    }
+    if (np) TIMED(d, "k_dec_sig_pt", h.s, launch_dec_sig_pt(dsig, (uint32_t)np, pts, mst0, h.s, hit));
     if (ta_tail(d, w, pts, nullptr, mst0, didx, dgoff, ng, np, mode, (uint8_t*)dout, (uint8_t*)dst, nullptr, h.s))
       return -1;
     if (ws_release(w, h.s)) return -1;
@@ -2170,6 +2279,19 @@ int hbls_pubkey_cache_add(const uint8_t* pks, size_t n) {
   return 0;
 }
 
+size_t hbls_sig_cache(size_t entries) {
+  if (ensure_init()) return 0;
+  while (entries & (entries - 1)) entries &= entries - 1;
+  entries = std::min<size_t>(entries, size_t(1) << 30);
+  const size_t old = g_sc_cap.exchange(entries);
+  for (Dev* d : devs()) {  // drop the contents: the next put allocates at the new capacity
+    std::lock_guard<std::mutex> lk(d->mu);
+    d->sc_filled = 0;
+    d->sc_cap = 0;
+  }
+  return old;
+}
+
 int hbls_pubkey_cache_clear(void) {
   std::lock_guard<std::mutex> al(g_kc_add_mu);
   std::lock_guard<std::mutex> lk(g_kc_mu);
@@ -2290,7 +2412,8 @@ int hbls_slot_device(const hbls_slot* a, void* stream) {
   // messages: hash + Miller lines (side 2)
   hipStream_t sh = w.side[2];
   HCHK(hipStreamWaitEvent(sh, w.ev_fork, 0));
-  if (hash_messages(*d, a->msgs, a->msg_off, a->msg_len, a->n_msgs, (MsgEntry*)a->hm, sh)) return -1;
+  const bool defer = defer_lines(a->n_vgroups, a->n_msgs);
+  if (hash_messages(*d, a->msgs, a->msg_off, a->msg_len, a->n_msgs, (MsgEntry*)a->hm, sh, !defer)) return -1;
   HCHK(hipEventRecord(w.ev_side[2], sh));
   TaFold fold{};
   fold.ta_sigs = a->ta_sigs;
@@ -2311,7 +2434,7 @@ int hbls_slot_device(const hbls_slot* a, void* stream) {
   fold.dv_pk_table = (const G1AEntry*)a->dv_pk_table;
   fold.dv_pk_table_st = a->dv_pk_table_st;
   if (verify_pipeline(*d, w, a->pks, a->sigs, a->msg_idx, (const MsgEntry*)a->hm, a->n, a->vgrp_off, a->n_vgroups,
-                      a->vstatus, s, w.ev_side[2], &fold))
+                      a->vstatus, s, w.ev_side[2], &fold, nullptr, nullptr, defer ? a->n_msgs : 0))
     return -1;
   HCHK(hipStreamWaitEvent(s, w.ev_side[2], 0));
   return ws_release(w, s);

@@ -134,7 +134,7 @@ void launch_hash_to_g2(const uint8_t* msgs, const uint64_t* off, const uint32_t*
 // the staged form (hashsplit.hip): uses hm[i].lines[0..3] as hand-over space (k_lines_msg overwrites it)
 void launch_hash_to_g2_split(const uint8_t* msgs, const uint64_t* off, const uint32_t* len, uint32_t n, MsgEntry* hm,
                              hipStream_t s);
-void launch_lines_msg(MsgEntry* hm, uint32_t n, hipStream_t s);
+void launch_lines_msg(MsgEntry* hm, uint32_t n, hipStream_t s, const uint8_t* guard = nullptr);
 
 // k_pair3 arguments.  Unit u of a launch pairs (P, H(m)) and (-g1, S) where S's lines evaluated at
 // -g1 are sig_lines[j * stride + u].  Direct mode (list == nullptr): unit u is entry u of pk /
@@ -188,6 +188,9 @@ void launch_pair3_prod(const Pair3Args& a, hipStream_t s);
 // msg_idx, hm, f_n of the same arguments), line j of pair i at sig_lines[j f_n + i]
 void launch_pair3_mml(const Pair3Args& a, hipStream_t s);
 void launch_mml_eval(const Pair3Args& a, LineEntry* ev, hipStream_t s);
+// the same evaluated lines computed from H(m_g) directly (pipeline.hip k_lines_at_p; calls that
+// deferred the messages' unevaluated lines)
+void launch_lines_at_p(const Pair3Args& a, LineEntry* ev, hipStream_t s);
 // MLS: f_out[e] = the Miller loop of (-g1, S) alone from sig_lines (unit e at sig_lines[j stride + e]),
 // stored unexponentiated; the final exponentiation then runs with sig_lines == nullptr (FIN: no loop
 // of its own, the product of its f_range stored values, exponentiated)
@@ -219,7 +222,14 @@ constexpr uint32_t MML_PAIRS = 4;  // pairs per multi-Miller loop of the slot-wi
 // Batched verification (vbatch.hip).
 void launch_item_group(const uint32_t* grp_off, uint32_t n_groups, uint32_t n, uint32_t* item_grp, hipStream_t s);
 void launch_dec_pk(const uint8_t* pks, uint32_t n, G1AEntry* out, uint8_t* st, hipStream_t s);
-void launch_dec_sig_pt(const uint8_t* sigs, uint32_t n, HmEntry* out, uint8_t* st, hipStream_t s);
+void launch_dec_sig_pt(const uint8_t* sigs, uint32_t n, HmEntry* out, uint8_t* st, hipStream_t s,
+                       const uint8_t* skip = nullptr);
+void launch_sc_put(const uint8_t* sigs, const HmEntry* pts, const uint8_t* st, uint32_t n, uint32_t base, uint32_t cap,
+                   void* key, HmEntry* ent, uint8_t* est, uint32_t* tab, uint32_t tcap, uint64_t k0, uint64_t k1,
+                   hipStream_t s);
+void launch_sc_get(const uint8_t* sigs, uint32_t n, const void* key, const HmEntry* ent, const uint8_t* est,
+                   const uint32_t* tab, uint32_t tcap, uint64_t k0, uint64_t k1, HmEntry* out, uint8_t* st, uint8_t* hit,
+                   hipStream_t s);
 void launch_pk_gather(const uint8_t* pks, const uint32_t* idx, const G1AEntry* tab, const uint8_t* tst, uint32_t n,
                       G1AEntry* out, uint8_t* st, hipStream_t s);
 // Chunk plans and the multi-scalar random linear combination (vbatch.hip k_plan_*, k_rlc_msm).

@@ -116,12 +116,13 @@ HD LineCoeffs line28_store(const Line28& l) {
 // The Miller chain of an affine G2 point (lines.h line_chain in lazy limbs): 68 lines, line j
 // handed to put(j, LineCoeffs) (the stored-word line, pairing.h / layout.h LineEntry layout).
 // load() returns Q again at each of the five additions (not held across the chain).
-template <bool EVAL, class LoadQ, class Put>
-HD void line_chain28(const LoadQ& load, const Put& put) {
+// line_chain28_st: each lazy line handed to store() first (e.g. evaluated at a variable P).
+template <class LoadQ, class Store, class Put>
+HD void line_chain28_st(const LoadQ& load, const Store& store, const Put& put) {
   const G2A Q = load();
   G2P28 T = {f2l_from(Q.x), f2l_from(Q.y), f2l_one()};
   int j = 0;
-  auto emit = [&](const Line28& l) { put(j++, line28_store<EVAL>(l)); };
+  auto emit = [&](const Line28& l) { put(j++, store(l)); };
   HB_NOUNROLL for (int i = 62; i >= 0; i--) {
     l2_dbl_line(T, emit);
     if ((HB_X_ABS >> i) & 1) {
@@ -132,6 +133,10 @@ HD void line_chain28(const LoadQ& load, const Put& put) {
       l2_add_line(T, f2l_from(q2.x), f2l_from(q2.y), emit);
     }
   }
+}
+template <bool EVAL, class LoadQ, class Put>
+HD void line_chain28(const LoadQ& load, const Put& put) {
+  line_chain28_st(load, [](const Line28& l) { return line28_store<EVAL>(l); }, put);
 }
 
 // ---- Fp4 = Fp2[s]/(s^2 - xi) in lazy limbs: the lane values of pair3.h's three-lane Fp12

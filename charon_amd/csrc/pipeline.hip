@@ -21,11 +21,44 @@ constexpr int BLOCK = 64;
 #define HB_MML28 1
 #endif
 
-// One lane per distinct message: the unevaluated line chain of H(m).
-__global__ KB_OCC(HB_OCC_LINES) void k_lines_msg(MsgEntry* __restrict__ hm, uint32_t n) {
+// One lane per distinct message: the unevaluated line chain of H(m).  guard (nullable): only if
+// *guard != 0 (the lines of a call that deferred them, needed only behind a failed slot-wide check)
+__global__ KB_OCC(HB_OCC_LINES) void k_lines_msg(MsgEntry* __restrict__ hm, uint32_t n, const uint8_t* __restrict__ guard) {
+  if (guard && *guard == 0) return;
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   line_chain_ld<false>(&hm[i].h, hm[i].lines, 1);
+}
+
+// One lane per verification group of a call whose messages have one group each (distinct
+// per-validator messages, BASELINE configs[2]): the Miller chain of H(m_g) evaluated at the group's
+// P_g straight into the multi-Miller loops' layout ev[j * n + g] (k_mml_eval's output) -- no
+// unevaluated lines written and read back (k_lines_msg + k_mml_eval moved 68 x 288 B per message
+// through HBM three times), and lanes write consecutive entries.  A unit line (1, 0, 0) for groups
+// that are not READY (pk_st nonzero).  The lines are those of k_lines_msg (the same chain) times
+// (1, x_P, y_P), as k_mml_eval computes them.
+__global__ KB_OCC(HB_OCC_LINES) void k_lines_at_p(const G1AEntry* __restrict__ pk, const uint8_t* __restrict__ pk_st,
+                                                  const uint32_t* __restrict__ msg_idx, const MsgEntry* __restrict__ hm,
+                                                  uint32_t n, LineEntry* __restrict__ ev) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n) return;
+  LineEntry* out = ev + g;
+  if (pk_st && pk_st[g]) {
+    const LineEntry unit = {f2_one(), f2_zero(), f2_zero()};
+    for (int j = 0; j < N_LINES; j++) out[(size_t)j * n] = unit;
+    return;
+  }
+  const G1AEntry P = pk[g];
+  const L28 xp = l_from(P.x), yp = l_from(P.y);
+  const HmEntry* src = &hm[msg_idx[g]].h;
+  line_chain28_st([src]() { return hm_load(*src); },
+                  [&](const Line28& l) {
+                    return LineCoeffs{f2l_join(l.a0), {l_join(l_mul(l.a1.c0, xp)), l_join(l_mul(l.a1.c1, xp))},
+                                      {l_join(l_mul(l.b1.c0, yp)), l_join(l_mul(l.b1.c1, yp))}};
+                  },
+                  [&](int j, const LineCoeffs& c) { out[(size_t)j * n] = {c.a0, c.a1, c.b1}; });
+#endif
 }
 
 // THREE lanes per pairing (pair3.h): Miller loop over the streamed lines of (P, H(m)) and
@@ -419,8 +452,12 @@ void launch_lml_p(const LmlArgs& a, hipStream_t s) {
   if (a.n) hipLaunchKernelGGL(k_lml<1>, dim3(a.n), dim3(128), 0, s, a);
 }
 
-void launch_lines_msg(MsgEntry* hm, uint32_t n, hipStream_t s) {
-  if (n) hipLaunchKernelGGL(k_lines_msg, dim3(blocks_for(n)), dim3(BLOCK), 0, s, hm, n);
+void launch_lines_msg(MsgEntry* hm, uint32_t n, hipStream_t s, const uint8_t* guard) {
+  if (n) hipLaunchKernelGGL(k_lines_msg, dim3(blocks_for(n)), dim3(BLOCK), 0, s, hm, n, guard);
+}
+void launch_lines_at_p(const Pair3Args& a, LineEntry* ev, hipStream_t s) {
+  if (a.f_n)
+    hipLaunchKernelGGL(k_lines_at_p, dim3(blocks_for(a.f_n)), dim3(BLOCK), 0, s, a.pk, a.pk_st, a.msg_idx, a.hm, a.f_n, ev);
 }
 template <int MODE>
 static void pair3_launch(const Pair3Args& a, hipStream_t s) {

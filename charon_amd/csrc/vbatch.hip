@@ -42,9 +42,6 @@ __global__ KB void k_item_group(const uint32_t* __restrict__ grp_off, uint32_t n
   item_grp[i] = grp_off ? find_group_vb(grp_off, n_groups, i) : i;
 }
 
-#ifndef HB_DECPK_FUSED
-#define HB_DECPK_FUSED 0  // 1: the subgroup check inside k_dec_pk (A/B variant)
-#endif
 // One lane per partial: decompress + subgroup-check the public key (herumi.go:290
 // PublicKey.Deserialize).  A rejected key is replaced by g1 so later stages run the same
 // arithmetic on well-formed values; its status byte decides the verdict.
@@ -53,7 +50,7 @@ __global__ KB_OCC(HB_OCC_DECPK) void k_dec_pk(const uint8_t* __restrict__ pks, u
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   G1A p;
-  uint8_t bad = g1_decompress(p, pks + 48ull * i, HB_DECPK_FUSED != 0);
+  uint8_t bad = g1_decompress(p, pks + 48ull * i, false);  // the subgroup check: k_g1_subgroup
   if (bad) p = g1_generator();
   G1AEntry e;
   e.x = p.x;
@@ -66,19 +63,13 @@ __global__ KB_OCC(HB_OCC_DECPK) void k_dec_pk(const uint8_t* __restrict__ pks, u
 
 // The subgroup check of k_dec_pk's points, a kernel of its own like k_g2_subgroup (the fused
 // kernel spilled the square root's window table beside the ladder).  The ladders run in lazily
-// reduced 28-bit limbs (ec28.h; HB_G1_LAZY=0: the stored-word ec.h test, for A/B runs).
-#ifndef HB_G1_LAZY
-#define HB_G1_LAZY 1
-#endif
-#ifndef HB_G2_LAZY
-#define HB_G2_LAZY 1  // k_g2_subgroup likewise (ec28.h g2_in_subgroup28)
-#endif
+// reduced 28-bit limbs (ec28.h g1_in_subgroup28 / g2_in_subgroup28_l).
 __global__ KB_OCC(HB_OCC_SUBG) void k_g1_subgroup(uint32_t n, G1AEntry* __restrict__ pts, uint8_t* __restrict__ st) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const G1AEntry e = pts[i];
   if (st[i] || e.inf) return;
-  if (!(HB_G1_LAZY ? g1_in_subgroup28(G1A{e.x, e.y, false}) : g1_in_subgroup(G1A{e.x, e.y, false}))) {
+  if (!g1_in_subgroup28(G1A{e.x, e.y, false})) {
     const G1A g = g1_generator();
     G1AEntry z;
     z.x = g.x;
@@ -95,10 +86,11 @@ __global__ KB_OCC(HB_OCC_SUBG) void k_g1_subgroup(uint32_t n, G1AEntry* __restri
 // through index arrays, the ThresholdAggregate of the same partials.
 // Two kernels: the square root (k_dec_sig_pt) and the subgroup check (k_g2_subgroup), so that
 // neither holds the other's working set (one kernel spilled 4 KB per lane to scratch).
+// skip (nullable): items already filled from the decompressed-signature cache (k_sc_get)
 __global__ KB_OCC(HB_OCC_DECSIG) void k_dec_sig_pt(const uint8_t* __restrict__ sigs, uint32_t n, HmEntry* __restrict__ out,
-                                uint8_t* __restrict__ st) {
+                                uint8_t* __restrict__ st, const uint8_t* __restrict__ skip) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  if (i >= n || (skip && skip[i])) return;
   G2A q;
   uint8_t bad = g2_decompress(q, sigs + 96ull * i, false);
   if (bad) q = {f2_zero(), f2_zero(), true};
@@ -111,17 +103,14 @@ __global__ KB_OCC(HB_OCC_DECSIG) void k_dec_sig_pt(const uint8_t* __restrict__ s
   st[i] = bad;
 }
 
-__global__ KB_OCC(HB_OCC_SUBG) void k_g2_subgroup(uint32_t n, HmEntry* __restrict__ pts, uint8_t* __restrict__ st) {
+__global__ KB_OCC(HB_OCC_SUBG) void k_g2_subgroup(uint32_t n, HmEntry* __restrict__ pts, uint8_t* __restrict__ st,
+                                                   const uint8_t* __restrict__ skip) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  if (i >= n || (skip && skip[i])) return;
   const HmEntry e = pts[i];
   if (st[i] || e.inf) return;
-#if HB_G2_LAZY
   const HmEntry* src = pts + i;
   if (!g2_in_subgroup28_l([src]() { return G2A{src->x, src->y, false}; })) {
-#else
-  if (!g2_in_subgroup(G2A{e.x, e.y, false})) {
-#endif
     HmEntry z;
     z.x = f2_zero();
     z.y = f2_zero();
@@ -155,6 +144,85 @@ __global__ KB_OCC(HB_OCC_DECPK) void k_pk_gather(const uint8_t* __restrict__ pks
   e.pad[0] = e.pad[1] = e.pad[2] = 0;
   out[i] = e;
   st[i] = bad;
+}
+
+// ---- decompressed-signature cache (host-buffer calls: hbls_verify_batch fills it,
+// hbls_threshold_aggregate_batch reads it -- charon's parsigex Verify -> parsigdb -> sigagg flow,
+// where the aggregation's partials are exactly partials verified before).  A ring of `cap`
+// entries (the compressed bytes, the decompressed point, its status) and an open-addressing index
+// of 2 cap slots (entry + 1, 0 = empty) probed linearly from a keyed hash of the bytes, at most
+// SC_PROBES slots.  Slots are never emptied: a slot whose entry was overwritten by the ring or no
+// longer hashes within SC_PROBES of it is stale and may be taken.  A lookup compares all 96 bytes,
+// so a stale or raced slot can only cause a miss (the partial is then decompressed), never a wrong
+// point.  Puts and gets are ordered on the device by the host (one event per device).
+constexpr uint32_t SC_PROBES = 16;
+__device__ __forceinline__ uint32_t sc_hash(const uint4* k, uint64_t k0, uint64_t k1) {
+  uint64_t h = k0;
+  HB_UNROLL for (int j = 0; j < 6; j++) {
+    const uint64_t v = ((uint64_t)k[j].y << 32 | k[j].x) ^ ((uint64_t)k[j].w << 32 | k[j].z) * 0x9e3779b97f4a7c15ull;
+    h = (h ^ v) * 0xff51afd7ed558ccdull + k1;
+    h ^= h >> 29;
+  }
+  h *= 0xc4ceb9fe1a85ec53ull;
+  return (uint32_t)(h >> 32);
+}
+__device__ __forceinline__ bool sc_eq(const uint4* a, const uint4* b) {
+  bool eq = true;
+  HB_UNROLL for (int j = 0; j < 6; j++) eq = eq && a[j].x == b[j].x && a[j].y == b[j].y && a[j].z == b[j].z && a[j].w == b[j].w;
+  return eq;
+}
+// entries (base + i) & (cap - 1) take item i: bytes, point, status; then the index
+__global__ __launch_bounds__(64) void k_sc_put(const uint8_t* __restrict__ sigs, const HmEntry* __restrict__ pts,
+                                               const uint8_t* __restrict__ st, uint32_t n, uint32_t base, uint32_t cap,
+                                               uint4* __restrict__ key, HmEntry* __restrict__ ent,
+                                               uint8_t* __restrict__ est, uint32_t* __restrict__ tab, uint32_t tcap,
+                                               uint64_t k0, uint64_t k1) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t e = (base + i) & (cap - 1);
+  uint4 kb[6];
+  HB_UNROLL for (int j = 0; j < 6; j++) kb[j] = ((const uint4*)(sigs + 96ull * i))[j];
+  HB_UNROLL for (int j = 0; j < 6; j++) key[6ull * e + j] = kb[j];
+  ent[e] = pts[i];
+  est[e] = st[i];
+  const uint32_t home = sc_hash(kb, k0, k1) & (tcap - 1);
+  for (uint32_t q = 0; q < SC_PROBES; q++) {
+    const uint32_t slot = (home + q) & (tcap - 1);
+    const uint32_t old = atomicCAS(&tab[slot], 0u, e + 1);
+    if (old == 0) return;
+    const uint32_t o = old - 1;
+    bool dead = ((o - base) & (cap - 1)) < n;  // rewritten by this put (possibly by this very item)
+    if (!dead) {
+      const uint4* ko = key + 6ull * o;
+      if (sc_eq(ko, kb)) dead = true;  // the same bytes put before: the newer entry wins
+      else dead = ((slot - (sc_hash(ko, k0, k1) & (tcap - 1))) & (tcap - 1)) >= SC_PROBES;  // unreachable
+    }
+    if (dead && atomicCAS(&tab[slot], old, e + 1) == old) return;
+  }
+}
+// one lane per signature: the cached point and status when its bytes are cached (hit = 1)
+__global__ __launch_bounds__(64) void k_sc_get(const uint8_t* __restrict__ sigs, uint32_t n,
+                                               const uint4* __restrict__ key, const HmEntry* __restrict__ ent,
+                                               const uint8_t* __restrict__ est, const uint32_t* __restrict__ tab,
+                                               uint32_t tcap, uint64_t k0, uint64_t k1, HmEntry* __restrict__ out,
+                                               uint8_t* __restrict__ st, uint8_t* __restrict__ hit) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint4 kb[6];
+  HB_UNROLL for (int j = 0; j < 6; j++) kb[j] = ((const uint4*)(sigs + 96ull * i))[j];
+  const uint32_t home = sc_hash(kb, k0, k1) & (tcap - 1);
+  uint8_t h = 0;
+  for (uint32_t q = 0; q < SC_PROBES; q++) {
+    const uint32_t v = tab[(home + q) & (tcap - 1)];
+    if (v == 0) break;
+    if (sc_eq(key + 6ull * (v - 1), kb)) {
+      out[i] = ent[v - 1];
+      st[i] = est[v - 1];
+      h = 1;
+      break;
+    }
+  }
+  hit[i] = h;
 }
 
 // the random coefficient r = a + b lambda of entry `item` (SHA-256 of key || item, one block)
@@ -456,19 +524,13 @@ __device__ __forceinline__ void rlc_tab_g2(const RlcMsmArgs& a, uint32_t first, 
 // the chunk's sums (ec28.h ladders; coefficients from the workspace) at its first item, infinity
 // at the others, so k_group_prep sums the items as before
 __device__ __forceinline__ void rlc_lad_g1(const RlcMsmArgs& a, uint32_t first, uint32_t cnt) {
-  const G1J rp = a.sparse ? (HB_G1_LAZY ? g1l_msm_ladder_sparse(a.t1, a.coef4, first, cnt)
-                                        : msm_ladder_sparse<Fp>(a.t1, a.coef4, first, cnt))
-                          : (HB_G1_LAZY ? g1l_msm_ladder(a.t1, a.coef, first, cnt)
-                                        : msm_ladder<Fp, true>(a.t1, a.coef, first, cnt));
+  const G1J rp = a.sparse ? g1l_msm_ladder_sparse(a.t1, a.coef4, first, cnt) : g1l_msm_ladder(a.t1, a.coef, first, cnt);
   a.pout[first] = {rp.X, rp.Y, rp.Z};
   const G1J zi = jac_infinity<Fp>();
   for (uint32_t k = 1; k < cnt; k++) a.pout[first + k] = {zi.X, zi.Y, zi.Z};
 }
 __device__ __forceinline__ void rlc_lad_g2(const RlcMsmArgs& a, uint32_t first, uint32_t cnt) {
-  const G2J rs = a.sparse ? (HB_G2_LAZY ? g2l_msm_ladder_sparse(a.t2, a.coef4, first, cnt)
-                                        : msm_ladder_sparse<Fp2>(a.t2, a.coef4, first, cnt))
-                          : (HB_G2_LAZY ? g2l_msm_ladder(a.t2, a.coef, first, cnt)
-                                        : msm_ladder<Fp2, true>(a.t2, a.coef, first, cnt));
+  const G2J rs = a.sparse ? g2l_msm_ladder_sparse(a.t2, a.coef4, first, cnt) : g2l_msm_ladder(a.t2, a.coef, first, cnt);
   a.sout[first] = {rs.X, rs.Y, rs.Z};
   const G2J zs = jac_infinity<Fp2>();
   for (uint32_t k = 1; k < cnt; k++) a.sout[first + k] = {zs.X, zs.Y, zs.Z};
@@ -584,16 +646,30 @@ void launch_item_group(const uint32_t* grp_off, uint32_t n_groups, uint32_t n, u
 void launch_dec_pk(const uint8_t* pks, uint32_t n, G1AEntry* out, uint8_t* st, hipStream_t s) {
   if (!n) return;
   hipLaunchKernelGGL(k_dec_pk, dim3(blocks_for(n)), dim3(BLOCK), 0, s, pks, n, out, st);
-  if (!HB_DECPK_FUSED) hipLaunchKernelGGL(k_g1_subgroup, dim3(blocks_for(n)), dim3(BLOCK), 0, s, n, out, st);
+  hipLaunchKernelGGL(k_g1_subgroup, dim3(blocks_for(n)), dim3(BLOCK), 0, s, n, out, st);
 }
 void launch_pk_gather(const uint8_t* pks, const uint32_t* idx, const G1AEntry* tab, const uint8_t* tst, uint32_t n,
                       G1AEntry* out, uint8_t* st, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_pk_gather, dim3(blocks_for(n)), dim3(BLOCK), 0, s, pks, idx, tab, tst, n, out, st);
 }
-void launch_dec_sig_pt(const uint8_t* sigs, uint32_t n, HmEntry* out, uint8_t* st, hipStream_t s) {
+void launch_dec_sig_pt(const uint8_t* sigs, uint32_t n, HmEntry* out, uint8_t* st, hipStream_t s, const uint8_t* skip) {
   if (!n) return;
-  hipLaunchKernelGGL(k_dec_sig_pt, dim3(blocks_for(n)), dim3(BLOCK), 0, s, sigs, n, out, st);
-  hipLaunchKernelGGL(k_g2_subgroup, dim3(blocks_for(n)), dim3(BLOCK), 0, s, n, out, st);
+  hipLaunchKernelGGL(k_dec_sig_pt, dim3(blocks_for(n)), dim3(BLOCK), 0, s, sigs, n, out, st, skip);
+  hipLaunchKernelGGL(k_g2_subgroup, dim3(blocks_for(n)), dim3(BLOCK), 0, s, n, out, st, skip);
+}
+void launch_sc_put(const uint8_t* sigs, const HmEntry* pts, const uint8_t* st, uint32_t n, uint32_t base, uint32_t cap,
+                   void* key, HmEntry* ent, uint8_t* est, uint32_t* tab, uint32_t tcap, uint64_t k0, uint64_t k1,
+                   hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_sc_put, dim3(blocks_for(n)), dim3(BLOCK), 0, s, sigs, pts, st, n, base, cap, (uint4*)key, ent, est,
+                     tab, tcap, k0, k1);
+}
+void launch_sc_get(const uint8_t* sigs, uint32_t n, const void* key, const HmEntry* ent, const uint8_t* est,
+                   const uint32_t* tab, uint32_t tcap, uint64_t k0, uint64_t k1, HmEntry* out, uint8_t* st, uint8_t* hit,
+                   hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_sc_get, dim3(blocks_for(n)), dim3(BLOCK), 0, s, sigs, n, (const uint4*)key, ent, est, tab, tcap,
+                     k0, k1, out, st, hit);
 }
 void launch_rlc(const G1AEntry* pk, const uint8_t* pk_st, const HmEntry* sig, const uint8_t* sig_st,
                 const uint32_t* item_grp, const uint32_t* grp_off, int always, uint32_t n, uint32_t key_base,

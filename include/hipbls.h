@@ -112,6 +112,15 @@ int hbls_signing_roots(const uint8_t* object_roots, size_t n, const uint8_t* dom
 int hbls_pubkey_cache_add(const uint8_t* pks, size_t n);
 int hbls_pubkey_cache_clear(void);
 size_t hbls_pubkey_cache_size(void);
+/* Decompressed-signature cache (new, no herumi counterpart): hbls_verify_batch keeps the
+ * decompressed, subgroup-checked points of the partials it verified (a ring of `entries` per
+ * device, keyed by all 96 bytes), and hbls_threshold_aggregate_batch takes its members from it
+ * instead of decompressing them again -- charon aggregates exactly the partials parsigex verified
+ * (core/parsigdb/memory.go:197-225 -> core/sigagg/sigagg.go:105).  Results are identical with or
+ * without it.  Sets the capacity (rounded down to a power of two; 0 = off; default 2^21, or
+ * HBLS_SIG_CACHE), drops the contents and returns the previous capacity.  Call while no host-buffer
+ * call is in flight. */
+size_t hbls_sig_cache(size_t entries);
 
 /* Test switch of the in-process multi-device split (charon is one process over every GPU of the
  * node, app/app.go:131): every device of the mask is driven through `copies` contexts (own streams,

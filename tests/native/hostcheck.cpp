@@ -946,3 +946,35 @@ extern "C" int hc_coalesce_stress(int threads, int reqs, int inflight, int windo
   out[4] = c.max_active;
   return 0;
 }
+
+// pipeline.hip k_lines_at_p's line (the lazy chain evaluated at a variable P inside the chain)
+// against k_lines_msg + k_mml_eval (the unevaluated lazy chain, then a1 x_P, b1 y_P by stored-word
+// products): q192 = Q (x0 x1 y0 y1), p96 = P (x y), canonical big-endian.  out: 68 x 288 B each,
+// canonical; returns 1 if a line at P is not below 2p (the multi-Miller loop's input bound).
+extern "C" int hc_lines_at_p(const uint8_t* q192, const uint8_t* p96, uint8_t* out_at_p, uint8_t* out_eval) {
+  const G2A Q = {{hc_fp_in(q192), hc_fp_in(q192 + 48)}, {hc_fp_in(q192 + 96), hc_fp_in(q192 + 144)}, false};
+  const Fp px = hc_fp_in(p96), py = hc_fp_in(p96 + 48);
+  const L28 xp = l_from(px), yp = l_from(py);
+  LineCoeffs la[N_LINES], lu[N_LINES];
+  line_chain28_st([&]() { return Q; },
+                  [&](const Line28& l) {
+                    return LineCoeffs{f2l_join(l.a0), {l_join(l_mul(l.a1.c0, xp)), l_join(l_mul(l.a1.c1, xp))},
+                                      {l_join(l_mul(l.b1.c0, yp)), l_join(l_mul(l.b1.c1, yp))}};
+                  },
+                  [&](int j, const LineCoeffs& c) { la[j] = c; });
+  line_chain28<false>([&]() { return Q; }, [&](int j, const LineCoeffs& c) { lu[j] = c; });
+  int bad = 0;
+  for (int j = 0; j < N_LINES; j++) {
+    const Fp2 e1 = f2_mul_fp(lu[j].a1, px), e2 = f2_mul_fp(lu[j].b1, py);
+    hc_f2_out(out_eval + 288 * j, lu[j].a0);
+    hc_f2_out(out_eval + 288 * j + 96, e1);
+    hc_f2_out(out_eval + 288 * j + 192, e2);
+    const Fp* v[6] = {&la[j].a0.c0, &la[j].a0.c1, &la[j].a1.c0, &la[j].a1.c1, &la[j].b1.c0, &la[j].b1.c1};
+    for (int k = 0; k < 6; k++) {
+      Fp d;
+      if (raw_sub_const(d, *v[k], P2_RAW) == 0) bad = 1;
+      hc_fp_out(out_at_p + 288 * j + 48 * k, *v[k]);
+    }
+  }
+  return bad;
+}

@@ -427,6 +427,26 @@ def test_line_chain28_matches(lib):
             assert cnt[0] == cnt[1] == 1571 + (68 * 4 if ev else 0)
 
 
+def test_lines_at_p_equal_evaluated_lines(lib):
+    """pipeline.hip k_lines_at_p (the chain of H(m) evaluated at the group's P inside the chain, the
+    distinct-message slots' path) gives exactly k_lines_msg + k_mml_eval's evaluated lines, every
+    value below 2p, for G2 points and P on and off the generator's multiples (P = g1, random
+    multiples, x = 0 edge coordinates)"""
+    lib.hc_lines_at_p.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p]
+    rng = random.Random(2842)
+    qs = [B.G2_GEN, B.g2_mul(B.G2_GEN, rng.randrange(1, B.R)), _random_twist_point(rng)]
+    ps = [B.G1_GEN, B.g1_mul(B.G1_GEN, rng.randrange(1, B.R)), B.g1_mul(B.G1_GEN, B.R - 1)]
+    for q in qs:
+        (x0, x1), (y0, y1) = q
+        qraw = b"".join(v.to_bytes(48, "big") for v in (x0, x1, y0, y1))
+        for p in ps:
+            praw = p[0].to_bytes(48, "big") + p[1].to_bytes(48, "big")
+            a = ctypes.create_string_buffer(68 * 288)
+            b = ctypes.create_string_buffer(68 * 288)
+            assert lib.hc_lines_at_p(qraw, praw, a, b) == 0, "a line at P at or above 2p"
+            assert a.raw == b.raw
+
+
 def _rand_f12(rng):
     return b"".join(rng.randrange(B.P).to_bytes(48, "big") for _ in range(12))
 
