@@ -130,6 +130,150 @@ HD L28 l_sqr(const L28& a) {
 }
 #endif
 
+// ---- Two independent products in one leaf (HB_LEAF_ILP): the two column chains interleaved, each
+// seeded with its own carry.  A lone chain makes the compiler start every column's multiply-adds
+// at zero and add the shifted carry afterwards (one v_lshl_add_u64 per column, 26 per product) to
+// keep dependent multiply-adds apart; with two chains the other chain's multiply-add sits between
+// them.  The register barrier after each multiply-add (HB_MADD) keeps the compiler from
+// reassociating the chain again.  Same values as two l_mul / l_sqr.
+#ifndef HB_LEAF_ILP
+#define HB_LEAF_ILP 0
+#endif
+#if defined(__HIP_DEVICE_COMPILE__)
+#define HB_MADD(acc, x, y)                \
+  do {                                    \
+    acc += (uint64_t)(x) * (y);           \
+    __asm__("" : "+v"(acc));              \
+  } while (0)
+#else
+#define HB_MADD(acc, x, y) acc += (uint64_t)(x) * (y)
+#endif
+// r0 = a0 b0 / R, r1 = a1 b1 / R (SQ: a0 = b0, a1 = b1, the squares' halved cross products)
+template <bool SQ>
+HD void mul28x2_core(uint32_t* r0, uint32_t* r1, const uint32_t* a0, const uint32_t* b0, const uint32_t* a1,
+                     const uint32_t* b1) {
+  uint32_t m0[14], m1[14], d0[14], d1[14];
+  if (SQ)
+    HB_UNROLL for (int j = 0; j < 14; j++) {
+      d0[j] = a0[j] << 1;
+      d1[j] = a1[j] << 1;
+    }
+  uint64_t c0 = 0, c1 = 0;
+  HB_UNROLL for (int k = 0; k < 27; k++) {
+    const int lo = k < 14 ? 0 : k - 13, hi = k < 14 ? k : 13;
+    HB_UNROLL for (int j = lo; j <= hi; j++) {
+      if (SQ) {
+        if (2 * j < k) {
+          HB_MADD(c0, d0[j], a0[k - j]);
+          HB_MADD(c1, d1[j], a1[k - j]);
+        } else if (2 * j == k) {
+          HB_MADD(c0, a0[j], a0[j]);
+          HB_MADD(c1, a1[j], a1[j]);
+        }
+      } else {
+        HB_MADD(c0, a0[j], b0[k - j]);
+        HB_MADD(c1, a1[j], b1[k - j]);
+      }
+    }
+    HB_UNROLL for (int j = lo; j <= hi; j++)
+      if (j < k || k >= 14) {
+        HB_MADD(c0, m0[j], P28[k - j]);
+        HB_MADD(c1, m1[j], P28[k - j]);
+      }
+    if (k < 14) {
+      m0[k] = ((uint32_t)c0 * HB_P_N0_28) & 0x0FFFFFFFu;
+      m1[k] = ((uint32_t)c1 * HB_P_N0_28) & 0x0FFFFFFFu;
+      HB_MADD(c0, m0[k], P28[0]);
+      HB_MADD(c1, m1[k], P28[0]);
+    } else {
+      r0[k - 14] = (uint32_t)c0 & 0x0FFFFFFFu;
+      r1[k - 14] = (uint32_t)c1 & 0x0FFFFFFFu;
+    }
+    c0 >>= 28;
+    c1 >>= 28;
+  }
+  r0[13] = (uint32_t)c0;
+  r1[13] = (uint32_t)c1;
+}
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef uint32_t u32x32 __attribute__((ext_vector_type(32)));
+// first operands in the argument VGPRs (a0: limbs 0..13, a1: 16..29), second operands through the
+// per-lane LDS slot of fp.h (pairs (b0_k, b1_k)), as f2l_mul_leaf
+__device__ __noinline__ static u32x32 l_mul2_leaf(u32x32 a) {
+  uint32_t x0[14], x1[14], y0[14], y1[14], r0[14], r1[14];
+  const uint32_t lane = threadIdx.x & (HB_ARG_LANES - 1u);
+  HB_UNROLL for (int k = 0; k < 14; k++) {
+    const uint2 v = hb_fp2_arg[k * HB_ARG_LANES + lane];
+    y0[k] = v.x;
+    y1[k] = v.y;
+    x0[k] = a[k];
+    x1[k] = a[16 + k];
+  }
+  mul28x2_core<false>(r0, r1, x0, y0, x1, y1);
+  u32x32 o;
+  HB_UNROLL for (int k = 0; k < 14; k++) {
+    o[k] = r0[k];
+    o[16 + k] = r1[k];
+  }
+  return o;
+}
+__device__ __noinline__ static u32x32 l_sqr2_leaf(u32x32 a) {
+  uint32_t x0[14], x1[14], r0[14], r1[14];
+  HB_UNROLL for (int k = 0; k < 14; k++) {
+    x0[k] = a[k];
+    x1[k] = a[16 + k];
+  }
+  mul28x2_core<true>(r0, r1, x0, x0, x1, x1);
+  u32x32 o;
+  HB_UNROLL for (int k = 0; k < 14; k++) {
+    o[k] = r0[k];
+    o[16 + k] = r1[k];
+  }
+  return o;
+}
+#endif
+// (a b, c d) and (a^2, c^2): one dual-chain leaf with HB_LEAF_ILP, else two single products
+HD void l_mul2(const L28& a, const L28& b, const L28& c, const L28& d, L28& r0, L28& r1) {
+#if defined(__HIP_DEVICE_COMPILE__) && HB_LEAF_ILP
+  HB_COUNT_FP_MUL();
+  HB_COUNT_FP_MUL();
+  u32x32 av;
+  const uint32_t lane = threadIdx.x & (HB_ARG_LANES - 1u);
+  HB_UNROLL for (int k = 0; k < 14; k++) {
+    av[k] = a.l[k];
+    av[16 + k] = c.l[k];
+    hb_fp2_arg[k * HB_ARG_LANES + lane] = make_uint2(b.l[k], d.l[k]);
+  }
+  const u32x32 o = l_mul2_leaf(av);
+  HB_UNROLL for (int k = 0; k < 14; k++) {
+    r0.l[k] = o[k];
+    r1.l[k] = o[16 + k];
+  }
+#else
+  r0 = l_mul(a, b);
+  r1 = l_mul(c, d);
+#endif
+}
+HD void l_sqr2(const L28& a, const L28& c, L28& r0, L28& r1) {
+#if defined(__HIP_DEVICE_COMPILE__) && HB_LEAF_ILP
+  HB_COUNT_FP_MUL();
+  HB_COUNT_FP_MUL();
+  u32x32 av;
+  HB_UNROLL for (int k = 0; k < 14; k++) {
+    av[k] = a.l[k];
+    av[16 + k] = c.l[k];
+  }
+  const u32x32 o = l_sqr2_leaf(av);
+  HB_UNROLL for (int k = 0; k < 14; k++) {
+    r0.l[k] = o[k];
+    r1.l[k] = o[16 + k];
+  }
+#else
+  r0 = l_sqr(a);
+  r1 = l_sqr(c);
+#endif
+}
+
 // a == 0 mod p for a NORMALISED value a < 2^392 without a product: a is k p only for
 // k = rint(a / p), read off the top 56 bits (the low 336 bits of p move the ratio by < 2^-38 for
 // the k < 2^20 of any lazy value), then one pass compares a with k p limb by limb
@@ -180,16 +324,18 @@ struct G1L {
 
 // dbl-2009-l (lazy28.py dbl)
 HDNI G1L g1l_dbl(const G1L& p) {
-  const L28 A = l_sqr(p.X), B = l_sqr(p.Y), C = l_sqr(B);
-  const L28 T = l_sqr(l_add(p.X, B));
+  L28 A, B, C, T;
+  l_sqr2(p.X, p.Y, A, B);
+  l_sqr2(B, l_add(p.X, B), C, T);
   const L28 E = l_add(l_add(A, A), A);
   const L28 F = l_sqr(E);
   const L28 D = l_norm(l_shl(l_sub<3, 2>(T, l_add(A, C)), 1));
   G1L r;
   r.X = l_norm(l_sub<17, 2>(F, l_shl(D, 1)));
   const L28 W = l_sub<19, 1>(D, r.X);
-  r.Y = l_norm(l_sub<9, 8>(l_mul(E, W), l_shl(C, 3)));
-  r.Z = l_mul(l_shl(p.Y, 1), p.Z);
+  L28 EW;
+  l_mul2(E, W, l_shl(p.Y, 1), p.Z, EW, r.Z);
+  r.Y = l_norm(l_sub<9, 8>(EW, l_shl(C, 3)));
   r.inf = p.inf;
   return r;
 }
@@ -308,12 +454,44 @@ HD void f2l_mul_core(uint32_t* r0, uint32_t* r1, const uint32_t* a0, const uint3
                      const uint32_t* b1) {
   uint32_t na1[14];
   HB_UNROLL for (int j = 0; j < 14; j++) na1[j] = kF2N.l[j] - a1[j];
+#if HB_LEAF_ILP
+  // the two passes interleaved (HB_MADD: see mul28x2_core)
+  uint32_t m0[14], m1[14];
+  uint64_t c0 = 0, c1 = 0;
+  HB_UNROLL for (int k = 0; k < 27; k++) {
+    const int lo = k < 14 ? 0 : k - 13, hi = k < 14 ? k : 13;
+    HB_UNROLL for (int j = lo; j <= hi; j++) {
+      HB_MADD(c0, a0[j], b0[k - j]);
+      HB_MADD(c1, a0[j], b1[k - j]);
+      HB_MADD(c0, na1[j], b1[k - j]);
+      HB_MADD(c1, a1[j], b0[k - j]);
+    }
+    HB_UNROLL for (int j = lo; j <= hi; j++)
+      if (j < k || k >= 14) {
+        HB_MADD(c0, m0[j], P28[k - j]);
+        HB_MADD(c1, m1[j], P28[k - j]);
+      }
+    if (k < 14) {
+      m0[k] = ((uint32_t)c0 * HB_P_N0_28) & 0x0FFFFFFFu;
+      m1[k] = ((uint32_t)c1 * HB_P_N0_28) & 0x0FFFFFFFu;
+      HB_MADD(c0, m0[k], P28[0]);
+      HB_MADD(c1, m1[k], P28[0]);
+    } else {
+      r0[k - 14] = (uint32_t)c0 & 0x0FFFFFFFu;
+      r1[k - 14] = (uint32_t)c1 & 0x0FFFFFFFu;
+    }
+    c0 >>= 28;
+    c1 >>= 28;
+  }
+  r0[13] = (uint32_t)c0;
+  r1[13] = (uint32_t)c1;
+#else
   f2l_dot_core(r0, a0, na1, b0, b1);  // real = a0 b0 + (K - a1) b1
   f2l_dot_core(r1, a0, a1, b1, b0);   // imag = a0 b1 + a1 b0
+#endif
 }
 
 #if defined(__HIP_DEVICE_COMPILE__)
-typedef uint32_t u32x32 __attribute__((ext_vector_type(32)));
 // first operand in the 32 argument VGPRs (limbs 0..13 | 16..29), the second through the per-lane
 // LDS slot of fp.h (14 pairs (b0_k, b1_k), k-major: conflict-free 64-bit accesses)
 static_assert(HB_FP2_ARG_SLOTS >= 14, "hb_fp2_arg holds 14 pairs per lane");
@@ -373,12 +551,16 @@ HD F2L f2l_mul(const F2L& a, const F2L& b) {
 #endif
 // (a0 + a1)(a0 + K - a1) + 2 a0 a1 u, K = 36 p (lazy28.KSITE["2Q"]): two Fp products
 HD F2L f2l_sqr(const F2L& a) {
-  return {l_mul(l_add(a.c0, a.c1), l_sub<36, 1>(a.c0, a.c1)), l_mul(l_shl(a.c0, 1), a.c1)};
+  F2L r;
+  l_mul2(l_add(a.c0, a.c1), l_sub<36, 1>(a.c0, a.c1), l_shl(a.c0, 1), a.c1, r.c0, r.c1);
+  return r;
 }
 // f2l_sqr with the site's constant K = S p
 template <uint32_t S, uint32_t T>
 HD F2L f2l_sqr_k(const F2L& a) {
-  return {l_mul(l_add(a.c0, a.c1), l_sub<S, T>(a.c0, a.c1)), l_mul(l_shl(a.c0, 1), a.c1)};
+  F2L r;
+  l_mul2(l_add(a.c0, a.c1), l_sub<S, T>(a.c0, a.c1), l_shl(a.c0, 1), a.c1, r.c0, r.c1);
+  return r;
 }
 
 // Who computes a formula's Fp2 products.  F2One: this lane alone (f2l_mul / f2l_sqr_k).  F2Half

@@ -357,6 +357,7 @@ struct Hc {
   hipStream_t s = nullptr;
   DevBuf io[I_COUNT];
   bool busy = false;
+  hipEvent_t ev = nullptr;  // a chunked call's hand-overs between contexts (verify_chunks)
 };
 
 // one record per call that could take the slot-wide check: did it fail (or, skipped, did any batch
@@ -521,6 +522,7 @@ int dev_create(int ord, Dev** out) {
     HCHK(hipEventCreateWithFlags(&w.ev_msm, hipEventDisableTiming));
     HCHK(hipEventCreateWithFlags(&w.ev_h, hipEventDisableTiming));
     HCHK(hipStreamCreateWithPriority(&d->hc[k_ws].s, hipStreamNonBlocking, prio_lo));
+    HCHK(hipEventCreateWithFlags(&d->hc[k_ws].ev, hipEventDisableTiming));
   }
   HCHK(hipHostMalloc((void**)&d->res_host, N_RES * sizeof(SlotRes), hipHostMallocDefault));
   for (unsigned k = 0; k < N_RES; k++) HCHK(hipEventCreateWithFlags(&d->res_ev[k], hipEventDisableTiming));
@@ -645,6 +647,16 @@ void hc_release(Dev& d, Hc& h) {
   }
   d.hc_cv.notify_one();
 }
+// a free context or nullptr (never waits: a chunked call takes only what is idle)
+Hc* hc_try_acquire(Dev& d) {
+  std::lock_guard<std::mutex> lk(d.hc_mu);
+  for (int k = 0; k < g_ws_sets; k++)
+    if (!d.hc[k].busy) {
+      d.hc[k].busy = true;
+      return &d.hc[k];
+    }
+  return nullptr;
+}
 
 // per-call random linear combination key (OS CSPRNG)
 int rlc_key(RlcKey& k) {
@@ -762,15 +774,15 @@ int ta_tail(Dev& d, Ws& w, const HmEntry* pts, const uint32_t* src, const uint8_
   return 0;
 }
 
-// defer_msgs: the caller hashed its defer_msgs messages without their Miller lines (hm[].lines
-// unset; callers whose messages have about one verification group each, batched final
-// exponentiation sizes): the slot-wide check evaluates each group's chain at P directly
-// (k_lines_at_p) and the unevaluated lines are computed only behind a failed check; any other path
-// computes them first.
+// defer_hm / defer_msgs: the caller hashed the defer_msgs messages at defer_hm (the call's messages
+// or a contiguous range of them) without their Miller lines (callers whose messages have about one
+// verification group each, batched final exponentiation sizes): the slot-wide check evaluates each
+// group's chain at P directly (k_lines_at_p) and the unevaluated lines are computed only behind a
+// failed check; any other path computes them first.
 int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, const uint32_t* didx,
                     const MsgEntry* hm, size_t n, const uint32_t* dgoff, size_t n_groups, uint8_t* dst,
                     hipStream_t s, hipEvent_t hm_ready, const TaFold* fold, const uint32_t* kc_idx = nullptr,
-                    hipEvent_t h_ready = nullptr, size_t defer_msgs = 0) {
+                    hipEvent_t h_ready = nullptr, MsgEntry* defer_hm = nullptr, size_t defer_msgs = 0) {
   if (!dgoff) n_groups = n;
   G1AEntry* vpk;
   HmEntry* vsig;
@@ -994,7 +1006,7 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
   if (defer_msgs && !bfe) return set_err("verify: deferred Miller lines need the batched final exponentiation");
   const bool lines_at_p = defer_msgs && smsm && !skip_msm;
   if (defer_msgs && !lines_at_p)  // the per-batch check reads the unevaluated lines
-    TIMED(d, "k_lines_msg", s, launch_lines_msg(const_cast<MsgEntry*>(hm), (uint32_t)defer_msgs, s));
+    TIMED(d, "k_lines_msg", s, launch_lines_msg(defer_hm, (uint32_t)defer_msgs, s));
   Fp4Entry* f1 = nullptr;
   uint8_t* f1bad = nullptr;
   G2JEntry* f1S = nullptr;
@@ -1124,7 +1136,7 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
           TIMED(d, "k_slot_verdict", s, launch_slot_verdict(gst, sfail, ng, gver + g0, s));
           // deferred lines: the per-batch check behind a failed slot-wide check reads them
           if (lines_at_p)
-            TIMED(d, "k_lines_msg", s, launch_lines_msg(const_cast<MsgEntry*>(hm), (uint32_t)defer_msgs, s, sfail));
+            TIMED(d, "k_lines_msg", s, launch_lines_msg(defer_hm, (uint32_t)defer_msgs, s, sfail));
           // the slot-wide check failed: the per-batch check (signature sides per item and group;
           // computed in the first pass when the check was skipped)
           if (rlc_fallback_chunks) {
@@ -1666,6 +1678,120 @@ static double now_ms() {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// A large one-device Verify batch in chunks of whole groups, each on its own host-call context
+// (stream, staging buffers) and workspace set, so that -- like consecutive slots in flight -- one
+// chunk's decompression and hashing overlap the previous chunk's pairings and latency-bound tail
+// instead of the call running as one slot with nothing beside it.  The caller's keys, signatures
+// and messages are uploaded once (context h0); each chunk gathers its items in group order,
+// hashes its own contiguous range of the message table (items are sorted by message), verifies,
+// fills the signature cache and scatters its statuses into the call's status array, downloaded
+// once.  Extra contexts are taken only if idle (hc_try_acquire); with none the call is one chunk.
+constexpr size_t CHUNK_MIN_ITEMS = size_t(1) << 18;
+int verify_chunks(Dev& d, Hc& h0, std::unique_lock<std::mutex>& lk, const uint8_t* pks, const uint8_t* sigs,
+                  const MsgTable& all, const std::vector<uint32_t>& order32, const std::vector<size_t>& gstart,
+                  size_t n_groups, size_t n, uint8_t* status) {
+  lk.unlock();
+  std::vector<uint32_t> midx(n);
+  for (size_t k = 0; k < n; k++) midx[k] = all.idx[order32[k]];
+  std::vector<Hc*> hcs{&h0};
+  const size_t k_want = std::min<size_t>((size_t)g_ws_sets, std::max<size_t>(1, n / CHUNK_MIN_ITEMS));
+  while (hcs.size() < k_want) {
+    Hc* x = hc_try_acquire(d);
+    if (!x) break;
+    hcs.push_back(x);
+  }
+  struct RelExtra {
+    Dev& d;
+    std::vector<Hc*>& h;
+    ~RelExtra() {
+      for (size_t c = 1; c < h.size(); c++) hc_release(d, *h[c]);
+    }
+  } rel{d, hcs};
+  // chunk boundaries at group starts, about n / K items each
+  const size_t K = hcs.size();
+  std::vector<size_t> cg{0};
+  for (size_t c = 1; c < K; c++) {
+    const size_t target = n * c / K;
+    const size_t g = (size_t)(std::lower_bound(gstart.begin(), gstart.begin() + n_groups, target) - gstart.begin());
+    if (g > cg.back() && g < n_groups) cg.push_back(g);
+  }
+  cg.push_back(n_groups);
+  std::vector<std::vector<uint32_t>> goffs(cg.size() - 1);
+  for (size_t c = 0; c + 1 < cg.size(); c++) {
+    goffs[c].resize(cg[c + 1] - cg[c] + 1);
+    for (size_t g = cg[c]; g <= cg[c + 1]; g++) goffs[c][g - cg[c]] = (uint32_t)(gstart[g] - gstart[cg[c]]);
+  }
+  lk.lock();
+  std::vector<uint32_t> kc;
+  const bool use_kc = kc_lookup(pks, n, kc, order32.data());
+  // shared uploads on h0
+  uint8_t *rpk, *rsig;
+  uint32_t *dord, *dmidx, *dkc = nullptr;
+  uint8_t* dmsg;
+  uint64_t* doff;
+  uint32_t* dlen;
+  void *hmp, *stp;
+  if (upload(d, I_PK, pks, 48 * n, &rpk, &h0) || upload(d, I_SIG, sigs, 96 * n, &rsig, &h0) ||
+      upload(d, I_IDX, order32.data(), n, &dord, &h0) || upload(d, I_MIDX, midx.data(), n, &dmidx, &h0) ||
+      upload(d, I_MSG, all.bytes.data(), all.bytes.size(), &dmsg, &h0) ||
+      upload(d, I_OFF, all.off.data(), all.off.size(), &doff, &h0) ||
+      upload(d, I_LEN, all.len.data(), all.len.size(), &dlen, &h0) ||
+      ensure_buf(h0.io[I_HM], all.len.size() * sizeof(MsgEntry), &hmp) || ensure_buf(h0.io[I_HM2], n, &stp))
+    return -1;
+  if (use_kc && upload(d, I_KC, kc.data(), n, &dkc, &h0)) return -1;
+  MsgEntry* hm = (MsgEntry*)hmp;
+  uint8_t* dst_out = (uint8_t*)stp;
+  HCHK(hipEventRecord(h0.ev, h0.s));
+  for (size_t c = 0; c + 1 < cg.size(); c++) {
+    Hc& hc = *hcs[c];
+    hipStream_t sc = hc.s;
+    if (c) HCHK(hipStreamWaitEvent(sc, h0.ev, 0));
+    const size_t ib = gstart[cg[c]], m = gstart[cg[c + 1]] - ib, ng = cg[c + 1] - cg[c];
+    const size_t mfirst = midx[ib], mcount = midx[ib + m - 1] + 1 - mfirst;  // the chunk's messages
+    Ws& w = ws_acquire(d, sc);
+    // the chunk's items in group order
+    void *pio, *sio;
+    uint32_t* dgoff;
+    if (ensure_buf(hc.io[I_OUT], 144 * m, &pio) || ensure_buf(hc.io[I_STAT], m, &sio) ||
+        upload(d, I_VGOFF, goffs[c].data(), goffs[c].size(), &dgoff, &hc))
+      return -1;
+    uint8_t* dpk = (uint8_t*)pio;
+    uint8_t* dsig = dpk + 48 * m;
+    uint8_t* dst = (uint8_t*)sio;
+    LAUNCH(k_gather_items, m, sc, (const uint4*)rpk, (const uint4*)rsig, dord + ib, (uint32_t)m, (uint4*)dpk,
+           (uint4*)dsig);
+    // its messages hashed on the workspace's hashing stream (lines deferred when the groups have
+    // one message each)
+    const bool defer = defer_lines(ng, mcount);
+    HCHK(hipEventRecord(w.ev_ta, sc));
+    hipStream_t hs = w.side[2];
+    HCHK(hipStreamWaitEvent(hs, w.ev_ta, 0));
+    TIMED(d, "k_hash_to_g2", hs, launch_hash_to_g2(dmsg, doff + mfirst, dlen + mfirst, (uint32_t)mcount, hm + mfirst, hs));
+    HCHK(hipEventRecord(w.ev_h, hs));
+    if (!defer) TIMED(d, "k_lines_msg", hs, launch_lines_msg(hm + mfirst, (uint32_t)mcount, hs));
+    HCHK(hipEventRecord(w.ev_side[2], hs));
+    if (verify_pipeline(d, w, dpk, dsig, dmidx + ib, hm, m, dgoff, ng, dst, sc, w.ev_side[2], nullptr,
+                        dkc ? dkc + ib : nullptr, w.ev_h, hm + mfirst, defer ? mcount : 0))
+      return -1;
+    {
+      HmEntry* vsig;
+      uint8_t* vsigst;
+      if (wsbuf(w, W_VSIG, m, &vsig) || wsbuf(w, W_VSIGST, m, &vsigst) || sc_put(d, dsig, vsig, vsigst, m, sc))
+        return -1;
+    }
+    LAUNCH(k_scatter_status, m, sc, dst, dord + ib, (uint32_t)m, dst_out);
+    if (ws_release(w, sc)) return -1;
+    if (c) {
+      HCHK(hipEventRecord(hc.ev, sc));
+      HCHK(hipStreamWaitEvent(h0.s, hc.ev, 0));
+    }
+  }
+  lk.unlock();  // enqueued: other callers may enqueue while this one waits
+  HCHK(hipMemcpyAsync(status, dst_out, n, hipMemcpyDeviceToHost, h0.s));
+  HCHK(hipStreamSynchronize(h0.s));
+  return 0;
+}
+
 int verify_host(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msgs, const uint64_t* msg_off,
                 const uint32_t* msg_len, size_t n, uint8_t* status) {
   if (n == 0) return 0;
@@ -1698,11 +1824,13 @@ int verify_host(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msgs, co
   return for_each_device_hc(n_groups, [&](Dev& d, Hc& h, size_t gb, size_t ge, std::unique_lock<std::mutex>& lk) -> int {
     const size_t ib = gstart[gb], ie = gstart[ge], m = ie - ib;
     if (m == 0) return 0;
+    const bool whole = gb == 0 && ge == n_groups;
+    if (whole && n >= 2 * CHUNK_MIN_ITEMS && g_ws_sets > 1 && defer_lines(n_groups, all.len.size()))
+      return verify_chunks(d, h, lk, pks, sigs, all, order32, gstart, n_groups, n, status);
     // host preparation without the device lock (other callers enqueue meanwhile): the shard's
     // distinct messages and each item's message index in group order -- the whole call's table
     // when one device takes every group
     lk.unlock();
-    const bool whole = gb == 0 && ge == n_groups;
     MsgTable tl;
     std::vector<uint32_t> midx;
     if (whole) {
@@ -1764,7 +1892,7 @@ int verify_host(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msgs, co
     if (upload(d, I_MIDX, tidx.data(), m, &didx, &h) || upload(d, I_VGOFF, goff.data(), goff.size(), &dgoff, &h))
       return -1;
     if (use_kc && upload(d, I_KC, kc.data(), m, &dkc, &h)) return -1;
-    if (verify_pipeline(d, w, dpk, dsig, didx, hm, m, dgoff, ge - gb, dst, h.s, hm_ready, nullptr, dkc, h_ready,
+    if (verify_pipeline(d, w, dpk, dsig, didx, hm, m, dgoff, ge - gb, dst, h.s, hm_ready, nullptr, dkc, h_ready, hm,
                         defer ? t.len.size() : 0))
       return -1;
     {  // the decompressed partials into the signature cache (the aggregation of these partials reads them)
@@ -2434,7 +2562,7 @@ int hbls_slot_device(const hbls_slot* a, void* stream) {
   fold.dv_pk_table = (const G1AEntry*)a->dv_pk_table;
   fold.dv_pk_table_st = a->dv_pk_table_st;
   if (verify_pipeline(*d, w, a->pks, a->sigs, a->msg_idx, (const MsgEntry*)a->hm, a->n, a->vgrp_off, a->n_vgroups,
-                      a->vstatus, s, w.ev_side[2], &fold, nullptr, nullptr, defer ? a->n_msgs : 0))
+                      a->vstatus, s, w.ev_side[2], &fold, nullptr, nullptr, (MsgEntry*)a->hm, defer ? a->n_msgs : 0))
     return -1;
   HCHK(hipStreamWaitEvent(s, w.ev_side[2], 0));
   return ws_release(w, s);

@@ -260,6 +260,21 @@ def test_slot_c3_adversarial(L, monkeypatch):
         clean = d["exp_agg"] == OK
         assert np.array_equal(tout[clean], d["root_sigs"].reshape(V, 96)[clean])
     assert {int(x) for x in np.unique(d["exp_agg"])} == {OK, BAD_SIGNATURE, NOT_VERIFIED}
+    # the host-buffer entry points on the same slot: the 1 M-item Verify in chunks over the host-call
+    # contexts (hipbls.hip verify_chunks, deferred Miller lines), then ThresholdAggregate taking its
+    # members from the decompressed-signature cache -- every status exact, clean aggregates equal
+    hst = np.zeros(NP, dtype=np.uint8)
+    assert L.hbls_verify_batch(_p(d["pks"]), _p(d["sigs"]), _p(d["item_msgs"]), _p(d["item_off"]), _p(d["item_len"]),
+                               NP, _p(hst)) == 0, L.hbls_last_error()
+    bad = np.nonzero(hst != d["exp_v"])[0]
+    assert len(bad) == 0, [(int(i), int(hst[i]), int(d["exp_v"][i])) for i in bad[:10]]
+    hout = np.zeros(V * 96, dtype=np.uint8)
+    hts = np.zeros(V, dtype=np.uint8)
+    assert L.hbls_threshold_aggregate_batch(_p(d["ta_sigs"]), _p(d["ta_idx"]), _p(d["grp_off"]), V, _p(hout),
+                                            _p(hts)) == 0, L.hbls_last_error()
+    assert np.array_equal(hts, d["exp_ta"])
+    clean = d["exp_agg"] == OK  # every member valid: the aggregate is the root signature
+    assert np.array_equal(hout.reshape(V, 96)[clean], d["root_sigs"].reshape(V, 96)[clean])
     # oracle: two partials of every class (class k % 5 in sample order), 16 clean partials
     sample = [bad_items[k] for k in range(10)]
     cl = random.Random(304)
