@@ -525,6 +525,9 @@ def main(argv=None):
                     help="also time the slot with decompressed-key tables built once (steady state)")
     ap.add_argument("--host-api", type=int, default=1,
                     help="also time the host-buffer (PCIe-inclusive) entry points on the same inputs (0: skip)")
+    ap.add_argument("--bad-frac", type=float, default=None,
+                    help="fraction of the partials corrupted in equal fifths (bench.corrupt; default: the "
+                         "workload's, 0.01 for c5) -- the attack curve: c5 at 0.01 / 0.05 / 0.10")
     ap.add_argument("--host-runs", type=int, default=3,
                     help="timed runs of the host-buffer pair after one warm-up (the median is reported)")
     ap.add_argument("--host-threads", type=int, default=3,
@@ -557,8 +560,9 @@ def main(argv=None):
     wl = WORKLOADS[args.workload]
     V = args.validators or wl["validators"]
     d = setup_inputs(L, wl, V, rank)
-    if wl.get("adversarial"):
-        corrupt(L, d, wl["adversarial"], seed=7 + rank)
+    bad_frac = args.bad_frac if args.bad_frac is not None else wl.get("adversarial", 0.0)
+    if bad_frac:
+        corrupt(L, d, bad_frac, seed=7 + rank)
     n, t, NP, M = d["n"], d["t"], d["NP"], d["M"]
     dev = torch.device("cuda", local)
 
@@ -853,7 +857,7 @@ def main(argv=None):
                    "aggregated_share_indices": [int(x) + 1 for x in ta_share_positions(n, t)],
                    "distinct_messages": M, "partials_per_gpu": NP, "parallelism": f"validator-sharded x{world}",
                    "slots_in_flight": n_sets, "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
-                   **({"corrupted_partials_per_gpu": d["n_corrupted"]} if "exp_v" in d else {})},
+                   **({"corrupted_partials_per_gpu": d["n_corrupted"], "bad_frac": bad_frac} if "exp_v" in d else {})},
         "verify_per_s": round(world * NP / (elapsed / args.steps), 1),
         "threshold_aggregate_per_s": round(world * V / (elapsed / args.steps), 1),
         "aggregate_verify_per_s": None if staged else round(world * V / (elapsed / args.steps), 1),

@@ -511,10 +511,9 @@ int dev_create(int ord, Dev** out) {
     Ws& w = d->ws[k_ws];
     HCHK(hipEventCreateWithFlags(&w.free_ev, hipEventDisableTiming));
     for (int k = 0; k < N_SIDE; k++) {
-      // side 3 (the slot's ThresholdAggregate): high priority like the others (HBLS_TA_PRIO=0: the
-      // lowest; measured 134.2-134.9 vs 135.7-135.9 ms per C3 slot, three slots in flight)
-      const bool ta_hi = env_size("HBLS_TA_PRIO", 1) != 0;
-      HCHK(hipStreamCreateWithPriority(&w.side[k], hipStreamNonBlocking, (k == 3 && !ta_hi) ? prio_lo : prio_hi));
+      // side 3 (the slot's ThresholdAggregate) at high priority like the others (the lowest measured
+      // 135.7-135.9 against 134.2-134.9 ms per C3 slot, three slots in flight)
+      HCHK(hipStreamCreateWithPriority(&w.side[k], hipStreamNonBlocking, prio_hi));
       HCHK(hipEventCreateWithFlags(&w.ev_side[k], hipEventDisableTiming));
     }
     HCHK(hipEventCreateWithFlags(&w.ev_fork, hipEventDisableTiming));
@@ -1078,20 +1077,7 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
         TIMED(d, "k_msm_sum", sm, launch_msm_sum(ma, sm));
         // the signature side's Miller loop, beside the multi-Miller loops and their product tree:
         // the final exponentiation's second factor, pfin[1] (lines and loop in one kernel, k_lml)
-#if defined(HB_NO_LML)
-        TIMED(d, "k_slines", sm, launch_slines(ma.total, nullptr, nullptr, 1, blines, 1, bbad, sm));
-        {
-          Pair3Args ps{};
-          ps.sig_lines = blines;
-          ps.stride = 1;
-          ps.n = 1;
-          ps.f_out = pfin;
-          ps.f_out_off = 1;
-          TIMED(d, "k_pair3_mls", sm, launch_pair3_mls(ps, sm));
-        }
-#else
         TIMED(d, "k_pair3_mls", sm, launch_lml(ma.total, 1, pfin, 1, 1, bbad, sm));
-#endif
         }
         HCHK(hipEventRecord(w.ev_side[0], sm));
         // multi-Miller loops over mmlk groups (shared squarings), then a product tree of fan-in

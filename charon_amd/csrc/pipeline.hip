@@ -15,11 +15,6 @@ namespace hb {
 
 constexpr int BLOCK = 64;
 
-// HB_MML28 = 0: the stored-word multi-Miller loop (A/B runs); default: the lazy-limb arithmetic of
-// pair28.h
-#ifndef HB_MML28
-#define HB_MML28 1
-#endif
 
 // One lane per distinct message: the unevaluated line chain of H(m).  guard (nullable): only if
 // *guard != 0 (the lines of a call that deferred them, needed only behind a failed slot-wide check)
@@ -127,38 +122,25 @@ __global__ KB_OCC(HB_OCC_PAIR3) void k_pair3(Pair3Args a) {
     const uint32_t cnt = first < a.f_n ? min(a.f_range, a.f_n - first) : 0u;
     const LineEntry* ev = a.sig_lines;
     const size_t fn = a.f_n;
-#if HB_MML28
     // the accumulator in lazy limbs (pair28.h g4_sqr / g4_mul_line), reduced below 2p after every
     // step; the stored-word lines are split as they are read
     F4L f = g4_one(g);
-#else
-    Fp4 f = g_one(g);
-#endif
     int bit = 62;
     bool pending_add = false;
     LineEntry Ln = ev[first];
     HB_NOUNROLL for (int j = 0; j < N_LINES; j++) {
       const bool dbl = !pending_add;
-#if HB_MML28
       if (dbl && j > 0) f = g4_sqr(g, f);
-#else
-      if (dbl && j > 0) f = g_sqr(g, f);
-#endif
       HB_NOUNROLL for (uint32_t k = 0; k < a.f_range; k++) {
         const LineEntry L = Ln;
         // prefetch: the next pair of this line, else the first pair of the next line
         const uint32_t k1 = k + 1 < a.f_range ? k + 1 : 0u;
         const int j1 = k + 1 < a.f_range ? j : (j + 1 < N_LINES ? j + 1 : j);
         Ln = ev[(size_t)j1 * fn + (k1 < cnt ? first + k1 : first)];
-#if HB_MML28
         F2L l0, l1, l2;
         line_split(L, l0, l1, l2);
         const F4L t = g4_mul_line(g, f, l0, l1, l2);
         f = f4l_select(k < cnt, f, t);
-#else
-        const Fp4 t = g_mul_line(g, f, L.a0, L.a1, L.b1);
-        f4_select(f, k < cnt, f, t);
-#endif
       }
       if (dbl) {
         pending_add = ((HB_X_ABS >> bit) & 1) != 0;
@@ -167,11 +149,7 @@ __global__ KB_OCC(HB_OCC_PAIR3) void k_pair3(Pair3Args a) {
         pending_add = false;
       }
     }
-#if HB_MML28
     if (valid) a.f_out[3 * f_out_index(a, e) + g.k] = f4l_store(f);
-#else
-    if (valid) a.f_out[3 * f_out_index(a, e) + g.k] = Fp4Entry{f.x, f.y};
-#endif
     return;
   }
   if (MODE != P3_FIN && MODE != P3_MLS) {

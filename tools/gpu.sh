@@ -6,6 +6,7 @@
 #   pmc    TAG                      kernel trace + SQ / FETCH_SIZE / WRITE_SIZE passes over one C3 slot
 #   final  TAG                      tests, smoke, lines, trace of the default C3 line, pmc
 #   single TAG [calls]              kernel trace of single-item Verify calls (tools/diag_single.py)
+#   peak   TAG                      int_rates microbenchmark: plain, kernel trace, PMC pass (the peak)
 # Every GPU step has its own time limit and the steps are chained with &&: the first failure,
 # abort or time-out ends the script.
 set -o pipefail
@@ -50,6 +51,16 @@ pmc() {
    timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d "$P/fetch" -o run --output-format csv -- python3 "$B" $A > "$P.fetch.log" 2>&1 &&
    timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d "$P/write" -o run --output-format csv -- python3 "$B" $A > "$P.write.log" 2>&1)
 }
+peak() {  # the roofline peak pinned by counters (tools/microbench/int_rates_pmc.py)
+  local P="$O/peak_$TAG"
+  local X="$GRAFT_REPO_ROOT/tools/microbench/int_rates"
+  mkdir -p "$P"
+  timeout -k 10 120 "$X" > "$P/int_rates_plain.txt" 2>&1 &&
+  (cd /tmp && export TMPDIR=/tmp &&
+   timeout -k 10 120 rocprofv3 --kernel-trace -d "$P/trace" -o run --output-format csv -- "$X" > "$P/int_rates.txt" 2>&1 &&
+   timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d "$P/pmc" -o run \
+     --output-format csv -- "$X" > "$P/pmc.log" 2>&1)
+}
 single() {
   (cd /tmp && export TMPDIR=/tmp &&
    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/single_$TAG" -o run --output-format csv -- python3 \
@@ -79,5 +90,6 @@ case "$WHAT" in
   final) tests && smoke && lines && trace --steps 5 --warmup 2 --cpu-seconds 0 --callers 0 --aggregate-verify 0 --host-api 0 && pmc ;;
   ab) ab "$@" ;;
   single) single "$@" ;;
-  *) echo "usage: bash tools/gpu.sh tests|bench|lines|trace|pmc|final|ab|single TAG [args]" >&2; exit 2 ;;
+  peak) peak ;;
+  *) echo "usage: bash tools/gpu.sh tests|bench|lines|trace|pmc|final|ab|single|peak TAG [args]" >&2; exit 2 ;;
 esac
