@@ -2255,6 +2255,45 @@ int hbls_signing_roots(const uint8_t* object_roots, size_t n, const uint8_t* dom
   return roots_host(1, object_roots, n, domains, n_domains, dom_idx, roots);
 }
 
+int hbls_duty_signing_roots(int kind, const uint8_t* data, const uint64_t* off, const uint32_t* len, size_t n,
+                            const uint8_t* domains, size_t n_domains, const uint32_t* dom_idx, uint8_t* roots,
+                            uint8_t* status) {
+  if (ensure_init()) return -1;
+  if (n == 0) return 0;
+  if (kind < 1 || kind > 5) return set_err("duty signing roots: unknown kind");
+  if (n_domains == 0) return set_err("signing roots: no domain");
+  if (dom_idx)
+    for (size_t i = 0; i < n; i++)
+      if (dom_idx[i] >= n_domains) return set_err("signing roots: domain index out of range");
+  return for_each_device(n, [&](Dev& d, size_t b, size_t e) -> int {
+    const size_t m = e - b;
+    // the shard's objects packed: their bytes from the first object's offset on, offsets rebased
+    uint64_t lo = ~0ull, hi = 0;
+    for (size_t i = b; i < e; i++) {
+      lo = std::min(lo, off[i]);
+      hi = std::max(hi, off[i] + len[i]);
+    }
+    std::vector<uint64_t> roff(m);
+    for (size_t i = 0; i < m; i++) roff[i] = off[b + i] - lo;
+    uint8_t *dd, *ddom;
+    uint64_t* doff;
+    uint32_t *dlen, *didx = nullptr;
+    if (upload(d, I_SIG, data + lo, hi - lo, &dd) || upload(d, I_PK, domains, n_domains * 32, &ddom) ||
+        upload(d, I_OFF, roff.data(), m, &doff) || upload(d, I_LEN, len + b, m, &dlen))
+      return -1;
+    if (dom_idx && upload(d, I_MIDX, dom_idx + b, m, &didx)) return -1;
+    void *out, *st;
+    if (ensure_buf(d.io[I_OUT], m * 32, &out) || ensure_buf(d.io[I_STAT], m, &st)) return -1;
+    TIMED(d, "k_duty_roots", d.stream,
+          launch_duty_roots(kind, dd, doff, dlen, (uint32_t)m, ddom, (uint32_t)n_domains, didx, (uint8_t*)out,
+                            (uint8_t*)st, d.stream));
+    HCHK(hipMemcpyAsync(roots + 32 * b, out, m * 32, hipMemcpyDeviceToHost, d.stream));
+    HCHK(hipMemcpyAsync(status + b, st, m, hipMemcpyDeviceToHost, d.stream));
+    HCHK(hipStreamSynchronize(d.stream));
+    return 0;
+  });
+}
+
 int hbls_sign_batch(const uint8_t* sks, const uint8_t* msgs, const uint64_t* msg_off, const uint32_t* msg_len,
                     size_t n, uint8_t* sigs, uint8_t* status) {
   if (ensure_init()) return -1;

@@ -379,6 +379,9 @@ void launch_fb_lines(const uint32_t* list, const uint32_t* count, uint32_t base,
                      const HmEntry* agg_sig, uint32_t n_items, LineEntry* lines, hipStream_t s);
 
 // Signing roots (roots.hip): SSZ AttestationData -> GetDataRoot, and SigningData of object roots.
+void launch_duty_roots(int kind, const uint8_t* data, const uint64_t* off, const uint32_t* len, uint32_t n,
+                       const uint8_t* domains, uint32_t n_domains, const uint32_t* dom_idx, uint8_t* roots,
+                       uint8_t* status, hipStream_t s);
 void launch_attestation_roots(const uint8_t* data, uint32_t n, const uint8_t* domains, uint32_t n_domains,
                               const uint32_t* dom_idx, uint8_t* roots, hipStream_t s);
 void launch_signing_roots(const uint8_t* obj, uint32_t n, const uint8_t* domains, uint32_t n_domains,

@@ -69,3 +69,34 @@ def signing_roots(object_roots: Sequence[bytes], domains: Sequence[bytes],
         raise TblsError("signing roots: object roots must be 32 bytes")
     blob = np.frombuffer(b"".join(object_roots) or b"\0", dtype=np.uint8).copy()
     return _run("hbls_signing_roots", blob, len(object_roots), domains, dom_idx)
+
+
+# hbls_duty_signing_roots kinds (include/hipbls.h): the other duty types of core/signeddata.go
+AGGREGATE_AND_PROOF = 1        # SignedAggregateAndProof: phase0.AggregateAndProof SSZ
+CONTRIBUTION_AND_PROOF = 2     # SignedSyncContributionAndProof: altair.ContributionAndProof SSZ (264 B)
+SYNC_SELECTION = 3             # SyncContributionAndProof / SyncCommitteeSelection: slot || subcommittee_index
+SLOT = 4                       # BeaconCommitteeSelection: the uint64 slot (8 B little-endian)
+SYNC_MESSAGE = 5               # SignedSyncMessage: the beacon block root (32 B)
+
+
+def duty_signing_roots(kind: int, objects: Sequence[bytes], domains: Sequence[bytes],
+                       dom_idx: Optional[Sequence[int]] = None):
+    """Signing roots of SSZ-encoded duty objects of one kind (the object root computed on the
+    device, core/signeddata.go MessageRoot).  Returns (roots, statuses): status 6 (HBLS_BAD_INPUT)
+    for a malformed object, whose root is then all zero."""
+    n = len(objects)
+    dom, idx = _domains(domains, dom_idx, n)
+    blob = np.frombuffer(b"".join(objects) or b"\0", dtype=np.uint8).copy()
+    lens = np.asarray([len(o) for o in objects] or [0], dtype=np.uint32)
+    offs = np.zeros(max(n, 1), dtype=np.uint64)
+    if n:
+        offs[1:n] = np.cumsum(lens[:-1], dtype=np.uint64)
+    out = np.zeros(32 * max(n, 1), dtype=np.uint8)
+    st = np.zeros(max(n, 1), dtype=np.uint8)
+    if n:
+        L = _lib.lib()
+        rc = L.hbls_duty_signing_roots(kind, _p(blob), _p(offs), _p(lens), n, _p(dom), len(domains),
+                                       None if idx is None else _p(idx), _p(out), _p(st))
+        if rc != 0:
+            raise TblsError(L.hbls_last_error().decode(errors="replace"))
+    return [out[32 * i:32 * i + 32].tobytes() for i in range(n)], [int(x) for x in st[:n]]

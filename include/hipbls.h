@@ -103,6 +103,18 @@ int hbls_attestation_signing_roots(const uint8_t* data, size_t n, const uint8_t*
                                    const uint32_t* dom_idx, uint8_t* roots);
 int hbls_signing_roots(const uint8_t* object_roots, size_t n, const uint8_t* domains, size_t n_domains,
                        const uint32_t* dom_idx, uint8_t* roots);
+/* The signing roots of the other duty types charon verifies per slot, from their SSZ encodings
+ * (core/signeddata.go MessageRoot; no host SSZ pass): object i is data[off[i] .. off[i]+len[i]).
+ *   kind 1  phase0.AggregateAndProof          (SignedAggregateAndProof.MessageRoot, :979)
+ *   kind 2  altair.ContributionAndProof, 264 B (SignedSyncContributionAndProof.MessageRoot, :1227)
+ *   kind 3  altair.SyncAggregatorSelectionData{slot, subcommittee_index}, 16 B
+ *           (SyncContributionAndProof / SyncCommitteeSelection.MessageRoot, :1135 / :915)
+ *   kind 4  uint64 slot, 8 B little-endian (BeaconCommitteeSelection, eth2util.SlotHashRoot, :852)
+ *   kind 5  beacon block root, 32 B (SignedSyncMessage.MessageRoot, :1056)
+ * roots: n x 32 bytes; status: 0, or HBLS_BAD_INPUT for a malformed object (its root all zero). */
+int hbls_duty_signing_roots(int kind, const uint8_t* data, const uint64_t* off, const uint32_t* len, size_t n,
+                            const uint8_t* domains, size_t n_domains, const uint32_t* dom_idx, uint8_t* roots,
+                            uint8_t* status);
 
 /* Public-key cache for the host-buffer verification (hbls_verify_batch): keys added here are
  * decompressed and subgroup-checked once, on every device of the mask; later calls take cached

@@ -98,3 +98,78 @@ def attestation_data_root(b: bytes) -> bytes:
 def attestation_signing_root(b: bytes, domain: bytes) -> bytes:
     """GetDataRoot (signing.go:63-77) of an attestation: SigningData{HTR(data), domain}."""
     return signing_root(attestation_data_root(b), domain)
+
+
+# ---- the other duty types whose signing roots charon verifies in bulk (core/signeddata.go
+# MessageRoot): SignedAggregateAndProof (:979, phase0.AggregateAndProof.HashTreeRoot),
+# SignedSyncMessage (:1056, the beacon block root itself), SyncContributionAndProof (:1135,
+# altair.SyncAggregatorSelectionData{slot, subcommittee_index}.HashTreeRoot),
+# SignedSyncContributionAndProof (:1227, altair.ContributionAndProof.HashTreeRoot),
+# BeaconCommitteeSelection (:852, eth2util.SlotHashRoot: the uint64 slot as one chunk).
+MAX_VALIDATORS_PER_COMMITTEE = 2048
+SYNC_SUBCOMMITTEE_SIZE = 128  # SYNC_COMMITTEE_SIZE / SYNC_COMMITTEE_SUBNET_COUNT (mainnet)
+
+
+def mix_in_length(root: bytes, length: int) -> bytes:
+    return _h(root, length.to_bytes(32, "little"))
+
+
+def bitlist_root(b: bytes, limit: int) -> bytes:
+    """hash_tree_root of an SSZ Bitlist[limit] from its encoding (delimiter bit after the last)."""
+    assert len(b) >= 1 and b[-1] != 0, "bitlist without delimiter"
+    nbits = 8 * (len(b) - 1) + b[-1].bit_length() - 1
+    assert nbits <= limit
+    v = int.from_bytes(b, "little") ^ (1 << nbits)  # drop the delimiter
+    data = v.to_bytes((nbits + 7) // 8, "little") if nbits else b""
+    chunks = [_chunk(data[i:i + 32]) for i in range(0, len(data), 32)]
+    limit_chunks = (limit + 255) // 256
+    layer = chunks + [bytes(32)] * (limit_chunks - len(chunks))
+    return mix_in_length(merkleize(layer), nbits)
+
+
+def signature_root(sig: bytes) -> bytes:
+    assert len(sig) == 96
+    return htr_bytes_fixed(sig)
+
+
+def attestation_root(b: bytes) -> bytes:
+    """phase0.Attestation{aggregation_bits Bitlist[2048], data AttestationData, signature}: the
+    fixed part is the bits' offset, the 128-byte data and the 96-byte signature."""
+    off = int.from_bytes(b[0:4], "little")
+    assert off == 228 and len(b) > off
+    return merkleize([bitlist_root(b[off:], MAX_VALIDATORS_PER_COMMITTEE), attestation_data_root(b[4:132]),
+                      signature_root(b[132:228])])
+
+
+def aggregate_and_proof_root(b: bytes) -> bytes:
+    """phase0.AggregateAndProof{aggregator_index, aggregate Attestation, selection_proof}."""
+    off = int.from_bytes(b[8:12], "little")
+    assert off == 108 and len(b) > off
+    return merkleize([htr_uint64(int.from_bytes(b[0:8], "little")), attestation_root(b[off:]),
+                      signature_root(b[12:108])])
+
+
+def sync_committee_contribution_root(b: bytes) -> bytes:
+    """altair.SyncCommitteeContribution{slot, beacon_block_root, subcommittee_index,
+    aggregation_bits Bitvector[128], signature}: 160 bytes."""
+    assert len(b) == 160
+    u = lambda o: int.from_bytes(b[o:o + 8], "little")  # noqa: E731
+    return merkleize([htr_uint64(u(0)), b[8:40], htr_uint64(u(40)), htr_bytes_fixed(b[48:64]),
+                      signature_root(b[64:160])])
+
+
+def contribution_and_proof_root(b: bytes) -> bytes:
+    """altair.ContributionAndProof{aggregator_index, contribution, selection_proof}: 264 bytes."""
+    assert len(b) == 264
+    return merkleize([htr_uint64(int.from_bytes(b[0:8], "little")), sync_committee_contribution_root(b[8:168]),
+                      signature_root(b[168:264])])
+
+
+def sync_selection_root(slot: int, subcommittee_index: int) -> bytes:
+    """altair.SyncAggregatorSelectionData{slot, subcommittee_index}."""
+    return merkleize([htr_uint64(slot), htr_uint64(subcommittee_index)])
+
+
+def slot_root(slot: int) -> bytes:
+    """eth2util.SlotHashRoot (eth2util/hash.go:13-30): one uint64 merkleized alone = its chunk."""
+    return htr_uint64(slot)

@@ -9,6 +9,10 @@ Sources:
   * eth2util/signing/signing_test.go:24-74  (teku-produced registration; sk, pk, sig, domain)
   * eth2util/deposit/deposit_test.go:215-259 + testdata/TestMarshalDepositData.golden
   * cluster/examples/cluster-lock-00{0..3}.json  (cluster/cluster_test.go:242-260 TestExamples)
+  * core/testdata/TestSSZSerialisation_{SignedAggregateAndProof, SignedSyncContributionAndProof,
+    SyncContributionAndProof, SignedSyncMessage}.ssz.golden and the JSON goldens of
+    BeaconCommitteeSelection / SyncCommitteeSelection: the other duty types' objects, each checked
+    against its JSON twin; their object roots re-derived with oracle/ssz.py (duty_roots_kats)
   * core/testdata/TestSSZSerialisation_AttestationData.ssz.golden + the .json.golden of the same
     value (core/ssz_test.go): the SSZ bytes of one phase0.AttestationData, cross-checked field by
     field against the JSON; its hash-tree-root is re-derived with oracle/ssz.py (no reference
@@ -121,9 +125,68 @@ def attestation_data_kat():
     return {"ssz": data.hex(), "htr_oracle": ssz.attestation_data_root(data).hex()}
 
 
+def _td(name):
+    return os.path.join(REF, "core/testdata", name)
+
+
+def duty_roots_kats():
+    """The other duty types' SSZ goldens (core/ssz_test.go, core/testdata), each cross-checked field
+    by field against its JSON twin; object roots re-derived with oracle/ssz.py (no reference file
+    states them).  kind: hbls_duty_signing_roots's (include/hipbls.h)."""
+    out = []
+    # SignedAggregateAndProof: {message offset, signature}; message = AggregateAndProof
+    raw = open(_td("TestSSZSerialisation_SignedAggregateAndProof.ssz.golden"), "rb").read()
+    js = json.load(open(_td("TestJSONSerialisation_SignedAggregateAndProof.json.golden")))["message"]
+    m = raw[int.from_bytes(raw[0:4], "little"):]
+    assert int.from_bytes(m[0:8], "little") == int(js["aggregator_index"])
+    assert m[12:108] == _b(js["selection_proof"])
+    att = m[int.from_bytes(m[8:12], "little"):]
+    assert att[228:] == _b(js["aggregate"]["aggregation_bits"]) and att[132:228] == _b(js["aggregate"]["signature"])
+    ad = js["aggregate"]["data"]
+    assert ssz.parse_attestation_data(att[4:132])[:3] == (int(ad["slot"]), int(ad["index"]), _b(ad["beacon_block_root"]))
+    out.append({"kind": 1, "name": "SignedAggregateAndProof", "ssz": m.hex(),
+                "object_root": ssz.aggregate_and_proof_root(m).hex()})
+    # SignedSyncContributionAndProof: message = ContributionAndProof (264 B, fixed)
+    raw = open(_td("TestSSZSerialisation_SignedSyncContributionAndProof.ssz.golden"), "rb").read()
+    js = json.load(open(_td("TestJSONSerialisation_SignedSyncContributionAndProof.json.golden")))["message"]
+    m = raw[:264]
+    c = js["contribution"]
+    assert int.from_bytes(m[0:8], "little") == int(js["aggregator_index"]) and m[168:264] == _b(js["selection_proof"])
+    assert int.from_bytes(m[8:16], "little") == int(c["slot"]) and m[16:48] == _b(c["beacon_block_root"])
+    assert int.from_bytes(m[48:56], "little") == int(c["subcommittee_index"])
+    assert m[56:72] == _b(c["aggregation_bits"]) and m[72:168] == _b(c["signature"])
+    out.append({"kind": 2, "name": "SignedSyncContributionAndProof", "ssz": m.hex(),
+                "object_root": ssz.contribution_and_proof_root(m).hex()})
+    # SyncContributionAndProof: the selection data of its contribution
+    raw = open(_td("TestSSZSerialisation_SyncContributionAndProof.ssz.golden"), "rb").read()
+    js = json.load(open(_td("TestJSONSerialisation_SyncContributionAndProof.json.golden")))
+    slot, sub = int.from_bytes(raw[8:16], "little"), int.from_bytes(raw[48:56], "little")
+    assert (slot, sub) == (int(js["contribution"]["slot"]), int(js["contribution"]["subcommittee_index"]))
+    sel = slot.to_bytes(8, "little") + sub.to_bytes(8, "little")
+    out.append({"kind": 3, "name": "SyncContributionAndProof", "ssz": sel.hex(),
+                "object_root": ssz.sync_selection_root(slot, sub).hex()})
+    # SyncCommitteeSelection (JSON only): the same selection data
+    js = json.load(open(_td("TestJSONSerialisation_SyncCommitteeSelection.json.golden")))
+    slot, sub = int(js["slot"]), int(js["subcommittee_index"])
+    out.append({"kind": 3, "name": "SyncCommitteeSelection",
+                "ssz": (slot.to_bytes(8, "little") + sub.to_bytes(8, "little")).hex(),
+                "object_root": ssz.sync_selection_root(slot, sub).hex()})
+    # BeaconCommitteeSelection (JSON only): SlotHashRoot(slot)
+    js = json.load(open(_td("TestJSONSerialisation_BeaconCommitteeSelection.json.golden")))
+    slot = int(js["slot"])
+    out.append({"kind": 4, "name": "BeaconCommitteeSelection", "ssz": slot.to_bytes(8, "little").hex(),
+                "object_root": ssz.slot_root(slot).hex()})
+    # SignedSyncMessage: {slot, beacon_block_root, validator_index, signature}; root = block root
+    raw = open(_td("TestSSZSerialisation_SignedSyncMessage.ssz.golden"), "rb").read()
+    js = json.load(open(_td("TestJSONSerialisation_SignedSyncMessage.json.golden")))
+    assert int.from_bytes(raw[0:8], "little") == int(js["slot"]) and raw[8:40] == _b(js["beacon_block_root"])
+    out.append({"kind": 5, "name": "SignedSyncMessage", "ssz": raw[8:40].hex(), "object_root": raw[8:40].hex()})
+    return out
+
+
 def main():
     kats = {"registration": registration_kat(), "deposit": deposit_kats(), "locks": lock_kats(),
-            "attestation_data": attestation_data_kat()}
+            "attestation_data": attestation_data_kat(), "duty_roots": duty_roots_kats()}
     with open(os.path.join(HERE, "kat_reference.json"), "w") as f:
         json.dump(kats, f, indent=1)
     print("wrote", os.path.join(HERE, "kat_reference.json"))

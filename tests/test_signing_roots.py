@@ -79,3 +79,71 @@ def test_signing_roots_bad_input():
         sr.attestation_signing_roots([bytes(127)], [bytes(32)])
     with pytest.raises(TblsError):
         sr.signing_roots([bytes(32)], [bytes(31)])
+
+
+# ---- the other duty types (core/signeddata.go MessageRoot; hbls_duty_signing_roots)
+_ORACLE_ROOT = {1: ssz.aggregate_and_proof_root, 2: ssz.contribution_and_proof_root,
+                3: lambda b: ssz.sync_selection_root(int.from_bytes(b[:8], "little"), int.from_bytes(b[8:], "little")),
+                4: lambda b: ssz.slot_root(int.from_bytes(b, "little")), 5: lambda b: b}
+
+
+def test_duty_fixtures_oracle(kats):
+    """the oracle's object roots of the reference's duty goldens (committed by make_kats.py, each
+    SSZ golden cross-checked against its JSON twin there) recompute; bitlist edge cases"""
+    assert {k["name"] for k in kats["duty_roots"]} >= {"SignedAggregateAndProof", "SignedSyncContributionAndProof",
+                                                       "SyncContributionAndProof", "BeaconCommitteeSelection",
+                                                       "SignedSyncMessage"}
+    for k in kats["duty_roots"]:
+        assert _ORACLE_ROOT[k["kind"]](bytes.fromhex(k["ssz"])).hex() == k["object_root"], k["name"]
+    # Bitlist[2048]: empty (delimiter only), one bit, a full chunk, the maximum
+    h = lambda x, y: hashlib.sha256(x + y).digest()  # noqa: E731
+    z = bytes(32)
+    zero8 = ssz.merkleize([z] * 8)
+    assert ssz.bitlist_root(b"\x01", 2048) == h(zero8, bytes(32))
+    assert ssz.bitlist_root(b"\x03", 2048) == h(ssz.merkleize([b"\x01" + bytes(31)] + [z] * 7), (1).to_bytes(32, "little"))
+    full = bytes([0xff] * 256) + b"\x01"
+    assert ssz.bitlist_root(full, 2048) == h(ssz.merkleize([bytes([0xff] * 32)] * 8), (2048).to_bytes(32, "little"))
+    with pytest.raises(AssertionError):
+        ssz.bitlist_root(bytes([0xff] * 256) + b"\x03", 2048)  # 2049 bits
+
+
+def _aggregate_and_proof(rng, nbits):
+    bits = rng.getrandbits(nbits) if nbits else 0
+    bl = (bits | (1 << nbits)).to_bytes(nbits // 8 + 1, "little")
+    att = (228).to_bytes(4, "little") + _random_data(rng, 1)[0] + rng.randbytes(96) + bl
+    return rng.randrange(2 ** 64).to_bytes(8, "little") + (108).to_bytes(4, "little") + rng.randbytes(96) + att
+
+
+@pytest.mark.gpu
+def test_duty_roots_gpu(kats, hipbls):
+    """device object and signing roots of every duty kind equal the oracle's: the reference's
+    goldens, random objects (bitlists of 0..2048 bits), one shared and per-item domains, and
+    malformed objects rejected with HBLS_BAD_INPUT and a zero root"""
+    from charon_amd import signing_roots as sr
+    rng = random.Random(12)
+    domains = [rng.randbytes(32) for _ in range(3)]
+    gold = {}
+    for k in kats["duty_roots"]:
+        gold.setdefault(k["kind"], []).append(bytes.fromhex(k["ssz"]))
+    objs = {1: gold[1] + [_aggregate_and_proof(rng, nb) for nb in (0, 1, 7, 8, 9, 255, 256, 257, 1000, 2047, 2048)],
+            2: gold[2] + [rng.randbytes(264) for _ in range(20)],
+            3: gold[3] + [rng.randbytes(16) for _ in range(20)],
+            4: gold[4] + [rng.randbytes(8) for _ in range(20)],
+            5: gold[5] + [rng.randbytes(32) for _ in range(20)]}
+    for kind, obs in objs.items():
+        idx = [rng.randrange(3) for _ in obs]
+        roots, st = sr.duty_signing_roots(kind, obs, domains, idx)
+        assert st == [0] * len(obs), kind
+        for o, r, i in zip(obs, roots, idx):
+            assert r == ssz.signing_root(_ORACLE_ROOT[kind](o), domains[i]), kind
+        roots1, _ = sr.duty_signing_roots(kind, obs[:3], domains[:1])
+        assert roots1 == [ssz.signing_root(_ORACLE_ROOT[kind](o), domains[0]) for o in obs[:3]]
+    good = _aggregate_and_proof(rng, 20)
+    bad = [good[:200],                                            # truncated
+           good[:8] + (100).to_bytes(4, "little") + good[12:],    # wrong offset
+           good[:-1] + b"\x00",                                   # no delimiter
+           _aggregate_and_proof(rng, 2048)[:-1] + b"\x03"]        # 2049 bits
+    roots, st = sr.duty_signing_roots(1, [good] + bad, domains)
+    assert st == [0, 6, 6, 6, 6] and all(r == bytes(32) for r in roots[1:])
+    roots, st = sr.duty_signing_roots(2, [rng.randbytes(263)], domains)
+    assert st == [6] and roots == [bytes(32)]
