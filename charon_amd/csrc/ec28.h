@@ -136,18 +136,6 @@ HD L28 l_sqr(const L28& a) {
 // keep dependent multiply-adds apart; with two chains the other chain's multiply-add sits between
 // them.  The register barrier after each multiply-add (HB_MADD) keeps the compiler from
 // reassociating the chain again.  Same values as two l_mul / l_sqr.
-#ifndef HB_LEAF_ILP
-#define HB_LEAF_ILP 0
-#endif
-#if defined(__HIP_DEVICE_COMPILE__)
-#define HB_MADD(acc, x, y)                \
-  do {                                    \
-    acc += (uint64_t)(x) * (y);           \
-    __asm__("" : "+v"(acc));              \
-  } while (0)
-#else
-#define HB_MADD(acc, x, y) acc += (uint64_t)(x) * (y)
-#endif
 // r0 = a0 b0 / R, r1 = a1 b1 / R (SQ: a0 = b0, a1 = b1, the squares' halved cross products)
 template <bool SQ>
 HD void mul28x2_core(uint32_t* r0, uint32_t* r1, const uint32_t* a0, const uint32_t* b0, const uint32_t* a1,

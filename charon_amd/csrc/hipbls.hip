@@ -293,6 +293,10 @@ std::atomic<size_t> g_slot_msm_min{32768};
 // saves the signature-side MSM, its lines and Miller loop, the product tree and one final
 // exponentiation per slot.  Verdicts are the same either way.
 std::atomic<bool> g_adaptive{true};
+// HBLS_SINGLE_MAX / hbls_single_max: host Verify batches of fewer items check every item alone
+// (SINGLE_MAX_DEFAULT: the batched final exponentiation's threshold, g_fe_batch_min)
+constexpr size_t SINGLE_MAX_DEFAULT = ~size_t(0);
+std::atomic<size_t> g_single_max{SINGLE_MAX_DEFAULT};
 // HBLS_FE6=0: the final exponentiations without lines in three lanes (k_pair3<FIN>) instead of six
 // (k_pair6_fin, pair6.h)
 bool g_fe6 = true;
@@ -559,6 +563,7 @@ int init_mask(uint32_t mask) {
   g_fe_batch_min = env_size("HBLS_FE_BATCH", g_fe_batch_min.load());
   g_slot_msm_min = env_size("HBLS_SLOT_MSM", g_slot_msm_min.load());
   g_adaptive = env_size("HBLS_ADAPTIVE", 1) != 0;
+  g_single_max = env_size("HBLS_SINGLE_MAX", SINGLE_MAX_DEFAULT);
   g_ws_sets = (int)std::min<size_t>(N_WS_MAX, std::max<size_t>(1, env_size("HBLS_WS_SETS", 3)));
   {
     size_t fb = std::min<size_t>(FE_BATCH, std::max<size_t>(2, env_size("HBLS_FALLBACK_BATCH", g_fb_batch)));
@@ -1794,10 +1799,10 @@ int verify_host(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msgs, co
   // coalesced single-item callers) checks every item alone: a group of several items needs random
   // coefficients, i.e. a 64-bit scalar ladder per item on the call's critical path (~3.7 ms for a
   // lone lane), where separate checks only add lanes to kernels that have them to spare
-  // (HBLS_SINGLE_MAX, read once: items below which every item is its own group; default the
-  // batched final exponentiation's group threshold)
-  static const size_t single_max_env = env_size("HBLS_SINGLE_MAX", 0);  // read once
-  const size_t single_max = single_max_env ? single_max_env : g_fe_batch_min.load();
+  // (HBLS_SINGLE_MAX at init, hbls_single_max at run time: items below which every item is its own
+  // group; default the batched final exponentiation's group threshold)
+  const size_t sm = g_single_max.load();
+  const size_t single_max = sm == SINGLE_MAX_DEFAULT ? g_fe_batch_min.load() : sm;
   const size_t gmax = n < single_max ? 1 : g_gmax;
   std::vector<size_t> gstart;  // group starts in `order`
   for (size_t k = 0; k < n; k++)
@@ -2629,6 +2634,10 @@ int hbls_stats(uint64_t* out, size_t n) {
 
 size_t hbls_fe_batch(size_t min_groups) { return g_fe_batch_min.exchange(min_groups); }
 int hbls_adaptive(int on) { return g_adaptive.exchange(on != 0) ? 1 : 0; }
+size_t hbls_single_max(size_t items) {
+  if (ensure_init()) return 0;
+  return g_single_max.exchange(items);
+}
 size_t hbls_slot_msm(size_t min_items) {
   // a new setting starts from a clean history (tests count the slot-wide checks that ran)
   for (Dev* d : devs()) {

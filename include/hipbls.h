@@ -272,6 +272,10 @@ size_t hbls_slot_msm(size_t min_items);
  * slot-wide check failed, the next calls take the per-batch check directly until one passes every
  * batch.  Returns the previous setting.  Verdicts do not depend on it. */
 int hbls_adaptive(int on);
+/* Host Verify batches of fewer than `items` check every item alone (no random-combination ladder
+ * on the latency path); SIZE_MAX = the default (the batched final exponentiation's threshold).
+ * Returns the previous setting (HBLS_SINGLE_MAX at init).  Verdicts never depend on it. */
+size_t hbls_single_max(size_t items);
 /* Tuning: the random linear combination's public-key side groups a verification group's items
  * into shared-doubling chunks sized to keep about `lanes` lanes busy (at most 16 items per chunk;
  * calls of fewer than 2 lanes' worth keep one ladder per item).  0 restores the default 65536

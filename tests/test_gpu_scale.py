@@ -467,9 +467,9 @@ def test_slot_msm_clean_and_cancelling_errors(L, hipbls, monkeypatch):
 def test_batched_groups_pass_without_fallback(L, hipbls, monkeypatch):
     """Clean partials over a few messages: every verification group passes its combined check,
     no item is re-checked alone (the random linear combination is effective, not just correct).
-    (HBLS_SINGLE_MAX=0: a call this small would otherwise check every item alone.)"""
+    (hbls_single_max(0): a call this small would otherwise check every item alone.)"""
     monkeypatch.setenv("HBLS_STATS", "1")
-    monkeypatch.setenv("HBLS_SINGLE_MAX", "0")
+    prev_single = L.hbls_single_max(0)
     keys = [hipbls.generate_secret_key() for _ in range(48)]
     msgs = [hashlib.sha256(b"committee %d" % (k % 3)).digest() for k in range(48)]
     sigs = hipbls.sign_batch(keys, msgs)
@@ -488,7 +488,7 @@ def test_batched_groups_pass_without_fallback(L, hipbls, monkeypatch):
     assert d[2] == 16, d
     # the default for so small a call: every item its own group (its check the item's verdict),
     # no combination, no re-check
-    monkeypatch.delenv("HBLS_SINGLE_MAX")
+    L.hbls_single_max(prev_single)
     s0 = _stats(L)
     st = hipbls.verify_batch(pks, msgs, bad)
     assert st == [NOT_VERIFIED if i == 5 else OK for i in range(48)]

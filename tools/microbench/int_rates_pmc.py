@@ -10,8 +10,8 @@ Per timed dispatch (the second launch of each kernel and occupancy; the first is
   * VALU instructions per wave (SQ_INSTS_VALU / SQ_WAVES) against the copies the kernel issues
     (ITERS x UNROLL, plus the few outside the loop): a rate above 64 lane-ops/clk/CU with the
     expected count means the instruction dual-issues, with a higher count the accounting is wrong;
-  * the effective clock, GRBM_GUI_ACTIVE (GPU busy cycles, one counter for the device) over the
-    dispatch's duration in the kernel trace, against the in-kernel clock the binary prints;
+  * the effective clock, GRBM_GUI_ACTIVE (busy cycles, summed over the eight XCDs' GRBMs) / 8 over
+    the dispatch's duration in the kernel trace, against the in-kernel clock the binary prints;
   * lane-ops/s from counters: SQ_INSTS_VALU x 64 / duration -- for v_mad_u64_u32 at 16 waves per
     CU this must reproduce opcounts.PEAK_MAD_TOPS (29.944 T) within 3 %.
 """
@@ -25,6 +25,9 @@ import sys
 NAMES = {"k_mad64": "v_mad_u64_u32", "k_mullo": "v_mul_lo_u32", "k_mulhi": "v_mul_hi_u32", "k_add": "v_add_u32",
          "k_add3": "v_add3_u32", "k_and": "v_and_b32", "k_mad24": "v_mad_u32_u24", "k_lshr64": "v_lshrrev_b64",
          "k_lshladd64": "v_lshl_add_u64", "k_fma64": "v_fma_f64"}
+
+
+XCDS = 8  # MI355X: 8 XCDs x 32 CUs
 
 
 def _kname(s):
@@ -45,7 +48,7 @@ def main():
         if m:
             own[(int(m.group(1)), m.group(2))] = {"T_lane_ops": float(m.group(3)), "ms": float(m.group(4)),
                                                   "eff_MHz": float(m.group(5))}
-    copies = 4096 * 16
+    copies = int(os.environ.get("INT_RATES_COPIES", 16384 * 16))
     # dispatches in launch order: per kernel name, warm-up then timed, for 8 then 16 waves per CU
     tr = collections.defaultdict(list)
     for r in trace:
@@ -66,7 +69,9 @@ def main():
             e = {"instruction": instr, "waves_per_cu": wpc, "duration_ms_trace": round(dur * 1e3, 4),
                  "valu_per_wave": round(valu / waves, 1) if waves else None,
                  "valu_lane_ops_T_from_counters": round(valu * 64 / dur / 1e12, 3) if dur else None,
-                 "grbm_gui_active": gui, "clock_MHz_from_grbm": round(gui / dur / 1e6, 1) if dur else None,
+                 "grbm_gui_active": gui,
+                 # one GRBM per XCD: the counter sums the eight XCDs' busy cycles
+                 "clock_MHz_from_grbm": round(gui / XCDS / dur / 1e6, 1) if dur else None,
                  **{f"binary_{k}": v for k, v in own.get((wpc, instr), {}).items()}}
             out["kernels"].append(e)
     mad = [k for k in out["kernels"] if k["instruction"] == "v_mad_u64_u32" and k["waves_per_cu"] == 16]
