@@ -130,12 +130,15 @@ HD L28 l_sqr(const L28& a) {
 }
 #endif
 
-// ---- Two independent products in one leaf (HB_LEAF_ILP): the two column chains interleaved, each
-// seeded with its own carry.  A lone chain makes the compiler start every column's multiply-adds
-// at zero and add the shifted carry afterwards (one v_lshl_add_u64 per column, 26 per product) to
-// keep dependent multiply-adds apart; with two chains the other chain's multiply-add sits between
-// them.  The register barrier after each multiply-add (HB_MADD) keeps the compiler from
-// reassociating the chain again.  Same values as two l_mul / l_sqr.
+// ---- Two independent products in one leaf, for the G1 formulas (g1l_dbl): the two column chains
+// interleaved, each seeded with its own carry (HB_MADD keeps the compiler from reassociating
+// them).  A lone chain makes the compiler start every column's multiply-adds at zero and add the
+// shifted carry afterwards (one v_lshl_add_u64 per column) to keep dependent multiply-adds apart;
+// with two chains the other chain's multiply-add sits between them.  Measured (round 5,
+// profiles/r05c_leaf_ab.txt): the G1 kernels gain (k_dec_pk 24.7 -> 23.6-24.5 ms, k_rlc 10.6-10.9
+// -> 10.2-10.3 ms alone), the same pairing of the G2 formulas' Fp2 products -- and an interleaved
+// Fp2 product -- lose (k_msm_bucket +25 %, k_ta_small +13 %, hashing +2.5 %): G2 keeps the lone
+// chains.  Same values as two l_mul / l_sqr.
 // r0 = a0 b0 / R, r1 = a1 b1 / R (SQ: a0 = b0, a1 = b1, the squares' halved cross products)
 template <bool SQ>
 HD void mul28x2_core(uint32_t* r0, uint32_t* r1, const uint32_t* a0, const uint32_t* b0, const uint32_t* a1,
@@ -220,9 +223,9 @@ __device__ __noinline__ static u32x32 l_sqr2_leaf(u32x32 a) {
   return o;
 }
 #endif
-// (a b, c d) and (a^2, c^2): one dual-chain leaf with HB_LEAF_ILP, else two single products
+// (a b, c d) and (a^2, c^2): one dual-chain leaf on the device, two products on the host
 HD void l_mul2(const L28& a, const L28& b, const L28& c, const L28& d, L28& r0, L28& r1) {
-#if defined(__HIP_DEVICE_COMPILE__) && HB_LEAF_ILP
+#if defined(__HIP_DEVICE_COMPILE__)
   HB_COUNT_FP_MUL();
   HB_COUNT_FP_MUL();
   u32x32 av;
@@ -243,7 +246,7 @@ HD void l_mul2(const L28& a, const L28& b, const L28& c, const L28& d, L28& r0, 
 #endif
 }
 HD void l_sqr2(const L28& a, const L28& c, L28& r0, L28& r1) {
-#if defined(__HIP_DEVICE_COMPILE__) && HB_LEAF_ILP
+#if defined(__HIP_DEVICE_COMPILE__)
   HB_COUNT_FP_MUL();
   HB_COUNT_FP_MUL();
   u32x32 av;
@@ -331,10 +334,13 @@ HDNI G1L g1l_dbl(const G1L& p) {
 // the common tail of the additions (I = 4 HH folded into shifts: J = 4 H HH, V = 4 U1 HH)
 HD G1L g1l_add_tail(const L28& H, const L28& rr, const L28& U1, const L28& S1, const L28& Zs) {
   const L28 HH = l_sqr(H);
-  const L28 J1 = l_mul(H, HH), V1 = l_mul(U1, HH);
+  L28 J1, V1;
+  l_mul2(H, HH, U1, HH, J1, V1);
   G1L r;
   r.X = l_norm(l_sub<13, 12>(l_sqr(rr), l_add(l_shl(J1, 2), l_shl(V1, 3))));
-  r.Y = l_norm(l_sub<9, 8>(l_mul(rr, l_sub<15, 1>(l_shl(V1, 2), r.X)), l_shl(l_mul(S1, J1), 3)));
+  L28 t, sj;
+  l_mul2(rr, l_sub<15, 1>(l_shl(V1, 2), r.X), S1, J1, t, sj);
+  r.Y = l_norm(l_sub<9, 8>(t, l_shl(sj, 3)));
   r.Z = l_mul(Zs, H);
   r.inf = false;
   return r;
@@ -442,41 +448,8 @@ HD void f2l_mul_core(uint32_t* r0, uint32_t* r1, const uint32_t* a0, const uint3
                      const uint32_t* b1) {
   uint32_t na1[14];
   HB_UNROLL for (int j = 0; j < 14; j++) na1[j] = kF2N.l[j] - a1[j];
-#if HB_LEAF_ILP
-  // the two passes interleaved (HB_MADD: see mul28x2_core)
-  uint32_t m0[14], m1[14];
-  uint64_t c0 = 0, c1 = 0;
-  HB_UNROLL for (int k = 0; k < 27; k++) {
-    const int lo = k < 14 ? 0 : k - 13, hi = k < 14 ? k : 13;
-    HB_UNROLL for (int j = lo; j <= hi; j++) {
-      HB_MADD(c0, a0[j], b0[k - j]);
-      HB_MADD(c1, a0[j], b1[k - j]);
-      HB_MADD(c0, na1[j], b1[k - j]);
-      HB_MADD(c1, a1[j], b0[k - j]);
-    }
-    HB_UNROLL for (int j = lo; j <= hi; j++)
-      if (j < k || k >= 14) {
-        HB_MADD(c0, m0[j], P28[k - j]);
-        HB_MADD(c1, m1[j], P28[k - j]);
-      }
-    if (k < 14) {
-      m0[k] = ((uint32_t)c0 * HB_P_N0_28) & 0x0FFFFFFFu;
-      m1[k] = ((uint32_t)c1 * HB_P_N0_28) & 0x0FFFFFFFu;
-      HB_MADD(c0, m0[k], P28[0]);
-      HB_MADD(c1, m1[k], P28[0]);
-    } else {
-      r0[k - 14] = (uint32_t)c0 & 0x0FFFFFFFu;
-      r1[k - 14] = (uint32_t)c1 & 0x0FFFFFFFu;
-    }
-    c0 >>= 28;
-    c1 >>= 28;
-  }
-  r0[13] = (uint32_t)c0;
-  r1[13] = (uint32_t)c1;
-#else
   f2l_dot_core(r0, a0, na1, b0, b1);  // real = a0 b0 + (K - a1) b1
   f2l_dot_core(r1, a0, a1, b1, b0);   // imag = a0 b1 + a1 b0
-#endif
 }
 
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -539,16 +512,12 @@ HD F2L f2l_mul(const F2L& a, const F2L& b) {
 #endif
 // (a0 + a1)(a0 + K - a1) + 2 a0 a1 u, K = 36 p (lazy28.KSITE["2Q"]): two Fp products
 HD F2L f2l_sqr(const F2L& a) {
-  F2L r;
-  l_mul2(l_add(a.c0, a.c1), l_sub<36, 1>(a.c0, a.c1), l_shl(a.c0, 1), a.c1, r.c0, r.c1);
-  return r;
+  return {l_mul(l_add(a.c0, a.c1), l_sub<36, 1>(a.c0, a.c1)), l_mul(l_shl(a.c0, 1), a.c1)};
 }
 // f2l_sqr with the site's constant K = S p
 template <uint32_t S, uint32_t T>
 HD F2L f2l_sqr_k(const F2L& a) {
-  F2L r;
-  l_mul2(l_add(a.c0, a.c1), l_sub<S, T>(a.c0, a.c1), l_shl(a.c0, 1), a.c1, r.c0, r.c1);
-  return r;
+  return {l_mul(l_add(a.c0, a.c1), l_sub<S, T>(a.c0, a.c1)), l_mul(l_shl(a.c0, 1), a.c1)};
 }
 
 // Who computes a formula's Fp2 products.  F2One: this lane alone (f2l_mul / f2l_sqr_k).  F2Half

@@ -154,19 +154,8 @@ HD void fp_join28(uint32_t* w, const uint32_t* l) {  // 14 x 28 (normalised, < 2
   }
 }
 
-// HB_LEAF_ILP (per translation unit; tools/microbench/leaf_variants.hip measured the forms):
-//   0  every product leaf as the compiler schedules it: a lone multiply-add chain per column is
-//      started at zero and the shifted carry added after it (one v_lshl_add_u64 per column);
-//   1  the Fp2 product's two passes interleaved and independent Fp products / squares of the
-//      point formulas paired in one leaf (ec28.h mul28x2_core, l_mul2 / l_sqr2): each chain seeded
-//      with its carry, the other chain's multiply-add between dependent ones (+2.8 % products/s at
-//      two waves per SIMD, -1.9 % at one);
-//   2  as 1, and the lone chains of fp_mul28 / fp_sqr28 (the exponentiations) seeded with their
-//      carry too (+4 % at two waves per SIMD, -29 % at one: for kernels of two or more waves only).
-// HB_MADD: a multiply-add whose accumulator the compiler may not reassociate (a register barrier).
-#ifndef HB_LEAF_ILP
-#define HB_LEAF_ILP 0
-#endif
+// HB_MADD: a multiply-add whose accumulator the compiler may not reassociate (a register barrier;
+// ec28.h mul28x2_core, the paired G1 products).
 #if defined(__HIP_DEVICE_COMPILE__)
 #define HB_MADD(acc, x, y)                \
   do {                                    \
@@ -176,17 +165,12 @@ HD void fp_join28(uint32_t* w, const uint32_t* l) {  // 14 x 28 (normalised, < 2
 #else
 #define HB_MADD(acc, x, y) acc += (uint64_t)(x) * (y)
 #endif
-#if HB_LEAF_ILP >= 2
-#define HB_MADD1(acc, x, y) HB_MADD(acc, x, y)
-#else
-#define HB_MADD1(acc, x, y) acc += (uint64_t)(x) * (y)
-#endif
 
 // one column of the reduction: m_k p_{k-j} terms for the columns k >= 14 (and j < k below)
 #define HB_MONT28_TAIL(acc, m, k, r)                                                     \
   if ((k) < 14) {                                                                       \
     m[(k)] = ((uint32_t)(acc) * HB_P_N0_28) & 0x0FFFFFFFu;                               \
-    HB_MADD1(acc, m[(k)], P28[0]);                                                       \
+    acc += (uint64_t)m[(k)] * P28[0];                                                    \
   } else {                                                                              \
     r[(k) - 14] = (uint32_t)(acc) & 0x0FFFFFFFu;                                          \
   }                                                                                     \
@@ -199,9 +183,9 @@ HD void fp_mul28_core(uint32_t* r, const uint32_t* a, const uint32_t* b) {
   uint64_t acc = 0;
   HB_UNROLL for (int k = 0; k < 27; k++) {
     const int lo = k < 14 ? 0 : k - 13, hi = k < 14 ? k : 13;
-    HB_UNROLL for (int j = lo; j <= hi; j++) HB_MADD1(acc, a[j], b[k - j]);
+    HB_UNROLL for (int j = lo; j <= hi; j++) acc += (uint64_t)a[j] * b[k - j];
     HB_UNROLL for (int j = lo; j <= hi; j++)
-      if (j < k || k >= 14) HB_MADD1(acc, m[j], P28[k - j]);
+      if (j < k || k >= 14) acc += (uint64_t)m[j] * P28[k - j];
     HB_MONT28_TAIL(acc, m, k, r)
   }
   r[13] = (uint32_t)acc;
@@ -215,11 +199,11 @@ HD void fp_sqr28_core(uint32_t* r, const uint32_t* a) {
   HB_UNROLL for (int k = 0; k < 27; k++) {
     const int lo = k < 14 ? 0 : k - 13, hi = k < 14 ? k : 13;
     HB_UNROLL for (int j = lo; j <= hi; j++) {
-      if (2 * j < k) HB_MADD1(acc, a2[j], a[k - j]);
-      else if (2 * j == k) HB_MADD1(acc, a[j], a[j]);
+      if (2 * j < k) acc += (uint64_t)a2[j] * a[k - j];
+      else if (2 * j == k) acc += (uint64_t)a[j] * a[j];
     }
     HB_UNROLL for (int j = lo; j <= hi; j++)
-      if (j < k || k >= 14) HB_MADD1(acc, m[j], P28[k - j]);
+      if (j < k || k >= 14) acc += (uint64_t)m[j] * P28[k - j];
     HB_MONT28_TAIL(acc, m, k, r)
   }
   r[13] = (uint32_t)acc;

@@ -341,7 +341,7 @@ struct Ws {
 };
 
 // host-call staging buffers (inputs and outputs of the host-buffer entry points)
-enum IoId { I_PK, I_SIG, I_MSG, I_OFF, I_LEN, I_MIDX, I_HM, I_STAT, I_IDX, I_GOFF, I_OUT, I_SK, I_VGOFF, I_KC, I_HM2, I_COUNT };
+enum IoId { I_PK, I_SIG, I_MSG, I_OFF, I_LEN, I_MIDX, I_HM, I_STAT, I_IDX, I_GOFF, I_OUT, I_SK, I_VGOFF, I_HM2, I_COUNT };
 
 constexpr int N_WS_MAX = 8;  // workspace sets per device: HBLS_WS_SETS (default 3)
 int g_ws_sets = 3;
@@ -386,6 +386,10 @@ struct Dev {
   // public-key cache (hbls_pubkey_cache_add): decompressed entries + statuses, every device holds
   // all g_kc_n of them
   DevBuf kc_tab, kc_st;
+  // its compressed keys and their open-addressing index (vbatch.hip k_kc_index / k_pk_cached):
+  // kc_n entries indexed, kc_tcap slots (a power of two >= 2 kc_n)
+  DevBuf kc_keys, kc_hidx;
+  size_t kc_n = 0, kc_tcap = 0;
   // decompressed-signature cache (vbatch.hip k_sc_put / k_sc_get): filled by host-buffer Verify
   // batches, read by host-buffer ThresholdAggregate batches.  sc_ev orders every put and get on
   // the device (recorded after each, waited for before the next: a put rewrites ring entries a get
@@ -785,7 +789,7 @@ int ta_tail(Dev& d, Ws& w, const HmEntry* pts, const uint32_t* src, const uint8_
 // failed check; any other path computes them first.
 int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, const uint32_t* didx,
                     const MsgEntry* hm, size_t n, const uint32_t* dgoff, size_t n_groups, uint8_t* dst,
-                    hipStream_t s, hipEvent_t hm_ready, const TaFold* fold, const uint32_t* kc_idx = nullptr,
+                    hipStream_t s, hipEvent_t hm_ready, const TaFold* fold, bool kc = false,
                     hipEvent_t h_ready = nullptr, MsgEntry* defer_hm = nullptr, size_t defer_msgs = 0) {
   if (!dgoff) n_groups = n;
   G1AEntry* vpk;
@@ -893,10 +897,11 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
   if (fold && fold->pk_table) {
     vpk = const_cast<G1AEntry*>(fold->pk_table);
     vpkst = const_cast<uint8_t*>(fold->pk_table_st);
-  } else if (kc_idx) {  // host-buffer call with the key cache: cached entries, the rest decompressed
+  } else if (kc && d.kc_n) {  // host-buffer call with the key cache: cached entries, the rest decompressed
     TIMED(d, "k_dec_pk", w.side[0],
-          launch_pk_gather(dpk, kc_idx, (const G1AEntry*)d.kc_tab.p, (const uint8_t*)d.kc_st.p, (uint32_t)n, vpk,
-                           vpkst, w.side[0]));
+          launch_pk_cached(dpk, (uint32_t)n, (const uint8_t*)d.kc_keys.p, (const G1AEntry*)d.kc_tab.p,
+                           (const uint8_t*)d.kc_st.p, (const uint32_t*)d.kc_hidx.p, (uint32_t)d.kc_tcap, g_sc_k0,
+                           g_sc_k1, vpk, vpkst, w.side[0]));
   } else {
     TIMED(d, "k_dec_pk", w.side[0], launch_dec_pk(dpk, (uint32_t)n, vpk, vpkst, w.side[0]));
   }
@@ -1548,13 +1553,11 @@ int for_each_device_hc(size_t n_units, const HcFn& fn) {
 
 // Verify n host-buffer items (tbls.Verify per item): items are ordered by message and grouped
 // (at most g_gmax per group), the groups sharded over the devices, statuses scattered back.
-// Cache indices of m packed compressed keys (0xffffffff: not cached).  false when the cache is
-// empty or holds none of them (the call then decompresses every key).
 // Decompress m compressed keys into entries first .. first+m-1 of d's key table (grown, keeping
 // the entries before `first`).  Caller holds d.mu.
 int kc_fill(Dev& d, const uint8_t* keys, size_t first, size_t m) {
   HCHK(hipSetDevice(d.ord));
-  // launches enqueued earlier may still read the table: its only reader, launch_pk_gather of a
+  // launches enqueued earlier may still read the table: its only reader, launch_pk_cached of a
   // host-buffer verification, runs on a workspace side stream, so the library's own streams (the
   // library stream, the host-call contexts' and the workspaces' side streams) are drained before
   // any entry is rewritten or the table moves -- not the whole device: caller, torch and RCCL
@@ -1585,25 +1588,35 @@ int kc_fill(Dev& d, const uint8_t* keys, size_t first, size_t m) {
   if (upload(d, I_PK, keys, 48 * m, &dpk)) return -1;
   TIMED(d, "k_dec_pk", d.stream,
         launch_dec_pk(dpk, (uint32_t)m, (G1AEntry*)d.kc_tab.p + first, (uint8_t*)d.kc_st.p + first, d.stream));
+  // the keys and the device index (grown to >= 2 x the entries: every entry re-inserted)
+  if (d.kc_keys.cap < tot * 48) {
+    DevBuf nk;
+    void* p;
+    if (ensure_buf(nk, tot * 48, &p)) return -1;
+    if (first) HCHK(hipMemcpyAsync(nk.p, d.kc_keys.p, first * 48, hipMemcpyDeviceToDevice, d.stream));
+    HCHK(hipStreamSynchronize(d.stream));
+    if (d.kc_keys.p) HCHK(hipFree(d.kc_keys.p));
+    d.kc_keys = nk;
+  }
+  HCHK(hipMemcpyAsync((uint8_t*)d.kc_keys.p + 48 * first, dpk, 48 * m, hipMemcpyDeviceToDevice, d.stream));
+  size_t tcap = std::max<size_t>(d.kc_tcap, 1024);
+  while (tcap < 2 * tot) tcap *= 2;
+  size_t from = first;
+  if (tcap != d.kc_tcap || first < d.kc_n) {  // a new index: every entry
+    void* p;
+    if (ensure_buf(d.kc_hidx, tcap * sizeof(uint32_t), &p)) return -1;
+    HCHK(hipMemsetAsync(d.kc_hidx.p, 0, tcap * sizeof(uint32_t), d.stream));
+    d.kc_tcap = tcap;
+    from = 0;
+  }
+  TIMED(d, "k_kc_index", d.stream,
+        launch_kc_index((const uint8_t*)d.kc_keys.p, (uint32_t)from, (uint32_t)(tot - from), (uint32_t*)d.kc_hidx.p,
+                        (uint32_t)tcap, g_sc_k0, g_sc_k1, d.stream));
   HCHK(hipStreamSynchronize(d.stream));
+  d.kc_n = tot;
   return 0;
 }
 
-// (order: nullable; key k is pks + 48 * order[k] when given)
-bool kc_lookup(const uint8_t* pks, size_t m, std::vector<uint32_t>& idx, const uint32_t* order = nullptr) {
-  std::lock_guard<std::mutex> lk(g_kc_mu);
-  if (g_kc_map.empty()) return false;
-  idx.assign(m, 0xffffffffu);
-  bool any = false;
-  for (size_t k = 0; k < m; k++) {
-    auto it = g_kc_map.find(std::string((const char*)pks + 48 * (order ? order[k] : k), 48));
-    if (it != g_kc_map.end()) {
-      idx[k] = it->second;
-      any = true;
-    }
-  }
-  return any;
-}
 
 // ---- decompressed-signature cache (Dev::sc_*; kernels in vbatch.hip).  Both run under d.mu.
 // sc_ready: the device's cache at the current capacity (allocated on first use; a capacity change
@@ -1680,7 +1693,8 @@ static double now_ms() {
 constexpr size_t CHUNK_MIN_ITEMS = size_t(1) << 18;
 int verify_chunks(Dev& d, Hc& h0, std::unique_lock<std::mutex>& lk, const uint8_t* pks, const uint8_t* sigs,
                   const MsgTable& all, const std::vector<uint32_t>& order32, const std::vector<size_t>& gstart,
-                  size_t n_groups, size_t n, uint8_t* status) {
+                  size_t n_groups, size_t n, uint8_t* status, double t_start, double t_grouped) {
+  const double t_called = now_ms();
   lk.unlock();
   std::vector<uint32_t> midx(n);
   for (size_t k = 0; k < n; k++) midx[k] = all.idx[order32[k]];
@@ -1712,12 +1726,12 @@ int verify_chunks(Dev& d, Hc& h0, std::unique_lock<std::mutex>& lk, const uint8_
     goffs[c].resize(cg[c + 1] - cg[c] + 1);
     for (size_t g = cg[c]; g <= cg[c + 1]; g++) goffs[c][g - cg[c]] = (uint32_t)(gstart[g] - gstart[cg[c]]);
   }
+  const double t_prep = now_ms();
   lk.lock();
-  std::vector<uint32_t> kc;
-  const bool use_kc = kc_lookup(pks, n, kc, order32.data());
+  const double t_locked = now_ms();
   // shared uploads on h0
   uint8_t *rpk, *rsig;
-  uint32_t *dord, *dmidx, *dkc = nullptr;
+  uint32_t *dord, *dmidx;
   uint8_t* dmsg;
   uint64_t* doff;
   uint32_t* dlen;
@@ -1729,7 +1743,6 @@ int verify_chunks(Dev& d, Hc& h0, std::unique_lock<std::mutex>& lk, const uint8_
       upload(d, I_LEN, all.len.data(), all.len.size(), &dlen, &h0) ||
       ensure_buf(h0.io[I_HM], all.len.size() * sizeof(MsgEntry), &hmp) || ensure_buf(h0.io[I_HM2], n, &stp))
     return -1;
-  if (use_kc && upload(d, I_KC, kc.data(), n, &dkc, &h0)) return -1;
   MsgEntry* hm = (MsgEntry*)hmp;
   uint8_t* dst_out = (uint8_t*)stp;
   HCHK(hipEventRecord(h0.ev, h0.s));
@@ -1761,8 +1774,8 @@ int verify_chunks(Dev& d, Hc& h0, std::unique_lock<std::mutex>& lk, const uint8_
     HCHK(hipEventRecord(w.ev_h, hs));
     if (!defer) TIMED(d, "k_lines_msg", hs, launch_lines_msg(hm + mfirst, (uint32_t)mcount, hs));
     HCHK(hipEventRecord(w.ev_side[2], hs));
-    if (verify_pipeline(d, w, dpk, dsig, dmidx + ib, hm, m, dgoff, ng, dst, sc, w.ev_side[2], nullptr,
-                        dkc ? dkc + ib : nullptr, w.ev_h, hm + mfirst, defer ? mcount : 0))
+    if (verify_pipeline(d, w, dpk, dsig, dmidx + ib, hm, m, dgoff, ng, dst, sc, w.ev_side[2], nullptr, true, w.ev_h,
+                        hm + mfirst, defer ? mcount : 0))
       return -1;
     {
       HmEntry* vsig;
@@ -1778,8 +1791,13 @@ int verify_chunks(Dev& d, Hc& h0, std::unique_lock<std::mutex>& lk, const uint8_
     }
   }
   lk.unlock();  // enqueued: other callers may enqueue while this one waits
+  const double t_enq = now_ms();
   HCHK(hipMemcpyAsync(status, dst_out, n, hipMemcpyDeviceToHost, h0.s));
   HCHK(hipStreamSynchronize(h0.s));
+  if (host_timing())
+    fprintf(stderr, "hbls verify_chunks n=%zu chunks=%zu: group %.2f ms, context wait %.2f, prep %.2f, lock wait %.2f, "
+            "enqueue+upload %.2f, device %.2f\n", n, cg.size() - 1, t_grouped - t_start, t_called - t_grouped,
+            t_prep - t_called, t_locked - t_prep, t_enq - t_locked, now_ms() - t_enq);
   return 0;
 }
 
@@ -1817,7 +1835,7 @@ int verify_host(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msgs, co
     if (m == 0) return 0;
     const bool whole = gb == 0 && ge == n_groups;
     if (whole && n >= 2 * CHUNK_MIN_ITEMS && g_ws_sets > 1 && defer_lines(n_groups, all.len.size()))
-      return verify_chunks(d, h, lk, pks, sigs, all, order32, gstart, n_groups, n, status);
+      return verify_chunks(d, h, lk, pks, sigs, all, order32, gstart, n_groups, n, status, t_start, t_grouped);
     // host preparation without the device lock (other callers enqueue meanwhile): the shard's
     // distinct messages and each item's message index in group order -- the whole call's table
     // when one device takes every group
@@ -1846,11 +1864,6 @@ int verify_host(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msgs, co
     const double t_prep = now_ms();
     lk.lock();
     const double t_locked = now_ms();
-    // the key-cache lookup under Dev::mu: entries of d's table are only (re)written under it, after
-    // every launch that may still read them has completed (kc_fill), so the indices stay valid for
-    // what this call enqueues
-    std::vector<uint32_t> kc;
-    const bool use_kc = whole ? kc_lookup(pks, m, kc, order32.data()) : kc_lookup(hpk.data(), m, kc);
     // the messages hash on a side stream while the keys and signatures decompress (latency of
     // one call: the two chains run side by side)
     Ws& w = ws_acquire(d, h.s);
@@ -1859,7 +1872,7 @@ int verify_host(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msgs, co
     const bool defer = defer_lines(ge - gb, t.len.size());
     if (hash_table(d, t, &hm, !defer, &w, &hm_ready, &h, &h_ready)) return -1;
     uint8_t *dpk, *dsig, *dst, *dst_out = nullptr;
-    uint32_t *didx, *dgoff, *dkc = nullptr, *dord = nullptr;
+    uint32_t *didx, *dgoff, *dord = nullptr;
     if (whole) {  // caller order up, group order on the device
       uint8_t *rpk, *rsig;
       void *p1, *p2, *p3;
@@ -1882,8 +1895,9 @@ int verify_host(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msgs, co
     }
     if (upload(d, I_MIDX, tidx.data(), m, &didx, &h) || upload(d, I_VGOFF, goff.data(), goff.size(), &dgoff, &h))
       return -1;
-    if (use_kc && upload(d, I_KC, kc.data(), m, &dkc, &h)) return -1;
-    if (verify_pipeline(d, w, dpk, dsig, didx, hm, m, dgoff, ge - gb, dst, h.s, hm_ready, nullptr, dkc, h_ready, hm,
+    // the key cache is looked up on the device (k_pk_cached): its tables are only rewritten under
+    // Dev::mu, held while this call enqueues, after every launch that may still read them
+    if (verify_pipeline(d, w, dpk, dsig, didx, hm, m, dgoff, ge - gb, dst, h.s, hm_ready, nullptr, true, h_ready, hm,
                         defer ? t.len.size() : 0))
       return -1;
     {  // the decompressed partials into the signature cache (the aggregation of these partials reads them)
@@ -2452,6 +2466,11 @@ size_t hbls_sig_cache(size_t entries) {
 
 int hbls_pubkey_cache_clear(void) {
   std::lock_guard<std::mutex> al(g_kc_add_mu);
+  for (Dev* dp : devs()) {  // no verification enqueued after this sees the old entries
+    std::lock_guard<std::mutex> dl(dp->mu);
+    dp->kc_n = 0;
+    dp->kc_tcap = 0;  // the next fill builds a fresh index
+  }
   std::lock_guard<std::mutex> lk(g_kc_mu);
   g_kc_map.clear();
   g_kc_n = 0;
@@ -2592,7 +2611,7 @@ int hbls_slot_device(const hbls_slot* a, void* stream) {
   fold.dv_pk_table = (const G1AEntry*)a->dv_pk_table;
   fold.dv_pk_table_st = a->dv_pk_table_st;
   if (verify_pipeline(*d, w, a->pks, a->sigs, a->msg_idx, (const MsgEntry*)a->hm, a->n, a->vgrp_off, a->n_vgroups,
-                      a->vstatus, s, w.ev_side[2], &fold, nullptr, nullptr, (MsgEntry*)a->hm, defer ? a->n_msgs : 0))
+                      a->vstatus, s, w.ev_side[2], &fold, false, nullptr, (MsgEntry*)a->hm, defer ? a->n_msgs : 0))
     return -1;
   HCHK(hipStreamWaitEvent(s, w.ev_side[2], 0));
   return ws_release(w, s);

@@ -230,8 +230,11 @@ void launch_sc_put(const uint8_t* sigs, const HmEntry* pts, const uint8_t* st, u
 void launch_sc_get(const uint8_t* sigs, uint32_t n, const void* key, const HmEntry* ent, const uint8_t* est,
                    const uint32_t* tab, uint32_t tcap, uint64_t k0, uint64_t k1, HmEntry* out, uint8_t* st, uint8_t* hit,
                    hipStream_t s);
-void launch_pk_gather(const uint8_t* pks, const uint32_t* idx, const G1AEntry* tab, const uint8_t* tst, uint32_t n,
-                      G1AEntry* out, uint8_t* st, hipStream_t s);
+void launch_kc_index(const uint8_t* keys, uint32_t first, uint32_t m, uint32_t* tab, uint32_t tcap, uint64_t k0,
+                     uint64_t k1, hipStream_t s);
+void launch_pk_cached(const uint8_t* pks, uint32_t n, const uint8_t* keys, const G1AEntry* tabe, const uint8_t* tst,
+                      const uint32_t* tab, uint32_t tcap, uint64_t k0, uint64_t k1, G1AEntry* out, uint8_t* st,
+                      hipStream_t s);
 // Chunk plans and the multi-scalar random linear combination (vbatch.hip k_plan_*, k_rlc_msm).
 constexpr uint32_t RLC_CHUNK = 16;  // items per lane of k_rlc_msm
 struct RlcMsmArgs {

@@ -15,11 +15,6 @@
 // sum.  If the slot-wide check fails, the per-group path runs (hipbls.hip verify_pipeline), so
 // verdicts are those of the per-group check.
 #define HB_FAST_FPMUL 1
-// product leaves (fp.h HB_LEAF_ILP): at most form 1 here -- the reduction and sums run one wave per SIMD
-#if defined(HB_LEAF_ILP) && HB_LEAF_ILP > 1
-#undef HB_LEAF_ILP
-#define HB_LEAF_ILP 1
-#endif
 #include "lines.h"
 #include "pair3.h"
 

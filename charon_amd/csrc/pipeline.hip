@@ -4,11 +4,6 @@
 // Compiled with HB_FAST_FPMUL: every field / curve / tower function is inlined; the Fp product and
 // square are the only calls (fp.h fp_mul_leaf / fp_sqr_leaf, compiler-visible C++).
 #define HB_FAST_FPMUL 1
-// product leaves (fp.h HB_LEAF_ILP): at most form 0 here -- the pairing kernels run one wave per SIMD
-#if defined(HB_LEAF_ILP) && HB_LEAF_ILP > 0
-#undef HB_LEAF_ILP
-#define HB_LEAF_ILP 0
-#endif
 #define HB_ARG_LANES 128  // k_lml: two-wave workgroups
 #include "lines.h"
 #include "pair3.h"

@@ -121,31 +121,6 @@ __global__ KB_OCC(HB_OCC_SUBG) void k_g2_subgroup(uint32_t n, HmEntry* __restric
   }
 }
 
-// One lane per public key of a host-buffer call with a key cache (hbls_pubkey_cache_add): the
-// cached entry when idx[i] names one, else decompressed here like k_dec_pk.
-__global__ KB_OCC(HB_OCC_DECPK) void k_pk_gather(const uint8_t* __restrict__ pks, const uint32_t* __restrict__ idx,
-                                                 const G1AEntry* __restrict__ tab, const uint8_t* __restrict__ tst,
-                                                 uint32_t n, G1AEntry* __restrict__ out, uint8_t* __restrict__ st) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t k = idx[i];
-  if (k != 0xffffffffu) {
-    out[i] = tab[k];
-    st[i] = tst[k];
-    return;
-  }
-  G1A p;
-  uint8_t bad = g1_decompress(p, pks + 48ull * i);
-  if (bad) p = {fp_zero(), fp_zero(), true};
-  G1AEntry e;
-  e.x = p.x;
-  e.y = p.y;
-  e.inf = p.inf ? 1u : 0u;
-  e.pad[0] = e.pad[1] = e.pad[2] = 0;
-  out[i] = e;
-  st[i] = bad;
-}
-
 // ---- decompressed-signature cache (host-buffer calls: hbls_verify_batch fills it,
 // hbls_threshold_aggregate_batch reads it -- charon's parsigex Verify -> parsigdb -> sigagg flow,
 // where the aggregation's partials are exactly partials verified before).  A ring of `cap`
@@ -223,6 +198,74 @@ __global__ __launch_bounds__(64) void k_sc_get(const uint8_t* __restrict__ sigs,
     }
   }
   hit[i] = h;
+}
+
+// ---- public-key cache on the device (hbls_pubkey_cache_add): the compressed keys of the table's
+// entries and an open-addressing index of them (entry + 1, 0 = empty; SC_PROBES slots from a keyed
+// hash of the 48 bytes), so a host-buffer verification finds its keys on the device instead of
+// looking each one up on the host (1 M host lookups cost ~0.3 s).  Entries are only added (and the
+// whole table dropped by hbls_pubkey_cache_clear), so no slot is ever stale.
+__device__ __forceinline__ uint32_t kc_hash(const uint4* k, uint64_t k0, uint64_t k1) {
+  uint64_t h = k1;
+  HB_UNROLL for (int j = 0; j < 3; j++) {
+    const uint64_t v = ((uint64_t)k[j].y << 32 | k[j].x) ^ ((uint64_t)k[j].w << 32 | k[j].z) * 0x9e3779b97f4a7c15ull;
+    h = (h ^ v) * 0xff51afd7ed558ccdull + k0;
+    h ^= h >> 29;
+  }
+  h *= 0xc4ceb9fe1a85ec53ull;
+  return (uint32_t)(h >> 32);
+}
+__device__ __forceinline__ void kc_key_load(const uint8_t* p, uint4* k) {
+  HB_UNROLL for (int j = 0; j < 3; j++) k[j] = ((const uint4*)p)[j];
+}
+// entries first .. first + m - 1 (keys already at keys[48 e]) into the index
+__global__ __launch_bounds__(64) void k_kc_index(const uint8_t* __restrict__ keys, uint32_t first, uint32_t m,
+                                                 uint32_t* __restrict__ tab, uint32_t tcap, uint64_t k0, uint64_t k1) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  const uint32_t e = first + i;
+  uint4 kb[3];
+  kc_key_load(keys + 48ull * e, kb);
+  const uint32_t home = kc_hash(kb, k0, k1) & (tcap - 1);
+  for (uint32_t q = 0; q < tcap; q++)  // load factor <= 1/2: a free slot exists
+    if (atomicCAS(&tab[(home + q) & (tcap - 1)], 0u, e + 1) == 0u) return;
+}
+// One lane per public key: the cached entry when its 48 bytes are in the index, else decompressed
+// here like k_dec_pk (+ the subgroup check)
+__global__ KB_OCC(HB_OCC_DECPK) void k_pk_cached(const uint8_t* __restrict__ pks, uint32_t n,
+                                                 const uint8_t* __restrict__ keys, const G1AEntry* __restrict__ tabe,
+                                                 const uint8_t* __restrict__ tst, const uint32_t* __restrict__ tab,
+                                                 uint32_t tcap, uint64_t k0, uint64_t k1, G1AEntry* __restrict__ out,
+                                                 uint8_t* __restrict__ st) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint4 kb[3];
+  kc_key_load(pks + 48ull * i, kb);
+  const uint32_t home = kc_hash(kb, k0, k1) & (tcap - 1);
+  for (uint32_t q = 0; q < tcap; q++) {
+    const uint32_t v = tab[(home + q) & (tcap - 1)];
+    if (v == 0) break;
+    uint4 ke[3];
+    kc_key_load(keys + 48ull * (v - 1), ke);
+    bool eq = true;
+    HB_UNROLL for (int j = 0; j < 3; j++)
+      eq = eq && ke[j].x == kb[j].x && ke[j].y == kb[j].y && ke[j].z == kb[j].z && ke[j].w == kb[j].w;
+    if (eq) {
+      out[i] = tabe[v - 1];
+      st[i] = tst[v - 1];
+      return;
+    }
+  }
+  G1A p;
+  uint8_t bad = g1_decompress(p, pks + 48ull * i);
+  if (bad) p = {fp_zero(), fp_zero(), true};
+  G1AEntry e;
+  e.x = p.x;
+  e.y = p.y;
+  e.inf = p.inf ? 1u : 0u;
+  e.pad[0] = e.pad[1] = e.pad[2] = 0;
+  out[i] = e;
+  st[i] = bad;
 }
 
 // the random coefficient r = a + b lambda of entry `item` (SHA-256 of key || item, one block)
@@ -648,9 +691,16 @@ void launch_dec_pk(const uint8_t* pks, uint32_t n, G1AEntry* out, uint8_t* st, h
   hipLaunchKernelGGL(k_dec_pk, dim3(blocks_for(n)), dim3(BLOCK), 0, s, pks, n, out, st);
   hipLaunchKernelGGL(k_g1_subgroup, dim3(blocks_for(n)), dim3(BLOCK), 0, s, n, out, st);
 }
-void launch_pk_gather(const uint8_t* pks, const uint32_t* idx, const G1AEntry* tab, const uint8_t* tst, uint32_t n,
-                      G1AEntry* out, uint8_t* st, hipStream_t s) {
-  if (n) hipLaunchKernelGGL(k_pk_gather, dim3(blocks_for(n)), dim3(BLOCK), 0, s, pks, idx, tab, tst, n, out, st);
+void launch_kc_index(const uint8_t* keys, uint32_t first, uint32_t m, uint32_t* tab, uint32_t tcap, uint64_t k0,
+                     uint64_t k1, hipStream_t s) {
+  if (m) hipLaunchKernelGGL(k_kc_index, dim3(blocks_for(m)), dim3(BLOCK), 0, s, keys, first, m, tab, tcap, k0, k1);
+}
+void launch_pk_cached(const uint8_t* pks, uint32_t n, const uint8_t* keys, const G1AEntry* tabe, const uint8_t* tst,
+                      const uint32_t* tab, uint32_t tcap, uint64_t k0, uint64_t k1, G1AEntry* out, uint8_t* st,
+                      hipStream_t s) {
+  if (n)
+    hipLaunchKernelGGL(k_pk_cached, dim3(blocks_for(n)), dim3(BLOCK), 0, s, pks, n, keys, tabe, tst, tab, tcap, k0, k1,
+                       out, st);
 }
 void launch_dec_sig_pt(const uint8_t* sigs, uint32_t n, HmEntry* out, uint8_t* st, hipStream_t s, const uint8_t* skip) {
   if (!n) return;

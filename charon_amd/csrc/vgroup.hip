@@ -6,11 +6,6 @@
 // a compiler-visible product was exact (tests/native/devcheck_vb.hip).  That
 // subroutine is gone; the kernel is compiled like the other fast units.
 #define HB_FAST_FPMUL 1
-// product leaves (fp.h HB_LEAF_ILP): at most form 0 here -- the line kernels run one wave per SIMD
-#if defined(HB_LEAF_ILP) && HB_LEAF_ILP > 0
-#undef HB_LEAF_ILP
-#define HB_LEAF_ILP 0
-#endif
 #include "lines.h"
 #include "pair3.h"
 

@@ -619,7 +619,7 @@ extern "C" int hc_mul64_selftest(int iters, uint64_t seed) {
     const F2L fr = f2l_mul(fa, fb);
     for (int i = 0; i < 14; i++) m0[i] = fr.c0.l[i], m1[i] = fr.c1.l[i];
     bad += memcmp(l0, m0, sizeof l0) != 0 || memcmp(l1, m1, sizeof l1) != 0;
-    // the paired leaves' core (ec28.h mul28x2_core, HB_LEAF_ILP): two products / squares at once
+    // the paired leaves' core (ec28.h mul28x2_core, the G1 formulas): two products / squares at once
     for (int lazy = 0; lazy < 2; lazy++) {
       limbs(x, lazy ? 30 : 28), limbs(y, lazy ? 30 : 28), limbs(z, lazy ? 30 : 28), limbs(u, lazy ? 30 : 28);
       mul28x2_core<false>(l0, l1, x, y, z, u);

@@ -259,22 +259,12 @@ def test_fp_inv_divsteps(hc):
     assert worst <= 34, worst  # FP_INV_BATCHES = 40
 
 
-def test_leaf_ilp_cores_match():
-    """the product cores as the HB_LEAF_ILP=2 build compiles them (the Fp2 product's passes
-    interleaved, the paired products / squares, the carry-seeded single chains) return bit for bit
-    the 64-bit host products: a separate build of the harness"""
-    from charon_amd.build import build_hostcheck
-    lib = ctypes.CDLL(build_hostcheck(verbose=False, defines=("HB_LEAF_ILP=2",),
-                                      out=os.path.join(os.path.dirname(__file__), "native", "libhbls_hostcheck_ilp.so")))
-    lib.hc_mul64_selftest.argtypes = [ctypes.c_int, ctypes.c_uint64]
-    assert lib.hc_mul64_selftest(3000, 2835) == 0
-
-
 def test_host_mul64_matches_r28(hc):
     """hostmul64.h (the host builds' 64-bit Montgomery products: the CPU baseline and this harness)
     returns bit for bit what the 28-bit cores of fp.h / ec28.h return: stored-word products and
     squares, the Fp2 product with its signed real part, 28-bit-limb products on normalised and
-    lazy limbs, the lazy Fp2 dot product and f2l_mul"""
+    lazy limbs, the lazy Fp2 dot product, f2l_mul and the paired products / squares of the G1
+    formulas (ec28.h mul28x2_core)"""
     hc.hc_mul64_selftest.argtypes = [ctypes.c_int, ctypes.c_uint64]
     assert hc.hc_mul64_selftest(4000, 2834) == 0
 
