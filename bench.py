@@ -795,11 +795,19 @@ def main(argv=None):
                           "k_pair3_mls": (1, tuple(a + b for a, b in zip(per_unit["k_pair3_mls"], per_unit["k_slines"]))),
                           "k_pair3_mml": (V, opcounts.pair3_mml(pairs=mmlk)),
                           "k_mml_eval": (V, per_unit["k_mml_eval"]),
+                          "k_lines_at_p": (0, per_unit["k_lines_at_p"]),
                           "k_pair3_prod": (n_prod, per_unit["k_pair3_prod"]),
                           "k_pair3_fin": (1, fin), "k_slines": (1, per_unit["k_slines"]),
                           "k_msm_bucket": (opcounts.MSM_ENTRIES_PER_ITEM * n_rlc, per_unit["k_msm_bucket"]),
                           "k_msm_reduce": (opcounts.MSM_PARTS, per_unit["k_msm_reduce"]),
                           "k_msm_sum": (opcounts.MSM_PARTS + opcounts.MSM_PARTS // 128, per_unit["k_msm_sum"])})
+            if M >= V and not fallback:
+                # distinct messages, one group each (hipbls.hip defer_lines): the chains evaluated at
+                # P by k_lines_at_p; the unevaluated lines only behind a failed check (k_lines_msg
+                # guarded, k_mml_eval not launched)
+                units["k_lines_at_p"] = (V, per_unit["k_lines_at_p"])
+                units["k_lines_msg"] = (0, per_unit["k_lines_msg"])
+                units["k_mml_eval"] = (0, per_unit["k_mml_eval"])
             if fallback:
                 for kname in ("k_group_prep", "k_pair3_fin", "k_slines", "k_pair3_ml", "k_pair3_fallback", "k_fb_lines"):
                     units[kname] = (0, units.get(kname, (0, (0, 0)))[1])

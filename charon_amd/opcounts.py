@@ -344,6 +344,8 @@ def per_unit(b=BLOCKS, group_size=1, t=1):
         "k_pair3_prod": (b["f12_mul"], 3 * 18),
         "k_pair3_mml": pair3_mml(b),
         "k_mml_eval": mml_eval(b),
+        # distinct-message slots (round 5): the chain of H(m_g) evaluated at P_g inside it
+        "k_lines_at_p": (b["lines_uneval"] + mml_eval(b)[0],) * 2,
         "k_msm_bucket": (msm_bucket(b),) * 2,
         "k_msm_reduce": (msm_reduce(b),) * 2,
         "k_msm_sum": (b["jac_add_g2"],) * 2,
@@ -359,7 +361,7 @@ UNITS = {"k_pair3": "pairing check", "k_pair3_fallback": "pairing check", "k_dec
          "k_pair3_ml": "verification group", "k_pair3_fin": "final exponentiation",
          "k_slines": "batch of 64 groups", "k_group_prep_p": "verification group",
          "k_pair3_prod": "stored Miller loop", "k_pair3_mml": "verification group", "k_msm_bucket": "bucket entry", "k_msm_reduce": "chunk of 16 buckets",
-         "k_msm_sum": "point", "k_mml_eval": "verification group", "k_pair3_mls": "final exponentiation", "k_ta_small": "aggregation group (validator)"}
+         "k_msm_sum": "point", "k_mml_eval": "verification group", "k_lines_at_p": "verification group", "k_pair3_mls": "final exponentiation", "k_ta_small": "aggregation group (validator)"}
 
 # SHA-256 compressions per attestation signing root (roots.hip: 8 two-block hashes)
 SHA256_PER_ATTESTATION_ROOT = 16
