@@ -20,7 +20,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 SOURCES = ["hipbls.hip", "pipeline.hip", "threshold.hip", "vbatch.hip", "vgroup.hip", "roots.hip", "hash.hip", "msm.hip",
            "hashsplit.hip"]
 HEADERS = ["hd.h", "consts.h", "fp.h", "fr.h", "tower.h", "ec.h", "ec28.h", "sha256.h", "h2c.h", "pairing.h", "ops.h", "pair3.h",
-           "pair6.h", "layout.h", "lines.h", "rlc.h", "ta_small.h", "pair28.h", "hostmul64.h", "coalesce.h"]
+           "pair6.h", "layout.h", "lines.h", "rlc.h", "ta_small.h", "pair28.h", "hostmul64.h", "coalesce.h", "msgtable.h"]
 
 
 def _newer(target, deps):

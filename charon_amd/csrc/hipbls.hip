@@ -10,6 +10,7 @@
 #include "layout.h"
 #include "../../include/hipbls.h"
 #include "coalesce.h"
+#include "msgtable.h"
 
 #include <rccl/rccl.h>
 #include <sys/random.h>
@@ -1392,64 +1393,6 @@ bool defer_lines(size_t n_groups, size_t n_msgs) {
 // ---------------------------------------------------------------------------------------
 // Host-buffer calls: staging, message dedup, multi-device sharding
 // ---------------------------------------------------------------------------------------
-struct MsgTable {
-  std::vector<uint8_t> bytes;
-  std::vector<uint64_t> off;
-  std::vector<uint32_t> len;
-  std::vector<uint32_t> idx;  // per item
-};
-
-// 64-bit words of the message folded by multiply-xorshift steps (messages are usually 32-byte
-// signing roots, already uniform: four steps instead of FNV's 32 byte-wise multiplies)
-inline uint64_t msg_hash(const uint8_t* p, uint32_t n) {
-  uint64_t h = 0xcbf29ce484222325ull ^ n;
-  uint32_t k = 0;
-  for (; k + 8 <= n; k += 8) {
-    uint64_t w;
-    memcpy(&w, p + k, 8);
-    h = (h ^ w) * 0x9e3779b97f4a7c15ull;
-    h ^= h >> 31;
-  }
-  for (; k < n; k++) h = (h ^ p[k]) * 0x100000001b3ull;
-  h ^= h >> 29;
-  h *= 0xbf58476d1ce4e5b9ull;
-  return h ^ (h >> 32);
-}
-
-// distinct messages of the items (open addressing on item indices: no per-message allocation;
-// a slot's million host-buffer partials dedup in a few milliseconds)
-void dedup_messages(const uint8_t* msgs, const uint64_t* off, const uint32_t* len, size_t n, const size_t* items,
-                    MsgTable& t) {
-  size_t cap = 16;
-  while (cap < 2 * n + 2) cap <<= 1;
-  std::vector<uint32_t> slot(cap, 0xffffffffu);  // distinct-message id, or empty
-  std::vector<uint64_t> src;                      // first item of each distinct message
-  t.idx.resize(n);
-  for (size_t k = 0; k < n; k++) {
-    const size_t i = items ? items[k] : k;
-    const uint8_t* m = msgs + off[i];
-    const uint32_t l = len[i];
-    size_t h = (size_t)msg_hash(m, l) & (cap - 1);
-    uint32_t id;
-    for (;;) {
-      id = slot[h];
-      if (id == 0xffffffffu) break;
-      const uint64_t j = src[id];
-      if (len[j] == l && memcmp(msgs + off[j], m, l) == 0) break;
-      h = (h + 1) & (cap - 1);
-    }
-    if (id == 0xffffffffu) {
-      id = (uint32_t)t.len.size();
-      slot[h] = id;
-      src.push_back(i);
-      t.off.push_back(t.bytes.size());
-      t.len.push_back(l);
-      t.bytes.insert(t.bytes.end(), m, m + l);
-    }
-    t.idx[k] = id;
-  }
-}
-
 // Upload the distinct messages (library stream) and hash them; with a workspace set, the hashing
 // runs on its side stream 2 (beside the decompression the verification forks next) and *ready is
 // the event the verification waits on before it needs H(m).
@@ -1807,7 +1750,11 @@ int verify_host(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msgs, co
   const double t_start = now_ms();
   // global message ids, order items by (message, position), groups of <= g_gmax
   MsgTable all;
-  dedup_messages(msgs, msg_off, msg_len, n, nullptr, all);
+  const unsigned hw = std::thread::hardware_concurrency();
+  if (n >= (1u << 16) && hw >= 4)
+    dedup_messages_par(msgs, msg_off, msg_len, n, all, hw >= 8 ? 8u : 4u);
+  else
+    dedup_messages(msgs, msg_off, msg_len, n, nullptr, all);
   // items ordered by message id, stable (a counting sort: one pass, no comparisons)
   std::vector<size_t> order(n), mstart(all.len.size() + 1, 0);
   for (size_t k = 0; k < n; k++) mstart[all.idx[k] + 1]++;
@@ -1937,9 +1884,11 @@ int check_offsets(const uint32_t* grp_off, size_t n_groups) {
 int group_op_host(const uint8_t* sigs, const int64_t* idx, const uint32_t* grp_off, size_t n_groups, int mode,
                   uint8_t* out, uint8_t* status) {
   if (check_offsets(grp_off, n_groups)) return -1;
+  const double t_start = now_ms();
   return for_each_device_hc(n_groups, [&](Dev& d, Hc& h, size_t gb, size_t ge, std::unique_lock<std::mutex>& lk) -> int {
     const size_t ng = ge - gb, pb = grp_off[gb], np = grp_off[ge] - pb;
     if (ng == 0) return 0;
+    const double t_locked = now_ms();
     std::vector<uint32_t> goff(ng + 1);
     for (size_t g = 0; g <= ng; g++) goff[g] = grp_off[gb + g] - (uint32_t)pb;
     uint8_t* dsig;
@@ -1965,9 +1914,13 @@ int group_op_host(const uint8_t* sigs, const int64_t* idx, const uint32_t* grp_o
       return -1;
     if (ws_release(w, h.s)) return -1;
     lk.unlock();  // enqueued: other callers may enqueue while this one waits for its stream
+    const double t_enq = now_ms();
     HCHK(hipMemcpyAsync(out + 96 * gb, dout, ng * 96, hipMemcpyDeviceToHost, h.s));
     HCHK(hipMemcpyAsync(status + gb, dst, ng, hipMemcpyDeviceToHost, h.s));
     HCHK(hipStreamSynchronize(h.s));
+    if (host_timing())
+      fprintf(stderr, "hbls group_op mode=%d groups=%zu members=%zu cache=%d: lock wait %.2f ms, enqueue+upload %.2f, "
+              "device %.2f\n", mode, ng, np, hit ? 1 : 0, t_locked - t_start, t_enq - t_locked, now_ms() - t_enq);
     return 0;
   });
 }

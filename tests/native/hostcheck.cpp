@@ -990,3 +990,21 @@ extern "C" int hc_lines_at_p(const uint8_t* q192, const uint8_t* p96, uint8_t* o
   }
   return bad;
 }
+
+// msgtable.h: the distinct messages of n items by the sequential dedup (threads 0) or the parallel
+// one (threads 4 / 8).  idx: each item's id; returns the number of distinct messages, or -1 if a
+// table entry's bytes differ from an item it names.
+#include "../../charon_amd/csrc/msgtable.h"
+extern "C" long hc_dedup(const uint8_t* msgs, const uint64_t* off, const uint32_t* len, size_t n, int threads,
+                         uint32_t* idx) {
+  MsgTable t;
+  if (threads) dedup_messages_par(msgs, off, len, n, t, (unsigned)threads);
+  else dedup_messages(msgs, off, len, n, nullptr, t);
+  for (size_t k = 0; k < n; k++) {
+    const uint32_t id = t.idx[k];
+    idx[k] = id;
+    if (id >= t.len.size() || t.len[id] != len[k] || memcmp(t.bytes.data() + t.off[id], msgs + off[k], len[k]) != 0)
+      return -1;
+  }
+  return (long)t.len.size();
+}
