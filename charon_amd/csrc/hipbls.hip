@@ -342,7 +342,8 @@ struct Ws {
 };
 
 // host-call staging buffers (inputs and outputs of the host-buffer entry points)
-enum IoId { I_PK, I_SIG, I_MSG, I_OFF, I_LEN, I_MIDX, I_HM, I_STAT, I_IDX, I_GOFF, I_OUT, I_SK, I_VGOFF, I_HM2, I_COUNT };
+enum IoId { I_PK, I_SIG, I_MSG, I_OFF, I_LEN, I_MIDX, I_HM, I_STAT, I_IDX, I_GOFF, I_OUT, I_SK, I_VGOFF, I_HM2,
+            I_DPK, I_DPKST, I_DSIG, I_DSIGST, I_COUNT };
 
 constexpr int N_WS_MAX = 8;  // workspace sets per device: HBLS_WS_SETS (default 3)
 int g_ws_sets = 3;
@@ -714,6 +715,16 @@ struct TaFold {
   const uint8_t* dv_pk_table_st;
 };
 
+// Keys and signatures a host-buffer call decompressed in the caller's order before its grouping
+// was known (verify_large): verify_pipeline gathers them in group order instead of decompressing.
+struct PreDec {
+  const G1AEntry* pk;
+  const uint8_t* pk_st;
+  const HmEntry* sig;
+  const uint8_t* sig_st;
+  const uint32_t* order;  // group-order item i = caller item order[i]
+};
+
 // ThresholdAggregate (mode 0) / Aggregate (mode 1) of groups whose members are already
 // decompressed (pts, mst) into ta_out / ta_status; agg_pt (nullable) gets the affine results.
 int ta_tail(Dev& d, Ws& w, const HmEntry* pts, const uint32_t* src, const uint8_t* mst_in, const int64_t* didx,
@@ -791,7 +802,8 @@ int ta_tail(Dev& d, Ws& w, const HmEntry* pts, const uint32_t* src, const uint8_
 int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, const uint32_t* didx,
                     const MsgEntry* hm, size_t n, const uint32_t* dgoff, size_t n_groups, uint8_t* dst,
                     hipStream_t s, hipEvent_t hm_ready, const TaFold* fold, bool kc = false,
-                    hipEvent_t h_ready = nullptr, MsgEntry* defer_hm = nullptr, size_t defer_msgs = 0) {
+                    hipEvent_t h_ready = nullptr, MsgEntry* defer_hm = nullptr, size_t defer_msgs = 0,
+                    const PreDec* pre = nullptr) {
   if (!dgoff) n_groups = n;
   G1AEntry* vpk;
   HmEntry* vsig;
@@ -895,7 +907,11 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
   for (int k = 0; k < 2; k++) HCHK(hipStreamWaitEvent(w.side[k], w.ev_fork, 0));
   // public keys: from the caller's decompressed-key tables when given (static per cluster lock:
   // decompressed and subgroup-checked once), else decompressed here
-  if (fold && fold->pk_table) {
+  if (pre) {  // decompressed before the grouping: gathered in group order
+    TIMED(d, "k_gather_dec", w.side[0],
+          launch_gather_dec(pre->pk, pre->pk_st, pre->sig, pre->sig_st, pre->order, (uint32_t)n, vpk, vpkst, vsig, vsigst,
+                            w.side[0]));
+  } else if (fold && fold->pk_table) {
     vpk = const_cast<G1AEntry*>(fold->pk_table);
     vpkst = const_cast<uint8_t*>(fold->pk_table_st);
   } else if (kc && d.kc_n) {  // host-buffer call with the key cache: cached entries, the rest decompressed
@@ -912,7 +928,7 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
   } else if (n_agg) {
     TIMED(d, "k_dec_pk", w.side[0], launch_dec_pk(fold->dv_pks, (uint32_t)n_agg, apk, apkst, w.side[0]));
   }
-  TIMED(d, "k_dec_sig_pt", w.side[1], launch_dec_sig_pt(dsig, (uint32_t)n, vsig, vsigst, w.side[1]));
+  if (!pre) TIMED(d, "k_dec_sig_pt", w.side[1], launch_dec_sig_pt(dsig, (uint32_t)n, vsig, vsigst, w.side[1]));
   HCHK(hipEventRecord(w.ev_side[0], w.side[0]));
   HCHK(hipEventRecord(w.ev_side[1], w.side[1]));
 
@@ -1625,24 +1641,75 @@ static double now_ms() {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-// A large one-device Verify batch in chunks of whole groups, each on its own host-call context
-// (stream, staging buffers) and workspace set, so that -- like consecutive slots in flight -- one
-// chunk's decompression and hashing overlap the previous chunk's pairings and latency-bound tail
-// instead of the call running as one slot with nothing beside it.  The caller's keys, signatures
-// and messages are uploaded once (context h0); each chunk gathers its items in group order,
-// hashes its own contiguous range of the message table (items are sorted by message), verifies,
-// fills the signature cache and scatters its statuses into the call's status array, downloaded
-// once.  Extra contexts are taken only if idle (hc_try_acquire); with none the call is one chunk.
+// A large one-device Verify batch.  Its keys and signatures are uploaded and decompressed in the
+// caller's order FIRST -- the grouping (message dedup and sort on the host, ~10-17 ms for a slot's
+// million partials) then runs while the GPU decompresses, instead of in front of everything --
+// and the signature cache is filled from them.  Then the groups run in chunks of whole groups,
+// each on its own host-call context (stream, staging buffers) and workspace set, so that -- like
+// consecutive slots in flight -- one chunk's hashing and combination overlap the previous chunk's
+// pairings and latency-bound tail; each chunk gathers its decompressed items in group order
+// (PreDec), hashes its own contiguous range of the message table (items are sorted by message;
+// chunks only when every message has one group), verifies and scatters its statuses into the
+// call's status array, downloaded once.  Extra contexts are taken only if idle (hc_try_acquire).
 constexpr size_t CHUNK_MIN_ITEMS = size_t(1) << 18;
-int verify_chunks(Dev& d, Hc& h0, std::unique_lock<std::mutex>& lk, const uint8_t* pks, const uint8_t* sigs,
-                  const MsgTable& all, const std::vector<uint32_t>& order32, const std::vector<size_t>& gstart,
-                  size_t n_groups, size_t n, uint8_t* status, double t_start, double t_grouped) {
-  const double t_called = now_ms();
+int verify_large(Dev& d, const uint8_t* pks, const uint8_t* sigs, const uint8_t* msgs, const uint64_t* msg_off,
+                 const uint32_t* msg_len, size_t n, uint8_t* status) {
+  const double t_start = now_ms();
+  Hc& h0 = hc_acquire(d);
+  struct Rel0 {
+    Dev& d;
+    Hc& h;
+    ~Rel0() { hc_release(d, h); }
+  } rel0{d, h0};
+  std::unique_lock<std::mutex> lk(d.mu);
+  if (hipSetDevice(d.ord) != hipSuccess) return set_err("hipSetDevice failed");
+  const double t_locked0 = now_ms();
+  // 1. keys and signatures up and decompressed in the caller's order (the key cache consulted)
+  uint8_t *rpk, *rsig;
+  void *pe, *pst, *se, *sst;
+  if (upload(d, I_PK, pks, 48 * n, &rpk, &h0) || upload(d, I_SIG, sigs, 96 * n, &rsig, &h0) ||
+      ensure_buf(h0.io[I_DPK], n * sizeof(G1AEntry), &pe) || ensure_buf(h0.io[I_DPKST], n, &pst) ||
+      ensure_buf(h0.io[I_DSIG], n * sizeof(HmEntry), &se) || ensure_buf(h0.io[I_DSIGST], n, &sst))
+    return -1;
+  G1AEntry* dpk = (G1AEntry*)pe;
+  HmEntry* dsg = (HmEntry*)se;
+  uint8_t *dpkst = (uint8_t*)pst, *dsgst = (uint8_t*)sst;
+  if (d.kc_n)
+    TIMED(d, "k_dec_pk", h0.s,
+          launch_pk_cached(rpk, (uint32_t)n, (const uint8_t*)d.kc_keys.p, (const G1AEntry*)d.kc_tab.p,
+                           (const uint8_t*)d.kc_st.p, (const uint32_t*)d.kc_hidx.p, (uint32_t)d.kc_tcap, g_sc_k0,
+                           g_sc_k1, dpk, dpkst, h0.s));
+  else
+    TIMED(d, "k_dec_pk", h0.s, launch_dec_pk(rpk, (uint32_t)n, dpk, dpkst, h0.s));
+  TIMED(d, "k_dec_sig_pt", h0.s, launch_dec_sig_pt(rsig, (uint32_t)n, dsg, dsgst, h0.s));
+  if (sc_put(d, rsig, dsg, dsgst, n, h0.s)) return -1;  // the aggregation of these partials reads them
   lk.unlock();
+  const double t_dec = now_ms();
+  // 2. the grouping on the host, beside the decompression: message ids, items ordered by message
+  // (a counting sort), groups of <= g_gmax items over one message
+  MsgTable all;
+  const unsigned hw = std::thread::hardware_concurrency();
+  if (hw >= 4)
+    dedup_messages_par(msgs, msg_off, msg_len, n, all, hw >= 8 ? 8u : 4u);
+  else
+    dedup_messages(msgs, msg_off, msg_len, n, nullptr, all);
+  const size_t nm = all.len.size();
+  std::vector<uint32_t> order32(n), mstart(nm + 1, 0);
+  for (size_t k = 0; k < n; k++) mstart[all.idx[k] + 1]++;
+  for (size_t j = 0; j < nm; j++) mstart[j + 1] += mstart[j];
+  for (size_t k = 0; k < n; k++) order32[mstart[all.idx[k]]++] = (uint32_t)k;
+  std::vector<size_t> gstart;
   std::vector<uint32_t> midx(n);
-  for (size_t k = 0; k < n; k++) midx[k] = all.idx[order32[k]];
+  for (size_t k = 0; k < n; k++) {
+    midx[k] = all.idx[order32[k]];
+    if (k == 0 || midx[k] != midx[k - 1] || k - gstart.back() >= g_gmax) gstart.push_back(k);
+  }
+  const size_t n_groups = gstart.size();
+  gstart.push_back(n);
+  const bool defer = defer_lines(n_groups, nm);
+  // chunks (one per idle context, messages of one group each) at group starts, ~n / K items each
   std::vector<Hc*> hcs{&h0};
-  const size_t k_want = std::min<size_t>((size_t)g_ws_sets, std::max<size_t>(1, n / CHUNK_MIN_ITEMS));
+  const size_t k_want = defer ? std::min<size_t>((size_t)g_ws_sets, std::max<size_t>(1, n / CHUNK_MIN_ITEMS)) : 1;
   while (hcs.size() < k_want) {
     Hc* x = hc_try_acquire(d);
     if (!x) break;
@@ -1655,12 +1722,10 @@ int verify_chunks(Dev& d, Hc& h0, std::unique_lock<std::mutex>& lk, const uint8_
       for (size_t c = 1; c < h.size(); c++) hc_release(d, *h[c]);
     }
   } rel{d, hcs};
-  // chunk boundaries at group starts, about n / K items each
   const size_t K = hcs.size();
   std::vector<size_t> cg{0};
   for (size_t c = 1; c < K; c++) {
-    const size_t target = n * c / K;
-    const size_t g = (size_t)(std::lower_bound(gstart.begin(), gstart.begin() + n_groups, target) - gstart.begin());
+    const size_t g = (size_t)(std::lower_bound(gstart.begin(), gstart.begin() + n_groups, n * c / K) - gstart.begin());
     if (g > cg.back() && g < n_groups) cg.push_back(g);
   }
   cg.push_back(n_groups);
@@ -1669,22 +1734,20 @@ int verify_chunks(Dev& d, Hc& h0, std::unique_lock<std::mutex>& lk, const uint8_
     goffs[c].resize(cg[c + 1] - cg[c] + 1);
     for (size_t g = cg[c]; g <= cg[c + 1]; g++) goffs[c][g - cg[c]] = (uint32_t)(gstart[g] - gstart[cg[c]]);
   }
-  const double t_prep = now_ms();
+  const double t_grouped = now_ms();
   lk.lock();
   const double t_locked = now_ms();
-  // shared uploads on h0
-  uint8_t *rpk, *rsig;
+  // 3. the grouping up (h0, after the decompression), then the chunks
   uint32_t *dord, *dmidx;
   uint8_t* dmsg;
   uint64_t* doff;
   uint32_t* dlen;
   void *hmp, *stp;
-  if (upload(d, I_PK, pks, 48 * n, &rpk, &h0) || upload(d, I_SIG, sigs, 96 * n, &rsig, &h0) ||
-      upload(d, I_IDX, order32.data(), n, &dord, &h0) || upload(d, I_MIDX, midx.data(), n, &dmidx, &h0) ||
+  if (upload(d, I_IDX, order32.data(), n, &dord, &h0) || upload(d, I_MIDX, midx.data(), n, &dmidx, &h0) ||
       upload(d, I_MSG, all.bytes.data(), all.bytes.size(), &dmsg, &h0) ||
       upload(d, I_OFF, all.off.data(), all.off.size(), &doff, &h0) ||
       upload(d, I_LEN, all.len.data(), all.len.size(), &dlen, &h0) ||
-      ensure_buf(h0.io[I_HM], all.len.size() * sizeof(MsgEntry), &hmp) || ensure_buf(h0.io[I_HM2], n, &stp))
+      ensure_buf(h0.io[I_HM], nm * sizeof(MsgEntry), &hmp) || ensure_buf(h0.io[I_HM2], n, &stp))
     return -1;
   MsgEntry* hm = (MsgEntry*)hmp;
   uint8_t* dst_out = (uint8_t*)stp;
@@ -1694,22 +1757,14 @@ int verify_chunks(Dev& d, Hc& h0, std::unique_lock<std::mutex>& lk, const uint8_
     hipStream_t sc = hc.s;
     if (c) HCHK(hipStreamWaitEvent(sc, h0.ev, 0));
     const size_t ib = gstart[cg[c]], m = gstart[cg[c + 1]] - ib, ng = cg[c + 1] - cg[c];
-    const size_t mfirst = midx[ib], mcount = midx[ib + m - 1] + 1 - mfirst;  // the chunk's messages
+    // the chunk's messages: all of them for one chunk, else its contiguous range
+    const size_t mfirst = K == 1 ? 0 : midx[ib], mcount = K == 1 ? nm : midx[ib + m - 1] + 1 - midx[ib];
     Ws& w = ws_acquire(d, sc);
-    // the chunk's items in group order
-    void *pio, *sio;
+    void* sio;
     uint32_t* dgoff;
-    if (ensure_buf(hc.io[I_OUT], 144 * m, &pio) || ensure_buf(hc.io[I_STAT], m, &sio) ||
-        upload(d, I_VGOFF, goffs[c].data(), goffs[c].size(), &dgoff, &hc))
+    if (ensure_buf(hc.io[I_STAT], m, &sio) || upload(d, I_VGOFF, goffs[c].data(), goffs[c].size(), &dgoff, &hc))
       return -1;
-    uint8_t* dpk = (uint8_t*)pio;
-    uint8_t* dsig = dpk + 48 * m;
     uint8_t* dst = (uint8_t*)sio;
-    LAUNCH(k_gather_items, m, sc, (const uint4*)rpk, (const uint4*)rsig, dord + ib, (uint32_t)m, (uint4*)dpk,
-           (uint4*)dsig);
-    // its messages hashed on the workspace's hashing stream (lines deferred when the groups have
-    // one message each)
-    const bool defer = defer_lines(ng, mcount);
     HCHK(hipEventRecord(w.ev_ta, sc));
     hipStream_t hs = w.side[2];
     HCHK(hipStreamWaitEvent(hs, w.ev_ta, 0));
@@ -1717,15 +1772,10 @@ int verify_chunks(Dev& d, Hc& h0, std::unique_lock<std::mutex>& lk, const uint8_
     HCHK(hipEventRecord(w.ev_h, hs));
     if (!defer) TIMED(d, "k_lines_msg", hs, launch_lines_msg(hm + mfirst, (uint32_t)mcount, hs));
     HCHK(hipEventRecord(w.ev_side[2], hs));
-    if (verify_pipeline(d, w, dpk, dsig, dmidx + ib, hm, m, dgoff, ng, dst, sc, w.ev_side[2], nullptr, true, w.ev_h,
-                        hm + mfirst, defer ? mcount : 0))
+    const PreDec pre{dpk, dpkst, dsg, dsgst, dord + ib};
+    if (verify_pipeline(d, w, nullptr, nullptr, dmidx + ib, hm, m, dgoff, ng, dst, sc, w.ev_side[2], nullptr, false,
+                        w.ev_h, hm + mfirst, defer ? mcount : 0, &pre))
       return -1;
-    {
-      HmEntry* vsig;
-      uint8_t* vsigst;
-      if (wsbuf(w, W_VSIG, m, &vsig) || wsbuf(w, W_VSIGST, m, &vsigst) || sc_put(d, dsig, vsig, vsigst, m, sc))
-        return -1;
-    }
     LAUNCH(k_scatter_status, m, sc, dst, dord + ib, (uint32_t)m, dst_out);
     if (ws_release(w, sc)) return -1;
     if (c) {
@@ -1738,15 +1788,21 @@ int verify_chunks(Dev& d, Hc& h0, std::unique_lock<std::mutex>& lk, const uint8_
   HCHK(hipMemcpyAsync(status, dst_out, n, hipMemcpyDeviceToHost, h0.s));
   HCHK(hipStreamSynchronize(h0.s));
   if (host_timing())
-    fprintf(stderr, "hbls verify_chunks n=%zu chunks=%zu: group %.2f ms, context wait %.2f, prep %.2f, lock wait %.2f, "
-            "enqueue+upload %.2f, device %.2f\n", n, cg.size() - 1, t_grouped - t_start, t_called - t_grouped,
-            t_prep - t_called, t_locked - t_prep, t_enq - t_locked, now_ms() - t_enq);
+    fprintf(stderr, "hbls verify_large n=%zu chunks=%zu: lock %.2f ms, upload+decompress enqueue %.2f, grouping %.2f "
+            "(beside the GPU), lock wait %.2f, enqueue %.2f, device %.2f\n", n, cg.size() - 1, t_locked0 - t_start,
+            t_dec - t_locked0, t_grouped - t_dec, t_locked - t_grouped, t_enq - t_locked, now_ms() - t_enq);
   return 0;
 }
 
 int verify_host(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msgs, const uint64_t* msg_off,
                 const uint32_t* msg_len, size_t n, uint8_t* status) {
   if (n == 0) return 0;
+  if (n >= 0xffffffffull) return set_err("verify batch: too many items");
+  {
+    const std::vector<Dev*> ds = devs();
+    if (ds.size() == 1 && n >= 2 * CHUNK_MIN_ITEMS && g_ws_sets > 1)
+      return verify_large(*ds[0], pks, sigs, msgs, msg_off, msg_len, n, status);
+  }
   const double t_start = now_ms();
   // global message ids, order items by (message, position), groups of <= g_gmax
   MsgTable all;
@@ -1781,8 +1837,6 @@ int verify_host(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msgs, co
     const size_t ib = gstart[gb], ie = gstart[ge], m = ie - ib;
     if (m == 0) return 0;
     const bool whole = gb == 0 && ge == n_groups;
-    if (whole && n >= 2 * CHUNK_MIN_ITEMS && g_ws_sets > 1 && defer_lines(n_groups, all.len.size()))
-      return verify_chunks(d, h, lk, pks, sigs, all, order32, gstart, n_groups, n, status, t_start, t_grouped);
     // host preparation without the device lock (other callers enqueue meanwhile): the shard's
     // distinct messages and each item's message index in group order -- the whole call's table
     // when one device takes every group

@@ -200,6 +200,22 @@ __global__ __launch_bounds__(64) void k_sc_get(const uint8_t* __restrict__ sigs,
   hit[i] = h;
 }
 
+// One lane per item of a host-buffer call decompressed in the caller's order (hipbls.hip
+// verify_large): the entries of group-order item i from caller item order[i]
+__global__ __launch_bounds__(64) void k_gather_dec(const G1AEntry* __restrict__ pk, const uint8_t* __restrict__ pk_st,
+                                                   const HmEntry* __restrict__ sig, const uint8_t* __restrict__ sig_st,
+                                                   const uint32_t* __restrict__ order, uint32_t n,
+                                                   G1AEntry* __restrict__ opk, uint8_t* __restrict__ opk_st,
+                                                   HmEntry* __restrict__ osig, uint8_t* __restrict__ osig_st) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t j = order[i];
+  opk[i] = pk[j];
+  opk_st[i] = pk_st[j];
+  osig[i] = sig[j];
+  osig_st[i] = sig_st[j];
+}
+
 // ---- public-key cache on the device (hbls_pubkey_cache_add): the compressed keys of the table's
 // entries and an open-addressing index of them (entry + 1, 0 = empty; SC_PROBES slots from a keyed
 // hash of the 48 bytes), so a host-buffer verification finds its keys on the device instead of
@@ -690,6 +706,13 @@ void launch_dec_pk(const uint8_t* pks, uint32_t n, G1AEntry* out, uint8_t* st, h
   if (!n) return;
   hipLaunchKernelGGL(k_dec_pk, dim3(blocks_for(n)), dim3(BLOCK), 0, s, pks, n, out, st);
   hipLaunchKernelGGL(k_g1_subgroup, dim3(blocks_for(n)), dim3(BLOCK), 0, s, n, out, st);
+}
+void launch_gather_dec(const G1AEntry* pk, const uint8_t* pk_st, const HmEntry* sig, const uint8_t* sig_st,
+                       const uint32_t* order, uint32_t n, G1AEntry* opk, uint8_t* opk_st, HmEntry* osig, uint8_t* osig_st,
+                       hipStream_t s) {
+  if (n)
+    hipLaunchKernelGGL(k_gather_dec, dim3(blocks_for(n)), dim3(BLOCK), 0, s, pk, pk_st, sig, sig_st, order, n, opk, opk_st,
+                       osig, osig_st);
 }
 void launch_kc_index(const uint8_t* keys, uint32_t first, uint32_t m, uint32_t* tab, uint32_t tcap, uint64_t k0,
                      uint64_t k1, hipStream_t s) {
