@@ -342,8 +342,7 @@ struct Ws {
 };
 
 // host-call staging buffers (inputs and outputs of the host-buffer entry points)
-enum IoId { I_PK, I_SIG, I_MSG, I_OFF, I_LEN, I_MIDX, I_HM, I_STAT, I_IDX, I_GOFF, I_OUT, I_SK, I_VGOFF, I_HM2,
-            I_DPK, I_DPKST, I_DSIG, I_DSIGST, I_COUNT };
+enum IoId { I_PK, I_SIG, I_MSG, I_OFF, I_LEN, I_MIDX, I_HM, I_STAT, I_IDX, I_GOFF, I_OUT, I_SK, I_VGOFF, I_HM2, I_COUNT };
 
 constexpr int N_WS_MAX = 8;  // workspace sets per device: HBLS_WS_SETS (default 3)
 int g_ws_sets = 3;
@@ -363,7 +362,28 @@ struct Hc {
   hipStream_t s = nullptr;
   DevBuf io[I_COUNT];
   bool busy = false;
-  hipEvent_t ev = nullptr;  // a chunked call's hand-overs between contexts (verify_chunks)
+  hipEvent_t ev = nullptr;  // a chunked call's hand-overs between contexts (verify_large)
+  // pinned staging for uploads queued behind the call's own kernels: a pageable hipMemcpyAsync is
+  // staged by the runtime and returns only once staged, so one queued behind the decompression
+  // held the calling thread until that finished (verify_large's grouping: 20 ms measured; on a
+  // stream of its own beside the kernels the pageable copies took over a second)
+  uint8_t* pin = nullptr;
+  size_t pin_cap = 0;
+};
+
+// host arrays packed into a context's pinned staging, then one asynchronous copy each
+struct PinnedUploads {
+  struct Item {
+    IoId id;
+    const void* src;
+    size_t bytes;
+    void** dst;
+  };
+  std::vector<Item> items;
+  template <class T>
+  void add(IoId id, const T* src, size_t count, T** dst) {
+    items.push_back({id, src, count * sizeof(T), (void**)dst});
+  }
 };
 
 // one record per call that could take the slot-wide check: did it fail (or, skipped, did any batch
@@ -639,6 +659,34 @@ int upload(Dev& d, IoId id, const T* src, size_t count, T** dst, Hc* h = nullptr
   return 0;
 }
 
+// the uploads through h's pinned staging, on h's stream (never blocks the calling thread; the
+// staging is reused by the context's next call only, after this one's stream synchronisation)
+int upload_pinned(Dev& d, Hc& h, const PinnedUploads& u) {
+  auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+  size_t total = 0;
+  for (const auto& it : u.items) total += al(it.bytes);
+  if (total > h.pin_cap) {
+    if (h.pin) HCHK(hipHostFree(h.pin));
+    h.pin = nullptr;
+    h.pin_cap = 0;
+    const size_t cap = std::max(total + total / 4, size_t(1) << 20);
+    HCHK(hipHostMalloc((void**)&h.pin, cap, hipHostMallocDefault));
+    h.pin_cap = cap;
+  }
+  size_t o = 0;
+  for (const auto& it : u.items) {
+    void* p;
+    if (ensure_buf(h.io[it.id], it.bytes, &p)) return -1;
+    if (it.bytes) {
+      memcpy(h.pin + o, it.src, it.bytes);
+      HCHK(hipMemcpyAsync(p, h.pin + o, it.bytes, hipMemcpyHostToDevice, h.s));
+    }
+    *it.dst = p;
+    o += al(it.bytes);
+  }
+  return 0;
+}
+
 Hc& hc_acquire(Dev& d) {
   std::unique_lock<std::mutex> lk(d.hc_mu);
   for (;;) {
@@ -689,7 +737,7 @@ int rlc_key(RlcKey& k) {
 // post-aggregate verification under the DV keys (sigagg.go:117) into the same groups.
 // ---------------------------------------------------------------------------------------
 // verification statistics (HBLS_STATS=1): items, groups, items re-checked alone
-std::atomic<uint64_t> g_stats[6];
+std::atomic<uint64_t> g_stats[8];
 bool stats_on() {
   const char* v = getenv("HBLS_STATS");
   return v && v[0] == '1';
@@ -715,15 +763,6 @@ struct TaFold {
   const uint8_t* dv_pk_table_st;
 };
 
-// Keys and signatures a host-buffer call decompressed in the caller's order before its grouping
-// was known (verify_large): verify_pipeline gathers them in group order instead of decompressing.
-struct PreDec {
-  const G1AEntry* pk;
-  const uint8_t* pk_st;
-  const HmEntry* sig;
-  const uint8_t* sig_st;
-  const uint32_t* order;  // group-order item i = caller item order[i]
-};
 
 // ThresholdAggregate (mode 0) / Aggregate (mode 1) of groups whose members are already
 // decompressed (pts, mst) into ta_out / ta_status; agg_pt (nullable) gets the affine results.
@@ -802,8 +841,7 @@ int ta_tail(Dev& d, Ws& w, const HmEntry* pts, const uint32_t* src, const uint8_
 int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, const uint32_t* didx,
                     const MsgEntry* hm, size_t n, const uint32_t* dgoff, size_t n_groups, uint8_t* dst,
                     hipStream_t s, hipEvent_t hm_ready, const TaFold* fold, bool kc = false,
-                    hipEvent_t h_ready = nullptr, MsgEntry* defer_hm = nullptr, size_t defer_msgs = 0,
-                    const PreDec* pre = nullptr) {
+                    hipEvent_t h_ready = nullptr, MsgEntry* defer_hm = nullptr, size_t defer_msgs = 0) {
   if (!dgoff) n_groups = n;
   G1AEntry* vpk;
   HmEntry* vsig;
@@ -907,11 +945,7 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
   for (int k = 0; k < 2; k++) HCHK(hipStreamWaitEvent(w.side[k], w.ev_fork, 0));
   // public keys: from the caller's decompressed-key tables when given (static per cluster lock:
   // decompressed and subgroup-checked once), else decompressed here
-  if (pre) {  // decompressed before the grouping: gathered in group order
-    TIMED(d, "k_gather_dec", w.side[0],
-          launch_gather_dec(pre->pk, pre->pk_st, pre->sig, pre->sig_st, pre->order, (uint32_t)n, vpk, vpkst, vsig, vsigst,
-                            w.side[0]));
-  } else if (fold && fold->pk_table) {
+  if (fold && fold->pk_table) {
     vpk = const_cast<G1AEntry*>(fold->pk_table);
     vpkst = const_cast<uint8_t*>(fold->pk_table_st);
   } else if (kc && d.kc_n) {  // host-buffer call with the key cache: cached entries, the rest decompressed
@@ -928,7 +962,7 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
   } else if (n_agg) {
     TIMED(d, "k_dec_pk", w.side[0], launch_dec_pk(fold->dv_pks, (uint32_t)n_agg, apk, apkst, w.side[0]));
   }
-  if (!pre) TIMED(d, "k_dec_sig_pt", w.side[1], launch_dec_sig_pt(dsig, (uint32_t)n, vsig, vsigst, w.side[1]));
+  TIMED(d, "k_dec_sig_pt", w.side[1], launch_dec_sig_pt(dsig, (uint32_t)n, vsig, vsigst, w.side[1]));
   HCHK(hipEventRecord(w.ev_side[0], w.side[0]));
   HCHK(hipEventRecord(w.ev_side[1], w.side[1]));
 
@@ -1641,16 +1675,16 @@ static double now_ms() {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-// A large one-device Verify batch.  Its keys and signatures are uploaded and decompressed in the
-// caller's order FIRST -- the grouping (message dedup and sort on the host, ~10-17 ms for a slot's
-// million partials) then runs while the GPU decompresses, instead of in front of everything --
-// and the signature cache is filled from them.  Then the groups run in chunks of whole groups,
-// each on its own host-call context (stream, staging buffers) and workspace set, so that -- like
-// consecutive slots in flight -- one chunk's hashing and combination overlap the previous chunk's
-// pairings and latency-bound tail; each chunk gathers its decompressed items in group order
-// (PreDec), hashes its own contiguous range of the message table (items are sorted by message;
-// chunks only when every message has one group), verifies and scatters its statuses into the
-// call's status array, downloaded once.  Extra contexts are taken only if idle (hc_try_acquire).
+// A large one-device Verify batch.  Its keys and signatures go up in the caller's order while the
+// host groups them (message dedup and sort, ~7-12 ms for a slot's million partials: beside the
+// PCIe upload instead of in front of it); then the groups run in chunks of whole groups, each on
+// its own host-call context (stream) and workspace set, so that -- like consecutive slots in
+// flight -- one chunk's gather, decompression and hashing overlap the previous chunk's pairings
+// and latency-bound tail.  Each chunk gathers its items in group order on the device
+// (k_gather_items), hashes its own contiguous range of the message table (items are sorted by
+// message; chunks only when every message has one group), verifies, enters its signatures into
+// the signature cache and scatters its statuses into the call's status array, downloaded once.
+// Extra contexts are taken only if idle (hc_try_acquire).
 constexpr size_t CHUNK_MIN_ITEMS = size_t(1) << 18;
 int verify_large(Dev& d, const uint8_t* pks, const uint8_t* sigs, const uint8_t* msgs, const uint64_t* msg_off,
                  const uint32_t* msg_len, size_t n, uint8_t* status) {
@@ -1664,29 +1698,13 @@ int verify_large(Dev& d, const uint8_t* pks, const uint8_t* sigs, const uint8_t*
   std::unique_lock<std::mutex> lk(d.mu);
   if (hipSetDevice(d.ord) != hipSuccess) return set_err("hipSetDevice failed");
   const double t_locked0 = now_ms();
-  // 1. keys and signatures up and decompressed in the caller's order (the key cache consulted)
+  // 1. keys and signatures up in the caller's order
   uint8_t *rpk, *rsig;
-  void *pe, *pst, *se, *sst;
-  if (upload(d, I_PK, pks, 48 * n, &rpk, &h0) || upload(d, I_SIG, sigs, 96 * n, &rsig, &h0) ||
-      ensure_buf(h0.io[I_DPK], n * sizeof(G1AEntry), &pe) || ensure_buf(h0.io[I_DPKST], n, &pst) ||
-      ensure_buf(h0.io[I_DSIG], n * sizeof(HmEntry), &se) || ensure_buf(h0.io[I_DSIGST], n, &sst))
-    return -1;
-  G1AEntry* dpk = (G1AEntry*)pe;
-  HmEntry* dsg = (HmEntry*)se;
-  uint8_t *dpkst = (uint8_t*)pst, *dsgst = (uint8_t*)sst;
-  if (d.kc_n)
-    TIMED(d, "k_dec_pk", h0.s,
-          launch_pk_cached(rpk, (uint32_t)n, (const uint8_t*)d.kc_keys.p, (const G1AEntry*)d.kc_tab.p,
-                           (const uint8_t*)d.kc_st.p, (const uint32_t*)d.kc_hidx.p, (uint32_t)d.kc_tcap, g_sc_k0,
-                           g_sc_k1, dpk, dpkst, h0.s));
-  else
-    TIMED(d, "k_dec_pk", h0.s, launch_dec_pk(rpk, (uint32_t)n, dpk, dpkst, h0.s));
-  TIMED(d, "k_dec_sig_pt", h0.s, launch_dec_sig_pt(rsig, (uint32_t)n, dsg, dsgst, h0.s));
-  if (sc_put(d, rsig, dsg, dsgst, n, h0.s)) return -1;  // the aggregation of these partials reads them
+  if (upload(d, I_PK, pks, 48 * n, &rpk, &h0) || upload(d, I_SIG, sigs, 96 * n, &rsig, &h0)) return -1;
   lk.unlock();
-  const double t_dec = now_ms();
-  // 2. the grouping on the host, beside the decompression: message ids, items ordered by message
-  // (a counting sort), groups of <= g_gmax items over one message
+  const double t_up = now_ms();
+  // 2. the grouping on the host, beside the upload: message ids, items ordered by message (a
+  // counting sort), groups of <= g_gmax items over one message
   MsgTable all;
   const unsigned hw = std::thread::hardware_concurrency();
   if (hw >= 4)
@@ -1729,28 +1747,34 @@ int verify_large(Dev& d, const uint8_t* pks, const uint8_t* sigs, const uint8_t*
     if (g > cg.back() && g < n_groups) cg.push_back(g);
   }
   cg.push_back(n_groups);
-  std::vector<std::vector<uint32_t>> goffs(cg.size() - 1);
+  // the chunks' group offsets, concatenated (chunk c's at goff_base[c])
+  std::vector<uint32_t> goffs;
+  std::vector<size_t> goff_base;
   for (size_t c = 0; c + 1 < cg.size(); c++) {
-    goffs[c].resize(cg[c + 1] - cg[c] + 1);
-    for (size_t g = cg[c]; g <= cg[c + 1]; g++) goffs[c][g - cg[c]] = (uint32_t)(gstart[g] - gstart[cg[c]]);
+    goff_base.push_back(goffs.size());
+    for (size_t g = cg[c]; g <= cg[c + 1]; g++) goffs.push_back((uint32_t)(gstart[g] - gstart[cg[c]]));
   }
   const double t_grouped = now_ms();
   lk.lock();
   const double t_locked = now_ms();
-  // 3. the grouping up (h0, after the decompression), then the chunks
-  uint32_t *dord, *dmidx;
+  // 3. the grouping up (pinned: queued behind the raw upload without waiting for it), then the chunks
+  uint32_t *dord, *dmidx, *dlen, *dgoffs;
   uint8_t* dmsg;
   uint64_t* doff;
-  uint32_t* dlen;
-  void *hmp, *stp;
-  if (upload(d, I_IDX, order32.data(), n, &dord, &h0) || upload(d, I_MIDX, midx.data(), n, &dmidx, &h0) ||
-      upload(d, I_MSG, all.bytes.data(), all.bytes.size(), &dmsg, &h0) ||
-      upload(d, I_OFF, all.off.data(), all.off.size(), &doff, &h0) ||
-      upload(d, I_LEN, all.len.data(), all.len.size(), &dlen, &h0) ||
-      ensure_buf(h0.io[I_HM], nm * sizeof(MsgEntry), &hmp) || ensure_buf(h0.io[I_HM2], n, &stp))
+  void *hmp, *stp, *gp;
+  PinnedUploads up;
+  up.add(I_IDX, order32.data(), n, &dord);
+  up.add(I_MIDX, midx.data(), n, &dmidx);
+  up.add(I_MSG, all.bytes.data(), all.bytes.size(), &dmsg);
+  up.add(I_OFF, all.off.data(), all.off.size(), &doff);
+  up.add(I_LEN, all.len.data(), all.len.size(), &dlen);
+  up.add(I_VGOFF, goffs.data(), goffs.size(), &dgoffs);
+  if (upload_pinned(d, h0, up) || ensure_buf(h0.io[I_HM], nm * sizeof(MsgEntry), &hmp) ||
+      ensure_buf(h0.io[I_HM2], n, &stp) || ensure_buf(h0.io[I_OUT], 144 * n, &gp))
     return -1;
   MsgEntry* hm = (MsgEntry*)hmp;
   uint8_t* dst_out = (uint8_t*)stp;
+  uint8_t *gpk = (uint8_t*)gp, *gsig = gpk + 48 * n;  // group order
   HCHK(hipEventRecord(h0.ev, h0.s));
   for (size_t c = 0; c + 1 < cg.size(); c++) {
     Hc& hc = *hcs[c];
@@ -1761,10 +1785,11 @@ int verify_large(Dev& d, const uint8_t* pks, const uint8_t* sigs, const uint8_t*
     const size_t mfirst = K == 1 ? 0 : midx[ib], mcount = K == 1 ? nm : midx[ib + m - 1] + 1 - midx[ib];
     Ws& w = ws_acquire(d, sc);
     void* sio;
-    uint32_t* dgoff;
-    if (ensure_buf(hc.io[I_STAT], m, &sio) || upload(d, I_VGOFF, goffs[c].data(), goffs[c].size(), &dgoff, &hc))
-      return -1;
+    if (ensure_buf(hc.io[I_STAT], m, &sio)) return -1;
     uint8_t* dst = (uint8_t*)sio;
+    uint8_t *cpk = gpk + 48 * ib, *csig = gsig + 96 * ib;
+    LAUNCH(k_gather_items, m, sc, (const uint4*)rpk, (const uint4*)rsig, dord + ib, (uint32_t)m, (uint4*)cpk,
+           (uint4*)csig);
     HCHK(hipEventRecord(w.ev_ta, sc));
     hipStream_t hs = w.side[2];
     HCHK(hipStreamWaitEvent(hs, w.ev_ta, 0));
@@ -1772,10 +1797,17 @@ int verify_large(Dev& d, const uint8_t* pks, const uint8_t* sigs, const uint8_t*
     HCHK(hipEventRecord(w.ev_h, hs));
     if (!defer) TIMED(d, "k_lines_msg", hs, launch_lines_msg(hm + mfirst, (uint32_t)mcount, hs));
     HCHK(hipEventRecord(w.ev_side[2], hs));
-    const PreDec pre{dpk, dpkst, dsg, dsgst, dord + ib};
-    if (verify_pipeline(d, w, nullptr, nullptr, dmidx + ib, hm, m, dgoff, ng, dst, sc, w.ev_side[2], nullptr, false,
-                        w.ev_h, hm + mfirst, defer ? mcount : 0, &pre))
+    // the key cache is looked up on the device (k_pk_cached): its tables are only rewritten under
+    // Dev::mu, held while this call enqueues, after every launch that may still read them
+    if (verify_pipeline(d, w, cpk, csig, dmidx + ib, hm, m, dgoffs + goff_base[c], ng, dst, sc, w.ev_side[2], nullptr,
+                        true, w.ev_h, hm + mfirst, defer ? mcount : 0))
       return -1;
+    {  // the decompressed partials into the signature cache (the aggregation of these partials reads them)
+      HmEntry* vsig;
+      uint8_t* vsigst;
+      if (wsbuf(w, W_VSIG, m, &vsig) || wsbuf(w, W_VSIGST, m, &vsigst) || sc_put(d, csig, vsig, vsigst, m, sc))
+        return -1;
+    }
     LAUNCH(k_scatter_status, m, sc, dst, dord + ib, (uint32_t)m, dst_out);
     if (ws_release(w, sc)) return -1;
     if (c) {
@@ -1788,9 +1820,9 @@ int verify_large(Dev& d, const uint8_t* pks, const uint8_t* sigs, const uint8_t*
   HCHK(hipMemcpyAsync(status, dst_out, n, hipMemcpyDeviceToHost, h0.s));
   HCHK(hipStreamSynchronize(h0.s));
   if (host_timing())
-    fprintf(stderr, "hbls verify_large n=%zu chunks=%zu: lock %.2f ms, upload+decompress enqueue %.2f, grouping %.2f "
-            "(beside the GPU), lock wait %.2f, enqueue %.2f, device %.2f\n", n, cg.size() - 1, t_locked0 - t_start,
-            t_dec - t_locked0, t_grouped - t_dec, t_locked - t_grouped, t_enq - t_locked, now_ms() - t_enq);
+    fprintf(stderr, "hbls verify_large n=%zu chunks=%zu: lock %.2f ms, upload enqueue %.2f, grouping %.2f (beside the "
+            "upload), lock wait %.2f, enqueue %.2f, device %.2f\n", n, cg.size() - 1, t_locked0 - t_start,
+            t_up - t_locked0, t_grouped - t_up, t_locked - t_grouped, t_enq - t_locked, now_ms() - t_enq);
   return 0;
 }
 
@@ -1972,9 +2004,20 @@ int group_op_host(const uint8_t* sigs, const int64_t* idx, const uint32_t* grp_o
     HCHK(hipMemcpyAsync(out + 96 * gb, dout, ng * 96, hipMemcpyDeviceToHost, h.s));
     HCHK(hipMemcpyAsync(status + gb, dst, ng, hipMemcpyDeviceToHost, h.s));
     HCHK(hipStreamSynchronize(h.s));
-    if (host_timing())
-      fprintf(stderr, "hbls group_op mode=%d groups=%zu members=%zu cache=%d: lock wait %.2f ms, enqueue+upload %.2f, "
-              "device %.2f\n", mode, ng, np, hit ? 1 : 0, t_locked - t_start, t_enq - t_locked, now_ms() - t_enq);
+    size_t hits = 0;
+    if (hit && (host_timing() || stats_on())) {  // diagnosis: the cache's hits (the workspace is
+      // released, but a caller of these switches runs nothing else on it while this host waits)
+      std::vector<uint8_t> hh(np);
+      HCHK(hipMemcpy(hh.data(), hit, np, hipMemcpyDeviceToHost));
+      for (uint8_t x : hh) hits += x;
+      g_stats[6] += np;
+      g_stats[7] += hits;
+    }
+    if (host_timing()) {
+      fprintf(stderr, "hbls group_op mode=%d groups=%zu members=%zu cache=%d hits=%zu: lock wait %.2f ms, enqueue+upload "
+              "%.2f, device %.2f\n", mode, ng, np, hit ? 1 : 0, hits, t_locked - t_start, t_enq - t_locked,
+              now_ms() - t_enq);
+    }
     return 0;
   });
 }
@@ -2654,7 +2697,7 @@ int hbls_timing_read(const char** names, float* ms, size_t max_n, size_t* n_out)
 }
 
 int hbls_stats(uint64_t* out, size_t n) {
-  for (size_t k = 0; k < n && k < 6; k++) out[k] = g_stats[k].load();
+  for (size_t k = 0; k < n && k < 8; k++) out[k] = g_stats[k].load();
   return stats_on() ? 0 : set_err("statistics are collected only with HBLS_STATS=1");
 }
 

@@ -230,9 +230,6 @@ void launch_sc_put(const uint8_t* sigs, const HmEntry* pts, const uint8_t* st, u
 void launch_sc_get(const uint8_t* sigs, uint32_t n, const void* key, const HmEntry* ent, const uint8_t* est,
                    const uint32_t* tab, uint32_t tcap, uint64_t k0, uint64_t k1, HmEntry* out, uint8_t* st, uint8_t* hit,
                    hipStream_t s);
-void launch_gather_dec(const G1AEntry* pk, const uint8_t* pk_st, const HmEntry* sig, const uint8_t* sig_st,
-                       const uint32_t* order, uint32_t n, G1AEntry* opk, uint8_t* opk_st, HmEntry* osig, uint8_t* osig_st,
-                       hipStream_t s);
 void launch_kc_index(const uint8_t* keys, uint32_t first, uint32_t m, uint32_t* tab, uint32_t tcap, uint64_t k0,
                      uint64_t k1, hipStream_t s);
 void launch_pk_cached(const uint8_t* pks, uint32_t n, const uint8_t* keys, const G1AEntry* tabe, const uint8_t* tst,

@@ -146,32 +146,37 @@ __device__ __forceinline__ bool sc_eq(const uint4* a, const uint4* b) {
   HB_UNROLL for (int j = 0; j < 6; j++) eq = eq && a[j].x == b[j].x && a[j].y == b[j].y && a[j].z == b[j].z && a[j].w == b[j].w;
   return eq;
 }
-// entries (base + i) & (cap - 1) take item i: bytes, point, status; then the index
-__global__ __launch_bounds__(64) void k_sc_put(const uint8_t* __restrict__ sigs, const HmEntry* __restrict__ pts,
-                                               const uint8_t* __restrict__ st, uint32_t n, uint32_t base, uint32_t cap,
-                                               uint4* __restrict__ key, HmEntry* __restrict__ ent,
-                                               uint8_t* __restrict__ est, uint32_t* __restrict__ tab, uint32_t tcap,
-                                               uint64_t k0, uint64_t k1) {
+// entries (base + i) & (cap - 1) take item i: bytes, point, status (k_sc_write); then, once all of
+// them are written, the index (k_sc_index).  An occupied slot is taken over only when its entry
+// holds the same bytes (put again: the newer entry wins) or no longer hashes within SC_PROBES of
+// the slot (its ring entry was rewritten with other bytes); an entry of this very put with other
+// bytes is live.  (One kernel judging slots by "rewritten by this put" let lanes of one put evict
+// each other: 4.5 % of a 1M-signature put went unindexed.)
+__global__ __launch_bounds__(64) void k_sc_write(const uint8_t* __restrict__ sigs, const HmEntry* __restrict__ pts,
+                                                 const uint8_t* __restrict__ st, uint32_t n, uint32_t base, uint32_t cap,
+                                                 uint4* __restrict__ key, HmEntry* __restrict__ ent,
+                                                 uint8_t* __restrict__ est) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t e = (base + i) & (cap - 1);
+  HB_UNROLL for (int j = 0; j < 6; j++) key[6ull * e + j] = ((const uint4*)(sigs + 96ull * i))[j];
+  ent[e] = pts[i];
+  est[e] = st[i];
+}
+__global__ __launch_bounds__(64) void k_sc_index(uint32_t n, uint32_t base, uint32_t cap, const uint4* __restrict__ key,
+                                                 uint32_t* __restrict__ tab, uint32_t tcap, uint64_t k0, uint64_t k1) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint32_t e = (base + i) & (cap - 1);
   uint4 kb[6];
-  HB_UNROLL for (int j = 0; j < 6; j++) kb[j] = ((const uint4*)(sigs + 96ull * i))[j];
-  HB_UNROLL for (int j = 0; j < 6; j++) key[6ull * e + j] = kb[j];
-  ent[e] = pts[i];
-  est[e] = st[i];
+  HB_UNROLL for (int j = 0; j < 6; j++) kb[j] = key[6ull * e + j];
   const uint32_t home = sc_hash(kb, k0, k1) & (tcap - 1);
   for (uint32_t q = 0; q < SC_PROBES; q++) {
     const uint32_t slot = (home + q) & (tcap - 1);
     const uint32_t old = atomicCAS(&tab[slot], 0u, e + 1);
-    if (old == 0) return;
-    const uint32_t o = old - 1;
-    bool dead = ((o - base) & (cap - 1)) < n;  // rewritten by this put (possibly by this very item)
-    if (!dead) {
-      const uint4* ko = key + 6ull * o;
-      if (sc_eq(ko, kb)) dead = true;  // the same bytes put before: the newer entry wins
-      else dead = ((slot - (sc_hash(ko, k0, k1) & (tcap - 1))) & (tcap - 1)) >= SC_PROBES;  // unreachable
-    }
+    if (old == 0 || old == e + 1) return;
+    const uint4* ko = key + 6ull * (old - 1);
+    const bool dead = sc_eq(ko, kb) || ((slot - (sc_hash(ko, k0, k1) & (tcap - 1))) & (tcap - 1)) >= SC_PROBES;
     if (dead && atomicCAS(&tab[slot], old, e + 1) == old) return;
   }
 }
@@ -198,22 +203,6 @@ __global__ __launch_bounds__(64) void k_sc_get(const uint8_t* __restrict__ sigs,
     }
   }
   hit[i] = h;
-}
-
-// One lane per item of a host-buffer call decompressed in the caller's order (hipbls.hip
-// verify_large): the entries of group-order item i from caller item order[i]
-__global__ __launch_bounds__(64) void k_gather_dec(const G1AEntry* __restrict__ pk, const uint8_t* __restrict__ pk_st,
-                                                   const HmEntry* __restrict__ sig, const uint8_t* __restrict__ sig_st,
-                                                   const uint32_t* __restrict__ order, uint32_t n,
-                                                   G1AEntry* __restrict__ opk, uint8_t* __restrict__ opk_st,
-                                                   HmEntry* __restrict__ osig, uint8_t* __restrict__ osig_st) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t j = order[i];
-  opk[i] = pk[j];
-  opk_st[i] = pk_st[j];
-  osig[i] = sig[j];
-  osig_st[i] = sig_st[j];
 }
 
 // ---- public-key cache on the device (hbls_pubkey_cache_add): the compressed keys of the table's
@@ -707,13 +696,6 @@ void launch_dec_pk(const uint8_t* pks, uint32_t n, G1AEntry* out, uint8_t* st, h
   hipLaunchKernelGGL(k_dec_pk, dim3(blocks_for(n)), dim3(BLOCK), 0, s, pks, n, out, st);
   hipLaunchKernelGGL(k_g1_subgroup, dim3(blocks_for(n)), dim3(BLOCK), 0, s, n, out, st);
 }
-void launch_gather_dec(const G1AEntry* pk, const uint8_t* pk_st, const HmEntry* sig, const uint8_t* sig_st,
-                       const uint32_t* order, uint32_t n, G1AEntry* opk, uint8_t* opk_st, HmEntry* osig, uint8_t* osig_st,
-                       hipStream_t s) {
-  if (n)
-    hipLaunchKernelGGL(k_gather_dec, dim3(blocks_for(n)), dim3(BLOCK), 0, s, pk, pk_st, sig, sig_st, order, n, opk, opk_st,
-                       osig, osig_st);
-}
 void launch_kc_index(const uint8_t* keys, uint32_t first, uint32_t m, uint32_t* tab, uint32_t tcap, uint64_t k0,
                      uint64_t k1, hipStream_t s) {
   if (m) hipLaunchKernelGGL(k_kc_index, dim3(blocks_for(m)), dim3(BLOCK), 0, s, keys, first, m, tab, tcap, k0, k1);
@@ -734,8 +716,9 @@ void launch_sc_put(const uint8_t* sigs, const HmEntry* pts, const uint8_t* st, u
                    void* key, HmEntry* ent, uint8_t* est, uint32_t* tab, uint32_t tcap, uint64_t k0, uint64_t k1,
                    hipStream_t s) {
   if (!n) return;
-  hipLaunchKernelGGL(k_sc_put, dim3(blocks_for(n)), dim3(BLOCK), 0, s, sigs, pts, st, n, base, cap, (uint4*)key, ent, est,
-                     tab, tcap, k0, k1);
+  hipLaunchKernelGGL(k_sc_write, dim3(blocks_for(n)), dim3(BLOCK), 0, s, sigs, pts, st, n, base, cap, (uint4*)key, ent,
+                     est);
+  hipLaunchKernelGGL(k_sc_index, dim3(blocks_for(n)), dim3(BLOCK), 0, s, n, base, cap, (const uint4*)key, tab, tcap, k0, k1);
 }
 void launch_sc_get(const uint8_t* sigs, uint32_t n, const void* key, const HmEntry* ent, const uint8_t* est,
                    const uint32_t* tab, uint32_t tcap, uint64_t k0, uint64_t k1, HmEntry* out, uint8_t* st, uint8_t* hit,

@@ -256,7 +256,8 @@ int hbls_timing_read(const char** names, float* ms, size_t max_n, size_t* n_out)
  * synchronises): out[0] items verified, out[1] verification groups, out[2] items re-checked
  * alone because their group's combined check failed, out[3] groups checked alone because their
  * batch's shared final exponentiation failed, out[4] slot-wide checks run, out[5] slot-wide
- * checks that failed (the call then took the per-batch check).  n <= 6. */
+ * checks that failed (the call then took the per-batch check), out[6] ThresholdAggregate /
+ * Aggregate members looked up in the decompressed-signature cache, out[7] those found.  n <= 8. */
 int hbls_stats(uint64_t* out, size_t n);
 /* Tuning: verifications of at least min_groups groups share one final exponentiation among 64
  * groups (0 = one per group; default 128, HBLS_FE_BATCH).  Returns the previous value.  Verdicts

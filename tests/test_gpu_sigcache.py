@@ -1,5 +1,5 @@
 """The decompressed-signature cache (hbls_sig_cache; hipbls.hip sc_put / sc_get, vbatch.hip
-k_sc_put / k_sc_get) on the GPU: ThresholdAggregate of partials an earlier host-buffer Verify batch
+k_sc_write / k_sc_index / k_sc_get) on the GPU: ThresholdAggregate of partials an earlier host-buffer Verify batch
 decompressed takes them from the cache, and every aggregate and status equals the uncached run --
 with valid partials, undecodable and off-subgroup partials (cached with their rejection status),
 members never verified (misses, decompressed), duplicate signatures in one Verify batch, and a ring
@@ -96,3 +96,28 @@ def test_aggregate_without_prior_verify(L, hipbls):
     hipbls.verify_batch(pks, ms, sigs)
     outs, sts = hipbls.threshold_aggregate_batch(groups2)
     assert sts == [OK] * 40 and outs == roots2
+
+
+@pytest.mark.parametrize("cap", [1 << 21, 1024], ids=["ring_large", "index_half_full"])
+def test_every_verified_member_hits(L, hipbls, monkeypatch, cap):
+    """Every member of an aggregation over just-verified partials is found in the cache (HBLS_STATS
+    counters 6 and 7: lookups and hits).  With a 1024-entry ring the 480 partials fill the index
+    (2048 slots) to a quarter, so many of them hash onto slots another partial of the same put
+    took: a put must never evict its own entries (the one-kernel put lost 4.5 % of a 1M put)."""
+    import ctypes
+    monkeypatch.setenv("HBLS_STATS", "1")
+    rng = random.Random(57)
+    V, n, t = 96, 7, 5
+    pks, ms, sigs, groups, roots = _cluster(hipbls, rng, V, n, t, b"hits")
+    prev = L.hbls_sig_cache(cap)
+    try:
+        st = hipbls.verify_batch(pks, ms, sigs)
+        s0 = (ctypes.c_uint64 * 8)()
+        assert L.hbls_stats(s0, 8) == 0
+        outs, sts = hipbls.threshold_aggregate_batch(groups)
+        s1 = (ctypes.c_uint64 * 8)()
+        assert L.hbls_stats(s1, 8) == 0
+    finally:
+        L.hbls_sig_cache(prev)
+    assert st == [OK] * (V * t) and sts == [OK] * V and outs == roots
+    assert s1[6] - s0[6] == V * t and s1[7] - s0[7] == V * t, (s1[6] - s0[6], s1[7] - s0[7])
