@@ -831,6 +831,10 @@ def main(argv=None):
             roofline = {"bound": "valu", "kernel": dom, "unit_of_work": opcounts.UNITS.get(dom),
                         "achieved": x["achieved_Tops_alg"], "peak": opcounts.PEAK_MAD_TOPS,
                         "unit": "Tops/s (32-bit multiply-add lane-ops, v_mad_u64_u32)",
+                        # the peak: measured (16 waves/CU, event-timed, counters agree), the clock
+                        # it ran at, and the architectural issue bound at the nominal clock
+                        "peak_measured": opcounts.PEAK_MAD_TOPS, "peak_nominal": opcounts.PEAK_MAD_TOPS_NOMINAL,
+                        "peak_effective_clock_MHz": opcounts.PEAK_CLOCK_MHZ, "peak_source": opcounts.PEAK_SOURCE,
                         "frac": round(x["achieved_Tops_alg"] / opcounts.PEAK_MAD_TOPS, 4),
                         "frac_executed": round(x["achieved_Tops_exec"] / opcounts.PEAK_MAD_TOPS, 4),
                         "frac_vs_nominal_clock": round(x["achieved_Tops_alg"] / opcounts.PEAK_MAD_TOPS_NOMINAL, 4),

@@ -6,9 +6,14 @@ blocks below are counted by the op-counting host build of the kernels' own arith
 product is MAC_PER_FPMUL = 2*12*12 + 12 = 300 32x32->64-bit multiply-adds (textbook 12-limb
 CIOS), the unit of the peak.
 
-PEAK_MAD_TOPS: v_mad_u64_u32 lane-ops/s on MI355X, measured by tools/microbench/int_rates.hip
-(profiles/r01_int_rates_microbench.txt, 16 waves/CU: 29.944 Tops/s, i.e. the chip's clock under
-that load; 39.3 T at the nominal 2.4 GHz with half-rate issue).
+PEAK_MAD_TOPS: v_mad_u64_u32 lane-ops/s on MI355X, measured by tools/microbench/int_rates.hip at
+16 waves/CU with 2 ms kernels (profiles/r05b_int_rates_traced.txt: 32.654 Tops/s, event-timed) and
+pinned by counters (profiles/r05b_peak_from_counters.json: SQ_INSTS_VALU x 64 over the traced
+duration 32.739 T, 262 185 VALU instructions per wave for the 262 144 issued; GRBM_GUI_ACTIVE / 8
+XCDs: 2365 MHz).  That is 53.9 lane-ops per clock per CU, 84 % of the 64 a wave64 instruction per
+SIMD per 4 clocks allows.  PEAK_MAD_TOPS_NOMINAL: the 64 lane-ops/clk/CU x 256 CUs at the nominal
+2.4 GHz.  (Round 1's 29.944 T came from 0.5 ms kernels that ran at ~2.16 GHz: the same 53.9 per
+clock at a lower clock.)
 
 Per kernel two counts: `alg` is the textbook tower-arithmetic work of the unit (what a one-lane
 implementation of the same algorithm executes); `exec` is what the kernel executes (e.g. the
@@ -16,8 +21,10 @@ three-lane pairing evaluates every H(m) line in all three lanes and inverts in a
 """
 
 MAC_PER_FPMUL = 2 * 12 * 12 + 12
-PEAK_MAD_TOPS = 29.944
-PEAK_MAD_TOPS_NOMINAL = 39.3
+PEAK_MAD_TOPS = 32.654
+PEAK_MAD_TOPS_NOMINAL = 39.322
+PEAK_CLOCK_MHZ = 2365  # the effective clock PEAK_MAD_TOPS was measured at
+PEAK_SOURCE = "profiles/r05b_peak_from_counters.json"
 
 # hc_count_blocks, in its order
 BLOCK_NAMES = ("f12_sqr", "f12_mul_line", "final_exp", "fp_inv", "g1_dec", "g2_dec", "rlc_g1", "rlc_g2",
