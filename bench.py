@@ -668,7 +668,11 @@ def main(argv=None):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    _chk(L, L.hbls_timing(1))
+    # no per-launch event instrumentation inside the timed region (the per-kernel figures come
+    # from the serialised slot after it); HBLS_BENCH_TIMED_EVENTS=1 keeps it on, for comparison
+    timed_events = os.environ.get("HBLS_BENCH_TIMED_EVENTS") == "1"
+    if timed_events:
+        _chk(L, L.hbls_timing(1))
     evs = [mk() for _ in range(args.steps)]
     t0 = time.perf_counter()
     for k in range(args.steps):
@@ -682,8 +686,8 @@ def main(argv=None):
 
     seg = np.array([[e[i].elapsed_time(e[i + 1]) for i in range(n_ev - 1)] for e in evs])  # ms
     k_ms = seg.mean(axis=0)
-    recs_overlapped = _lib.timing_read(L)
-    _chk(L, L.hbls_timing(0))
+    if timed_events:
+        _chk(L, L.hbls_timing(0))
 
     # parity of the timed outputs: every partial verifies, every aggregate is byte-identical to the
     # root-key signature (tbls_test.go:72-97 property) and verifies under the DV key

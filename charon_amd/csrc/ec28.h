@@ -313,11 +313,21 @@ struct G1L {
   bool inf;
 };
 
+// Who computes the G1 formulas' pairs of independent products.  G1One: this lane, both in one
+// dual-chain leaf (l_mul2 / l_sqr2).  G1Half (device, below): the two lanes of a pair, each one of
+// the two products, then an exchange -- for the latency-bound small calls, like F2Half for Fp2.
+struct G1One {
+  static constexpr bool kSplit = false;
+};
+HD void p_mul2(G1One, const L28& a, const L28& b, const L28& c, const L28& d, L28& r0, L28& r1) { l_mul2(a, b, c, d, r0, r1); }
+HD void p_sqr2(G1One, const L28& a, const L28& c, L28& r0, L28& r1) { l_sqr2(a, c, r0, r1); }
+
 // dbl-2009-l (lazy28.py dbl)
-HDNI G1L g1l_dbl(const G1L& p) {
+template <class M = G1One>
+HDNI G1L g1l_dbl(const G1L& p, M m = M()) {
   L28 A, B, C, T;
-  l_sqr2(p.X, p.Y, A, B);
-  l_sqr2(B, l_add(p.X, B), C, T);
+  p_sqr2(m, p.X, p.Y, A, B);
+  p_sqr2(m, B, l_add(p.X, B), C, T);
   const L28 E = l_add(l_add(A, A), A);
   const L28 F = l_sqr(E);
   const L28 D = l_norm(l_shl(l_sub<3, 2>(T, l_add(A, C)), 1));
@@ -325,23 +335,34 @@ HDNI G1L g1l_dbl(const G1L& p) {
   r.X = l_norm(l_sub<17, 2>(F, l_shl(D, 1)));
   const L28 W = l_sub<19, 1>(D, r.X);
   L28 EW;
-  l_mul2(E, W, l_shl(p.Y, 1), p.Z, EW, r.Z);
+  p_mul2(m, E, W, l_shl(p.Y, 1), p.Z, EW, r.Z);
   r.Y = l_norm(l_sub<9, 8>(EW, l_shl(C, 3)));
   r.inf = p.inf;
   return r;
 }
 
 // the common tail of the additions (I = 4 HH folded into shifts: J = 4 H HH, V = 4 U1 HH)
-HD G1L g1l_add_tail(const L28& H, const L28& rr, const L28& U1, const L28& S1, const L28& Zs) {
-  const L28 HH = l_sqr(H);
+// (G1Half pairs the products that G1One, measured on the C3 ladders, keeps single)
+template <class M = G1One>
+HD G1L g1l_add_tail(const L28& H, const L28& rr, const L28& U1, const L28& S1, const L28& Zs, M m = M()) {
+  L28 HH, Z3;
+  if constexpr (M::kSplit) {
+    p_mul2(m, H, H, Zs, H, HH, Z3);
+  } else {
+    HH = l_sqr(H);
+  }
   L28 J1, V1;
-  l_mul2(H, HH, U1, HH, J1, V1);
+  p_mul2(m, H, HH, U1, HH, J1, V1);
   G1L r;
   r.X = l_norm(l_sub<13, 12>(l_sqr(rr), l_add(l_shl(J1, 2), l_shl(V1, 3))));
   L28 t, sj;
-  l_mul2(rr, l_sub<15, 1>(l_shl(V1, 2), r.X), S1, J1, t, sj);
+  p_mul2(m, rr, l_sub<15, 1>(l_shl(V1, 2), r.X), S1, J1, t, sj);
   r.Y = l_norm(l_sub<9, 8>(t, l_shl(sj, 3)));
-  r.Z = l_mul(Zs, H);
+  if constexpr (M::kSplit) {
+    r.Z = Z3;
+  } else {
+    r.Z = l_mul(Zs, H);
+  }
   r.inf = false;
   return r;
 }
@@ -354,35 +375,55 @@ HD G1L g1l_infinity() {
 }
 
 // madd-2007-bl: p + (x2, y2), the affine point finite and normalised below 2p (lazy28.py madd)
-HDNI G1L g1l_madd(const G1L& p, const L28& x2, const L28& y2) {
+template <class M = G1One>
+HDNI G1L g1l_madd(const G1L& p, const L28& x2, const L28& y2, M m = M()) {
   if (p.inf) return {x2, y2, l_from(fp_one()), false};
-  const L28 Z1Z1 = l_sqr(p.Z);
-  const L28 U2 = l_mul(x2, Z1Z1);
-  const L28 S2 = l_mul(l_mul(y2, p.Z), Z1Z1);
+  L28 Z1Z1, U2, S2;
+  if constexpr (M::kSplit) {
+    L28 yZ;
+    p_mul2(m, p.Z, p.Z, y2, p.Z, Z1Z1, yZ);
+    p_mul2(m, x2, Z1Z1, yZ, Z1Z1, U2, S2);
+  } else {
+    Z1Z1 = l_sqr(p.Z);
+    U2 = l_mul(x2, Z1Z1);
+    S2 = l_mul(l_mul(y2, p.Z), Z1Z1);
+  }
   const L28 H = l_sub<21, 1>(U2, p.X);
   const L28 rr = l_norm(l_sub<41, 2>(l_shl(S2, 1), l_shl(p.Y, 1)));
   if (l_is_zero(H)) {
-    if (l_is_zero(rr)) return g1l_dbl(p);
+    if (l_is_zero(rr)) return g1l_dbl(p, m);
     return g1l_infinity();
   }
-  return g1l_add_tail(H, rr, p.X, p.Y, l_shl(p.Z, 1));
+  return g1l_add_tail(H, rr, p.X, p.Y, l_shl(p.Z, 1), m);
 }
 
 // add-2007-bl (lazy28.py jadd)
-HDNI G1L g1l_add(const G1L& p, const G1L& q) {
+template <class M = G1One>
+HDNI G1L g1l_add(const G1L& p, const G1L& q, M m = M()) {
   if (p.inf) return q;
   if (q.inf) return p;
-  const L28 Z1Z1 = l_sqr(p.Z), Z2Z2 = l_sqr(q.Z);
-  const L28 U1 = l_mul(p.X, Z2Z2), U2 = l_mul(q.X, Z1Z1);
-  const L28 S1 = l_mul(l_mul(p.Y, q.Z), Z2Z2);
-  const L28 S2 = l_mul(l_mul(q.Y, p.Z), Z1Z1);
+  L28 Z1Z1, Z2Z2, U1, U2, S1, S2;
+  if constexpr (M::kSplit) {
+    L28 pYqZ, qYpZ;
+    p_sqr2(m, p.Z, q.Z, Z1Z1, Z2Z2);
+    p_mul2(m, p.Y, q.Z, q.Y, p.Z, pYqZ, qYpZ);
+    p_mul2(m, p.X, Z2Z2, q.X, Z1Z1, U1, U2);
+    p_mul2(m, pYqZ, Z2Z2, qYpZ, Z1Z1, S1, S2);
+  } else {
+    Z1Z1 = l_sqr(p.Z);
+    Z2Z2 = l_sqr(q.Z);
+    U1 = l_mul(p.X, Z2Z2);
+    U2 = l_mul(q.X, Z1Z1);
+    S1 = l_mul(l_mul(p.Y, q.Z), Z2Z2);
+    S2 = l_mul(l_mul(q.Y, p.Z), Z1Z1);
+  }
   const L28 H = l_sub<21, 1>(U2, U1);
   const L28 rr = l_norm(l_sub<41, 2>(l_shl(S2, 1), l_shl(S1, 1)));
   if (l_is_zero(H)) {
-    if (l_is_zero(rr)) return g1l_dbl(p);
+    if (l_is_zero(rr)) return g1l_dbl(p, m);
     return g1l_infinity();
   }
-  return g1l_add_tail(H, rr, U1, S1, l_mul(l_shl(p.Z, 1), q.Z));
+  return g1l_add_tail(H, rr, U1, S1, l_mul(l_shl(p.Z, 1), q.Z), m);
 }
 
 HD G1J g1l_to_jac(const G1L& p) {
@@ -391,18 +432,19 @@ HD G1J g1l_to_jac(const G1L& p) {
 }
 
 // P in G1  <=>  phi(P) == [-x^2] P (ec.h g1_in_subgroup), the two ladders in lazy limbs
-HDNI bool g1_in_subgroup28(const G1A& p) {
+template <class M = G1One>
+HDNI bool g1_in_subgroup28(const G1A& p, M m = M()) {
   if (p.inf) return true;
   const L28 x = l_from(p.x), y = l_from(p.y);
   G1L t = {x, y, l_from(fp_one()), false};
   HB_NOUNROLL for (int i = 62; i >= 0; i--) {
-    t = g1l_dbl(t);
-    if ((HB_X_ABS >> i) & 1) t = g1l_madd(t, x, y);
+    t = g1l_dbl(t, m);
+    if ((HB_X_ABS >> i) & 1) t = g1l_madd(t, x, y, m);
   }
   G1L u = t;
   HB_NOUNROLL for (int i = 62; i >= 0; i--) {
-    u = g1l_dbl(u);
-    if ((HB_X_ABS >> i) & 1) u = g1l_add(u, t);
+    u = g1l_dbl(u, m);
+    if ((HB_X_ABS >> i) & 1) u = g1l_add(u, t, m);
   }
   const G1J phi = jac_from_aff(G1A{fp_mul(p.x, fp_from_const(G1_BETA)), p.y, false});
   return jac_eq(phi, jac_neg(g1l_to_jac(u)));
@@ -606,6 +648,29 @@ __device__ __forceinline__ F2L f2h_join(F2Half m, const L28& mine) {
   const L28 other = l_xch(mine, m.partner);
   return {l_pick(m.h != 0, mine, other), l_pick(m.h != 0, other, mine)};
 }
+// G1Half: lane h of the pair computes product h of the two and takes the other from its partner
+struct G1Half {
+  static constexpr bool kSplit = true;
+  int h, partner;
+};
+__device__ __forceinline__ G1Half g1half_make() {
+  const F2Half f = f2half_make();
+  return {f.h, f.partner};
+}
+__device__ __forceinline__ void g1h_join(G1Half m, const L28& mine, L28& r0, L28& r1) {
+  const L28 other = l_xch(mine, m.partner);
+  r0 = l_pick(m.h != 0, mine, other);
+  r1 = l_pick(m.h != 0, other, mine);
+}
+__device__ __forceinline__ void p_mul2(G1Half m, const L28& a, const L28& b, const L28& c, const L28& d, L28& r0,
+                                       L28& r1) {
+  const bool h = m.h != 0;
+  g1h_join(m, l_mul(l_pick(h, a, c), l_pick(h, b, d)), r0, r1);
+}
+__device__ __forceinline__ void p_sqr2(G1Half m, const L28& a, const L28& c, L28& r0, L28& r1) {
+  g1h_join(m, l_sqr(l_pick(m.h != 0, a, c)), r0, r1);
+}
+
 // coefficient 0: a0 b0 + (K - a1) b1 (K = kF2N, as f2l_mul_core), coefficient 1: a0 b1 + a1 b0
 __device__ __forceinline__ F2L fm(F2Half m, const F2L& a, const F2L& b) {
   L28 na1;
@@ -855,19 +920,19 @@ HD G2J g2l_msm_ladder_sparse(const G2J* __restrict__ tab, const Quad* __restrict
 // Q in G2  <=>  psi(Q) == [x] Q (ec.h g2_in_subgroup), the ladder in lazy limbs.  `load` returns
 // Q again at each of the five mixed additions instead of the ladder holding its 56 limbs across
 // every product call (the kernel re-reads its entry; LICM is kept from hoisting that read)
-template <class LoadQ>
-HDNI bool g2_in_subgroup28_l(const LoadQ& load) {
+template <class LoadQ, class M = F2One>
+HDNI bool g2_in_subgroup28_l(const LoadQ& load, M m = M()) {
   const G2A q = load();
   if (q.inf) return true;
   G2L t = {f2l_from(q.x), f2l_from(q.y), {l_from(fp_one()), l_from(fp_zero())}, false};
   HB_NOUNROLL for (int i = 62; i >= 0; i--) {
-    t = g2l_dbl(t);
+    t = g2l_dbl(t, m);
     if ((HB_X_ABS >> i) & 1) {
 #if defined(__HIP_DEVICE_COMPILE__)
       __asm__ volatile("" ::: "memory");
 #endif
       const G2A q2 = load();
-      t = g2l_madd(t, f2l_from(q2.x), f2l_from(q2.y));
+      t = g2l_madd(t, f2l_from(q2.x), f2l_from(q2.y), m);
     }
   }
   const G2A q3 = load();

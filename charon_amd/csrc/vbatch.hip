@@ -121,6 +121,59 @@ __global__ KB_OCC(HB_OCC_SUBG) void k_g2_subgroup(uint32_t n, HmEntry* __restric
   }
 }
 
+// The subgroup checks with each item's ladder split over a lane pair (ec28.h G1Half: each lane one
+// of every pair of independent products; F2Half: each lane one coefficient of every Fp2 product),
+// for calls with too few items to fill the chip, where the ladders' latency, not their
+// lane-cycles, is what the slot waits for.  Same outputs as k_g1_subgroup / k_g2_subgroup.
+__global__ KB_OCC(HB_OCC_SUBG) void k_g1_subgroup_h(uint32_t n, G1AEntry* __restrict__ pts, uint8_t* __restrict__ st) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;
+  if (i >= n) return;  // both lanes of a pair
+  const G1AEntry e = pts[i];
+  if (st[i] || e.inf) return;
+  const G1Half m = g1half_make();
+  if (!g1_in_subgroup28(G1A{e.x, e.y, false}, m) && m.h == 0) {
+    const G1A g = g1_generator();
+    G1AEntry z;
+    z.x = g.x;
+    z.y = g.y;
+    z.inf = 0u;
+    z.pad[0] = z.pad[1] = z.pad[2] = 0;
+    pts[i] = z;
+    st[i] = 1;
+  }
+#endif
+}
+__global__ KB_OCC(HB_OCC_SUBG) void k_g2_subgroup_h(uint32_t n, HmEntry* __restrict__ pts, uint8_t* __restrict__ st,
+                                                     const uint8_t* __restrict__ skip) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;
+  if (i >= n || (skip && skip[i])) return;
+  const HmEntry e = pts[i];
+  if (st[i] || e.inf) return;
+  const F2Half m = f2half_make();
+  const HmEntry* src = pts + i;
+  if (!g2_in_subgroup28_l([src]() { return G2A{src->x, src->y, false}; }, m) && m.h == 0) {
+    HmEntry z;
+    z.x = f2_zero();
+    z.y = f2_zero();
+    z.inf = 1u;
+    z.pad[0] = z.pad[1] = z.pad[2] = 0;
+    pts[i] = z;
+    st[i] = 1;
+  }
+#endif
+}
+
+// items up to which the subgroup checks run on lane pairs (HBLS_DEC_PAIR_MAX, read once)
+static size_t dec_pair_max() {
+  static const size_t v = [] {
+    const char* e = getenv("HBLS_DEC_PAIR_MAX");
+    return e ? (size_t)strtoull(e, nullptr, 0) : (size_t)0;
+  }();
+  return v;
+}
+
 // ---- decompressed-signature cache (host-buffer calls: hbls_verify_batch fills it,
 // hbls_threshold_aggregate_batch reads it -- charon's parsigex Verify -> parsigdb -> sigagg flow,
 // where the aggregation's partials are exactly partials verified before).  A ring of `cap`
@@ -694,7 +747,10 @@ void launch_item_group(const uint32_t* grp_off, uint32_t n_groups, uint32_t n, u
 void launch_dec_pk(const uint8_t* pks, uint32_t n, G1AEntry* out, uint8_t* st, hipStream_t s) {
   if (!n) return;
   hipLaunchKernelGGL(k_dec_pk, dim3(blocks_for(n)), dim3(BLOCK), 0, s, pks, n, out, st);
-  hipLaunchKernelGGL(k_g1_subgroup, dim3(blocks_for(n)), dim3(BLOCK), 0, s, n, out, st);
+  if (n <= dec_pair_max())
+    hipLaunchKernelGGL(k_g1_subgroup_h, dim3(blocks_for(2 * n)), dim3(BLOCK), 0, s, n, out, st);
+  else
+    hipLaunchKernelGGL(k_g1_subgroup, dim3(blocks_for(n)), dim3(BLOCK), 0, s, n, out, st);
 }
 void launch_kc_index(const uint8_t* keys, uint32_t first, uint32_t m, uint32_t* tab, uint32_t tcap, uint64_t k0,
                      uint64_t k1, hipStream_t s) {
@@ -710,7 +766,10 @@ void launch_pk_cached(const uint8_t* pks, uint32_t n, const uint8_t* keys, const
 void launch_dec_sig_pt(const uint8_t* sigs, uint32_t n, HmEntry* out, uint8_t* st, hipStream_t s, const uint8_t* skip) {
   if (!n) return;
   hipLaunchKernelGGL(k_dec_sig_pt, dim3(blocks_for(n)), dim3(BLOCK), 0, s, sigs, n, out, st, skip);
-  hipLaunchKernelGGL(k_g2_subgroup, dim3(blocks_for(n)), dim3(BLOCK), 0, s, n, out, st, skip);
+  if (n <= dec_pair_max())
+    hipLaunchKernelGGL(k_g2_subgroup_h, dim3(blocks_for(2 * n)), dim3(BLOCK), 0, s, n, out, st, skip);
+  else
+    hipLaunchKernelGGL(k_g2_subgroup, dim3(blocks_for(n)), dim3(BLOCK), 0, s, n, out, st, skip);
 }
 void launch_sc_put(const uint8_t* sigs, const HmEntry* pts, const uint8_t* st, uint32_t n, uint32_t base, uint32_t cap,
                    void* key, HmEntry* ent, uint8_t* est, uint32_t* tab, uint32_t tcap, uint64_t k0, uint64_t k1,
