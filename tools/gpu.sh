@@ -7,6 +7,7 @@
 #   final  TAG                      tests, smoke, lines, trace of the default C3 line, pmc
 #   single TAG [calls]              kernel trace of single-item Verify calls (tools/diag_single.py)
 #   peak   TAG                      int_rates microbenchmark: plain, kernel trace, PMC pass (the peak)
+#   attack TAG                      C5 at 5 % and 10 % corrupted partials (the 1 % point is in `lines`)
 # Every GPU step has its own time limit and the steps are chained with &&: the first failure,
 # abort or time-out ends the script.
 set -o pipefail
@@ -61,6 +62,13 @@ peak() {  # the roofline peak pinned by counters (tools/microbench/int_rates_pmc
    timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d "$P/pmc" -o run \
      --output-format csv -- "$X" > "$P/pmc.log" 2>&1)
 }
+attack() {
+  local f
+  for f in 0.05 0.10; do
+    bench c5 --bad-frac $f --cpu-seconds 0 --callers 0 --key-tables 0 --host-api 0 &&
+    mv "$O/bench_c5_$TAG.json" "$O/bench_c5_bad${f}_$TAG.json" && mv "$O/bench_c5_$TAG.err" "$O/bench_c5_bad${f}_$TAG.err" || return 1
+  done
+}
 single() {
   (cd /tmp && export TMPDIR=/tmp &&
    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/single_$TAG" -o run --output-format csv -- python3 \
@@ -91,5 +99,6 @@ case "$WHAT" in
   ab) ab "$@" ;;
   single) single "$@" ;;
   peak) peak ;;
-  *) echo "usage: bash tools/gpu.sh tests|bench|lines|trace|pmc|final|ab|single|peak TAG [args]" >&2; exit 2 ;;
+  attack) attack ;;
+  *) echo "usage: bash tools/gpu.sh tests|bench|lines|trace|pmc|final|ab|single|peak|attack TAG [args]" >&2; exit 2 ;;
 esac
