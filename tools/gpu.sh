@@ -65,8 +65,8 @@ peak() {  # the roofline peak pinned by counters (tools/microbench/int_rates_pmc
 attack() {
   local f
   for f in 0.05 0.10; do
-    bench c5 --bad-frac $f --cpu-seconds 0 --callers 0 --key-tables 0 --host-api 0 &&
-    mv "$O/bench_c5_$TAG.json" "$O/bench_c5_bad${f}_$TAG.json" && mv "$O/bench_c5_$TAG.err" "$O/bench_c5_bad${f}_$TAG.err" || return 1
+    timeout -k 10 600 python -u bench.py --workload c5 --bad-frac $f --cpu-seconds 0 --callers 0 --key-tables 0 \
+      --host-api 0 > "$O/bench_c5_bad${f}_$TAG.json" 2> "$O/bench_c5_bad${f}_$TAG.err" || return 1
   done
 }
 single() {
