@@ -16,7 +16,7 @@ LABELS = {  # bench.py / TIMED label -> kernel symbols of the slot
               "k_rlc_msm<1, 0>", "k_rlc_msm<1, 1>", "k_rlc_msm<1, 2>", "k_rlc_msm<2, 0>", "k_rlc_msm<2, 1>",
               "k_rlc_msm<2, 2>", "k_rlc_msm<3, 0>", "k_rlc_msm<3, 1>"], "k_group_prep": ["k_group_prep_p", "k_group_prep_b"],
     "k_msm_bucket": ["k_msm_bucket"], "k_msm_reduce": ["k_msm_reduce"], "k_msm_sum": ["k_msm_sum"],
-    "k_slines": ["k_slines"], "k_pair3_mml": ["k_pair3<4>"], "k_pair3_prod": ["k_pair3<3>"],
+    "k_slines": ["k_slines"], "k_lines_at_p": ["k_lines_at_p"], "k_pair3_mml": ["k_pair3<4>"], "k_pair3_prod": ["k_pair3<3>"],
     "k_pair3_fin": ["k_pair3<2>", "k_pair6_fin", "k_pair6_fin<3>", "k_pair6_fin<10>"], "k_pair3_ml": ["k_pair3<1>"], "k_attestation_roots": ["k_attestation_roots"],
 }
 
