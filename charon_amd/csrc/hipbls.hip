@@ -590,6 +590,7 @@ int init_mask(uint32_t mask) {
   g_slot_msm_min = env_size("HBLS_SLOT_MSM", g_slot_msm_min.load());
   g_adaptive = env_size("HBLS_ADAPTIVE", 1) != 0;
   g_single_max = env_size("HBLS_SINGLE_MAX", SINGLE_MAX_DEFAULT);
+  g_dec_pair_max = env_size("HBLS_DEC_PAIR_MAX", 0);
   g_ws_sets = (int)std::min<size_t>(N_WS_MAX, std::max<size_t>(1, env_size("HBLS_WS_SETS", 3)));
   {
     size_t fb = std::min<size_t>(FE_BATCH, std::max<size_t>(2, env_size("HBLS_FALLBACK_BATCH", g_fb_batch)));
@@ -2703,6 +2704,10 @@ int hbls_stats(uint64_t* out, size_t n) {
 
 size_t hbls_fe_batch(size_t min_groups) { return g_fe_batch_min.exchange(min_groups); }
 int hbls_adaptive(int on) { return g_adaptive.exchange(on != 0) ? 1 : 0; }
+size_t hbls_dec_pair_max(size_t items) {
+  if (ensure_init()) return 0;
+  return g_dec_pair_max.exchange(items);
+}
 size_t hbls_single_max(size_t items) {
   if (ensure_init()) return 0;
   return g_single_max.exchange(items);

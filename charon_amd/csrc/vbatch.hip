@@ -165,14 +165,10 @@ __global__ KB_OCC(HB_OCC_SUBG) void k_g2_subgroup_h(uint32_t n, HmEntry* __restr
 #endif
 }
 
-// items up to which the subgroup checks run on lane pairs (HBLS_DEC_PAIR_MAX, read once)
-static size_t dec_pair_max() {
-  static const size_t v = [] {
-    const char* e = getenv("HBLS_DEC_PAIR_MAX");
-    return e ? (size_t)strtoull(e, nullptr, 0) : (size_t)0;
-  }();
-  return v;
-}
+// items up to which the subgroup checks run on lane pairs (HBLS_DEC_PAIR_MAX at init,
+// hbls_dec_pair_max at run time; 0 = never: measured neutral at C2, profiles/r05_scheduling_ab.txt)
+std::atomic<size_t> g_dec_pair_max{0};
+static size_t dec_pair_max() { return g_dec_pair_max.load(std::memory_order_relaxed); }
 
 // ---- decompressed-signature cache (host-buffer calls: hbls_verify_batch fills it,
 // hbls_threshold_aggregate_batch reads it -- charon's parsigex Verify -> parsigdb -> sigagg flow,

@@ -277,6 +277,10 @@ int hbls_adaptive(int on);
  * on the latency path); SIZE_MAX = the default (the batched final exponentiation's threshold).
  * Returns the previous setting (HBLS_SINGLE_MAX at init).  Verdicts never depend on it. */
 size_t hbls_single_max(size_t items);
+/* Tuning: decompressions of at most `items` keys or signatures run their subgroup checks with each
+ * item's ladder split over a lane pair (latency for calls that do not fill the chip; 0 = never, the
+ * default, HBLS_DEC_PAIR_MAX).  Returns the previous value.  Verdicts do not depend on it. */
+size_t hbls_dec_pair_max(size_t items);
 /* Tuning: the random linear combination's public-key side groups a verification group's items
  * into shared-doubling chunks sized to keep about `lanes` lanes busy (at most 16 items per chunk;
  * calls of fewer than 2 lanes' worth keep one ladder per item).  0 restores the default 65536

@@ -155,3 +155,38 @@ def test_batch_mixed_random(hipbls):
     assert sts == [OK] * n_val
     assert outs == hipbls.sign_batch(secrets_, msgs)
     assert hipbls.verify_batch([hipbls.secret_to_public_key(s) for s in secrets_], msgs, outs) == [OK] * n_val
+
+
+def test_lane_pair_subgroup_checks(hipbls, fixtures, kats):
+    """The subgroup checks with each item's ladder split over a lane pair (hbls_dec_pair_max; the
+    non-default small-call path of vbatch.hip k_g1_subgroup_h / k_g2_subgroup_h) give the same
+    verdicts: the fixtures (off-subgroup keys and signatures, every encoding reject), the KATs, and
+    the off-subgroup G2 points, in batches below and above a pair threshold of 8."""
+    import json
+    import os
+
+    from charon_amd import _lib
+    L = _lib.load_library()
+    cs = fixtures["verify"]
+    P = [bytes.fromhex(c["pk"]) for c in cs]
+    M = [bytes.fromhex(c["msg"]) for c in cs]
+    S = [bytes.fromhex(c["sig"]) for c in cs]
+    exp = [c["status"] for c in cs]
+    with open(os.path.join(os.path.dirname(__file__), "golden", "off_subgroup_g2.json")) as f:
+        off = [bytes.fromhex(x) for x in json.load(f)["points"]]
+    vecs = [kats["registration"]] + kats["deposit"]
+    kp = [hipbls.secret_to_public_key(bytes.fromhex(v["sk"])) for v in vecs]
+    km = [bytes.fromhex(v["msg"]) for v in vecs]
+    ks = [bytes.fromhex(v["sig"]) for v in vecs]
+    P2, M2, S2 = kp + kp[:1] * len(off), km + km[:1] * len(off), ks + off
+    exp2 = [OK] * len(vecs) + [BAD_SIGNATURE] * len(off)
+    prev = L.hbls_dec_pair_max(1 << 30)
+    try:
+        assert hipbls.verify_batch(P, M, S) == exp
+        assert hipbls.verify_batch(P2, M2, S2) == exp2
+        L.hbls_dec_pair_max(8)  # a batch above it keeps the one-lane kernels, one below takes pairs
+        assert hipbls.verify_batch(P[:6], M[:6], S[:6]) == exp[:6]
+        assert hipbls.verify_batch(P, M, S) == exp
+    finally:
+        L.hbls_dec_pair_max(prev)
+    assert hipbls.verify_batch(P, M, S) == exp
