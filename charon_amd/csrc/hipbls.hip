@@ -338,6 +338,7 @@ struct Ws {
   bool used = false;
   hipStream_t side[N_SIDE] = {};
   hipEvent_t ev_fork = nullptr, ev_side[N_SIDE] = {}, ev_ta = nullptr, ev_msm = nullptr;
+  hipEvent_t ev_pk = nullptr;  // the partials' keys decompressed (side 0, before the DV keys)
   hipEvent_t ev_h = nullptr;  // host calls: the hashing done (before the messages' lines)
 };
 
@@ -550,6 +551,7 @@ int dev_create(int ord, Dev** out) {
     HCHK(hipEventCreateWithFlags(&w.ev_ta, hipEventDisableTiming));
     HCHK(hipEventCreateWithFlags(&w.ev_msm, hipEventDisableTiming));
     HCHK(hipEventCreateWithFlags(&w.ev_h, hipEventDisableTiming));
+    HCHK(hipEventCreateWithFlags(&w.ev_pk, hipEventDisableTiming));
     HCHK(hipStreamCreateWithPriority(&d->hc[k_ws].s, hipStreamNonBlocking, prio_lo));
     HCHK(hipEventCreateWithFlags(&d->hc[k_ws].ev, hipEventDisableTiming));
   }
@@ -591,6 +593,7 @@ int init_mask(uint32_t mask) {
   g_adaptive = env_size("HBLS_ADAPTIVE", 1) != 0;
   g_single_max = env_size("HBLS_SINGLE_MAX", SINGLE_MAX_DEFAULT);
   g_dec_pair_max = env_size("HBLS_DEC_PAIR_MAX", 0);
+  g_ta_pair_max = env_size("HBLS_TA_PAIR_MAX", g_ta_pair_max.load());
   g_ws_sets = (int)std::min<size_t>(N_WS_MAX, std::max<size_t>(1, env_size("HBLS_WS_SETS", 3)));
   {
     size_t fb = std::min<size_t>(FE_BATCH, std::max<size_t>(2, env_size("HBLS_FALLBACK_BATCH", g_fb_batch)));
@@ -957,6 +960,7 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
   } else {
     TIMED(d, "k_dec_pk", w.side[0], launch_dec_pk(dpk, (uint32_t)n, vpk, vpkst, w.side[0]));
   }
+  HCHK(hipEventRecord(w.ev_pk, w.side[0]));
   if (n_agg && fold->dv_pk_table) {
     apk = const_cast<G1AEntry*>(fold->dv_pk_table);
     apkst = const_cast<uint8_t*>(fold->dv_pk_table_st);
@@ -990,8 +994,9 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
     HCHK(hipEventRecord(w.ev_ta, st));
   }
 
-  // random linear combinations per item, then per group
-  HCHK(hipStreamWaitEvent(s, w.ev_side[0], 0));
+  // random linear combinations per item, then per group (the partials' keys only: the DV keys'
+  // decompression behind them on side 0 is waited for by the aggregates' combination below)
+  HCHK(hipStreamWaitEvent(s, w.ev_pk, 0));
   HCHK(hipStreamWaitEvent(s, w.ev_side[1], 0));
   TIMED(d, "k_item_group", s, launch_item_group(dgoff, (uint32_t)n_groups, (uint32_t)n, igrp, s));
   const uint32_t rlc_cmax = (uint32_t)std::min<size_t>(RLC_CHUNK, std::max<size_t>(1, n / g_rlc_lanes.load()));
@@ -1056,6 +1061,7 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
     // combined check exactly; with an invalid partial j beside it the check passes for one value
     // of the random r_j only) -- the group's items all take random coefficients (item_always)
     HCHK(hipStreamWaitEvent(s, w.ev_ta, 0));
+    HCHK(hipStreamWaitEvent(s, w.ev_side[0], 0));
     uint2* acoef = smsm && !skip_msm ? (coef_pi ? coef_pi : rlc_fallback.coef) + n : nullptr;
     TIMED(d, "k_rlc", s,
           launch_rlc(apk, apkst, asig, fold->ta_status, nullptr, nullptr, bfe ? 1 : 0, (uint32_t)n_agg, (uint32_t)n,

@@ -20,6 +20,7 @@
 #define HB_FAST_FPMUL 1
 #include "layout.h"
 #include "ta_small.h"
+#include <type_traits>
 
 namespace hb {
 
@@ -731,6 +732,10 @@ __global__ KB_OCC(HB_OCC_STRAUS) void k_ta_stab(const G2JEntry* __restrict__ q, 
 
 // One lane per validator of a wave k_ta_small took: [s] Q over Q's tables (k_ta_jladder's schedule
 // for one member), into the validator's first member slot of `out`, infinity into the others.
+// PAIR: each validator's ladder split over a lane pair (ec28.h F2Half: each lane one coefficient of
+// every Fp2 product), 32 validators per wave, for slots too small to fill the chip, where this
+// ladder is on the slot's critical path (aggregation -> the aggregates' combination -> the check).
+template <bool PAIR>
 __global__ KB_OCC(HB_OCC_STRAUS) void k_ta_sladder(const TaDigits* __restrict__ sdig, const uint8_t* __restrict__ done,
                                                       uint32_t n_groups, uint32_t t, uint4* __restrict__ tab,
                                                       G2JEntry* __restrict__ out) {
@@ -738,11 +743,12 @@ __global__ KB_OCC(HB_OCC_STRAUS) void k_ta_sladder(const TaDigits* __restrict__ 
   __shared__ int8_t naf[4][66];
   __shared__ int naf_top;
   const int lane = (int)(threadIdx.x & 63u);
-  const uint32_t v = blockIdx.x * 64 + (uint32_t)lane;
+  constexpr uint32_t VPW = PAIR ? 32u : 64u;  // validators per wave
+  const uint32_t v = blockIdx.x * VPW + (uint32_t)(PAIR ? lane >> 1 : lane);
   const bool valid = v < n_groups;
   const uint32_t vc = valid ? v : n_groups - 1;
   const uint8_t dn = done[vc];
-  if (dn == 0) return;  // wave-uniform (k_ta_small decides per wave)
+  if (dn == 0) return;  // wave-uniform (k_ta_small decides per wave of 64, which holds this wave)
   if (lane == 0) {
     const TaDigits d = sdig[vc];
     int top = 0;
@@ -750,22 +756,29 @@ __global__ KB_OCC(HB_OCC_STRAUS) void k_ta_sladder(const TaDigits* __restrict__ 
     naf_top = top;
   }
   __syncthreads();
-  const uint4* wt = tab + (size_t)blockIdx.x * 16 * TA_TAB_QUADS * 64 + lane;
+  // k_ta_stab's table layout: per wave of 64 validators, one column per validator
+  const uint4* wt = tab + (size_t)(vc / 64) * 16 * TA_TAB_QUADS * 64 + (vc % 64);
+  using M = typename std::conditional<PAIR, F2Half, F2One>::type;
+  M m{};
+  if constexpr (PAIR) m = f2half_make();
   G2L RL = g2l_infinity();  // the ladder in lazily reduced 28-bit limbs (ec28.h)
   const int top = naf_top;
   HB_NOUNROLL for (int i = top; i >= 0; i--) {
-    RL = g2l_dbl(RL);
+    RL = g2l_dbl(RL, m);
     HB_NOUNROLL for (int b = 0; b < 4; b++) {
       const int dg = naf[b][i];
       if (dg != 0) {  // wave-uniform
         const int e = 4 * b + ((dg < 0 ? -dg : dg) >> 1);
         G2A T = {f2_load_q(wt, e, 0), f2_load_q(wt, e, 6), false};
         if (dg < 0) T.y = f2_neg(T.y);
-        RL = g2l_madd(RL, f2l_from(T.x), f2l_from(T.y));
+        RL = g2l_madd(RL, f2l_from(T.x), f2l_from(T.y), m);
       }
     }
   }
   if (!valid) return;
+  if constexpr (PAIR) {
+    if (lane & 1) return;  // both lanes hold the result
+  }
   G2J R = g2l_to_jac(RL);
   if (dn == 2) R = jac_infinity<Fp2>();
   out[(size_t)v * t] = {R.X, R.Y, R.Z};
@@ -773,6 +786,11 @@ __global__ KB_OCC(HB_OCC_STRAUS) void k_ta_sladder(const TaDigits* __restrict__ 
   for (uint32_t k = 1; k < t; k++) out[(size_t)v * t + k] = {z.X, z.Y, z.Z};
 #endif
 }
+
+// validators up to which the [s] ladder runs on lane pairs (HBLS_TA_PAIR_MAX at init via
+// hbls_ta_pair_max; default 16384 as the hash's lane-pair threshold)
+std::atomic<size_t> g_ta_pair_max{16384};
+static size_t ta_pair_max() { return g_ta_pair_max.load(std::memory_order_relaxed); }
 
 size_t ta_small_table_bytes(uint32_t n_groups) { return (size_t)blocks_of(n_groups, 64) * 16 * sizeof(G2JEntry) * 64; }
 
@@ -784,7 +802,11 @@ void launch_ta_small(const HmEntry* pts, const uint32_t* src, const int64_t* idx
   hipLaunchKernelGGL(k_ta_sprep, grid, dim3(64), 0, s, idx, n_groups, t, csm, sdig, sok, nonuni);
   hipLaunchKernelGGL(k_ta_small, grid, dim3(64), 0, s, pts, src, csm, sdig, sok, n_groups, t, out, done);
   hipLaunchKernelGGL(k_ta_stab, grid, dim3(64), 0, s, (const G2JEntry*)out, n_groups, t, (uint4*)tab, done);
-  hipLaunchKernelGGL(k_ta_sladder, grid, dim3(64), 0, s, sdig, done, n_groups, t, (uint4*)tab, out);
+  if (n_groups <= ta_pair_max())
+    hipLaunchKernelGGL(k_ta_sladder<true>, dim3(blocks_of(n_groups, 32)), dim3(64), 0, s, sdig, done, n_groups, t,
+                       (uint4*)tab, out);
+  else
+    hipLaunchKernelGGL(k_ta_sladder<false>, grid, dim3(64), 0, s, sdig, done, n_groups, t, (uint4*)tab, out);
 }
 
 void launch_ta_lambda(const int64_t* idx, const uint32_t* grp_off, uint32_t n_groups,
