@@ -326,7 +326,7 @@ def per_unit(b=BLOCKS, group_size=1, t=1):
         "k_rlc": (rlc_msm(b, min(group_size, RLC_CHUNK)),) * 2,
         "k_group_prep": (prep,) * 2,
         "k_fb_lines": (b["lines_eval"],) * 2,
-        "k_ta_straus": (ta_msm(b, 1),) * 2,  # one ladder per member (HBLS_TA_MSM off)
+        "k_ta_straus": (ta_msm(b, 1),) * 2,  # one ladder per member
         "k_group_sum": (gsum,) * 2,
         # the two cofactor ladders in lazy limbs (ec28.h): one product more per doubling / addition
         "k_hash_to_g2": (HASH_TO_G2, HASH_TO_G2 + 2 * G2_DEC_LAZY_EXTRA),
