@@ -10,7 +10,7 @@ LABELS = {  # bench.py / TIMED label -> kernel symbols of the slot
     "k_hash_to_g2": ["k_hash_to_g2_1", "k_hash_to_g2", "k_h2c_field", "k_h2c_map", "k_h2c_clear1", "k_h2c_clear1b",
                      "k_h2c_clear2", "k_h2c_clear3", "k_h2c_clear1h", "k_h2c_clear2h"], "k_lines_msg": ["k_lines_msg"],
     "k_dec_pk": ["k_dec_pk", "k_g1_subgroup"], "k_dec_sig_pt": ["k_dec_sig_pt", "k_g2_subgroup"], "k_ta_straus": ["k_ta_jtab", "k_ta_jladder", "k_ta_jgeneral", "k_ta_joint", "k_ta_straus"],
-    "k_ta_small": ["k_ta_sprep", "k_ta_small", "k_ta_stab", "k_ta_sladder"], "k_mml_eval": ["k_mml_eval"],
+    "k_ta_small": ["k_ta_sprep", "k_ta_small", "k_ta_stab", "k_ta_sladder", "k_ta_sladder<false>", "k_ta_sladder<true>"], "k_mml_eval": ["k_mml_eval"],
     "k_pair3_mls": ["k_pair3<5>", "k_lml<0>", "k_lml<1>"],
     "k_group_sum": ["k_group_sum"], "k_rlc": ["k_rlc_msm<1>", "k_rlc<1>", "k_rlc_msm<2>", "k_rlc<2>", "k_rlc_msm<3>", "k_rlc<3>", "k_rlc_msm", "k_rlc",
               "k_rlc_msm<1, 0>", "k_rlc_msm<1, 1>", "k_rlc_msm<1, 2>", "k_rlc_msm<2, 0>", "k_rlc_msm<2, 1>",
