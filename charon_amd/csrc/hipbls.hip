@@ -413,7 +413,7 @@ struct Dev {
   // kc_n entries indexed, kc_tcap slots (a power of two >= 2 kc_n)
   DevBuf kc_keys, kc_hidx;
   size_t kc_n = 0, kc_tcap = 0;
-  // decompressed-signature cache (vbatch.hip k_sc_put / k_sc_get): filled by host-buffer Verify
+  // decompressed-signature cache (vbatch.hip k_sc_write / k_sc_index / k_sc_get): filled by host-buffer Verify
   // batches, read by host-buffer ThresholdAggregate batches.  sc_ev orders every put and get on
   // the device (recorded after each, waited for before the next: a put rewrites ring entries a get
   // may read); enqueued under `mu` like everything else.

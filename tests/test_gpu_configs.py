@@ -261,7 +261,7 @@ def test_slot_c3_adversarial(L, monkeypatch):
         assert np.array_equal(tout[clean], d["root_sigs"].reshape(V, 96)[clean])
     assert {int(x) for x in np.unique(d["exp_agg"])} == {OK, BAD_SIGNATURE, NOT_VERIFIED}
     # the host-buffer entry points on the same slot: the 1 M-item Verify in chunks over the host-call
-    # contexts (hipbls.hip verify_chunks, deferred Miller lines), then ThresholdAggregate taking its
+    # contexts (hipbls.hip verify_large, deferred Miller lines), then ThresholdAggregate taking its
     # members from the decompressed-signature cache -- every status exact, clean aggregates equal
     hst = np.zeros(NP, dtype=np.uint8)
     assert L.hbls_verify_batch(_p(d["pks"]), _p(d["sigs"]), _p(d["item_msgs"]), _p(d["item_off"]), _p(d["item_len"]),
