@@ -35,7 +35,7 @@ EXPORTS = (
     "hbls_signing_roots", "hbls_attestation_signing_roots_device", "hbls_pk_entry_bytes",
     "hbls_decompress_pubkeys_device", "hbls_pubkey_cache_add", "hbls_pubkey_cache_clear", "hbls_pubkey_cache_size",
     "hbls_debug_split", "hbls_build_id", "hbls_sig_cache", "hbls_duty_signing_roots",
-    "hbls_single_max", "hbls_dec_pair_max",
+    "hbls_single_max", "hbls_dec_pair_max", "hbls_tune",
 )
 
 ALL_DEVICES = 0xFFFFFFFF
@@ -153,6 +153,7 @@ def _declare(lib):
         "hbls_sig_cache": ([SZ], SZ),
         "hbls_single_max": ([SZ], SZ),
         "hbls_dec_pair_max": ([SZ], SZ),
+        "hbls_tune": ([ctypes.c_char_p, SZ, P], ctypes.c_int),
         "hbls_duty_signing_roots": ([ctypes.c_int, P, P, P, SZ, P, SZ, P, P, P], ctypes.c_int),
     }
     for name, (args, res) in sig.items():

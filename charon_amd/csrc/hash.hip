@@ -71,26 +71,20 @@ __global__ KB_OCC(HB_OCC_HASH) void k_hash_to_g2_1(const uint8_t* __restrict__ m
   hm[i].h = e;
 }
 
-// messages from which one lane per message fills the chip (HBLS_HASH_ONE_LANE, default 65536)
-static size_t hash_one_lane_min() {
-  static const size_t v = [] {
-    const char* e = getenv("HBLS_HASH_ONE_LANE");
-    return e ? (size_t)strtoull(e, nullptr, 0) : (size_t)65536;
-  }();
-  return v;
-}
+// messages from which one lane per message fills the chip (HBLS_HASH_ONE_LANE, default 65536);
+// g_hash_split = 0 (HBLS_HASH_SPLIT=0) takes the kernels of this file instead of hashsplit.hip's --
+// kept as the cross-check of tests/test_gpu_scale.py.  Both read at init, set by hbls_tune.
+std::atomic<size_t> g_hash_one_lane{65536}, g_hash_split{1};
 
 void launch_hash_to_g2(const uint8_t* msgs, const uint64_t* off, const uint32_t* len, uint32_t n, MsgEntry* hm,
                        hipStream_t s) {
   if (!n) return;
-  // default: the staged fast-unit kernels (hashsplit.hip); HBLS_HASH_SPLIT=0 (read per call) takes
-  // the kernels of this file -- kept as the cross-check of tests/test_gpu_scale.py
-  const char* sp = getenv("HBLS_HASH_SPLIT");
-  if (!(sp && sp[0] == '0')) {
+  // default: the staged fast-unit kernels (hashsplit.hip)
+  if (g_hash_split.load(std::memory_order_relaxed)) {
     launch_hash_to_g2_split(msgs, off, len, n, hm, s);
     return;
   }
-  if (n >= hash_one_lane_min())
+  if (n >= g_hash_one_lane.load(std::memory_order_relaxed))
     hipLaunchKernelGGL(k_hash_to_g2_1, dim3((unsigned)((n + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s, msgs, off, len,
                        n, hm);
   else

@@ -158,12 +158,11 @@ __global__ KB_OCC(HB_OCC_HASH) void k_h2c_clear3(uint32_t n, MsgEntry* __restric
 #endif
 }
 
-// messages up to which the ladders run on lane pairs (HBLS_HASH_PAIR_MAX, read per call; default
-// 16384: 512 wavefronts, half a wave per SIMD -- below it the one-lane ladders leave the chip idle)
-static size_t hash_pair_max() {
-  const char* e = getenv("HBLS_HASH_PAIR_MAX");
-  return e ? (size_t)strtoull(e, nullptr, 0) : (size_t)16384;
-}
+// messages up to which the ladders run on lane pairs (HBLS_HASH_PAIR_MAX, read once at init;
+// default 16384: 512 wavefronts, half a wave per SIMD -- below it the one-lane ladders leave the
+// chip idle)
+std::atomic<size_t> g_hash_pair_max{16384};
+static size_t hash_pair_max() { return g_hash_pair_max.load(std::memory_order_relaxed); }
 
 void launch_hash_to_g2_split(const uint8_t* msgs, const uint64_t* off, const uint32_t* len, uint32_t n, MsgEntry* hm,
                              hipStream_t s) {

@@ -594,6 +594,10 @@ int init_mask(uint32_t mask) {
   g_single_max = env_size("HBLS_SINGLE_MAX", SINGLE_MAX_DEFAULT);
   g_dec_pair_max = env_size("HBLS_DEC_PAIR_MAX", 0);
   g_ta_pair_max = env_size("HBLS_TA_PAIR_MAX", g_ta_pair_max.load());
+  g_hash_pair_max = env_size("HBLS_HASH_PAIR_MAX", g_hash_pair_max.load());
+  g_hash_one_lane = env_size("HBLS_HASH_ONE_LANE", g_hash_one_lane.load());
+  g_hash_split = env_size("HBLS_HASH_SPLIT", 1) != 0;
+  g_fe18_max = env_size("HBLS_FE18_MAX", g_fe18_max.load());
   g_ws_sets = (int)std::min<size_t>(N_WS_MAX, std::max<size_t>(1, env_size("HBLS_WS_SETS", 3)));
   {
     size_t fb = std::min<size_t>(FE_BATCH, std::max<size_t>(2, env_size("HBLS_FALLBACK_BATCH", g_fb_batch)));
@@ -2710,6 +2714,22 @@ int hbls_stats(uint64_t* out, size_t n) {
 
 size_t hbls_fe_batch(size_t min_groups) { return g_fe_batch_min.exchange(min_groups); }
 int hbls_adaptive(int on) { return g_adaptive.exchange(on != 0) ? 1 : 0; }
+// the latency-path layouts by name (tests switch between them within one process)
+int hbls_tune(const char* name, size_t value, size_t* previous) {
+  if (ensure_init()) return -1;
+  if (!name) return set_err("hbls_tune: no name");
+  static const std::pair<const char*, std::atomic<size_t>*> knobs[] = {
+      {"HBLS_HASH_PAIR_MAX", &g_hash_pair_max}, {"HBLS_HASH_ONE_LANE", &g_hash_one_lane},
+      {"HBLS_HASH_SPLIT", &g_hash_split},       {"HBLS_FE18_MAX", &g_fe18_max},
+      {"HBLS_TA_PAIR_MAX", &g_ta_pair_max},     {"HBLS_DEC_PAIR_MAX", &g_dec_pair_max}};
+  for (const auto& k : knobs)
+    if (strcmp(k.first, name) == 0) {
+      const size_t old = k.second->exchange(value);
+      if (previous) *previous = old;
+      return 0;
+    }
+  return set_err(std::string("hbls_tune: unknown setting ") + name);
+}
 size_t hbls_dec_pair_max(size_t items) {
   if (ensure_init()) return 0;
   return g_dec_pair_max.exchange(items);

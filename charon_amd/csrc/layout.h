@@ -223,7 +223,10 @@ constexpr uint32_t MML_PAIRS = 4;  // pairs per multi-Miller loop of the slot-wi
 // Batched verification (vbatch.hip).
 void launch_item_group(const uint32_t* grp_off, uint32_t n_groups, uint32_t n, uint32_t* item_grp, hipStream_t s);
 extern std::atomic<size_t> g_dec_pair_max;
-extern std::atomic<size_t> g_ta_pair_max;  // threshold.hip: the aggregation's [s] ladder on lane pairs up to this many validators  // vbatch.hip: subgroup checks on lane pairs up to this many items
+extern std::atomic<size_t> g_ta_pair_max;
+extern std::atomic<size_t> g_hash_pair_max;
+extern std::atomic<size_t> g_hash_one_lane, g_hash_split;  // hash.hip (the unsplit kernels, a cross-check)
+extern std::atomic<size_t> g_fe18_max;  // pipeline.hip: final exponentiations over eighteen lanes up to this many units  // hashsplit.hip: the cofactor ladders on lane pairs up to this many messages  // threshold.hip: the aggregation's [s] ladder on lane pairs up to this many validators  // vbatch.hip: subgroup checks on lane pairs up to this many items
 void launch_dec_pk(const uint8_t* pks, uint32_t n, G1AEntry* out, uint8_t* st, hipStream_t s);
 void launch_dec_sig_pt(const uint8_t* sigs, uint32_t n, HmEntry* out, uint8_t* st, hipStream_t s,
                        const uint8_t* skip = nullptr);

@@ -262,12 +262,10 @@ __global__ KB_OCC(HB_OCC_PAIR3) void k_pair6_fin(Pair3Args a) {
 #endif
 }
 
-// units up to which the eighteen-lane kernel runs (HBLS_FE18_MAX, read per call; default 256: a
-// few waves per XCD; beyond, the six-lane one's fewer duplicated additions per unit win)
-static uint32_t fe18_max() {
-  const char* e = getenv("HBLS_FE18_MAX");
-  return e ? (uint32_t)strtoul(e, nullptr, 0) : 256u;
-}
+// units up to which the eighteen-lane kernel runs (HBLS_FE18_MAX at init, hbls_tune; default 256:
+// a few waves per XCD; beyond, the six-lane one's fewer duplicated additions per unit win)
+std::atomic<size_t> g_fe18_max{256};
+static size_t fe18_max() { return g_fe18_max.load(std::memory_order_relaxed); }
 
 void launch_pair6_fin(const Pair3Args& a, hipStream_t s) {
   if (!a.n) return;

@@ -666,7 +666,14 @@ def test_threshold_aggregate_uneven_groups(L, hipbls, members):
     assert outs == roots
 
 
-def test_hash_paths_agree(L, monkeypatch):
+def _tune(L, name, value):
+    """hbls_tune: set a latency-path layout by name, return the previous value."""
+    prev = ctypes.c_size_t()
+    assert L.hbls_tune(name.encode(), value, ctypes.byref(prev)) == 0
+    return prev.value
+
+
+def test_hash_paths_agree(L):
     """hash_to_G2 of 65 536 messages through the staged fast kernels (hashsplit.hip, the default),
     then the first 512 of them again through each kernel of hash.hip (HBLS_HASH_SPLIT=0: the
     one-lane kernel for 65 536 messages, the two-lane one for 512; the latter KAT-pinned through
@@ -686,11 +693,13 @@ def test_hash_paths_agree(L, monkeypatch):
     sp = ctypes.c_void_p(s.cuda_stream)
     _chk(L, L.hbls_hash_to_g2_device(_p(dm), _p(off), _p(ln), n, _p(hm_s), sp))
     s.synchronize()
-    monkeypatch.setenv("HBLS_HASH_SPLIT", "0")
-    _chk(L, L.hbls_hash_to_g2_device(_p(dm), _p(off), _p(ln), n, _p(hm_a), sp))
-    _chk(L, L.hbls_hash_to_g2_device(_p(dm), _p(off), _p(ln), k, _p(hm_b), sp))
-    s.synchronize()
-    monkeypatch.delenv("HBLS_HASH_SPLIT")
+    _tune(L, "HBLS_HASH_SPLIT", 0)
+    try:
+        _chk(L, L.hbls_hash_to_g2_device(_p(dm), _p(off), _p(ln), n, _p(hm_a), sp))
+        _chk(L, L.hbls_hash_to_g2_device(_p(dm), _p(off), _p(ln), k, _p(hm_b), sp))
+        s.synchronize()
+    finally:
+        _tune(L, "HBLS_HASH_SPLIT", 1)
     a = hm_a.cpu().numpy().reshape(n, E)[:, :208]
     b = hm_b.cpu().numpy().reshape(k, E)[:, :208]
     assert np.array_equal(a[:k], b)  # the same operations: the same (lazily reduced) words
@@ -711,17 +720,19 @@ def test_hash_paths_agree(L, monkeypatch):
     hm_p = torch.zeros(k * E, dtype=torch.uint8, device=dev)
     hm_1 = torch.zeros(k * E, dtype=torch.uint8, device=dev)
     _chk(L, L.hbls_hash_to_g2_device(_p(dm), _p(off), _p(ln), k, _p(hm_p), sp))
-    monkeypatch.setenv("HBLS_HASH_PAIR_MAX", "0")
-    _chk(L, L.hbls_hash_to_g2_device(_p(dm), _p(off), _p(ln), k, _p(hm_1), sp))
-    s.synchronize()
-    monkeypatch.delenv("HBLS_HASH_PAIR_MAX")
+    prev = _tune(L, "HBLS_HASH_PAIR_MAX", 0)
+    try:
+        _chk(L, L.hbls_hash_to_g2_device(_p(dm), _p(off), _p(ln), k, _p(hm_1), sp))
+        s.synchronize()
+    finally:
+        _tune(L, "HBLS_HASH_PAIR_MAX", prev)
     hp = hm_p.cpu().numpy().reshape(k, E)[:, :208]
     h1 = hm_1.cpu().numpy().reshape(k, E)[:, :208]
     assert np.array_equal(hp, h1)  # the same formulas and values, products split or not
     assert canon(hp) == canon(a[:k])
 
 
-def test_small_calls_lane_layouts_agree(hipbls, monkeypatch):
+def test_small_calls_lane_layouts_agree(L, hipbls):
     """A small Verify batch (the latency path: k_lml with its lane-pair chain and eighteen-lane loop,
     the final exponentiation over eighteen lanes) against the same batch with the six-lane final
     exponentiation (HBLS_FE18_MAX=0) and one-lane hashing ladders (HBLS_HASH_PAIR_MAX=0): the
@@ -740,12 +751,13 @@ def test_small_calls_lane_layouts_agree(hipbls, monkeypatch):
             cases.append((pks[k], msgs[k], sigs[k], OK))
     pk, m, sg, want = zip(*cases)
     got = hipbls.verify_batch(list(pk), list(m), list(sg))
-    monkeypatch.setenv("HBLS_FE18_MAX", "0")
-    monkeypatch.setenv("HBLS_HASH_PAIR_MAX", "0")
-    got6 = hipbls.verify_batch(list(pk), list(m), list(sg))
-    one = hipbls.verify_batch([pk[1]], [m[1]], [sg[1]])
-    monkeypatch.delenv("HBLS_FE18_MAX")
-    monkeypatch.delenv("HBLS_HASH_PAIR_MAX")
+    fe18, hp = _tune(L, "HBLS_FE18_MAX", 0), _tune(L, "HBLS_HASH_PAIR_MAX", 0)
+    try:
+        got6 = hipbls.verify_batch(list(pk), list(m), list(sg))
+        one = hipbls.verify_batch([pk[1]], [m[1]], [sg[1]])
+    finally:
+        _tune(L, "HBLS_FE18_MAX", fe18)
+        _tune(L, "HBLS_HASH_PAIR_MAX", hp)
     assert list(got) == list(want) == list(got6)
     assert list(one) == [want[1]]
 
