@@ -673,6 +673,17 @@ def _tune(L, name, value):
     return prev.value
 
 
+def test_tune_names(L):
+    """hbls_tune: every documented name round-trips its value; an unknown name is an error that
+    names it (include/hipbls.h)."""
+    for name in ("HBLS_HASH_PAIR_MAX", "HBLS_HASH_ONE_LANE", "HBLS_HASH_SPLIT", "HBLS_FE18_MAX", "HBLS_TA_PAIR_MAX",
+                 "HBLS_DEC_PAIR_MAX"):
+        prev = _tune(L, name, 12345)
+        assert _tune(L, name, prev) == 12345, name
+    assert L.hbls_tune(b"HBLS_NO_SUCH_KNOB", 1, None) == -1
+    assert b"HBLS_NO_SUCH_KNOB" in L.hbls_last_error()
+
+
 def test_hash_paths_agree(L):
     """hash_to_G2 of 65 536 messages through the staged fast kernels (hashsplit.hip, the default),
     then the first 512 of them again through each kernel of hash.hip (HBLS_HASH_SPLIT=0: the
