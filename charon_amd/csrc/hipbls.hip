@@ -398,7 +398,6 @@ constexpr unsigned N_RES = 16;
 struct Dev {
   int ord = -1;
   int n_cu = 256;  // compute units (4 SIMDs each)
-  int prio_lo = 0;  // the lowest stream priority (the host-call contexts' streams)
   hipStream_t stream = nullptr;  // the library stream of host-buffer calls
   Ws ws[N_WS_MAX];
   unsigned next_ws = 0;
@@ -539,7 +538,6 @@ int dev_create(int ord, Dev** out) {
   int prio_lo = 0, prio_hi = 0;
   HCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
   HCHK(hipStreamCreateWithPriority(&d->stream, hipStreamNonBlocking, prio_lo));
-  d->prio_lo = prio_lo;
   for (int k_ws = 0; k_ws < g_ws_sets; k_ws++) {
     Ws& w = d->ws[k_ws];
     HCHK(hipEventCreateWithFlags(&w.free_ev, hipEventDisableTiming));
@@ -554,7 +552,8 @@ int dev_create(int ord, Dev** out) {
     HCHK(hipEventCreateWithFlags(&w.ev_msm, hipEventDisableTiming));
     HCHK(hipEventCreateWithFlags(&w.ev_h, hipEventDisableTiming));
     HCHK(hipEventCreateWithFlags(&w.ev_pk, hipEventDisableTiming));
-    HCHK(hipEventCreateWithFlags(&d->hc[k_ws].ev, hipEventDisableTiming));  // its stream: on first use
+    HCHK(hipStreamCreateWithPriority(&d->hc[k_ws].s, hipStreamNonBlocking, prio_lo));
+    HCHK(hipEventCreateWithFlags(&d->hc[k_ws].ev, hipEventDisableTiming));
   }
   HCHK(hipHostMalloc((void**)&d->res_host, N_RES * sizeof(SlotRes), hipHostMallocDefault));
   for (unsigned k = 0; k < N_RES; k++) HCHK(hipEventCreateWithFlags(&d->res_ev[k], hipEventDisableTiming));
@@ -696,20 +695,12 @@ int upload_pinned(Dev& d, Hc& h, const PinnedUploads& u) {
   return 0;
 }
 
-// a context's stream is created when a host-buffer call first takes it: a process that only uses
-// the device entry points (the slot path) holds no idle streams -- every stream the runtime maps
-// takes one of the process's hardware queues (a failed creation leaves the legacy null stream:
-// correct, serialised)
-static void hc_stream(Dev& d, Hc& h) {
-  if (!h.s && hipSetDevice(d.ord) == hipSuccess) (void)hipStreamCreateWithPriority(&h.s, hipStreamNonBlocking, d.prio_lo);
-}
 Hc& hc_acquire(Dev& d) {
   std::unique_lock<std::mutex> lk(d.hc_mu);
   for (;;) {
     for (int k = 0; k < g_ws_sets; k++)
       if (!d.hc[k].busy) {
         d.hc[k].busy = true;
-        hc_stream(d, d.hc[k]);
         return d.hc[k];
       }
     d.hc_cv.wait(lk);
@@ -728,7 +719,6 @@ Hc* hc_try_acquire(Dev& d) {
   for (int k = 0; k < g_ws_sets; k++)
     if (!d.hc[k].busy) {
       d.hc[k].busy = true;
-      hc_stream(d, d.hc[k]);
       return &d.hc[k];
     }
   return nullptr;
