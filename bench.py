@@ -674,8 +674,14 @@ def main(argv=None):
     if timed_events:
         _chk(L, L.hbls_timing(1))
     evs = [mk() for _ in range(args.steps)]
+    PACE = os.environ.get("HBLS_BENCH_PACE", "1") != "0"
     t0 = time.perf_counter()
     for k in range(args.steps):
+        # slot k is enqueued once slot k - n_sets (the one before it on its stream) has completed,
+        # as a node takes slots as they come, rather than every slot up front (HBLS_BENCH_PACE=0):
+        # 12.79-12.84 against 12.59-12.68 M items/s at 20 steps on one box (profiles/r05af_*)
+        if PACE and k >= n_sets:
+            evs[k - n_sets][-1].synchronize()
         step(evs[k])
     torch.cuda.synchronize()
     if world > 1:
