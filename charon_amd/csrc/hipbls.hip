@@ -339,6 +339,7 @@ struct Ws {
   hipStream_t side[N_SIDE] = {};
   hipEvent_t ev_fork = nullptr, ev_side[N_SIDE] = {}, ev_ta = nullptr, ev_msm = nullptr;
   hipEvent_t ev_pk = nullptr;  // the partials' keys decompressed (side 0, before the DV keys)
+  hipEvent_t ev_dec = nullptr;  // the partials' signatures decompressed (side 1, before their subgroup checks)
   hipEvent_t ev_h = nullptr;  // host calls: the hashing done (before the messages' lines)
 };
 
@@ -552,6 +553,7 @@ int dev_create(int ord, Dev** out) {
     HCHK(hipEventCreateWithFlags(&w.ev_msm, hipEventDisableTiming));
     HCHK(hipEventCreateWithFlags(&w.ev_h, hipEventDisableTiming));
     HCHK(hipEventCreateWithFlags(&w.ev_pk, hipEventDisableTiming));
+    HCHK(hipEventCreateWithFlags(&w.ev_dec, hipEventDisableTiming));
     HCHK(hipStreamCreateWithPriority(&d->hc[k_ws].s, hipStreamNonBlocking, prio_lo));
     HCHK(hipEventCreateWithFlags(&d->hc[k_ws].ev, hipEventDisableTiming));
   }
@@ -776,7 +778,7 @@ struct TaFold {
 // decompressed (pts, mst) into ta_out / ta_status; agg_pt (nullable) gets the affine results.
 int ta_tail(Dev& d, Ws& w, const HmEntry* pts, const uint32_t* src, const uint8_t* mst_in, const int64_t* didx,
             const uint32_t* dgoff, size_t n_groups, size_t np, int mode, uint8_t* out, uint8_t* status,
-            HmEntry* agg_pt, hipStream_t s) {
+            HmEntry* agg_pt, hipStream_t s, hipEvent_t mst_ready = nullptr) {
   uint8_t* mst;
   TaDigits* dig;
   void* tab;
@@ -797,9 +799,6 @@ int ta_tail(Dev& d, Ws& w, const HmEntry* pts, const uint32_t* src, const uint8_
                               : ta_table_bytes((uint32_t)np);
   if (wsbuf(w, W_TATAB, tab_bytes, (uint8_t**)&tab)) return -1;
   if (np) {
-    if (src) launch_ta_member_status(mst_in, src, (uint32_t)np, mst, s);
-    else HCHK(hipMemcpyAsync(mst, mst_in, np, hipMemcpyDeviceToDevice, s));
-    HCHK(hipGetLastError());
     // t_u > 1: the joint and small-scalar paths assume groups of exactly t_u members; k_ta_layout
     // flags any other layout in nonuni (the per-member ladders then run instead)
     uint8_t* nonuni = nullptr;
@@ -822,6 +821,13 @@ int ta_tail(Dev& d, Ws& w, const HmEntry* pts, const uint32_t* src, const uint8_
             launch_ta_small(pts, src, didx, (uint32_t)n_groups, (uint32_t)t_u, csm, sdig, sok, stab, sdone, pj, s,
                             nonuni));
     }
+    // the members' statuses are first read by the Lagrange digits: the small-scalar ladders above
+    // run on the decompressed points while their subgroup checks (mst_ready) finish; a member that
+    // fails them makes its group's status and output below whatever the ladders computed
+    if (mst_ready) HCHK(hipStreamWaitEvent(s, mst_ready, 0));
+    if (src) launch_ta_member_status(mst_in, src, (uint32_t)np, mst, s);
+    else HCHK(hipMemcpyAsync(mst, mst_in, np, hipMemcpyDeviceToDevice, s));
+    HCHK(hipGetLastError());
     TIMED(d, "k_ta_lambda", s,
           launch_ta_lambda(didx, dgoff, (uint32_t)n_groups, (uint32_t)np, mode, dig, mst, s, (uint32_t)t_u, nonuni,
                            sdone));
@@ -971,7 +977,7 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
   } else if (n_agg) {
     TIMED(d, "k_dec_pk", w.side[0], launch_dec_pk(fold->dv_pks, (uint32_t)n_agg, apk, apkst, w.side[0]));
   }
-  TIMED(d, "k_dec_sig_pt", w.side[1], launch_dec_sig_pt(dsig, (uint32_t)n, vsig, vsigst, w.side[1]));
+  TIMED(d, "k_dec_sig_pt", w.side[1], launch_dec_sig_pt(dsig, (uint32_t)n, vsig, vsigst, w.side[1], nullptr, w.ev_dec));
   HCHK(hipEventRecord(w.ev_side[0], w.side[0]));
   HCHK(hipEventRecord(w.ev_side[1], w.side[1]));
 
@@ -982,8 +988,10 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
     HCHK(hipStreamWaitEvent(st, w.ev_fork, 0));
     const HmEntry* pts = vsig;
     const uint8_t* mst_in = vsigst;
-    if (fold->ta_src) {
-      HCHK(hipStreamWaitEvent(st, w.ev_side[1], 0));
+    hipEvent_t mst_ready = nullptr;
+    if (fold->ta_src) {  // the points once decompressed; their subgroup statuses before the digits
+      HCHK(hipStreamWaitEvent(st, w.ev_dec, 0));
+      mst_ready = w.ev_side[1];
     } else {  // the aggregation members come as their own bytes: decompress them here
       HmEntry* tpts;
       uint8_t* tdst;
@@ -993,7 +1001,7 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
       mst_in = tdst;
     }
     if (ta_tail(d, w, pts, fold->ta_src, mst_in, fold->ta_idx, fold->grp_off, fold->n_groups, fold->n_partials, 0,
-                fold->ta_out, fold->ta_status, asig, st))
+                fold->ta_out, fold->ta_status, asig, st, mst_ready))
       return -1;
     HCHK(hipEventRecord(w.ev_ta, st));
   }

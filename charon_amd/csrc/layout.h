@@ -228,8 +228,10 @@ extern std::atomic<size_t> g_hash_pair_max;
 extern std::atomic<size_t> g_hash_one_lane, g_hash_split;  // hash.hip (the unsplit kernels, a cross-check)
 extern std::atomic<size_t> g_fe18_max;  // pipeline.hip: final exponentiations over eighteen lanes up to this many units  // hashsplit.hip: the cofactor ladders on lane pairs up to this many messages  // threshold.hip: the aggregation's [s] ladder on lane pairs up to this many validators  // vbatch.hip: subgroup checks on lane pairs up to this many items
 void launch_dec_pk(const uint8_t* pks, uint32_t n, G1AEntry* out, uint8_t* st, hipStream_t s);
+// decoded (nullable): recorded between the decompression and the subgroup checks (which set a
+// failing point to infinity and its status)
 void launch_dec_sig_pt(const uint8_t* sigs, uint32_t n, HmEntry* out, uint8_t* st, hipStream_t s,
-                       const uint8_t* skip = nullptr);
+                       const uint8_t* skip = nullptr, hipEvent_t decoded = nullptr);
 void launch_sc_put(const uint8_t* sigs, const HmEntry* pts, const uint8_t* st, uint32_t n, uint32_t base, uint32_t cap,
                    void* key, HmEntry* ent, uint8_t* est, uint32_t* tab, uint32_t tcap, uint64_t k0, uint64_t k1,
                    hipStream_t s);
