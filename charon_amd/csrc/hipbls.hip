@@ -1072,12 +1072,18 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
     // per combination may be fixed without losing soundness (an invalid aggregate alone fails the
     // combined check exactly; with an invalid partial j beside it the check passes for one value
     // of the random r_j only) -- the group's items all take random coefficients (item_always)
-    HCHK(hipStreamWaitEvent(s, w.ev_ta, 0));
+    //
+    // Key side only (sides1 1, the slot-wide check's MSM takes the signature side): the DV keys
+    // are all it reads, so it runs beside the slot's ThresholdAggregate; the aggregates' statuses
+    // and points are applied where the signature side is read (group_scan's with_agg, msm_take)
+    const bool key_only = sides1 == 1;
+    if (!key_only) HCHK(hipStreamWaitEvent(s, w.ev_ta, 0));
     HCHK(hipStreamWaitEvent(s, w.ev_side[0], 0));
     uint2* acoef = smsm && !skip_msm ? (coef_pi ? coef_pi : rlc_fallback.coef) + n : nullptr;
     TIMED(d, "k_rlc", s,
-          launch_rlc(apk, apkst, asig, fold->ta_status, nullptr, nullptr, bfe ? 1 : 0, (uint32_t)n_agg, (uint32_t)n,
-                     key, apr, asr, s, acoef, sides1));
+          launch_rlc(apk, apkst, key_only ? nullptr : asig, key_only ? nullptr : fold->ta_status, nullptr, nullptr,
+                     bfe ? 1 : 0, (uint32_t)n_agg, (uint32_t)n, key, apr, asr, s, acoef, sides1));
+    HCHK(hipStreamWaitEvent(s, w.ev_ta, 0));  // the groups' states below read the aggregates
   }
   // small calls (no batched final exponentiation): the groups' sums and signature lines do not
   // need the hashed messages, so they overlap the hashing; the wait comes before the pairing
@@ -1142,6 +1148,7 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
         HCHK(hipStreamWaitEvent(sm, w.ev_msm, 0));
         ma.sig = vsig;
         ma.agg_sig = asig;
+        ma.agg_st = n_agg ? fold->ta_status : nullptr;
         ma.coef = coef_pi ? coef_pi : rlc_fallback.coef;
         ma.igrp = igrp;
         ma.gst = gst;

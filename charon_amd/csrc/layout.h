@@ -340,6 +340,7 @@ constexpr uint32_t MSM_PARTS = MSM_KEYS / MSM_CHUNK;
 struct G2MsmArgs {
   const HmEntry* sig;      // items [0, n)
   const HmEntry* agg_sig;  // items [n, n + n_agg): the folded aggregates (group i - n)
+  const uint8_t* agg_st;   // [n_agg] their ThresholdAggregate statuses (nonzero: not in the sum)
   const uint2* coef;       // [n + n_agg]; (0, 0) = the item is not in the combination
   const uint32_t* igrp;    // [n] item -> group
   const uint8_t* gst;      // [groups] group state (G_READY ones enter)

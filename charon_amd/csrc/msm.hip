@@ -34,8 +34,11 @@ constexpr int BLOCK = 64;
 __device__ __forceinline__ bool msm_take(const G2MsmArgs& a, uint32_t i, uint2& ab) {
   ab = a.coef[i];
   if ((ab.x | ab.y) == 0) return false;
-  const uint32_t g = i < a.n ? a.igrp[i] : i - a.n;
-  return a.gst[g] == G_READY;
+  if (i < a.n) return a.gst[a.igrp[i]] == G_READY;
+  // an aggregate's coefficient was drawn before its ThresholdAggregate finished (key side only):
+  // the aggregate enters as group_scan's with_agg takes it -- status OK, not at infinity
+  const uint32_t g = i - a.n;
+  return a.gst[g] == G_READY && !a.agg_st[g] && !a.agg_sig[g].inf;
 }
 
 // one lane per item: bucket sizes

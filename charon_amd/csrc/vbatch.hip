@@ -359,7 +359,8 @@ __device__ __forceinline__ bool item_usable(const G1AEntry& p, uint8_t pst, cons
 // P' = r pk, S' = r sig, written for every item so that the group sums need no branches: unusable
 // items (undecodable, infinity) contribute the point at infinity, items of singleton groups keep
 // r = 1 unless `always` (the folded aggregates).  coef (nullable): the item's (a, b), (0, 0) when
-// unusable; sides 1 computes P' only and writes coef, sides 2 computes S' only from coef.
+// unusable; sides 1 computes P' only and writes coef, sides 2 computes S' only from coef.  sig and
+// sig_st null (sides 1 only): usability by the key alone, the signature's applied by the consumer.
 template <int sides>
 __global__ KB_OCC(HB_OCC_RLC) void k_rlc(const G1AEntry* __restrict__ pk, const uint8_t* __restrict__ pk_st,
                          const HmEntry* __restrict__ sig, const uint8_t* __restrict__ sig_st,
@@ -371,13 +372,13 @@ __global__ KB_OCC(HB_OCC_RLC) void k_rlc(const G1AEntry* __restrict__ pk, const 
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const G1AEntry pe = pk[i];
-  const HmEntry se = sig[i];
+  const HmEntry se = sig ? sig[i] : HmEntry{};
   const G1A P = {pe.x, pe.y, false};
   const G2A S = {se.x, se.y, false};
   G1J rp;
   G2J rs;
   uint32_t a = 0, b = 0;
-  if (!item_usable(pe, pk_st[i], se, sig_st[i])) {
+  if (sig ? !item_usable(pe, pk_st[i], se, sig_st[i]) : (pk_st[i] || pe.inf)) {
     rp = jac_infinity<Fp>();
     rs = jac_infinity<Fp2>();
   } else if (!always && (!grp_off || grp_off[item_grp[i] + 1] - grp_off[item_grp[i]] <= 1)) {
