@@ -1009,9 +1009,13 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
   // random linear combinations per item, then per group (the partials' keys only: the DV keys'
   // decompression behind them on side 0 is waited for by the aggregates' combination below)
   HCHK(hipStreamWaitEvent(s, w.ev_pk, 0));
-  HCHK(hipStreamWaitEvent(s, w.ev_side[1], 0));
-  TIMED(d, "k_item_group", s, launch_item_group(dgoff, (uint32_t)n_groups, (uint32_t)n, igrp, s));
+  // the partials' key side from the keys alone when the slot-wide MSM takes the signature side
+  // (sides1 1, the per-lane combination): it runs beside the signatures' subgroup checks, whose
+  // statuses group_scan and msm_take apply; otherwise the signatures' statuses first
   const uint32_t rlc_cmax = (uint32_t)std::min<size_t>(RLC_CHUNK, std::max<size_t>(1, n / g_rlc_lanes.load()));
+  const bool keys_only = sides1 == 1 && !(dgoff && g_rlc_msm && rlc_cmax > 1);
+  if (!keys_only) HCHK(hipStreamWaitEvent(s, w.ev_side[1], 0));
+  TIMED(d, "k_item_group", s, launch_item_group(dgoff, (uint32_t)n_groups, (uint32_t)n, igrp, s));
   RlcMsmArgs rlc_fallback{};
   uint32_t rlc_fallback_chunks = 0;
   uint2* coef_pi = nullptr;  // per-item path's coefficients (slot-wide check)
@@ -1064,8 +1068,9 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
   } else {
     if (smsm && wsbuf(w, W_COEF, n + n_agg, &coef_pi)) return -1;
     TIMED(d, "k_rlc", s,
-          launch_rlc(vpk, vpkst, vsig, vsigst, igrp, dgoff, item_always, (uint32_t)n, 0, key, pr, sr, s, coef_pi,
-                     sides1));
+          launch_rlc(vpk, vpkst, keys_only ? nullptr : vsig, keys_only ? nullptr : vsigst, igrp, dgoff, item_always,
+                     (uint32_t)n, 0, key, pr, sr, s, coef_pi, sides1));
+    HCHK(hipStreamWaitEvent(s, w.ev_side[1], 0));  // the groups' states below read the signatures
   }
   if (n_agg) {
     // without the batched final exponentiation the folded aggregate keeps r = 1: one coefficient
@@ -1100,6 +1105,7 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
   for (size_t g0 = 0; g0 < n_groups; g0 += gcap) {
     const uint32_t ng = (uint32_t)std::min(gcap, n_groups - g0);
     GroupPrepArgs ga{};
+    ga.keys_only = keys_only ? 1 : 0;
     ga.grp_off = dgoff;
     ga.g0 = (uint32_t)g0;
     ga.ng = ng;
@@ -1147,6 +1153,7 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
         if (!skip_msm) {
         HCHK(hipStreamWaitEvent(sm, w.ev_msm, 0));
         ma.sig = vsig;
+        ma.sig_st = vsigst;
         ma.agg_sig = asig;
         ma.agg_st = n_agg ? fold->ta_status : nullptr;
         ma.coef = coef_pi ? coef_pi : rlc_fallback.coef;

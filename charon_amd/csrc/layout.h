@@ -304,6 +304,7 @@ struct GroupPrepArgs {
   G2JEntry* bS;      // [ceil(ng / fe_batch)]
   uint32_t fe_batch; // groups per batch (a power of two <= FE_BATCH; 0 = FE_BATCH)
   int p_only;        // slot-wide check (msm.hip): the public-key side and the state only, no S
+  int keys_only;     // pr combined from the keys alone (per item, k_rlc): skip unusable items' pr
   const uint8_t* guard;  // nullable: nothing unless *guard != 0
   // small calls: do not read hm (the launch need not wait for the hashing); a message hashing to
   // infinity is then caught by the group's pairing check (its status, k_pair3<FML>) instead of
@@ -339,6 +340,7 @@ constexpr uint32_t MSM_CHUNK = HB_MSM_CHUNK;
 constexpr uint32_t MSM_PARTS = MSM_KEYS / MSM_CHUNK;
 struct G2MsmArgs {
   const HmEntry* sig;      // items [0, n)
+  const uint8_t* sig_st;   // [n] their decompression / subgroup statuses (nonzero: not in the sum)
   const HmEntry* agg_sig;  // items [n, n + n_agg): the folded aggregates (group i - n)
   const uint8_t* agg_st;   // [n_agg] their ThresholdAggregate statuses (nonzero: not in the sum)
   const uint2* coef;       // [n + n_agg]; (0, 0) = the item is not in the combination

@@ -34,9 +34,10 @@ constexpr int BLOCK = 64;
 __device__ __forceinline__ bool msm_take(const G2MsmArgs& a, uint32_t i, uint2& ab) {
   ab = a.coef[i];
   if ((ab.x | ab.y) == 0) return false;
-  if (i < a.n) return a.gst[a.igrp[i]] == G_READY;
-  // an aggregate's coefficient was drawn before its ThresholdAggregate finished (key side only):
-  // the aggregate enters as group_scan's with_agg takes it -- status OK, not at infinity
+  // coefficients are drawn from the keys alone (the combination runs beside the signatures'
+  // subgroup checks and the aggregation): an item enters as group_scan takes it -- signature
+  // status OK, not at infinity
+  if (i < a.n) return a.gst[a.igrp[i]] == G_READY && !a.sig_st[i] && !a.sig[i].inf;
   const uint32_t g = i - a.n;
   return a.gst[g] == G_READY && !a.agg_st[g] && !a.agg_sig[g].inf;
 }

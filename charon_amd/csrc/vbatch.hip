@@ -763,11 +763,11 @@ void launch_pk_cached(const uint8_t* pks, uint32_t n, const uint8_t* keys, const
 void launch_dec_sig_pt(const uint8_t* sigs, uint32_t n, HmEntry* out, uint8_t* st, hipStream_t s, const uint8_t* skip,
                        hipEvent_t decoded) {
   if (!n) {
-    if (decoded) hipEventRecord(decoded, s);
+    if (decoded) (void)hipEventRecord(decoded, s);
     return;
   }
   hipLaunchKernelGGL(k_dec_sig_pt, dim3(blocks_for(n)), dim3(BLOCK), 0, s, sigs, n, out, st, skip);
-  if (decoded) hipEventRecord(decoded, s);
+  if (decoded) (void)hipEventRecord(decoded, s);
   if (n <= dec_pair_max())
     hipLaunchKernelGGL(k_g2_subgroup_h, dim3(blocks_for(2 * n)), dim3(BLOCK), 0, s, n, out, st, skip);
   else

@@ -48,10 +48,13 @@ __device__ __forceinline__ uint8_t group_scan(const GroupPrepArgs& a, uint32_t l
     Sa = hm_load(a.sig[first]);
     return G_READY;
   }
-  // unusable items hold the point at infinity (k_rlc): a plain sum
+  // unusable items hold the point at infinity (k_rlc, k_rlc_msm: a chunk's sum sits in its first
+  // item's slot): a plain sum -- except a key side combined from the keys alone (keys_only, one
+  // item per slot), where a key whose signature then failed is skipped here
   G1J pacc = jac_infinity<Fp>();
   G2J sacc = jac_infinity<Fp2>();
   for (uint32_t i = b; i < e; i++) {
+    if (a.keys_only && !item_usable_g(a.pk[i], a.pk_st[i], a.sig[i], a.sig_st[i])) continue;
     const G1JEntry pj = a.pr[i];
     pacc = jac_add(pacc, G1J{pj.X, pj.Y, pj.Z});
     if (!P_ONLY) {
