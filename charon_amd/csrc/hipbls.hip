@@ -778,7 +778,7 @@ struct TaFold {
 // decompressed (pts, mst) into ta_out / ta_status; agg_pt (nullable) gets the affine results.
 int ta_tail(Dev& d, Ws& w, const HmEntry* pts, const uint32_t* src, const uint8_t* mst_in, const int64_t* didx,
             const uint32_t* dgoff, size_t n_groups, size_t np, int mode, uint8_t* out, uint8_t* status,
-            HmEntry* agg_pt, hipStream_t s, hipEvent_t mst_ready = nullptr) {
+            HmEntry* agg_pt, hipStream_t s, hipEvent_t mst_ready = nullptr, hipEvent_t pts_ready = nullptr) {
   uint8_t* mst;
   TaDigits* dig;
   void* tab;
@@ -819,8 +819,10 @@ int ta_tail(Dev& d, Ws& w, const HmEntry* pts, const uint32_t* src, const uint8_
         return -1;
       TIMED(d, "k_ta_small", s,
             launch_ta_small(pts, src, didx, (uint32_t)n_groups, (uint32_t)t_u, csm, sdig, sok, stab, sdone, pj, s,
-                            nonuni));
+                            nonuni, pts_ready));
+      pts_ready = nullptr;  // waited for inside, after the index-only split
     }
+    if (pts_ready) HCHK(hipStreamWaitEvent(s, pts_ready, 0));
     // the members' statuses are first read by the Lagrange digits: the small-scalar ladders above
     // run on the decompressed points while their subgroup checks (mst_ready) finish; a member that
     // fails them makes its group's status and output below whatever the ladders computed
@@ -988,9 +990,9 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
     HCHK(hipStreamWaitEvent(st, w.ev_fork, 0));
     const HmEntry* pts = vsig;
     const uint8_t* mst_in = vsigst;
-    hipEvent_t mst_ready = nullptr;
+    hipEvent_t mst_ready = nullptr, pts_ready = nullptr;
     if (fold->ta_src) {  // the points once decompressed; their subgroup statuses before the digits
-      HCHK(hipStreamWaitEvent(st, w.ev_dec, 0));
+      pts_ready = w.ev_dec;
       mst_ready = w.ev_side[1];
     } else {  // the aggregation members come as their own bytes: decompress them here
       HmEntry* tpts;
@@ -1001,7 +1003,7 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
       mst_in = tdst;
     }
     if (ta_tail(d, w, pts, fold->ta_src, mst_in, fold->ta_idx, fold->grp_off, fold->n_groups, fold->n_partials, 0,
-                fold->ta_out, fold->ta_status, asig, st, mst_ready))
+                fold->ta_out, fold->ta_status, asig, st, mst_ready, pts_ready))
       return -1;
     HCHK(hipEventRecord(w.ev_ta, st));
   }
@@ -1151,6 +1153,10 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
         HCHK(hipEventRecord(w.ev_msm, s));
         hipStream_t sm = w.side[0];
         if (!skip_msm) {
+        // the bucket counters zeroed before the wait (side 0 is idle since the keys' decompression;
+        // under three slots these fills wait for free CUs: ~1 ms on the check's chain otherwise)
+        HCHK(hipMemsetAsync(ma.cnt, 0, MSM_KEYS * sizeof(uint32_t), sm));
+        HCHK(hipMemsetAsync(ma.cur, 0, MSM_KEYS * sizeof(uint32_t), sm));
         HCHK(hipStreamWaitEvent(sm, w.ev_msm, 0));
         ma.sig = vsig;
         ma.sig_st = vsigst;
@@ -1161,8 +1167,6 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
         ma.gst = gst;
         ma.n = (uint32_t)n;
         ma.n_agg = (uint32_t)n_agg;
-        HCHK(hipMemsetAsync(ma.cnt, 0, MSM_KEYS * sizeof(uint32_t), sm));
-        HCHK(hipMemsetAsync(ma.cur, 0, MSM_KEYS * sizeof(uint32_t), sm));
         TIMED(d, "k_msm_count", sm, launch_msm_count(ma, sm));
         TIMED(d, "k_msm_scan", sm, launch_scan(ma.cnt, MSM_KEYS, ma.off, sm));
         TIMED(d, "k_msm_fill", sm, launch_msm_fill(ma, sm));

@@ -121,10 +121,11 @@ void launch_ta_joint(const HmEntry* pts, const uint32_t* src, const TaDigits* di
 // of exactly t members (idx: their share indices); done[g] != 0 for the groups it aggregated (their
 // sums at out[g t], infinity at the other members), the rest left to the per-member ladders
 // (skip = done).  Workspace: csm [n_groups t], sdig / sok / done [n_groups], tab ta_small_table_bytes.
+// pts_ready (nullable): waited for after the index-only split (k_ta_sprep), before pts is read.
 size_t ta_small_table_bytes(uint32_t n_groups);
 void launch_ta_small(const HmEntry* pts, const uint32_t* src, const int64_t* idx, uint32_t n_groups, uint32_t t,
                      int64_t* csm, TaDigits* sdig, uint8_t* sok, void* tab, uint8_t* done, G2JEntry* out,
-                     hipStream_t s, const uint8_t* nonuni);
+                     hipStream_t s, const uint8_t* nonuni, hipEvent_t pts_ready = nullptr);
 void launch_ta_member_status(const uint8_t* sig_st, const uint32_t* src, uint32_t n_partials, uint8_t* mstat,
                              hipStream_t s);
 

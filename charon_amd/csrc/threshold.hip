@@ -796,10 +796,15 @@ size_t ta_small_table_bytes(uint32_t n_groups) { return (size_t)blocks_of(n_grou
 
 void launch_ta_small(const HmEntry* pts, const uint32_t* src, const int64_t* idx, uint32_t n_groups, uint32_t t,
                      int64_t* csm, TaDigits* sdig, uint8_t* sok, void* tab, uint8_t* done, G2JEntry* out,
-                     hipStream_t s, const uint8_t* nonuni) {
-  if (!n_groups) return;
+                     hipStream_t s, const uint8_t* nonuni, hipEvent_t pts_ready) {
+  if (!n_groups) {
+    if (pts_ready) (void)hipStreamWaitEvent(s, pts_ready, 0);
+    return;
+  }
   const dim3 grid(blocks_of(n_groups, 64));
+  // the split reads the share indices only: it runs while the members are still being decompressed
   hipLaunchKernelGGL(k_ta_sprep, grid, dim3(64), 0, s, idx, n_groups, t, csm, sdig, sok, nonuni);
+  if (pts_ready) (void)hipStreamWaitEvent(s, pts_ready, 0);
   hipLaunchKernelGGL(k_ta_small, grid, dim3(64), 0, s, pts, src, csm, sdig, sok, n_groups, t, out, done);
   hipLaunchKernelGGL(k_ta_stab, grid, dim3(64), 0, s, (const G2JEntry*)out, n_groups, t, (uint4*)tab, done);
   if (n_groups <= ta_pair_max())
