@@ -34,7 +34,7 @@ bench() {
 }
 lines() {
   bench c3 &&
-  bench c2 $QUIET &&
+  bench c2 $QUIET --steps 20 --warmup 3 &&
   bench c4 $QUIET &&
   bench c5 --cpu-seconds 0 --callers 0 --key-tables 0 --host-api 0
 }
