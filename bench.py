@@ -57,8 +57,6 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 from charon_amd import opcounts  # noqa: E402
-from charon_amd.shard import (SlotExchange, init_library_comm, library_allgather, max_over_ranks,  # noqa: E402
-                               owned_validators, pack_layout, pack_views, unpack_gathered)
 
 METRIC = "verified partial sigs/sec + ThresholdAggregate/sec per node, 1-8 MI355X"
 
@@ -210,6 +208,7 @@ def corrupt(L, d, frac, seed, classes=(0, 1, 2, 3, 4)):
 def setup_inputs(L, wl, V, rank):
     """Synthetic cluster -> host arrays; keys and signatures are derived on the GPU."""
     from charon_amd import synth
+    from charon_amd.shard import owned_validators
     n, t = wl["n"], wl["t"]
     cl = synth.make_cluster(V, n, t, first_validator=owned_validators(rank, V).start, n_msgs=wl["n_msgs"] or 64,
                             distinct_messages=wl["distinct"])
@@ -272,8 +271,10 @@ def cpu_baseline(d, seconds: float):
     does) + one ThresholdAggregate over t partials, checked against the root-key signature.  The
     loop is native (tests/native/hostcheck.cpp hc_cpu_slot, std::thread workers); threads = usable
     host cores, at most 16."""
-    from charon_amd.build import build_hostcheck
-    hc = ctypes.CDLL(build_hostcheck(verbose=False))
+    from charon_amd.build import build_hostcheck, check_hostcheck
+    hc_path = build_hostcheck(verbose=False)
+    hc_id = check_hostcheck(hc_path)  # never time a harness built from other sources
+    hc = ctypes.CDLL(hc_path)
     n, t = d["n"], d["t"]
     midx = np.ascontiguousarray(d["midx"], dtype=np.uint32)
     ta_idx = np.ascontiguousarray(d["ta_idx"], dtype=np.int64)  # the aggregated share indices, per validator
@@ -299,7 +300,10 @@ def cpu_baseline(d, seconds: float):
                       f"(tests/native/hostcheck.cpp hc_cpu_slot, {threads} std::threads), one hash_to_G2 and one "
                       f"pairing check per Verify as herumi does; not herumi (absent offline), a lower bound on "
                       f"a CPU backend's rate",
-            "agrees_with_expected": bad == 0 and bad2 == 0, "wall_s": round(wall, 2)}
+            "agrees_with_expected": bad == 0 and bad2 == 0, "wall_s": round(wall, 2),
+            "per_core_items_per_s": round(units * (n + 1) / wall / threads, 2),
+            "single_thread_items_per_s": round((n + 1) / per_unit, 2),
+            "harness_build_id": hc_id}
 
 
 def concurrent_callers(L, d, threads: int, seconds: float):
@@ -509,6 +513,77 @@ def roofline_from_timing(recs, steps, units):
     return dom, per
 
 
+def launch_ranks(n: int, argv) -> int:
+    """`bench.py --gpus N` without a launcher: run N ranks of this script as child processes, one
+    per GPU, with the environment torch.distributed.run would give them (RANK, LOCAL_RANK,
+    WORLD_SIZE, MASTER_ADDR 127.0.0.1, a free MASTER_PORT).  This process never touches the GPU: it
+    starts the children, forwards nothing (they share its stdout, where rank 0 prints the one JSON
+    line), and returns the first failing child's exit status -- stopping the others, which would
+    otherwise wait at a barrier for the rank that died."""
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                print(f"bench.py: rank {procs.index(p)} exited with {code}; stopping the other ranks",
+                      file=sys.stderr)
+                for q in live:
+                    q.terminate()
+                for q in live:
+                    try:
+                        q.wait(timeout=20)
+                    except subprocess.TimeoutExpired:
+                        q.kill()
+                        q.wait()
+                live = []
+        time.sleep(0.05)
+    return rc
+
+
+def dry_run(args, rank: int, world: int, local: int) -> int:
+    """The launcher and the control plane without a GPU: every rank joins gloo, the ranks' own
+    environments and a stand-in step time are gathered, rank 0 prints the merged line."""
+    import torch.distributed as dist
+    if args.dry_run == 2 and rank == world - 1:  # the launcher test's failing rank
+        print(f"rank {rank}: failing on purpose (--dry-run 2)", file=sys.stderr)
+        return 3
+    mine = {"rank": rank, "local_rank": local, "world_size": world,
+            "master_addr": os.environ.get("MASTER_ADDR"), "master_port": os.environ.get("MASTER_PORT"),
+            "pid": os.getpid()}
+    t0 = time.perf_counter()
+    sum(i * i for i in range(20000 * (rank + 1)))
+    el = time.perf_counter() - t0
+    envs, times = [mine], [el]
+    if world > 1:
+        dist.init_process_group("gloo")
+        envs, times = [None] * world, [None] * world
+        dist.all_gather_object(envs, mine)
+        dist.all_gather_object(times, el)
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "dry_run": True, "ranks": envs,
+                          "per_rank_ms_per_step": [round(x * 1e3, 3) for x in times],
+                          "ms_per_step": round(max(times) * 1e3, 3)}), flush=True)
+    return 0
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser(description="charon BLS hot path on MI355X")
     ap.add_argument("--gpus", type=int, default=1)
@@ -538,16 +613,32 @@ def main(argv=None):
                     help="at one GPU: run the multi-GPU exchange (RCCL world of one) inside the timed region")
     ap.add_argument("--mode", default="slot", choices=["slot", "staged"],
                     help="slot: one hbls_slot_device call per step (stages overlap); staged: stage by stage")
+    ap.add_argument("--dry-run", type=int, default=0,
+                    help="1: no GPU -- every rank joins the gloo control plane, reports its rank environment "
+                         "and prints the merged line (tests the launcher on a CPU host); 2: the same with "
+                         "the last rank failing")
     args = ap.parse_args(argv)
 
+    if args.gpus < 1:
+        print(f"bench.py: --gpus {args.gpus}: need at least one", file=sys.stderr)
+        return 2
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no launcher: start the N ranks here, before anything in this process touches the GPU
+        return launch_ranks(args.gpus, sys.argv[1:] if argv is None else list(argv))
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
-    local = int(os.environ.get("LOCAL_RANK", 0))
-    if world != args.gpus and rank == 0:
-        print(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
+    local = int(os.environ.get("LOCAL_RANK", rank))
+    if world != args.gpus:
+        # never measure a world other than the one asked for (a line labelled with the wrong N)
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}: refusing to run", file=sys.stderr)
+        return 2
+    if args.dry_run:
+        return dry_run(args, rank, world, local)
 
     import torch
     import torch.distributed as dist
+    from charon_amd.shard import (SlotExchange, init_library_comm, library_allgather, max_over_ranks,
+                                   pack_layout, pack_views, unpack_gathered)
 
     torch.cuda.set_device(local)
     if world > 1:
@@ -687,7 +778,10 @@ def main(argv=None):
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    per_rank_s = [elapsed]
     if world > 1:
+        per_rank_s = [None] * world
+        dist.all_gather_object(per_rank_s, elapsed)
         elapsed = max_over_ranks(elapsed, torch.device("cpu"))
 
     seg = np.array([[e[i].elapsed_time(e[i + 1]) for i in range(n_ev - 1)] for e in evs])  # ms
@@ -871,6 +965,9 @@ def main(argv=None):
         "metric": METRIC, "value": round(value, 1),
         "unit": "items/s (verified partial signatures + ThresholdAggregates)",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
+        # the ranks' own times (the line takes the slowest) and the RCCL world the library joined
+        "per_rank_ms_per_step": [round(x / args.steps * 1e3, 3) for x in per_rank_s],
+        "rccl_world": L.hbls_comm_size() if xw else 0,
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "u32 (Fp/Fr Montgomery limbs, integer VALU)",
         "data": "synthetic: SHA-256-derived keys, Shamir shares and signing roots (charon_amd/synth.py); "
@@ -985,6 +1082,8 @@ def main(argv=None):
         out["cpu_baseline"] = cpu_baseline(d, args.cpu_seconds)
 
     if xw:
+        if L.hbls_comm_size() != world:
+            parity["rccl_world_matches"] = False
         _chk(L, L.hbls_comm_destroy())
     if world > 1:
         dist.destroy_process_group()

@@ -31,7 +31,7 @@ EXPORTS = (
     "hbls_verify_device", "hbls_threshold_aggregate_device", "hbls_verify_aggregate_device", "hbls_slot_device",
     "hbls_hm_entry_bytes", "hbls_sync", "hbls_status_bitmap",
     "hbls_timing", "hbls_timing_read", "hbls_comm_id_bytes", "hbls_comm_unique_id", "hbls_comm_init",
-    "hbls_allgather_device", "hbls_comm_destroy", "hbls_stats", "hbls_fe_batch", "hbls_slot_msm", "hbls_adaptive", "hbls_rlc_lanes", "hbls_ta_joint", "hbls_attestation_signing_roots",
+    "hbls_allgather_device", "hbls_comm_size", "hbls_comm_destroy", "hbls_stats", "hbls_fe_batch", "hbls_slot_msm", "hbls_adaptive", "hbls_rlc_lanes", "hbls_ta_joint", "hbls_attestation_signing_roots",
     "hbls_signing_roots", "hbls_attestation_signing_roots_device", "hbls_pk_entry_bytes",
     "hbls_decompress_pubkeys_device", "hbls_pubkey_cache_add", "hbls_pubkey_cache_clear", "hbls_pubkey_cache_size",
     "hbls_debug_split", "hbls_build_id", "hbls_sig_cache", "hbls_duty_signing_roots",
@@ -142,6 +142,7 @@ def _declare(lib):
         "hbls_comm_unique_id": ([P], ctypes.c_int),
         "hbls_comm_init": ([ctypes.c_int, ctypes.c_int, P], ctypes.c_int),
         "hbls_allgather_device": ([P, P, SZ, P], ctypes.c_int),
+        "hbls_comm_size": ([], ctypes.c_int),
         "hbls_comm_destroy": ([], ctypes.c_int),
         "hbls_stats": ([P, SZ], ctypes.c_int),
         "hbls_fe_batch": ([SZ], SZ),

@@ -19,15 +19,6 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 SOURCES = ["hipbls.hip", "pipeline.hip", "threshold.hip", "vbatch.hip", "vgroup.hip", "roots.hip", "hash.hip", "msm.hip",
            "hashsplit.hip"]
-HEADERS = ["hd.h", "consts.h", "fp.h", "fr.h", "tower.h", "ec.h", "ec28.h", "sha256.h", "h2c.h", "pairing.h", "ops.h", "pair3.h",
-           "pair6.h", "layout.h", "lines.h", "rlc.h", "ta_small.h", "pair28.h", "hostmul64.h", "coalesce.h", "msgtable.h"]
-
-
-def _newer(target, deps):
-    if not os.path.exists(target):
-        return False
-    t = os.path.getmtime(target)
-    return all(os.path.getmtime(d) <= t for d in deps)
 
 
 def build_id(defines=()) -> str:
@@ -72,16 +63,56 @@ def build_library(force: bool = False, verbose: bool = True, defines=(), out: st
     return LIB
 
 
+HOSTCHECK_PREFIX = "hbls-hostcheck:"
+HOSTCHECK_FLAGS = ["-O3", "-march=x86-64-v3", "-std=c++17", "-pthread", "-shared", "-fPIC"]
+
+
+def hostcheck_build_id(defines=(), flags=None, root: str = "") -> str:
+    """The id embedded in the CPU harness: sha256 (16 hex digits) over the harness source, every
+    header of charon_amd/csrc (it includes the kernels' arithmetic from there), the compiler flags
+    and the defines -- what `hc_build_id()` of a harness built from this tree returns."""
+    import hashlib
+    root = root or ROOT
+    csrc = os.path.join(root, "charon_amd", "csrc")
+    h = hashlib.sha256()
+    files = [os.path.join(root, "tests", "native", "hostcheck.cpp")] + \
+        sorted(os.path.join(csrc, f) for f in os.listdir(csrc) if f.endswith(".h"))
+    for f in files:
+        h.update(os.path.relpath(f, root).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+        h.update(b"\0")
+    h.update(" ".join((flags or HOSTCHECK_FLAGS) + ["-D" + d for d in defines]).encode())
+    return HOSTCHECK_PREFIX + h.hexdigest()[:16]
+
+
+def embedded_hostcheck_id(path: str) -> str:
+    """The harness id inside a built harness file, read from its bytes (no loading)."""
+    import re
+    with open(path, "rb") as f:
+        m = re.search(rb"hbls-hostcheck:[0-9a-f]{16}", f.read())
+    return m.group(0).decode() if m else ""
+
+
+def check_hostcheck(path: str, defines=(), root: str = "") -> str:
+    """The harness's id if it was built from the tree's sources (with these defines), else raise:
+    a stale harness would time or check code the kernels no longer run."""
+    got, want = embedded_hostcheck_id(path), hostcheck_build_id(defines, root=root)
+    if got != want:
+        raise RuntimeError(f"stale CPU harness {path}: built as {got or '(unstamped)'}, the tree is {want}")
+    return got
+
+
 def build_hostcheck(force: bool = False, verbose: bool = True, defines=(), out: str = "") -> str:
     """defines / out: another build of the harness (e.g. ("HB_FP_ILP",): the two-accumulator
-    products, tests/test_sanitizers.py)."""
+    products, tests/test_sanitizers.py).  A harness whose embedded id (hc_build_id) equals this
+    tree's is reused; any other -- a header touched, other flags -- is rebuilt."""
     src = os.path.join(ROOT, "tests", "native", "hostcheck.cpp")
     out = out or os.path.join(ROOT, "tests", "native", "libhbls_hostcheck.so")
-    deps = [src] + [os.path.join(CSRC, f) for f in HEADERS]
-    if not force and _newer(out, deps):
+    bid = hostcheck_build_id(defines)
+    if not force and os.path.exists(out) and embedded_hostcheck_id(out) == bid:
         return out
-    cmd = ["g++", "-O3", "-march=x86-64-v3", "-std=c++17", "-pthread", "-shared", "-fPIC", "-o", out + ".tmp", src]
-    cmd[1:1] = ["-D" + d for d in defines]
+    cmd = ["g++"] + HOSTCHECK_FLAGS + ["-D" + d for d in defines] + [f'-DHC_BUILD_ID="{bid}"', "-o", out + ".tmp", src]
     subprocess.run(cmd, check=True, timeout=900)
     os.replace(out + ".tmp", out)
     if verbose:
@@ -89,16 +120,20 @@ def build_hostcheck(force: bool = False, verbose: bool = True, defines=(), out: 
     return out
 
 
+SANITIZED_FLAGS = ["-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
+                   "-fno-sanitize-recover=undefined", "-std=c++17", "-pthread", "-shared", "-fPIC"]
+
+
 def build_hostcheck_sanitized(force: bool = False, verbose: bool = True) -> str:
     """The test harness under AddressSanitizer + UndefinedBehaviorSanitizer (host code only; the
-    GPU build has no sanitizer here).  tests/test_sanitizers.py runs the host tests against it."""
+    GPU build has no sanitizer here).  tests/test_sanitizers.py runs the host tests against it.
+    Reused only when its embedded id matches the tree (as build_hostcheck)."""
     src = os.path.join(ROOT, "tests", "native", "hostcheck.cpp")
     out = os.path.join(ROOT, "tests", "native", "libhbls_hostcheck_asan.so")
-    deps = [src] + [os.path.join(CSRC, f) for f in HEADERS]
-    if not force and _newer(out, deps):
+    bid = hostcheck_build_id(flags=SANITIZED_FLAGS)
+    if not force and os.path.exists(out) and embedded_hostcheck_id(out) == bid:
         return out
-    cmd = ["g++", "-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
-           "-fno-sanitize-recover=undefined", "-std=c++17", "-pthread", "-shared", "-fPIC", "-o", out + ".tmp", src]
+    cmd = ["g++"] + SANITIZED_FLAGS + [f'-DHC_BUILD_ID="{bid}"', "-o", out + ".tmp", src]
     subprocess.run(cmd, check=True, timeout=900)
     os.replace(out + ".tmp", out)
     if verbose:

@@ -42,6 +42,13 @@ constexpr int BLOCK = 64;
 // Serialize).  Status precedence follows herumi: any undecodable partial -> BAD_SIGNATURE
 // (deserialisation happens first, herumi.go:255-264), then combine failure.  agg_pt (nullable):
 // the affine result, for the folded post-aggregate verification of the slot entry point.
+//
+// Invariant the slot path relies on: a group with a member whose status is M_BAD_SIG never uses
+// its ladders' outputs (pts) -- it is zeroed here whatever they hold.  In hbls_slot_device the
+// aggregation ladders start once the partials are decoded (ev_dec) and only the Lagrange digits
+// wait for the subgroup statuses (mst_ready), so k_g2_subgroup may overwrite a failing member's
+// point with infinity while a ladder reads it; such a member's status is M_BAD_SIG by the time
+// this kernel runs (it is ordered after mst_ready), so the raced values are never published.
 __global__ KERNEL_BOUNDS void k_group_sum(const uint32_t* __restrict__ grp_off, uint32_t n_groups, int mode,
                                           const G2JEntry* __restrict__ pts, const uint8_t* __restrict__ mstat,
                                           uint8_t* __restrict__ out, uint8_t* __restrict__ status,
@@ -415,13 +422,22 @@ struct Dev {
   DevBuf kc_keys, kc_hidx;
   size_t kc_n = 0, kc_tcap = 0;
   // decompressed-signature cache (vbatch.hip k_sc_write / k_sc_index / k_sc_get): filled by host-buffer Verify
-  // batches, read by host-buffer ThresholdAggregate batches.  sc_ev orders every put and get on
-  // the device (recorded after each, waited for before the next: a put rewrites ring entries a get
-  // may read); enqueued under `mu` like everything else.
+  // batches, read by host-buffer ThresholdAggregate batches; enqueued under `mu` like everything
+  // else.  Puts run on their own stream sc_s, off the Verify call's critical path: each waits for
+  // its call's pipeline (`pipe`) and for every get enqueued before it (a put rewrites ring entries
+  // a get may read), and records `done`.  A get waits only for puts whose pipeline has already
+  // completed (a short kernel pair); the ring entries of puts still behind their pipeline are
+  // passed to it as a range of misses (sc_inflight is in ring order: puts are serialised on sc_s).
   DevBuf sc_key, sc_ent, sc_st, sc_tab;
   size_t sc_cap = 0, sc_cursor = 0, sc_filled = 0;
-  hipEvent_t sc_ev = nullptr;
-  bool sc_ev_valid = false;
+  hipStream_t sc_s = nullptr;
+  struct ScPut {
+    size_t start, m;
+    hipEvent_t pipe, done;
+  };
+  std::deque<ScPut> sc_inflight;
+  std::vector<hipEvent_t> sc_gets;     // gets not yet known complete
+  std::vector<hipEvent_t> sc_ev_pool;  // spare events
   // adaptive slot-wide check (HBLS_ADAPTIVE): outcomes of recent checked calls, copied to pinned host
   // memory asynchronously and read once their event has completed -- never a synchronisation
   SlotRes* res_host = nullptr;
@@ -940,7 +956,7 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
                wsbuf(w, W_MPART2, MSM_PARTS / 128, &ma.part2) || wsbuf(w, W_MTOT, 1, &ma.total) ||
                wsbuf(w, W_PBUF1, 3 * nb1, &pbuf1) || wsbuf(w, W_PBUF2, 3 * nb2, &pbuf2) ||
                wsbuf(w, W_PBUF3, 3 * nb2, &pbuf3) ||
-               wsbuf(w, W_SFAIL, 1, &sfail) || wsbuf(w, W_MLEV, N_LINES * gcap, &mlev)))
+               wsbuf(w, W_SFAIL, 2, &sfail) || wsbuf(w, W_MLEV, N_LINES * gcap, &mlev)))
     return -1;
   // adaptive: the outcome of the last completed checked call decides whether this one tries the
   // slot-wide check at all (skip: the fallback's kernels run unguarded, sfail set to 1)
@@ -1217,10 +1233,12 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
         pf.status = sfail;
         if (!skip_msm) {
           TIMED(d, "k_pair3_fin", s, g_fe6 ? launch_pair6_fin(pf, s) : launch_pair3_fin(pf, s));
+          HCHK(hipMemsetAsync(sfail + 1, 0, 1, s));
           TIMED(d, "k_slot_verdict", s, launch_slot_verdict(gst, sfail, ng, gver + g0, s));
-          // deferred lines: the per-batch check behind a failed slot-wide check reads them
+          // deferred lines: read by the per-batch check behind a failed slot-wide check and by
+          // the per-item fallback of any group that was not READY (k_slot_verdict sets sfail[1])
           if (lines_at_p)
-            TIMED(d, "k_lines_msg", s, launch_lines_msg(defer_hm, (uint32_t)defer_msgs, s, sfail));
+            TIMED(d, "k_lines_msg", s, launch_lines_msg(defer_hm, (uint32_t)defer_msgs, s, sfail + 1));
           // the slot-wide check failed: the per-batch check (signature sides per item and group;
           // computed in the first pass when the check was skipped)
           if (rlc_fallback_chunks) {
@@ -1651,25 +1669,55 @@ int kc_fill(Dev& d, const uint8_t* keys, size_t first, size_t m) {
 // ---- decompressed-signature cache (Dev::sc_*; kernels in vbatch.hip).  Both run under d.mu.
 // sc_ready: the device's cache at the current capacity (allocated on first use; a capacity change
 // drops the old contents), false when the cache is off.
+hipEvent_t sc_event(Dev& d) {
+  hipEvent_t e = nullptr;
+  if (!d.sc_ev_pool.empty()) {
+    e = d.sc_ev_pool.back();
+    d.sc_ev_pool.pop_back();
+  } else if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+    return nullptr;
+  }
+  return e;
+}
+// drop the records of completed puts and gets (wait: block until every one has completed)
+void sc_prune(Dev& d, bool wait) {
+  while (!d.sc_inflight.empty()) {
+    Dev::ScPut& p = d.sc_inflight.front();
+    if (wait) (void)hipEventSynchronize(p.done);
+    else if (hipEventQuery(p.done) != hipSuccess) break;
+    d.sc_ev_pool.push_back(p.pipe);
+    d.sc_ev_pool.push_back(p.done);
+    d.sc_inflight.pop_front();
+  }
+  std::vector<hipEvent_t> live;
+  for (hipEvent_t e : d.sc_gets) {
+    if (wait) (void)hipEventSynchronize(e);
+    if (wait || hipEventQuery(e) == hipSuccess) d.sc_ev_pool.push_back(e);
+    else live.push_back(e);
+  }
+  d.sc_gets.swap(live);
+}
 bool sc_ready(Dev& d, bool alloc) {
   const size_t cap = g_sc_cap.load();
   if (cap == 0) return false;
   if (d.sc_cap == cap) return true;
   if (!alloc) return false;
+  sc_prune(d, true);  // the buffers may be reallocated: nothing may still use them
   void* p;
   if (ensure_buf(d.sc_key, cap * 96, &p) || ensure_buf(d.sc_ent, cap * sizeof(HmEntry), &p) ||
       ensure_buf(d.sc_st, cap, &p) || ensure_buf(d.sc_tab, 2 * cap * sizeof(uint32_t), &p))
     return false;
   if (hipMemset(d.sc_tab.p, 0, 2 * cap * sizeof(uint32_t)) != hipSuccess) return false;
-  if (!d.sc_ev && hipEventCreateWithFlags(&d.sc_ev, hipEventDisableTiming) != hipSuccess) return false;
+  if (!d.sc_s && hipStreamCreateWithFlags(&d.sc_s, hipStreamNonBlocking) != hipSuccess) return false;
   d.sc_cap = cap;
   d.sc_cursor = d.sc_filled = 0;
   return true;
 }
-// after a Verify batch: its m signatures (bytes in group order, sig) and their decompressed points
-// and statuses (pts, st, the verification's workspace) enter the ring
-int sc_put(Dev& d, const uint8_t* sig, const HmEntry* pts, const uint8_t* st, size_t m, hipStream_t s) {
-  if (!m || !sc_ready(d, true)) return 0;
+// After a Verify batch's pipeline on s: its m signatures (bytes in group order, sig) and their
+// decompressed points and statuses (pts, st: the verification's workspace w) enter the ring on
+// sc_s, and the workspace is released behind the put -- or on s when nothing is put.
+int sc_put_release(Dev& d, Ws& w, const uint8_t* sig, const HmEntry* pts, const uint8_t* st, size_t m, hipStream_t s) {
+  if (!m || !sc_ready(d, true)) return ws_release(w, s);
   const size_t cap = d.sc_cap;
   if (m > cap) {  // only the last cap items fit
     sig += 96 * (m - cap);
@@ -1677,26 +1725,44 @@ int sc_put(Dev& d, const uint8_t* sig, const HmEntry* pts, const uint8_t* st, si
     st += m - cap;
     m = cap;
   }
-  if (d.sc_ev_valid) HCHK(hipStreamWaitEvent(s, d.sc_ev, 0));
-  TIMED(d, "k_sc_put", s,
+  sc_prune(d, false);
+  hipEvent_t pipe = sc_event(d), done = sc_event(d);
+  if (!pipe || !done) return set_err("signature cache: no event");
+  HCHK(hipEventRecord(pipe, s));
+  HCHK(hipStreamWaitEvent(d.sc_s, pipe, 0));
+  for (hipEvent_t g : d.sc_gets) HCHK(hipStreamWaitEvent(d.sc_s, g, 0));
+  TIMED(d, "k_sc_put", d.sc_s,
         launch_sc_put(sig, pts, st, (uint32_t)m, (uint32_t)d.sc_cursor, (uint32_t)cap, d.sc_key.p, (HmEntry*)d.sc_ent.p,
-                      (uint8_t*)d.sc_st.p, (uint32_t*)d.sc_tab.p, (uint32_t)(2 * cap), g_sc_k0, g_sc_k1, s));
-  HCHK(hipEventRecord(d.sc_ev, s));
-  d.sc_ev_valid = true;
+                      (uint8_t*)d.sc_st.p, (uint32_t*)d.sc_tab.p, (uint32_t)(2 * cap), g_sc_k0, g_sc_k1, d.sc_s));
+  HCHK(hipEventRecord(done, d.sc_s));
+  d.sc_inflight.push_back({d.sc_cursor, m, pipe, done});
   d.sc_cursor = (d.sc_cursor + m) & (cap - 1);
   d.sc_filled = std::min(cap, d.sc_filled + m);
-  return 0;
+  return ws_release(w, d.sc_s);
 }
 // before an aggregation's decompression: the cached points of its n members into pts / st, hit[i]
-// set for those (k_dec_sig_pt then skips them).  Returns whether the cache was consulted.
+// set for those (k_dec_sig_pt then skips them).  Returns whether the cache was consulted.  Never
+// waits for a Verify still in its pipeline: the entries its put will write are misses.
 bool sc_get(Dev& d, const uint8_t* sig, size_t n, HmEntry* pts, uint8_t* st, uint8_t* hit, hipStream_t s) {
   if (!n || !d.sc_filled || !sc_ready(d, false)) return false;
-  if (d.sc_ev_valid && hipStreamWaitEvent(s, d.sc_ev, 0) != hipSuccess) return false;
+  sc_prune(d, false);
+  size_t k = 0;
+  while (k < d.sc_inflight.size() && hipEventQuery(d.sc_inflight[k].pipe) == hipSuccess) k++;
+  if (k && hipStreamWaitEvent(s, d.sc_inflight[k - 1].done, 0) != hipSuccess) return false;
+  size_t busy_lo = 0, busy_len = 0;
+  if (k < d.sc_inflight.size()) {
+    busy_lo = d.sc_inflight[k].start;
+    for (size_t j = k; j < d.sc_inflight.size(); j++) busy_len += d.sc_inflight[j].m;
+    if (busy_len >= d.sc_cap) return false;  // every entry is being rewritten
+  }
+  hipEvent_t e = sc_event(d);
+  if (!e) return false;
   TIMED(d, "k_sc_get", s,
         launch_sc_get(sig, (uint32_t)n, d.sc_key.p, (const HmEntry*)d.sc_ent.p, (const uint8_t*)d.sc_st.p,
-                      (const uint32_t*)d.sc_tab.p, (uint32_t)(2 * d.sc_cap), g_sc_k0, g_sc_k1, pts, st, hit, s));
-  if (hipEventRecord(d.sc_ev, s) != hipSuccess) return false;
-  d.sc_ev_valid = true;
+                      (const uint32_t*)d.sc_tab.p, (uint32_t)(2 * d.sc_cap), g_sc_k0, g_sc_k1, pts, st, hit,
+                      (uint32_t)d.sc_cap, (uint32_t)busy_lo, (uint32_t)busy_len, s));
+  if (hipEventRecord(e, s) != hipSuccess) return false;
+  d.sc_gets.push_back(e);
   return true;
 }
 
@@ -1820,6 +1886,9 @@ int verify_large(Dev& d, const uint8_t* pks, const uint8_t* sigs, const uint8_t*
     const size_t ib = gstart[cg[c]], m = gstart[cg[c + 1]] - ib, ng = cg[c + 1] - cg[c];
     // the chunk's messages: all of them for one chunk, else its contiguous range
     const size_t mfirst = K == 1 ? 0 : midx[ib], mcount = K == 1 ? nm : midx[ib + m - 1] + 1 - midx[ib];
+    // deferred lines per chunk: verify_pipeline decides its batched final exponentiation from the
+    // chunk's own group count, so a chunk below that size computes its lines here
+    const bool cdefer = defer && defer_lines(ng, mcount);
     Ws& w = ws_acquire(d, sc);
     void* sio;
     if (ensure_buf(hc.io[I_STAT], m, &sio)) return -1;
@@ -1832,21 +1901,21 @@ int verify_large(Dev& d, const uint8_t* pks, const uint8_t* sigs, const uint8_t*
     HCHK(hipStreamWaitEvent(hs, w.ev_ta, 0));
     TIMED(d, "k_hash_to_g2", hs, launch_hash_to_g2(dmsg, doff + mfirst, dlen + mfirst, (uint32_t)mcount, hm + mfirst, hs));
     HCHK(hipEventRecord(w.ev_h, hs));
-    if (!defer) TIMED(d, "k_lines_msg", hs, launch_lines_msg(hm + mfirst, (uint32_t)mcount, hs));
+    if (!cdefer) TIMED(d, "k_lines_msg", hs, launch_lines_msg(hm + mfirst, (uint32_t)mcount, hs));
     HCHK(hipEventRecord(w.ev_side[2], hs));
     // the key cache is looked up on the device (k_pk_cached): its tables are only rewritten under
     // Dev::mu, held while this call enqueues, after every launch that may still read them
     if (verify_pipeline(d, w, cpk, csig, dmidx + ib, hm, m, dgoffs + goff_base[c], ng, dst, sc, w.ev_side[2], nullptr,
-                        true, w.ev_h, hm + mfirst, defer ? mcount : 0))
+                        true, w.ev_h, hm + mfirst, cdefer ? mcount : 0))
       return -1;
     {  // the decompressed partials into the signature cache (the aggregation of these partials reads them)
       HmEntry* vsig;
       uint8_t* vsigst;
-      if (wsbuf(w, W_VSIG, m, &vsig) || wsbuf(w, W_VSIGST, m, &vsigst) || sc_put(d, csig, vsig, vsigst, m, sc))
+      if (wsbuf(w, W_VSIG, m, &vsig) || wsbuf(w, W_VSIGST, m, &vsigst) ||
+          sc_put_release(d, w, csig, vsig, vsigst, m, sc))
         return -1;
     }
     LAUNCH(k_scatter_status, m, sc, dst, dord + ib, (uint32_t)m, dst_out);
-    if (ws_release(w, sc)) return -1;
     if (c) {
       HCHK(hipEventRecord(hc.ev, sc));
       HCHK(hipStreamWaitEvent(h0.s, hc.ev, 0));
@@ -1973,11 +2042,11 @@ int verify_host(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msgs, co
     {  // the decompressed partials into the signature cache (the aggregation of these partials reads them)
       HmEntry* vsig;
       uint8_t* vsigst;
-      if (wsbuf(w, W_VSIG, m, &vsig) || wsbuf(w, W_VSIGST, m, &vsigst) || sc_put(d, dsig, vsig, vsigst, m, h.s))
+      if (wsbuf(w, W_VSIG, m, &vsig) || wsbuf(w, W_VSIGST, m, &vsigst) ||
+          sc_put_release(d, w, dsig, vsig, vsigst, m, h.s))
         return -1;
     }
     if (whole) LAUNCH(k_scatter_status, m, h.s, dst, dord, (uint32_t)m, dst_out);
-    if (ws_release(w, h.s)) return -1;
     lk.unlock();  // enqueued: other callers may enqueue while this one waits for its stream
     const double t_enq = now_ms();
     if (whole) {
@@ -2035,6 +2104,13 @@ int group_op_host(const uint8_t* sigs, const int64_t* idx, const uint32_t* grp_o
     if (np) TIMED(d, "k_dec_sig_pt", h.s, launch_dec_sig_pt(dsig, (uint32_t)np, pts, mst0, h.s, hit));
     if (ta_tail(d, w, pts, nullptr, mst0, didx, dgoff, ng, np, mode, (uint8_t*)dout, (uint8_t*)dst, nullptr, h.s))
       return -1;
+    // diagnosis (HBLS_STATS / HBLS_HOST_TIMING): the cache's hit flags, copied on the call's stream
+    // before the workspace holding them is released to other callers
+    std::vector<uint8_t> hh;
+    if (hit && (host_timing() || stats_on())) {
+      hh.resize(np);
+      HCHK(hipMemcpyAsync(hh.data(), hit, np, hipMemcpyDeviceToHost, h.s));
+    }
     if (ws_release(w, h.s)) return -1;
     lk.unlock();  // enqueued: other callers may enqueue while this one waits for its stream
     const double t_enq = now_ms();
@@ -2042,10 +2118,7 @@ int group_op_host(const uint8_t* sigs, const int64_t* idx, const uint32_t* grp_o
     HCHK(hipMemcpyAsync(status + gb, dst, ng, hipMemcpyDeviceToHost, h.s));
     HCHK(hipStreamSynchronize(h.s));
     size_t hits = 0;
-    if (hit && (host_timing() || stats_on())) {  // diagnosis: the cache's hits (the workspace is
-      // released, but a caller of these switches runs nothing else on it while this host waits)
-      std::vector<uint8_t> hh(np);
-      HCHK(hipMemcpy(hh.data(), hit, np, hipMemcpyDeviceToHost));
+    if (!hh.empty()) {
       for (uint8_t x : hh) hits += x;
       g_stats[6] += np;
       g_stats[7] += hits;
@@ -2817,6 +2890,13 @@ int hbls_allgather_device(const void* send, void* recv, size_t bytes, void* stre
   if (!g_comm) return set_err("hbls_allgather_device: no communicator (hbls_comm_init)");
   NCHK(ncclAllGather(send, recv, bytes, ncclUint8, g_comm, (hipStream_t)stream));
   return 0;
+}
+
+int hbls_comm_size(void) {
+  if (!g_comm) return 0;
+  int n = 0;
+  if (ncclCommCount(g_comm, &n) != ncclSuccess) return -1;
+  return n;
 }
 
 int hbls_comm_destroy(void) {

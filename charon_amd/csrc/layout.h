@@ -238,7 +238,7 @@ void launch_sc_put(const uint8_t* sigs, const HmEntry* pts, const uint8_t* st, u
                    hipStream_t s);
 void launch_sc_get(const uint8_t* sigs, uint32_t n, const void* key, const HmEntry* ent, const uint8_t* est,
                    const uint32_t* tab, uint32_t tcap, uint64_t k0, uint64_t k1, HmEntry* out, uint8_t* st, uint8_t* hit,
-                   hipStream_t s);
+                   uint32_t cap, uint32_t busy_lo, uint32_t busy_len, hipStream_t s);
 void launch_kc_index(const uint8_t* keys, uint32_t first, uint32_t m, uint32_t* tab, uint32_t tcap, uint64_t k0,
                      uint64_t k1, hipStream_t s);
 void launch_pk_cached(const uint8_t* pks, uint32_t n, const uint8_t* keys, const G1AEntry* tabe, const uint8_t* tst,
@@ -325,7 +325,7 @@ void launch_batch_verdict(const uint8_t* gst, const uint8_t* bver, uint32_t ng, 
                           uint32_t* count, hipStream_t s, const uint8_t* guard = nullptr, uint32_t fe_batch = FE_BATCH);
 // slot-wide check passed (*sfail == 0): gver[g] = (gst[g] != READY); else nothing (the per-group
 // path decides)
-void launch_slot_verdict(const uint8_t* gst, const uint8_t* sfail, uint32_t ng, uint8_t* gver, hipStream_t s);
+void launch_slot_verdict(const uint8_t* gst, uint8_t* sfail, uint32_t ng, uint8_t* gver, hipStream_t s);
 
 // The signature side of a whole verification as one multi-scalar multiplication (msm.hip):
 // S = sum over the items i of READY groups of [a_i] sig_i + [b_i] (-psi^2 sig_i), bucket method

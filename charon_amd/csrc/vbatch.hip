@@ -229,12 +229,15 @@ __global__ __launch_bounds__(64) void k_sc_index(uint32_t n, uint32_t base, uint
     if (dead && atomicCAS(&tab[slot], old, e + 1) == old) return;
   }
 }
-// one lane per signature: the cached point and status when its bytes are cached (hit = 1)
+// one lane per signature: the cached point and status when its bytes are cached (hit = 1).
+// Ring entries [busy_lo, busy_lo + busy_len) (mod cap) belong to puts that may still be writing
+// them (sc_get): an index pointing there is a miss, whatever the bytes there say.
 __global__ __launch_bounds__(64) void k_sc_get(const uint8_t* __restrict__ sigs, uint32_t n,
                                                const uint4* __restrict__ key, const HmEntry* __restrict__ ent,
                                                const uint8_t* __restrict__ est, const uint32_t* __restrict__ tab,
                                                uint32_t tcap, uint64_t k0, uint64_t k1, HmEntry* __restrict__ out,
-                                               uint8_t* __restrict__ st, uint8_t* __restrict__ hit) {
+                                               uint8_t* __restrict__ st, uint8_t* __restrict__ hit, uint32_t cap,
+                                               uint32_t busy_lo, uint32_t busy_len) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint4 kb[6];
@@ -244,6 +247,7 @@ __global__ __launch_bounds__(64) void k_sc_get(const uint8_t* __restrict__ sigs,
   for (uint32_t q = 0; q < SC_PROBES; q++) {
     const uint32_t v = tab[(home + q) & (tcap - 1)];
     if (v == 0) break;
+    if (((v - 1 - busy_lo) & (cap - 1)) < busy_len) continue;
     if (sc_eq(key + 6ull * (v - 1), kb)) {
       out[i] = ent[v - 1];
       st[i] = est[v - 1];
@@ -783,10 +787,10 @@ void launch_sc_put(const uint8_t* sigs, const HmEntry* pts, const uint8_t* st, u
 }
 void launch_sc_get(const uint8_t* sigs, uint32_t n, const void* key, const HmEntry* ent, const uint8_t* est,
                    const uint32_t* tab, uint32_t tcap, uint64_t k0, uint64_t k1, HmEntry* out, uint8_t* st, uint8_t* hit,
-                   hipStream_t s) {
+                   uint32_t cap, uint32_t busy_lo, uint32_t busy_len, hipStream_t s) {
   if (!n) return;
   hipLaunchKernelGGL(k_sc_get, dim3(blocks_for(n)), dim3(BLOCK), 0, s, sigs, n, (const uint4*)key, ent, est, tab, tcap,
-                     k0, k1, out, st, hit);
+                     k0, k1, out, st, hit, cap, busy_lo, busy_len);
 }
 void launch_rlc(const G1AEntry* pk, const uint8_t* pk_st, const HmEntry* sig, const uint8_t* sig_st,
                 const uint32_t* item_grp, const uint32_t* grp_off, int always, uint32_t n, uint32_t key_base,

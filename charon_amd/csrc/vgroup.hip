@@ -205,11 +205,22 @@ __global__ __launch_bounds__(64) void k_batch_verdict(const uint8_t* __restrict_
   else list[atomicAdd(count, 1u)] = lg;
 }
 
-__global__ __launch_bounds__(64) void k_slot_verdict(const uint8_t* __restrict__ gst, const uint8_t* __restrict__ sfail,
+// sfail[0]: the slot-wide check's outcome; sfail[1] (zeroed before): set when anything will read
+// the messages' unevaluated Miller lines -- the per-batch check behind a failed slot-wide check,
+// or a group that was not READY (inconsistent messages, a degenerate combination), whose items
+// the per-item fallback checks alone.  The deferred k_lines_msg is guarded by it.
+__global__ __launch_bounds__(64) void k_slot_verdict(const uint8_t* __restrict__ gst, uint8_t* __restrict__ sfail,
                                                       uint32_t ng, uint8_t* __restrict__ gver) {
-  if (*sfail != 0) return;
   const uint32_t lg = blockIdx.x * blockDim.x + threadIdx.x;
-  if (lg < ng) gver[lg] = gst[lg] != G_READY ? 1 : 0;
+  if (sfail[0] != 0) {
+    if (lg == 0) sfail[1] = 1;
+    return;
+  }
+  if (lg < ng) {
+    const bool fb = gst[lg] != G_READY;
+    gver[lg] = fb ? 1 : 0;
+    if (fb) sfail[1] = 1;
+  }
 }
 
 void launch_group_prep(const GroupPrepArgs& a, hipStream_t s) {
@@ -233,7 +244,7 @@ void launch_batch_verdict(const uint8_t* gst, const uint8_t* bver, uint32_t ng, 
     hipLaunchKernelGGL(k_batch_verdict, dim3((ng + 63) / 64), dim3(64), 0, s, gst, bver, ng, gver, list, count, guard,
                        fe_batch ? fe_batch : FE_BATCH);
 }
-void launch_slot_verdict(const uint8_t* gst, const uint8_t* sfail, uint32_t ng, uint8_t* gver, hipStream_t s) {
+void launch_slot_verdict(const uint8_t* gst, uint8_t* sfail, uint32_t ng, uint8_t* gver, hipStream_t s) {
   if (ng) hipLaunchKernelGGL(k_slot_verdict, dim3((ng + 63) / 64), dim3(64), 0, s, gst, sfail, ng, gver);
 }
 

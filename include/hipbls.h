@@ -313,6 +313,9 @@ size_t hbls_comm_id_bytes(void);
 int hbls_comm_unique_id(uint8_t* id);
 int hbls_comm_init(int nranks, int rank, const uint8_t* id);
 int hbls_allgather_device(const void* send, void* recv, size_t bytes, void* stream);
+/* The number of ranks of the communicator as RCCL reports it (ncclCommCount), 0 without one:
+ * bench.py puts it in its line beside n_gpus. */
+int hbls_comm_size(void);
 int hbls_comm_destroy(void);
 
 #ifdef __cplusplus

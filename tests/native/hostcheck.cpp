@@ -281,6 +281,14 @@ int hc_h2c_sum(const uint8_t* msg, uint32_t len, uint8_t* out) {
 #include <atomic>
 #include <thread>
 #include <vector>
+// build provenance (charon_amd/build.py hostcheck_build_id): the sources and flags this harness was
+// compiled from; build_hostcheck reuses a harness only when the id matches the tree, and bench.py's
+// cpu_baseline reports it
+#ifndef HC_BUILD_ID
+#define HC_BUILD_ID "hbls-hostcheck:(unstamped)"
+#endif
+extern "C" const char* hc_build_id() { return HC_BUILD_ID; }
+
 extern "C" int hc_cpu_slot(int threads, int units, int n, int t, const uint8_t* pks, const uint8_t* sigs,
                            const uint8_t* msgs, const uint32_t* midx, const uint8_t* ta_sigs,
                            const uint8_t* root_sigs, const int64_t* ta_idx) {

@@ -49,3 +49,32 @@ def test_loaded_library_reports_its_id():
     assert L.hbls_build_id().decode() == build_id()
     # a variant build carries its defines after the hash; only the hash is compared
     _lib.check_build_id(build_id(("HB_X=1",)))
+
+
+def _copy_harness_tree(tmp_path):
+    root = _copy_tree(tmp_path)
+    os.makedirs(tmp_path / "tests" / "native")
+    shutil.copy(os.path.join(ROOT, "tests", "native", "hostcheck.cpp"), tmp_path / "tests" / "native")
+    return root
+
+
+def test_stale_cpu_harness_is_refused(tmp_path):
+    """The g++ harness behind cpu_baseline and the host tests carries the hash of its sources and
+    flags (hc_build_id); one built before a header changed is refused and rebuilt."""
+    import ctypes
+    from charon_amd import build
+    path = build.build_hostcheck(verbose=False)
+    hid = build.check_hostcheck(path)  # the in-tree harness matches the tree
+    assert hid.startswith(build.HOSTCHECK_PREFIX)
+    lib = ctypes.CDLL(path)
+    lib.hc_build_id.restype = ctypes.c_char_p
+    assert lib.hc_build_id().decode() == hid
+    root = _copy_harness_tree(tmp_path)
+    assert build.hostcheck_build_id(root=root) == hid
+    hdr = tmp_path / "charon_amd" / "csrc" / "fp.h"
+    hdr.write_text(hdr.read_text() + "\n// touched\n")
+    with pytest.raises(RuntimeError, match="stale CPU harness"):
+        build.check_hostcheck(path, root=root)
+    # other flags or defines are another harness
+    assert build.hostcheck_build_id(("HB_FP_ILP",)) != hid
+    assert build.hostcheck_build_id(flags=build.SANITIZED_FLAGS) != hid
