@@ -440,6 +440,51 @@ def aggregate_verify(L, d, d_pk, dev, sp, reps: int = 3, sync_size: int = 512):
     return out
 
 
+def first_error_verify(L, d, d_pk, d_sig, d_midx, d_vgoff, dev, sp, reps: int = 3):
+    """The corrupted shard's partials as ONE ordered set verified up to its first failure
+    (hbls_verify_device_first_error: the callers' first-error-aborts contract, parsigex.go:93-98,
+    sigagg.go:56-63) beside the exact per-item verdicts of the same items (hbls_verify_device),
+    hashing included in both; the first index is checked against the construction."""
+    import torch
+    NP, M = d["NP"], d["M"]
+    up = lambda a: torch.from_numpy(a).to(dev)  # noqa: E731
+    d_m, d_mo, d_ml = up(d["msgs"]), up(d["moff"].view(np.int64)), up(d["mlen"].view(np.int32))
+    hm = torch.zeros(M * L.hbls_hm_entry_bytes(), dtype=torch.uint8, device=dev)
+    st = torch.full((NP,), 255, dtype=torch.uint8, device=dev)
+    first = torch.zeros(1, dtype=torch.int32, device=dev)
+    V = d["V"]
+
+    def run(first_mode):
+        _chk(L, L.hbls_hash_to_g2_device(_p(d_m), _p(d_mo), _p(d_ml), M, _p(hm), sp))
+        if first_mode:
+            _chk(L, L.hbls_verify_device_first_error(_p(d_pk), _p(d_sig), _p(d_midx), _p(hm), NP, _p(d_vgoff), V,
+                                                     _p(st), _p(first), sp))
+        else:
+            _chk(L, L.hbls_verify_device(_p(d_pk), _p(d_sig), _p(d_midx), _p(hm), NP, _p(d_vgoff), V, _p(st), sp))
+
+    res = {}
+    for mode in (True, False):
+        run(mode)  # warm-up
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            run(mode)
+        torch.cuda.synchronize(dev)
+        res[mode] = (time.perf_counter() - t0) / reps
+    run(True)
+    torch.cuda.synchronize(dev)
+    f = int(first.cpu().numpy().view(np.uint32)[0])
+    bad = np.nonzero(d["exp_v"] != 0)[0]
+    want = int(bad[0]) if len(bad) else 0xFFFFFFFF
+    stv = st.cpu().numpy()
+    return {"items": NP, "ms": round(res[True] * 1e3, 3), "items_per_s": round(NP / res[True], 1),
+            "exact_ms": round(res[False] * 1e3, 3), "exact_items_per_s": round(NP / res[False], 1),
+            "first_index": f, "first_index_exact": f == want and (f == 0xFFFFFFFF or stv[f] == d["exp_v"][f]),
+            "unchecked_items": int((stv == 7).sum()),
+            "note": "hash + verify of the shard's partials as one ordered set, first-error mode against "
+                    "exact per-item statuses (no aggregation)"}
+
+
 def key_table_slots(L, d_pk, d_dvpk, outs, NP, V, steps, step, mk, items):
     """The same slots with the public keys taken from decompressed-key tables made once
     (hbls_decompress_pubkeys_device; pubshares are static per cluster lock): the
@@ -1068,6 +1113,10 @@ def main(argv=None):
         out["fallback_stats"] = dict(zip(("items", "groups", "fallback_items", "last_chunk_groups_checked",
                                           "slot_checks", "slot_checks_failed"), list(st)))
     out["kernels"], out["roofline"] = kernel_roofline()
+
+    if rank == 0 and world == 1 and "exp_v" in d and not staged:
+        out["first_error"] = first_error_verify(L, d, d_pk, d_sig, d_midx, d_vgoff, dev, sp)
+        parity["first_error_index_exact"] = out["first_error"]["first_index_exact"]
 
     if rank == 0 and world == 1 and args.aggregate_verify:
         out["verify_aggregate"] = aggregate_verify(L, d, d_pk, dev, sp)

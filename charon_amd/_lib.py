@@ -23,6 +23,7 @@ NOT_VERIFIED = 3
 COMBINE_FAILED = 4
 BAD_SECRET = 5
 BAD_INPUT = 6
+UNCHECKED = 7
 
 EXPORTS = (
     "hbls_init", "hbls_last_error", "hbls_available", "hbls_device_count", "hbls_verify_batch",
@@ -35,7 +36,8 @@ EXPORTS = (
     "hbls_signing_roots", "hbls_attestation_signing_roots_device", "hbls_pk_entry_bytes",
     "hbls_decompress_pubkeys_device", "hbls_pubkey_cache_add", "hbls_pubkey_cache_clear", "hbls_pubkey_cache_size",
     "hbls_debug_split", "hbls_build_id", "hbls_sig_cache", "hbls_duty_signing_roots",
-    "hbls_single_max", "hbls_dec_pair_max", "hbls_tune",
+    "hbls_single_max", "hbls_dec_pair_max", "hbls_tune", "hbls_verify_batch_first_error",
+    "hbls_verify_device_first_error",
 )
 
 ALL_DEVICES = 0xFFFFFFFF
@@ -112,6 +114,8 @@ def _declare(lib):
         "hbls_available": ([], ctypes.c_int),
         "hbls_device_count": ([], ctypes.c_int),
         "hbls_verify_batch": ([P, P, P, P, P, SZ, P], ctypes.c_int),
+        "hbls_verify_batch_first_error": ([P, P, P, P, P, SZ, P, P, P], ctypes.c_int),
+        "hbls_verify_device_first_error": ([P, P, P, P, SZ, P, SZ, P, P, P], ctypes.c_int),
         "hbls_threshold_aggregate_batch": ([P, P, P, SZ, P, P], ctypes.c_int),
         "hbls_aggregate_batch": ([P, P, SZ, P, P], ctypes.c_int),
         "hbls_verify_aggregate_batch": ([P, P, P, P, P, P, SZ, P], ctypes.c_int),

@@ -83,9 +83,16 @@ def parsigex_verify_set(impl, pubshares_by_key: Mapping[bytes, Mapping[int, byte
         pks.append(pubshare)
         msgs.append(ps.signing_root)
         sigs.append(ps.signature)
-    for s in impl.verify_batch(pks, msgs, sigs) if pks else []:
-        if s != OK:
-            raise _wrap("invalid partial signature", "invalid signature: " + _verr(s))
+    if pks and hasattr(impl, "verify_batch_first_error"):
+        # the set up to its first failure (hbls_verify_batch_first_error): under attack the library
+        # resolves only the first failing item instead of every item's verdict
+        first, st = impl.verify_batch_first_error(pks, msgs, sigs)
+        if first >= 0:
+            raise _wrap("invalid partial signature", "invalid signature: " + _verr(st))
+    else:
+        for s in impl.verify_batch(pks, msgs, sigs) if pks else []:
+            if s != OK:
+                raise _wrap("invalid partial signature", "invalid signature: " + _verr(s))
     if pre is not None:
         raise _wrap("invalid partial signature", pre)
 

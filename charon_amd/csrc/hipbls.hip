@@ -327,7 +327,7 @@ enum WsId {
   W_FBUF, W_GS, W_BS, W_BLINES, W_BBAD, W_BVER, W_GLIST, W_GCOUNT,  // batched final exponentiation
   W_MCNT, W_MOFF, W_MCUR, W_MORDER, W_MENT, W_MBUCKET, W_MPART, W_MPART2, W_MTOT, W_PBUF1, W_PBUF2, W_PBUF3, W_SFAIL,  // slot-wide check
   W_MLEV,                                                                          // its evaluated Miller lines
-  W_PFIN, W_TBUF, W_F1, W_F1BAD, W_F1S,                                                                  // final exponentiations' factors
+  W_PFIN, W_TBUF, W_F1, W_F1BAD, W_F1S, W_FIRST,                                                                  // final exponentiations' factors
   W_COUNT_
 };
 
@@ -873,7 +873,8 @@ int ta_tail(Dev& d, Ws& w, const HmEntry* pts, const uint32_t* src, const uint8_
 int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, const uint32_t* didx,
                     const MsgEntry* hm, size_t n, const uint32_t* dgoff, size_t n_groups, uint8_t* dst,
                     hipStream_t s, hipEvent_t hm_ready, const TaFold* fold, bool kc = false,
-                    hipEvent_t h_ready = nullptr, MsgEntry* defer_hm = nullptr, size_t defer_msgs = 0) {
+                    hipEvent_t h_ready = nullptr, MsgEntry* defer_hm = nullptr, size_t defer_msgs = 0,
+                    uint32_t* first_out = nullptr) {
   if (!dgoff) n_groups = n;
   G1AEntry* vpk;
   HmEntry* vsig;
@@ -915,6 +916,20 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
   const size_t fe_min = g_fe_batch_min.load();
   const bool bfe = fe_min && n_groups >= fe_min;
   const int item_always = (bfe || n_agg) ? 1 : 0;  // see the coefficient rule above
+  // First-error mode (first_out, the callers' contract: parsigex.go:93-98, sigagg.go:56-63 stop at
+  // the first failing item): behind a failed combined check only the FIRST failing batch descends
+  // to its groups and only the first failing group to its items -- groups and batches are in item
+  // order, so every item before the first failure has passed a check and every item left
+  // unresolved (ST_UNCHECKED) comes after it.  Without the batched final exponentiation every
+  // group is checked anyway (exact statuses).  *first_out: the first item whose status is decided
+  // and not OK (0xffffffff: none).
+  if (first_out && n_agg) return set_err("verify: the first-error mode takes no folded aggregates");
+  const bool first_only = first_out && bfe;
+  uint32_t* wfirst = nullptr;
+  if (first_only) {
+    if (wsbuf(w, W_FIRST, 2, &wfirst)) return -1;
+    HCHK(hipMemsetAsync(wfirst, 0xff, 2 * sizeof(uint32_t), s));
+  }
   // pairs per multi-Miller loop of the slot-wide check: enough that the loops fill at most one
   // round of waves (21 groups per wave, one wave per SIMD) -- a second, partial round would double
   // the kernel's span (HBLS_MML_PAIRS fixes it)
@@ -1281,7 +1296,8 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
         TIMED(d, "k_pair3_fin", s, launch_pair3_fin(pb, s));
         HCHK(hipMemsetAsync(gcount, 0, sizeof(uint32_t), s));
         TIMED(d, "k_batch_verdict", s,
-              launch_batch_verdict(gst, bver, ng, gver + g0, glist, gcount, s, sfail, (uint32_t)mmlk));
+              launch_batch_verdict(gst, bver, ng, gver + g0, glist, gcount, s, sfail, (uint32_t)mmlk, wfirst,
+                                   (uint32_t)g0));
         // groups of a failing batch: their own (P_g, H(m_g)) loops, then each group alone below
         pm.list = glist;
         pm.count = gcount;
@@ -1355,7 +1371,8 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
         TIMED(d, "k_pair3_fin", s, g_fe6 ? launch_pair6_fin(pf, s) : launch_pair3_fin(pf, s));
         // groups of a failing batch: checked one by one (their stored loop, their own S lines)
         HCHK(hipMemsetAsync(gcount, 0, sizeof(uint32_t), s));
-        TIMED(d, "k_batch_verdict", s, launch_batch_verdict(gst, bver, ng, gver + g0, glist, gcount, s, guard, fb));
+        TIMED(d, "k_batch_verdict", s,
+              launch_batch_verdict(gst, bver, ng, gver + g0, glist, gcount, s, guard, fb, wfirst, (uint32_t)g0));
       }
       TIMED(d, "k_slines", s, launch_slines(gS, glist, gcount, ng, glines, ng, nullptr, s));
       Pair3Args pg{};
@@ -1432,6 +1449,10 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
   sa.status = dst;
   sa.list = list;
   sa.count = count;
+  if (first_only) {
+    TIMED(d, "k_first_group", s, launch_first_group(gver, (uint32_t)n_groups, wfirst + 1, s));
+    sa.first_group = wfirst + 1;
+  }
   TIMED(d, "k_scatter", s, launch_scatter(sa, s));
   // fallback: every item of a failing group on its own; passes beyond the list end exit at once
   for (size_t base = 0; base < n + n_agg; base += fbcap) {
@@ -1453,6 +1474,10 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
     pa.status = dst;
     pa.agg_status = n_agg ? fold->agg_status : nullptr;
     TIMED(d, "k_pair3_fallback", s, launch_pair3(pa, s));
+  }
+  if (first_out) {
+    HCHK(hipMemsetAsync(first_out, 0xff, sizeof(uint32_t), s));
+    TIMED(d, "k_first_item", s, launch_first_item(dst, (uint32_t)n, first_out, s));
   }
   if (ta && !n_agg) {  // the aggregation ran beside the verification: join it
     HCHK(hipStreamWaitEvent(s, w.ev_ta, 0));
@@ -2065,6 +2090,83 @@ int verify_host(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msgs, co
   });
 }
 
+// First-error Verify of an ordered set (hbls_verify_batch_first_error): the callers' loops that
+// stop at their first failing item -- parsigex verifies a peer's set and drops it on the first
+// bad partial (core/parsigex/parsigex.go:93-98), sigagg returns on the first failure
+// (core/sigagg/sigagg.go:56-63), validatorapi on the first bad submission
+// (core/validatorapi/validatorapi.go:302-306).  Groups are runs of consecutive items over one
+// message in the caller's order (at most g_gmax items), so batches and groups are in item order
+// and verify_pipeline's first-error mode resolves only the first failing batch's groups and the
+// first failing group's items: under attack O(groups / batch + batch + group) checks instead of
+// one per item of every failing group.  One device (the order must not be split).
+int verify_first_host(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msgs, const uint64_t* msg_off,
+                      const uint32_t* msg_len, size_t n, int64_t* first, uint8_t* first_status, uint8_t* status) {
+  *first = -1;
+  if (first_status) *first_status = ST_OK;
+  if (n == 0) return 0;
+  if (n >= 0xffffffffull) return set_err("verify first error: too many items");
+  MsgTable all;
+  const unsigned hw = std::thread::hardware_concurrency();
+  if (n >= (1u << 16) && hw >= 4)
+    dedup_messages_par(msgs, msg_off, msg_len, n, all, hw >= 8 ? 8u : 4u);
+  else
+    dedup_messages(msgs, msg_off, msg_len, n, nullptr, all);
+  std::vector<uint32_t> goff;
+  for (size_t k = 0; k < n; k++)
+    if (k == 0 || all.idx[k] != all.idx[k - 1] || k - goff.back() >= g_gmax) goff.push_back((uint32_t)k);
+  const size_t n_groups = goff.size();
+  goff.push_back((uint32_t)n);
+  Dev& d = *devs()[0];
+  Hc& h = hc_acquire(d);
+  struct Rel {
+    Dev& d;
+    Hc& h;
+    ~Rel() { hc_release(d, h); }
+  } rel{d, h};
+  std::unique_lock<std::mutex> lk(d.mu);
+  if (hipSetDevice(d.ord) != hipSuccess) return set_err("hipSetDevice failed");
+  Ws& w = ws_acquire(d, h.s);
+  MsgEntry* hm;
+  hipEvent_t hm_ready = nullptr, h_ready = nullptr;
+  const bool defer = defer_lines(n_groups, all.len.size());
+  if (hash_table(d, all, &hm, !defer, &w, &hm_ready, &h, &h_ready)) return -1;
+  uint8_t *dpk, *dsig;
+  uint32_t *didx, *dgoff;
+  void *pst, *pfirst;
+  if (upload(d, I_PK, pks, 48 * n, &dpk, &h) || upload(d, I_SIG, sigs, 96 * n, &dsig, &h) ||
+      upload(d, I_MIDX, all.idx.data(), n, &didx, &h) || upload(d, I_VGOFF, goff.data(), goff.size(), &dgoff, &h) ||
+      ensure_buf(h.io[I_STAT], n, &pst) || ensure_buf(h.io[I_HM2], sizeof(uint32_t), &pfirst))
+    return -1;
+  uint8_t* dst = (uint8_t*)pst;
+  uint32_t* dfirst = (uint32_t*)pfirst;
+  if (verify_pipeline(d, w, dpk, dsig, didx, hm, n, dgoff, n_groups, dst, h.s, hm_ready, nullptr, true, h_ready, hm,
+                      defer ? all.len.size() : 0, dfirst))
+    return -1;
+  {  // the decoded signatures enter the signature cache as after hbls_verify_batch
+    HmEntry* vsig;
+    uint8_t* vsigst;
+    if (wsbuf(w, W_VSIG, n, &vsig) || wsbuf(w, W_VSIGST, n, &vsigst) || sc_put_release(d, w, dsig, vsig, vsigst, n, h.s))
+      return -1;
+  }
+  lk.unlock();
+  uint32_t f = 0;
+  std::vector<uint8_t> own;
+  uint8_t* hst = status;
+  if (!hst) {
+    own.resize(n);
+    hst = own.data();
+  }
+  HCHK(hipMemcpyAsync(&f, dfirst, sizeof(f), hipMemcpyDeviceToHost, h.s));
+  HCHK(hipMemcpyAsync(hst, dst, n, hipMemcpyDeviceToHost, h.s));
+  HCHK(hipStreamSynchronize(h.s));
+  if (f != 0xffffffffu) {
+    if (f >= n) return set_err("verify first error: index out of range");
+    *first = (int64_t)f;
+    if (first_status) *first_status = hst[f];
+  }
+  return 0;
+}
+
 int check_offsets(const uint32_t* grp_off, size_t n_groups) {
   if (grp_off[0] != 0) return set_err("grp_off[0] must be 0");
   for (size_t g = 0; g < n_groups; g++)
@@ -2338,6 +2440,14 @@ int hbls_verify_batch(const uint8_t* pks, const uint8_t* sigs, const uint8_t* ms
   return verify_coalesced(pks, sigs, msgs, msg_off, msg_len, n, status);
 }
 
+int hbls_verify_batch_first_error(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msgs, const uint64_t* msg_off,
+                                  const uint32_t* msg_len, size_t n, int64_t* first, uint8_t* first_status,
+                                  uint8_t* status) {
+  if (ensure_init()) return -1;
+  if (!first) return set_err("verify first error: no output for the index");
+  return verify_first_host(pks, sigs, msgs, msg_off, msg_len, n, first, first_status, status);
+}
+
 int hbls_threshold_aggregate_batch(const uint8_t* sigs, const int64_t* idx, const uint32_t* grp_off, size_t n_groups,
                                    uint8_t* out, uint8_t* status) {
   if (ensure_init()) return -1;
@@ -2577,6 +2687,26 @@ int hbls_verify_device(const uint8_t* pks, const uint8_t* sigs, const uint32_t* 
   Ws& w = ws_acquire(*d, s);
   if (verify_pipeline(*d, w, pks, sigs, msg_idx, (const MsgEntry*)hm, n, vgrp_off, n_vgroups, status, s, nullptr,
                       nullptr))
+    return -1;
+  return ws_release(w, s);
+}
+
+int hbls_verify_device_first_error(const uint8_t* pks, const uint8_t* sigs, const uint32_t* msg_idx, const void* hm,
+                                   size_t n, const uint32_t* vgrp_off, size_t n_vgroups, uint8_t* status,
+                                   uint32_t* first, void* stream) {
+  Dev* d;
+  hipStream_t s = (hipStream_t)stream;
+  if (dev_of_stream(s, &d)) return -1;
+  if (!first) return set_err("verify first error: no output for the index");
+  if (n == 0) {
+    HCHK(hipMemsetAsync(first, 0xff, sizeof(uint32_t), s));
+    return 0;
+  }
+  if (n >= 0xffffffffull) return set_err("verify first error: too many items");
+  std::lock_guard<std::mutex> lk(d->mu);
+  Ws& w = ws_acquire(*d, s);
+  if (verify_pipeline(*d, w, pks, sigs, msg_idx, (const MsgEntry*)hm, n, vgrp_off, n_vgroups, status, s, nullptr,
+                      nullptr, false, nullptr, nullptr, 0, first))
     return -1;
   return ws_release(w, s);
 }

@@ -319,13 +319,27 @@ void launch_batch_sum(const G2JEntry* gS, uint32_t ng, uint32_t k, G2JEntry* bS,
 // lines[j * stride + u]; bad[u] (nullable) = the point is infinity
 void launch_slines(const G2JEntry* pts, const uint32_t* list, const uint32_t* count, uint32_t n, LineEntry* lines,
                    uint32_t stride, uint8_t* bad, hipStream_t s, const uint8_t* guard = nullptr);
-// group verdicts from the batch verdicts: not READY -> 1, READY in a passing batch -> 0, else the
-// group joins list (its verdict comes from the per-group check)
+// Group verdicts (gver) of the batched paths: 0 passed; 1 .. 0x7f its own check failed (the
+// pairing kernels write their status byte); GV_UNCHECKED a failing batch the first-error mode did
+// not descend into; GV_NOT_READY not in any combined check (inconsistent messages, a degenerate
+// combination): its items are checked alone.
+enum : uint8_t { GV_PASS = 0, GV_UNCHECKED = 0x80, GV_NOT_READY = 0x81 };
+HD bool gv_failed(uint8_t v) { return v != GV_PASS && v < GV_UNCHECKED; }
+// group verdicts from the batch verdicts: not READY -> GV_NOT_READY, READY in a passing batch ->
+// GV_PASS, else the group joins list (its verdict comes from the per-group check).  first
+// (nullable, first-error mode): first[0] is the smallest key g0 + (first group of the batch) over
+// the failing batches (atomicMin, 0xffffffff before the first chunk); only that batch's groups join
+// the list, the other failing batches' groups get GV_UNCHECKED.
 void launch_batch_verdict(const uint8_t* gst, const uint8_t* bver, uint32_t ng, uint8_t* gver, uint32_t* list,
-                          uint32_t* count, hipStream_t s, const uint8_t* guard = nullptr, uint32_t fe_batch = FE_BATCH);
-// slot-wide check passed (*sfail == 0): gver[g] = (gst[g] != READY); else nothing (the per-group
-// path decides)
+                          uint32_t* count, hipStream_t s, const uint8_t* guard = nullptr, uint32_t fe_batch = FE_BATCH,
+                          uint32_t* first = nullptr, uint32_t g0 = 0);
+// slot-wide check passed (*sfail == 0): gver[g] = GV_NOT_READY or GV_PASS; else nothing (the
+// per-group path decides)
 void launch_slot_verdict(const uint8_t* gst, uint8_t* sfail, uint32_t ng, uint8_t* gver, hipStream_t s);
+// first-error mode: *first_group = the smallest g whose own check failed (atomicMin; 0xffffffff
+// before); *first_item = the smallest i with status[i] decided and not OK
+void launch_first_group(const uint8_t* gver, uint32_t n_groups, uint32_t* first_group, hipStream_t s);
+void launch_first_item(const uint8_t* status, uint32_t n, uint32_t* first_item, hipStream_t s);
 
 // The signature side of a whole verification as one multi-scalar multiplication (msm.hip):
 // S = sum over the items i of READY groups of [a_i] sig_i + [b_i] (-psi^2 sig_i), bucket method
@@ -387,6 +401,9 @@ struct ScatterArgs {
   uint8_t* status;
   uint32_t* list;
   uint32_t* count;
+  // first-error mode (nullable): first_group[0] = the first group whose own check failed; items of
+  // GV_FAIL groups after it and of GV_UNCHECKED groups get ST_UNCHECKED instead of a re-check
+  const uint32_t* first_group;
 };
 void launch_scatter(const ScatterArgs& a, hipStream_t s);
 // fallback: lines at -g1 of the listed signatures (entries >= n_items: folded aggregates)

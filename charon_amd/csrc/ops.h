@@ -18,6 +18,7 @@ enum : uint8_t {
   ST_COMBINE_FAILED = 4, // "cannot combine signatures"
   ST_BAD_SECRET = 5,     // "cannot unmarshal secret into Herumi secret key"
   ST_BAD_INPUT = 6,      // malformed batch description (offsets / lengths)
+  ST_UNCHECKED = 7,      // first-error mode: not decided (after the first failing item)
 };
 
 // Parse the 3 flag bits of a compressed encoding.  Returns false for an invalid combination;

@@ -707,7 +707,10 @@ __global__ KB void k_scatter(ScatterArgs a) {
     if (a.pk_st[i]) s = ST_BAD_PUBKEY;
     else if (a.sig_st[i]) s = ST_BAD_SIGNATURE;
     else if (a.pk[i].inf || a.sig[i].inf || a.hm[a.msg_idx[i]].h.inf) s = ST_NOT_VERIFIED;  // verify_core
-    else if (a.gverdict[a.item_grp[i]] == 0) s = ST_OK;
+    else if (a.gverdict[a.item_grp[i]] == GV_PASS) s = ST_OK;
+    else if (a.first_group && (a.gverdict[a.item_grp[i]] == GV_UNCHECKED ||
+                               (gv_failed(a.gverdict[a.item_grp[i]]) && a.item_grp[i] != *a.first_group)))
+      s = ST_UNCHECKED;  // first-error mode: after the first failing group, not resolved
     else if (!a.n_agg && (!a.grp_off || a.grp_off[a.item_grp[i] + 1] - a.grp_off[a.item_grp[i]] <= 1))
       s = ST_NOT_VERIFIED;  // a group of one item (with a folded aggregate it has a second member)
     else {

@@ -196,13 +196,34 @@ __global__ KB_OCC(HB_OCC_LINES) void k_slines(const G2JEntry* __restrict__ pts, 
 
 __global__ __launch_bounds__(64) void k_batch_verdict(const uint8_t* __restrict__ gst, const uint8_t* __restrict__ bver, uint32_t ng,
                                    uint8_t* __restrict__ gver, uint32_t* __restrict__ list,
-                                   uint32_t* __restrict__ count, const uint8_t* __restrict__ guard, uint32_t fb) {
+                                   uint32_t* __restrict__ count, const uint8_t* __restrict__ guard, uint32_t fb,
+                                   const uint32_t* __restrict__ first, uint32_t g0) {
   if (guard && *guard == 0) return;
   const uint32_t lg = blockIdx.x * blockDim.x + threadIdx.x;
   if (lg >= ng) return;
-  if (gst[lg] != G_READY) gver[lg] = 1;
-  else if (bver[lg / fb] == 0) gver[lg] = 0;
+  if (gst[lg] != G_READY) gver[lg] = GV_NOT_READY;
+  else if (bver[lg / fb] == 0) gver[lg] = GV_PASS;
+  else if (first && g0 + (lg / fb) * fb != *first) gver[lg] = GV_UNCHECKED;
   else list[atomicAdd(count, 1u)] = lg;
+}
+// first-error mode, before k_batch_verdict: the key of the first failing batch of READY groups
+__global__ __launch_bounds__(64) void k_first_batch(const uint8_t* __restrict__ gst, const uint8_t* __restrict__ bver,
+                                                     uint32_t ng, const uint8_t* __restrict__ guard, uint32_t fb,
+                                                     uint32_t* __restrict__ first, uint32_t g0) {
+  if (guard && *guard == 0) return;
+  const uint32_t lg = blockIdx.x * blockDim.x + threadIdx.x;
+  if (lg >= ng || gst[lg] != G_READY || bver[lg / fb] == 0) return;
+  atomicMin(first, g0 + (lg / fb) * fb);
+}
+__global__ __launch_bounds__(64) void k_first_group(const uint8_t* __restrict__ gver, uint32_t ng,
+                                                     uint32_t* __restrict__ first) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g < ng && gv_failed(gver[g])) atomicMin(first, g);
+}
+__global__ __launch_bounds__(64) void k_first_item(const uint8_t* __restrict__ st, uint32_t n,
+                                                    uint32_t* __restrict__ first) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && st[i] != ST_OK && st[i] != ST_UNCHECKED) atomicMin(first, i);
 }
 
 // sfail[0]: the slot-wide check's outcome; sfail[1] (zeroed before): set when anything will read
@@ -218,7 +239,7 @@ __global__ __launch_bounds__(64) void k_slot_verdict(const uint8_t* __restrict__
   }
   if (lg < ng) {
     const bool fb = gst[lg] != G_READY;
-    gver[lg] = fb ? 1 : 0;
+    gver[lg] = fb ? GV_NOT_READY : GV_PASS;
     if (fb) sfail[1] = 1;
   }
 }
@@ -239,10 +260,20 @@ void launch_slines(const G2JEntry* pts, const uint32_t* list, const uint32_t* co
     hipLaunchKernelGGL(k_slines, dim3((n + 63) / 64), dim3(64), 0, s, pts, list, count, n, lines, stride, bad, guard);
 }
 void launch_batch_verdict(const uint8_t* gst, const uint8_t* bver, uint32_t ng, uint8_t* gver, uint32_t* list,
-                          uint32_t* count, hipStream_t s, const uint8_t* guard, uint32_t fe_batch) {
-  if (ng)
-    hipLaunchKernelGGL(k_batch_verdict, dim3((ng + 63) / 64), dim3(64), 0, s, gst, bver, ng, gver, list, count, guard,
-                       fe_batch ? fe_batch : FE_BATCH);
+                          uint32_t* count, hipStream_t s, const uint8_t* guard, uint32_t fe_batch, uint32_t* first,
+                          uint32_t g0) {
+  if (!ng) return;
+  const uint32_t fb = fe_batch ? fe_batch : FE_BATCH;
+  if (first)
+    hipLaunchKernelGGL(k_first_batch, dim3((ng + 63) / 64), dim3(64), 0, s, gst, bver, ng, guard, fb, first, g0);
+  hipLaunchKernelGGL(k_batch_verdict, dim3((ng + 63) / 64), dim3(64), 0, s, gst, bver, ng, gver, list, count, guard,
+                     fb, (const uint32_t*)first, g0);
+}
+void launch_first_group(const uint8_t* gver, uint32_t n_groups, uint32_t* first_group, hipStream_t s) {
+  if (n_groups) hipLaunchKernelGGL(k_first_group, dim3((n_groups + 63) / 64), dim3(64), 0, s, gver, n_groups, first_group);
+}
+void launch_first_item(const uint8_t* status, uint32_t n, uint32_t* first_item, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_first_item, dim3((n + 63) / 64), dim3(64), 0, s, status, n, first_item);
 }
 void launch_slot_verdict(const uint8_t* gst, uint8_t* sfail, uint32_t ng, uint8_t* gver, hipStream_t s) {
   if (ng) hipLaunchKernelGGL(k_slot_verdict, dim3((ng + 63) / 64), dim3(64), 0, s, gst, sfail, ng, gver);

@@ -224,6 +224,25 @@ class HIPBLS:
         check(self._L.hbls_verify_batch(_buf(pk_blob), _buf(sig_blob), mb, mo, ml, n, st))
         return list(st.raw[:n])
 
+    def verify_batch_first_error(self, pks: Sequence[bytes], msgs: Sequence[bytes],
+                                 sigs: Sequence[bytes]) -> Tuple[int, int]:
+        """Batch tbls.Verify of an ordered set up to its first failure (hbls_verify_batch_first_error):
+        (index of the first failing item, its status), or (-1, OK) when every item verifies -- the
+        loops of parsigex.go:93-98 / sigagg.go:56-63 that return the first error."""
+        n = len(pks)
+        if not (n == len(msgs) == len(sigs)):
+            raise TblsError("verify_batch_first_error: length mismatch")
+        if n == 0:
+            return -1, OK
+        pk_blob = b"".join(_need(p, PUBKEY_LEN, "public key") for p in pks)
+        sig_blob = b"".join(_need(s, SIG_LEN, "signature") for s in sigs)
+        mb, mo, ml = _pack_msgs([bytes(m) for m in msgs])
+        first = ctypes.c_int64(-1)
+        fst = ctypes.c_uint8(0)
+        check(self._L.hbls_verify_batch_first_error(_buf(pk_blob), _buf(sig_blob), mb, mo, ml, n, ctypes.byref(first),
+                                                    ctypes.byref(fst), None))
+        return int(first.value), int(fst.value) if first.value >= 0 else OK
+
     def threshold_aggregate(self, partial_signatures_by_index: Mapping[int, bytes]) -> bytes:
         """herumi.go:249-286."""
         outs, sts = self.threshold_aggregate_batch([partial_signatures_by_index])

@@ -31,7 +31,8 @@ enum hbls_status {
                               "signature verification failed" (VerifyAggregate, herumi.go:338) */
   HBLS_COMBINE_FAILED = 4, /* "cannot combine signatures"                           herumi.go:282 */
   HBLS_BAD_SECRET = 5,     /* "cannot unmarshal secret into Herumi secret key"      herumi.go:310 */
-  HBLS_BAD_INPUT = 6       /* malformed batch description (offsets/lengths)  -- new, batch-only */
+  HBLS_BAD_INPUT = 6,      /* malformed batch description (offsets/lengths)  -- new, batch-only */
+  HBLS_UNCHECKED = 7       /* first-error calls only: after the first failing item, not resolved */
 };
 
 /* Return codes of the entry points themselves: 0 on success, <0 on a HIP/runtime error or a
@@ -70,6 +71,20 @@ const char* hbls_build_id(void);
  * (default 200; 0 disables). */
 int hbls_verify_batch(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msgs,
                       const uint64_t* msg_off, const uint32_t* msg_len, size_t n, uint8_t* status);
+
+/* Verify an ORDERED set up to its first failure (new; the callers' loops that stop at the first
+ * failing item: core/parsigex/parsigex.go:93-98 drops a peer's set, core/sigagg/sigagg.go:56-63
+ * and core/validatorapi/validatorapi.go:302-306 return the first error).  Same inputs as
+ * hbls_verify_batch.  *first = the smallest i whose tbls.Verify fails (-1: every item verifies)
+ * and *first_status (nullable) its status, exactly as hbls_verify_batch would report it.
+ * status (nullable, n bytes): every item before *first is OK; after it an item is either its
+ * exact status or HBLS_UNCHECKED.  Runs of consecutive items over one message are checked
+ * together and, behind a failing check, only the first failing batch of runs and the first failing
+ * run are resolved -- under attack the cost stays near a clean call's instead of one pairing per
+ * item of every failing run.  One device; not coalesced. */
+int hbls_verify_batch_first_error(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msgs,
+                                  const uint64_t* msg_off, const uint32_t* msg_len, size_t n, int64_t* first,
+                                  uint8_t* first_status, uint8_t* status);
 
 /* ThresholdAggregate over groups: group g holds partials grp_off[g] .. grp_off[g+1]-1 with
  * 96-byte signatures sigs[j] and share indices idx[j].  out[g] = sum_j lambda_j(0) sig_j,
@@ -169,6 +184,12 @@ int hbls_recover_secret(const uint8_t* shares, const int64_t* idx, size_t k, uin
  * --------------------------------------------------------------------------------------- */
 int hbls_hash_to_g2_device(const uint8_t* msgs, const uint64_t* msg_off, const uint32_t* msg_len,
                            size_t n_msgs, void* hm, void* stream);
+/* hbls_verify_batch_first_error on device buffers: the items in set order with vgrp_off's groups
+ * (consecutive items over one message); status as there; *first (a device uint32) = the first
+ * failing item, 0xffffffff when every item verifies. */
+int hbls_verify_device_first_error(const uint8_t* pks, const uint8_t* sigs, const uint32_t* msg_idx, const void* hm,
+                                   size_t n, const uint32_t* vgrp_off, size_t n_vgroups, uint8_t* status,
+                                   uint32_t* first, void* stream);
 int hbls_verify_device(const uint8_t* pks, const uint8_t* sigs, const uint32_t* msg_idx, const void* hm,
                        size_t n, const uint32_t* vgrp_off, size_t n_vgroups, uint8_t* status, void* stream);
 int hbls_threshold_aggregate_device(const uint8_t* sigs, const int64_t* idx, const uint32_t* grp_off,
