@@ -479,7 +479,7 @@ def first_error_verify(L, d, d_pk, d_sig, d_midx, d_vgoff, dev, sp, reps: int = 
     stv = st.cpu().numpy()
     return {"items": NP, "ms": round(res[True] * 1e3, 3), "items_per_s": round(NP / res[True], 1),
             "exact_ms": round(res[False] * 1e3, 3), "exact_items_per_s": round(NP / res[False], 1),
-            "first_index": f, "first_index_exact": f == want and (f == 0xFFFFFFFF or stv[f] == d["exp_v"][f]),
+            "first_index": f, "first_index_exact": bool(f == want and (f == 0xFFFFFFFF or stv[f] == d["exp_v"][f])),
             "unchecked_items": int((stv == 7).sum()),
             "note": "hash + verify of the shard's partials as one ordered set, first-error mode against "
                     "exact per-item statuses (no aggregation)"}
