@@ -2549,7 +2549,7 @@ int hbls_duty_signing_roots(int kind, const uint8_t* data, const uint64_t* off, 
                             uint8_t* status) {
   if (ensure_init()) return -1;
   if (n == 0) return 0;
-  if (kind < 1 || kind > 5) return set_err("duty signing roots: unknown kind");
+  if (kind < 1 || kind > 9) return set_err("duty signing roots: unknown kind");
   if (n_domains == 0) return set_err("signing roots: no domain");
   if (dom_idx)
     for (size_t i = 0; i < n; i++)

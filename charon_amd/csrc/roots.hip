@@ -119,6 +119,13 @@ __global__ __launch_bounds__(64) void k_signing_roots(const uint8_t* __restrict_
 //          SyncCommitteeSelection, :1135 / :915): 16 bytes
 //   kind 4 a uint64 slot (BeaconCommitteeSelection, :852, eth2util.SlotHashRoot): 8 bytes
 //   kind 5 the beacon block root (SignedSyncMessage, :1056): 32 bytes, the object root itself
+//   kind 6 v1.ValidatorRegistration{fee_recipient, gas_limit, timestamp, pubkey}
+//          (VersionedSignedValidatorRegistration, :661): 84 bytes
+//   kind 7 phase0.VoluntaryExit{epoch, validator_index} (SignedVoluntaryExit, :580): 16 bytes
+//   kind 8 the uint64 epoch of eth2util.SignedEpoch (SignedRandao, :791): 8 bytes
+//   kind 9 phase0.BeaconBlockHeader{slot, proposer_index, parent_root, state_root, body_root}
+//          (VersionedSignedProposal, :301): 112 bytes -- a block's hash-tree-root is its header's,
+//          so the caller passes the block body's root (every version's block shares this shape)
 __device__ __forceinline__ uint32_t rd_u32le(const uint8_t* p) {
   return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
 }
@@ -201,6 +208,21 @@ __global__ __launch_bounds__(64) void k_duty_roots(int kind, const uint8_t* __re
     ok = true;
   } else if (kind == 5 && L == 32) {
     root = chunk_load(p);
+    ok = true;
+  } else if (kind == 6 && L == 84) {
+    // Bytes20 fee recipient (one chunk, zero padded), two uint64, the 48-byte key as two chunks
+    const Chunk pk = h2(chunk_load(p + 36), chunk_bytes(p + 68, 16, 0, ~0u, 0));
+    root = h2(h2(chunk_bytes(p, 20, 0, ~0u, 0), chunk_u64(p + 20)), h2(chunk_u64(p + 28), pk));
+    ok = true;
+  } else if (kind == 7 && L == 16) {
+    root = h2(chunk_u64(p), chunk_u64(p + 8));
+    ok = true;
+  } else if (kind == 8 && L == 8) {
+    root = chunk_u64(p);
+    ok = true;
+  } else if (kind == 9 && L == 112) {
+    root = h2(h2(h2(chunk_u64(p), chunk_u64(p + 8)), h2(chunk_load(p + 16), chunk_load(p + 48))),
+              h2(h2(chunk_load(p + 80), z), h2(z, z)));
     ok = true;
   }
   const uint32_t d = dom_idx ? dom_idx[i] : 0u;

@@ -77,6 +77,10 @@ CONTRIBUTION_AND_PROOF = 2     # SignedSyncContributionAndProof: altair.Contribu
 SYNC_SELECTION = 3             # SyncContributionAndProof / SyncCommitteeSelection: slot || subcommittee_index
 SLOT = 4                       # BeaconCommitteeSelection: the uint64 slot (8 B little-endian)
 SYNC_MESSAGE = 5               # SignedSyncMessage: the beacon block root (32 B)
+VALIDATOR_REGISTRATION = 6     # VersionedSignedValidatorRegistration: v1.ValidatorRegistration SSZ (84 B)
+VOLUNTARY_EXIT = 7             # SignedVoluntaryExit: phase0.VoluntaryExit SSZ (16 B)
+RANDAO = 8                     # SignedRandao: the uint64 epoch (8 B little-endian)
+BLOCK_HEADER = 9               # VersionedSignedProposal: phase0.BeaconBlockHeader SSZ (112 B, body root given)
 
 
 def duty_signing_roots(kind: int, objects: Sequence[bytes], domains: Sequence[bytes],

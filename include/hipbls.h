@@ -126,6 +126,13 @@ int hbls_signing_roots(const uint8_t* object_roots, size_t n, const uint8_t* dom
  *           (SyncContributionAndProof / SyncCommitteeSelection.MessageRoot, :1135 / :915)
  *   kind 4  uint64 slot, 8 B little-endian (BeaconCommitteeSelection, eth2util.SlotHashRoot, :852)
  *   kind 5  beacon block root, 32 B (SignedSyncMessage.MessageRoot, :1056)
+ *   kind 6  v1.ValidatorRegistration{fee_recipient, gas_limit, timestamp, pubkey}, 84 B
+ *           (VersionedSignedValidatorRegistration.MessageRoot, :661; one per validator per epoch)
+ *   kind 7  phase0.VoluntaryExit{epoch, validator_index}, 16 B (SignedVoluntaryExit.MessageRoot, :580)
+ *   kind 8  uint64 epoch, 8 B little-endian (SignedRandao.MessageRoot = eth2util.SignedEpoch, :791)
+ *   kind 9  phase0.BeaconBlockHeader{slot, proposer_index, parent_root, state_root, body_root}, 112 B
+ *           (VersionedSignedProposal.MessageRoot, :301: a block's root is its header's; the
+ *           caller supplies the body root, which the beacon node's block already carries)
  * roots: n x 32 bytes; status: 0, or HBLS_BAD_INPUT for a malformed object (its root all zero). */
 int hbls_duty_signing_roots(int kind, const uint8_t* data, const uint64_t* off, const uint32_t* len, size_t n,
                             const uint8_t* domains, size_t n_domains, const uint32_t* dom_idx, uint8_t* roots,

@@ -173,3 +173,29 @@ def sync_selection_root(slot: int, subcommittee_index: int) -> bytes:
 def slot_root(slot: int) -> bytes:
     """eth2util.SlotHashRoot (eth2util/hash.go:13-30): one uint64 merkleized alone = its chunk."""
     return htr_uint64(slot)
+
+
+def voluntary_exit_root(b: bytes) -> bytes:
+    """phase0.VoluntaryExit{epoch, validator_index}: 16 bytes (core/signeddata.go:580)."""
+    assert len(b) == 16
+    return merkleize([htr_uint64(int.from_bytes(b[0:8], "little")), htr_uint64(int.from_bytes(b[8:16], "little"))])
+
+
+def epoch_root(epoch: int) -> bytes:
+    """eth2util.SignedEpoch.HashTreeRoot (eth2util/types.go:245-258): the epoch's uint64 chunk."""
+    return htr_uint64(epoch)
+
+
+def validator_registration_ssz_root(b: bytes) -> bytes:
+    """v1.ValidatorRegistration from its 84-byte SSZ: fee_recipient(20) gas_limit timestamp pubkey(48)."""
+    assert len(b) == 84
+    return validator_registration_root(b[0:20], int.from_bytes(b[20:28], "little"), int.from_bytes(b[28:36], "little"),
+                                       b[36:84])
+
+
+def block_header_root(b: bytes) -> bytes:
+    """phase0.BeaconBlockHeader{slot, proposer_index, parent_root, state_root, body_root}: 112
+    bytes; a BeaconBlock's hash-tree-root equals its header's (body replaced by its root)."""
+    assert len(b) == 112
+    return merkleize([htr_uint64(int.from_bytes(b[0:8], "little")), htr_uint64(int.from_bytes(b[8:16], "little")),
+                      b[16:48], b[48:80], b[80:112]])

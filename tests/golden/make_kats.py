@@ -10,8 +10,9 @@ Sources:
   * eth2util/deposit/deposit_test.go:215-259 + testdata/TestMarshalDepositData.golden
   * cluster/examples/cluster-lock-00{0..3}.json  (cluster/cluster_test.go:242-260 TestExamples)
   * core/testdata/TestSSZSerialisation_{SignedAggregateAndProof, SignedSyncContributionAndProof,
-    SyncContributionAndProof, SignedSyncMessage}.ssz.golden and the JSON goldens of
-    BeaconCommitteeSelection / SyncCommitteeSelection: the other duty types' objects, each checked
+    SyncContributionAndProof, SignedSyncMessage, SignedVoluntaryExit}.ssz.golden and the JSON goldens
+    of BeaconCommitteeSelection / SyncCommitteeSelection / SignedRandao, plus the teku registration
+    message: the other duty types' objects, each checked
     against its JSON twin; their object roots re-derived with oracle/ssz.py (duty_roots_kats)
   * core/testdata/TestSSZSerialisation_AttestationData.ssz.golden + the .json.golden of the same
     value (core/ssz_test.go): the SSZ bytes of one phase0.AttestationData, cross-checked field by
@@ -181,7 +182,35 @@ def duty_roots_kats():
     js = json.load(open(_td("TestJSONSerialisation_SignedSyncMessage.json.golden")))
     assert int.from_bytes(raw[0:8], "little") == int(js["slot"]) and raw[8:40] == _b(js["beacon_block_root"])
     out.append({"kind": 5, "name": "SignedSyncMessage", "ssz": raw[8:40].hex(), "object_root": raw[8:40].hex()})
+    # VersionedSignedValidatorRegistration: the teku registration of eth2util/signing/signing_test.go
+    # (its signature over this object's signing root is the registration KAT)
+    reg = registration_kat_message()
+    out.append({"kind": 6, "name": "VersionedSignedValidatorRegistration", "ssz": reg.hex(),
+                "object_root": ssz.validator_registration_ssz_root(reg).hex()})
+    # SignedVoluntaryExit: {message = VoluntaryExit{epoch, validator_index}, signature}
+    raw = open(_td("TestSSZSerialisation_SignedVoluntaryExit.ssz.golden"), "rb").read()
+    js = json.load(open(_td("TestJSONSerialisation_SignedVoluntaryExit.json.golden")))
+    assert len(raw) == 112 and raw[16:] == _b(js["signature"])
+    assert int.from_bytes(raw[0:8], "little") == int(js["message"]["epoch"])
+    assert int.from_bytes(raw[8:16], "little") == int(js["message"]["validator_index"])
+    out.append({"kind": 7, "name": "SignedVoluntaryExit", "ssz": raw[:16].hex(),
+                "object_root": ssz.voluntary_exit_root(raw[:16]).hex()})
+    # SignedRandao (JSON only): eth2util.SignedEpoch{epoch, signature}, root = the epoch's chunk
+    js = json.load(open(_td("TestJSONSerialisation_SignedRandao.json.golden")))
+    ep = int(js["epoch"])
+    out.append({"kind": 8, "name": "SignedRandao", "ssz": ep.to_bytes(8, "little").hex(),
+                "object_root": ssz.epoch_root(ep).hex()})
     return out
+
+
+def registration_kat_message() -> bytes:
+    """The teku registration message of signing_test.go as its 84-byte SSZ encoding."""
+    src = open(os.path.join(REF, "eth2util/signing/signing_test.go")).read()
+    fee = bytes.fromhex(re.search(r'"fee_recipient": "0x([0-9a-fA-F]{40})"', src).group(1))
+    gas = int(re.search(r'"gas_limit": "(\d+)"', src).group(1))
+    ts = int(re.search(r'"timestamp": "(\d+)"', src).group(1))
+    pk = bytes.fromhex(re.search(r'"pubkey": "0x([0-9a-f]{96})"', src).group(1))
+    return fee + gas.to_bytes(8, "little") + ts.to_bytes(8, "little") + pk
 
 
 def main():

@@ -101,7 +101,8 @@ def test_header_enum_matches_python():
     enum = _header_enum()
     assert enum == {"HBLS_OK": _lib.OK, "HBLS_BAD_PUBKEY": _lib.BAD_PUBKEY, "HBLS_BAD_SIGNATURE": _lib.BAD_SIGNATURE,
                     "HBLS_NOT_VERIFIED": _lib.NOT_VERIFIED, "HBLS_COMBINE_FAILED": _lib.COMBINE_FAILED,
-                    "HBLS_BAD_SECRET": _lib.BAD_SECRET, "HBLS_BAD_INPUT": _lib.BAD_INPUT}
+                    "HBLS_BAD_SECRET": _lib.BAD_SECRET, "HBLS_BAD_INPUT": _lib.BAD_INPUT,
+                    "HBLS_UNCHECKED": _lib.UNCHECKED}
 
 
 def test_go_status_strings_equal_python_table():

@@ -84,7 +84,9 @@ def test_signing_roots_bad_input():
 # ---- the other duty types (core/signeddata.go MessageRoot; hbls_duty_signing_roots)
 _ORACLE_ROOT = {1: ssz.aggregate_and_proof_root, 2: ssz.contribution_and_proof_root,
                 3: lambda b: ssz.sync_selection_root(int.from_bytes(b[:8], "little"), int.from_bytes(b[8:], "little")),
-                4: lambda b: ssz.slot_root(int.from_bytes(b, "little")), 5: lambda b: b}
+                4: lambda b: ssz.slot_root(int.from_bytes(b, "little")), 5: lambda b: b,
+                6: ssz.validator_registration_ssz_root, 7: ssz.voluntary_exit_root,
+                8: lambda b: ssz.epoch_root(int.from_bytes(b, "little")), 9: ssz.block_header_root}
 
 
 def test_duty_fixtures_oracle(kats):
@@ -92,9 +94,22 @@ def test_duty_fixtures_oracle(kats):
     SSZ golden cross-checked against its JSON twin there) recompute; bitlist edge cases"""
     assert {k["name"] for k in kats["duty_roots"]} >= {"SignedAggregateAndProof", "SignedSyncContributionAndProof",
                                                        "SyncContributionAndProof", "BeaconCommitteeSelection",
-                                                       "SignedSyncMessage"}
+                                                       "SignedSyncMessage", "VersionedSignedValidatorRegistration",
+                                                       "SignedVoluntaryExit", "SignedRandao"}
     for k in kats["duty_roots"]:
         assert _ORACLE_ROOT[k["kind"]](bytes.fromhex(k["ssz"])).hex() == k["object_root"], k["name"]
+    # the registration object's signing root under the builder domain is the pinned registration
+    # KAT message (its teku signature verifies over it, tests/test_oracle_kat.py)
+    reg = next(k for k in kats["duty_roots"] if k["kind"] == 6)
+    assert ssz.signing_root(bytes.fromhex(reg["object_root"]),
+                            bytes.fromhex(kats["registration"]["domain"])).hex() == kats["registration"]["msg"]
+    # a block header's root: the 5-field container (8 leaves, 3 zero)
+    hdr = bytes(range(112))
+    h = lambda x, y: hashlib.sha256(x + y).digest()  # noqa: E731
+    z = bytes(32)
+    leaves = [hdr[0:8] + bytes(24), hdr[8:16] + bytes(24), hdr[16:48], hdr[48:80], hdr[80:112]]
+    assert ssz.block_header_root(hdr) == h(h(h(leaves[0], leaves[1]), h(leaves[2], leaves[3])),
+                                           h(h(leaves[4], z), h(z, z)))
     # Bitlist[2048]: empty (delimiter only), one bit, a full chunk, the maximum
     h = lambda x, y: hashlib.sha256(x + y).digest()  # noqa: E731
     z = bytes(32)
@@ -129,7 +144,11 @@ def test_duty_roots_gpu(kats, hipbls):
             2: gold[2] + [rng.randbytes(264) for _ in range(20)],
             3: gold[3] + [rng.randbytes(16) for _ in range(20)],
             4: gold[4] + [rng.randbytes(8) for _ in range(20)],
-            5: gold[5] + [rng.randbytes(32) for _ in range(20)]}
+            5: gold[5] + [rng.randbytes(32) for _ in range(20)],
+            6: gold[6] + [rng.randbytes(84) for _ in range(20)],
+            7: gold[7] + [rng.randbytes(16) for _ in range(20)],
+            8: gold[8] + [rng.randbytes(8) for _ in range(20)],
+            9: [rng.randbytes(112) for _ in range(20)]}
     for kind, obs in objs.items():
         idx = [rng.randrange(3) for _ in obs]
         roots, st = sr.duty_signing_roots(kind, obs, domains, idx)
@@ -147,3 +166,20 @@ def test_duty_roots_gpu(kats, hipbls):
     assert st == [0, 6, 6, 6, 6] and all(r == bytes(32) for r in roots[1:])
     roots, st = sr.duty_signing_roots(2, [rng.randbytes(263)], domains)
     assert st == [6] and roots == [bytes(32)]
+    for kind, size in ((6, 84), (7, 16), (8, 8), (9, 112)):
+        roots, st = sr.duty_signing_roots(kind, [rng.randbytes(size - 1), rng.randbytes(size + 1)], domains)
+        assert st == [6, 6] and roots == [bytes(32)] * 2, kind
+
+
+@pytest.mark.gpu
+def test_registration_root_on_device_verifies_teku_signature(kats, hipbls):
+    """The teku registration (eth2util/signing/signing_test.go) through the device: its SSZ object
+    rooted under the builder domain by hbls_duty_signing_roots kind 6 is the message the teku
+    signature verifies over -- the reference's own vector pins the device's registration root."""
+    from charon_amd import signing_roots as sr
+    r = kats["registration"]
+    obj = bytes.fromhex(next(k for k in kats["duty_roots"] if k["kind"] == 6)["ssz"])
+    roots, st = sr.duty_signing_roots(sr.VALIDATOR_REGISTRATION, [obj], [bytes.fromhex(r["domain"])])
+    assert st == [0] and roots[0].hex() == r["msg"]
+    pk = hipbls.secret_to_public_key(bytes.fromhex(r["sk"]))
+    assert hipbls.verify_batch([pk], roots, [bytes.fromhex(r["sig"])]) == [0]
