@@ -923,7 +923,7 @@ def main(argv=None):
         ta_w = opcounts.ta_joint(ta_ids, jc) if jc else opcounts.ta_uniform(ta_ids)
         # the small-scalar aggregation (threshold.hip k_ta_small, one lane per validator) takes every
         # group whose index set it can split; the per-member ladders then have nothing to do
-        ta_small_w = opcounts.ta_small(ta_ids) if os.environ.get("HBLS_TA_SMALL", "1") != "0" else None
+        ta_small_w = opcounts.ta_small(ta_ids)
         prep_units = opcounts.per_unit(group_size=n + (0 if staged else 1), t=t)
         units = {"k_rlc": (n_rlc, (rlc_avg, rlc_avg)),
                  "k_dec_pk": (NP + (0 if staged else V), per_unit["k_dec_pk"]),
@@ -936,7 +936,7 @@ def main(argv=None):
         if smsm:
             # multi-Miller loops of MML_PAIRS groups, product tree of fan-in FE_BATCH to <= FE_BATCH
             n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
-            mmlk = int(os.environ.get("HBLS_MML_PAIRS", "0")) or opcounts.mml_pairs(V, n_cu)
+            mmlk = opcounts.mml_pairs(V, n_cu)
             n_prod = opcounts.prod_tree_inputs(-(-V // mmlk))
             fin = opcounts.pair3_fin(batch=2, lines=False)
             units.update({"k_group_prep": (V, prep_units["k_group_prep_p"]),

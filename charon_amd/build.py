@@ -32,7 +32,7 @@ def build_id(defines=()) -> str:
 
 
 def build_library(force: bool = False, verbose: bool = True, defines=(), out: str = LIB) -> str:
-    """defines / out: tuning variants (e.g. ("HB_OCC2=2",) -> charon_amd/lib/variants/...), used by
+    """defines / out: experiment variants (-D defines -> charon_amd/lib/variants/...), used by
     tools/ experiments through HBLS_LIBRARY; the product is the default build.  A library whose
     embedded build id equals the tree's is reused; any other is rebuilt."""
     from charon_amd._lib import embedded_build_id

@@ -256,9 +256,7 @@ size_t env_size(const char* name, size_t dflt) {
 // Verification groups are chunked for the line buffers: GCAP groups per pairing launch, FB_CAP
 // fallback items per pass (HBLS_GROUP_CHUNK / HBLS_FALLBACK_CHUNK).  Host-buffer calls build
 // groups of at most GMAX items over one message (HBLS_GROUP_MAX).
-size_t g_gcap = 131072, g_fbcap = 65536, g_gmax = 16;
-// HBLS_RLC_MSM=0: one ladder per item (k_rlc) instead of shared-doubling chunks (k_rlc_msm)
-bool g_rlc_msm = true;
+std::atomic<size_t> g_gcap{131072}, g_fbcap{65536}, g_gmax{16};
 std::atomic<size_t> g_rlc_lanes{65536};   // HBLS_RLC_LANES: lanes the chunk size aims to keep busy
 // public-key cache: compressed key -> entry index (the same on every device).  Lock order: an
 // adder (or clear) takes g_kc_add_mu, then one Dev::mu at a time to fill that device's table, then
@@ -276,17 +274,10 @@ std::vector<uint8_t> g_kc_keys;  // their compressed bytes, 48 B each (g_kc_add_
 // the same size t; 0 = auto (about TA_JOINT_LANES lanes, at most t and 8), 1 = one ladder per member
 // (k_ta_straus)
 std::atomic<size_t> g_ta_joint{0};
-// HBLS_TA_SMALL=0: no small-scalar aggregation (threshold.hip k_ta_small; ta_small.h)
-bool g_ta_small = true;
 constexpr size_t TA_JOINT_LANES = 98304;
 // HBLS_FE_BATCH: verifications of at least this many groups check FE_BATCH groups per final
 // exponentiation (vgroup.hip; 0 = one final exponentiation per group)
 std::atomic<size_t> g_fe_batch_min{2 * FE_BATCH};
-// HBLS_FALLBACK_BATCH: groups per final exponentiation of the per-batch check behind a FAILED
-// slot-wide check (a power of two <= FE_BATCH).  A failed slot has at least one bad item and often
-// many (an attack): smaller batches pass more often (group testing; C5, 1 % corrupted partials:
-// 64-group batches nearly all fail and every group then pays its own exponentiation).
-size_t g_fb_batch = 8;
 // HBLS_SLOT_MSM: batched verifications of at least this many items (partials + folded aggregates,
 // one chunk of groups) check every group at once -- the signature side as one multi-scalar
 // multiplication (msm.hip), one final exponentiation for the call -- and fall back to the
@@ -305,10 +296,6 @@ std::atomic<bool> g_adaptive{true};
 // (SINGLE_MAX_DEFAULT: the batched final exponentiation's threshold, g_fe_batch_min)
 constexpr size_t SINGLE_MAX_DEFAULT = ~size_t(0);
 std::atomic<size_t> g_single_max{SINGLE_MAX_DEFAULT};
-// HBLS_FE6=0: the final exponentiations without lines in three lanes (k_pair3<FIN>) instead of six
-// (k_pair6_fin, pair6.h)
-bool g_fe6 = true;
-size_t g_mml_pairs = 0;  // HBLS_MML_PAIRS: groups per multi-Miller loop of the slot-wide check (0: sized to the chip)
 
 struct DevBuf {
   void* p = nullptr;
@@ -598,14 +585,11 @@ int init_mask(uint32_t mask) {
   if ((mask & visible) != mask || mask == 0)
     return set_err("device mask " + std::to_string(mask) + " names devices that are not visible (" +
                    std::to_string(n) + " devices)");
-  g_gcap = env_size("HBLS_GROUP_CHUNK", g_gcap);
-  g_fbcap = env_size("HBLS_FALLBACK_CHUNK", g_fbcap);
-  g_gmax = std::max<size_t>(1, env_size("HBLS_GROUP_MAX", g_gmax));
-  g_rlc_msm = env_size("HBLS_RLC_MSM", 1) != 0;
+  g_gcap = std::max<size_t>(1, env_size("HBLS_GROUP_CHUNK", g_gcap.load()));
+  g_fbcap = std::max<size_t>(1, env_size("HBLS_FALLBACK_CHUNK", g_fbcap.load()));
+  g_gmax = std::max<size_t>(1, env_size("HBLS_GROUP_MAX", g_gmax.load()));
   g_rlc_lanes = std::max<size_t>(1, env_size("HBLS_RLC_LANES", g_rlc_lanes.load()));
   g_ta_joint = std::min<size_t>(8, env_size("HBLS_TA_JOINT", g_ta_joint.load()));
-  g_ta_small = env_size("HBLS_TA_SMALL", 1) != 0;
-  g_fe6 = env_size("HBLS_FE6", 1) != 0;
   g_fe_batch_min = env_size("HBLS_FE_BATCH", g_fe_batch_min.load());
   g_slot_msm_min = env_size("HBLS_SLOT_MSM", g_slot_msm_min.load());
   g_adaptive = env_size("HBLS_ADAPTIVE", 1) != 0;
@@ -617,12 +601,6 @@ int init_mask(uint32_t mask) {
   g_hash_split = env_size("HBLS_HASH_SPLIT", 1) != 0;
   g_fe18_max = env_size("HBLS_FE18_MAX", g_fe18_max.load());
   g_ws_sets = (int)std::min<size_t>(N_WS_MAX, std::max<size_t>(1, env_size("HBLS_WS_SETS", 3)));
-  {
-    size_t fb = std::min<size_t>(FE_BATCH, std::max<size_t>(2, env_size("HBLS_FALLBACK_BATCH", g_fb_batch)));
-    while (fb & (fb - 1)) fb &= fb - 1;  // a power of two
-    g_fb_batch = fb;
-  }
-  g_mml_pairs = std::min<size_t>(64, env_size("HBLS_MML_PAIRS", g_mml_pairs));
   {
     size_t sc = env_size("HBLS_SIG_CACHE", g_sc_cap.load());
     while (sc & (sc - 1)) sc &= sc - 1;  // a power of two
@@ -826,7 +804,7 @@ int ta_tail(Dev& d, Ws& w, const HmEntry* pts, const uint32_t* src, const uint8_
     // small-scalar path first (groups of exactly t members, wave-uniform index sets); the Lagrange
     // digits and the per-member ladders below skip the groups it aggregated
     uint8_t* sdone = nullptr;
-    if (mode == 0 && g_ta_small && t_u >= 2 && t_u <= (size_t)TA_SMALL_MAX) {
+    if (mode == 0 && t_u >= 2 && t_u <= (size_t)TA_SMALL_MAX) {
       int64_t* csm;
       TaDigits* sdig;
       uint8_t *sok, *stab;
@@ -884,9 +862,9 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
   G2JEntry* sr;
   G1AEntry* gP;
   LineEntry *glines, *fbl;
-  const size_t gcap = std::min(g_gcap, std::max<size_t>(n_groups, 1));
+  const size_t gcap = std::min(std::max<size_t>(1, g_gcap.load()), std::max<size_t>(n_groups, 1));
   const size_t n_agg = (fold && fold->dv_pks) ? fold->n_groups : 0;
-  const size_t fbcap = std::min(g_fbcap, std::max<size_t>(n + n_agg, 1));
+  const size_t fbcap = std::min(std::max<size_t>(1, g_fbcap.load()), std::max<size_t>(n + n_agg, 1));
   if (wsbuf(w, W_VPK, n, &vpk) || wsbuf(w, W_VPKST, n, &vpkst) || wsbuf(w, W_VSIG, n, &vsig) ||
       wsbuf(w, W_VSIGST, n, &vsigst) || wsbuf(w, W_IGRP, n, &igrp) || wsbuf(w, W_PR, n, &pr) ||
       wsbuf(w, W_SR, n, &sr) || wsbuf(w, W_GP, gcap, &gP) || wsbuf(w, W_GST, gcap, &gst) ||
@@ -908,8 +886,8 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
   // group keep r = 1 only when nothing else joins their group's check; with a folded aggregate
   // (which keeps r = 1 without the batched final exponentiation) every item takes a random one --
   // otherwise an error +D on a group's single partial and -D on its aggregate would cancel.
-  // Batched final exponentiation: a batch of groups (FE_BATCH; g_fb_batch behind a failed slot-wide
-  // check) shares one final exponentiation and one Miller
+  // Batched final exponentiation: a batch of groups (FE_BATCH; behind a failed slot-wide check the
+  // multi-Miller loops' chunks of mmlk groups) shares one final exponentiation and one Miller
   // loop of the signature side, checking prod_g e(P_g, H(m_g)) * e(-g1, sum_g S_g) == 1.  Every
   // item (singletons and folded aggregates included) then takes a random coefficient: with two
   // fixed coefficients in one combination, errors of two items could cancel.
@@ -932,11 +910,9 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
   }
   // pairs per multi-Miller loop of the slot-wide check: enough that the loops fill at most one
   // round of waves (21 groups per wave, one wave per SIMD) -- a second, partial round would double
-  // the kernel's span (HBLS_MML_PAIRS fixes it)
-  const size_t mmlk = g_mml_pairs ? g_mml_pairs
-                                  : std::min<size_t>(16, std::max<size_t>(1, (std::min(gcap, n_groups) +
-                                                                              GROUPS_PER_WAVE * 4 * d.n_cu - 1) /
-                                                                             (GROUPS_PER_WAVE * 4 * d.n_cu)));
+  // the kernel's span
+  const size_t mmlk = std::min<size_t>(16, std::max<size_t>(1, (std::min(gcap, n_groups) + GROUPS_PER_WAVE * 4 * d.n_cu - 1) /
+                                                              (GROUPS_PER_WAVE * 4 * d.n_cu)));
   const size_t nb1 = (gcap + mmlk - 1) / mmlk, nb2 = (nb1 + PROD_FAN - 1) / PROD_FAN;
   // batches of >= 2 groups (FE_BATCH), or behind a failed slot-wide check its multi-Miller loops' chunks
   const size_t nbcap = std::max((gcap + 1) / 2, nb1);
@@ -1046,13 +1022,13 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
   // (sides1 1, the per-lane combination): it runs beside the signatures' subgroup checks, whose
   // statuses group_scan and msm_take apply; otherwise the signatures' statuses first
   const uint32_t rlc_cmax = (uint32_t)std::min<size_t>(RLC_CHUNK, std::max<size_t>(1, n / g_rlc_lanes.load()));
-  const bool keys_only = sides1 == 1 && !(dgoff && g_rlc_msm && rlc_cmax > 1);
+  const bool keys_only = sides1 == 1 && !(dgoff && rlc_cmax > 1);
   if (!keys_only) HCHK(hipStreamWaitEvent(s, w.ev_side[1], 0));
   TIMED(d, "k_item_group", s, launch_item_group(dgoff, (uint32_t)n_groups, (uint32_t)n, igrp, s));
   RlcMsmArgs rlc_fallback{};
   uint32_t rlc_fallback_chunks = 0;
   uint2* coef_pi = nullptr;  // per-item path's coefficients (slot-wide check)
-  if (dgoff && g_rlc_msm && rlc_cmax > 1) {
+  if (dgoff && rlc_cmax > 1) {
     // chunks of a group's items share their ladders' doublings (k_rlc_msm); the chunk size keeps
     // about g_rlc_lanes lanes busy (at most RLC_CHUNK items, one item per lane for small calls)
     const uint32_t cmax = rlc_cmax;
@@ -1163,7 +1139,7 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
     ga.gst = gst;
     ga.glines = glines;
     if (bfe) {
-      const uint32_t fb = smsm ? (uint32_t)g_fb_batch : FE_BATCH;
+      const uint32_t fb = FE_BATCH;
       const uint32_t nb = (ng + fb - 1) / fb;
       ga.fe_batch = fb;
       Pair3Args pm{};
@@ -1247,7 +1223,7 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
         pf.f_n = 2;
         pf.status = sfail;
         if (!skip_msm) {
-          TIMED(d, "k_pair3_fin", s, g_fe6 ? launch_pair6_fin(pf, s) : launch_pair3_fin(pf, s));
+          TIMED(d, "k_pair3_fin", s, launch_pair6_fin(pf, s));
           HCHK(hipMemsetAsync(sfail + 1, 0, 1, s));
           TIMED(d, "k_slot_verdict", s, launch_slot_verdict(gst, sfail, ng, gver + g0, s));
           // deferred lines: read by the per-batch check behind a failed slot-wide check and by
@@ -1368,7 +1344,7 @@ int verify_pipeline(Dev& d, Ws& w, const uint8_t* dpk, const uint8_t* dsig, cons
         pf.f_n = 2 * nb;
         pf.status = bver;
         pf.guard = guard;
-        TIMED(d, "k_pair3_fin", s, g_fe6 ? launch_pair6_fin(pf, s) : launch_pair3_fin(pf, s));
+        TIMED(d, "k_pair3_fin", s, launch_pair6_fin(pf, s));
         // groups of a failing batch: checked one by one (their stored loop, their own S lines)
         HCHK(hipMemsetAsync(gcount, 0, sizeof(uint32_t), s));
         TIMED(d, "k_batch_verdict", s,
@@ -1848,7 +1824,7 @@ int verify_large(Dev& d, const uint8_t* pks, const uint8_t* sigs, const uint8_t*
   std::vector<uint32_t> midx(n);
   for (size_t k = 0; k < n; k++) {
     midx[k] = all.idx[order32[k]];
-    if (k == 0 || midx[k] != midx[k - 1] || k - gstart.back() >= g_gmax) gstart.push_back(k);
+    if (k == 0 || midx[k] != midx[k - 1] || k - gstart.back() >= g_gmax.load()) gstart.push_back(k);
   }
   const size_t n_groups = gstart.size();
   gstart.push_back(n);
@@ -1987,7 +1963,7 @@ int verify_host(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msgs, co
   // group; default the batched final exponentiation's group threshold)
   const size_t sm = g_single_max.load();
   const size_t single_max = sm == SINGLE_MAX_DEFAULT ? g_fe_batch_min.load() : sm;
-  const size_t gmax = n < single_max ? 1 : g_gmax;
+  const size_t gmax = n < single_max ? 1 : std::max<size_t>(1, g_gmax.load());
   std::vector<size_t> gstart;  // group starts in `order`
   for (size_t k = 0; k < n; k++)
     if (k == 0 || all.idx[order[k]] != all.idx[order[k - 1]] || k - gstart.back() >= gmax) gstart.push_back(k);
@@ -2113,7 +2089,8 @@ int verify_first_host(const uint8_t* pks, const uint8_t* sigs, const uint8_t* ms
     dedup_messages(msgs, msg_off, msg_len, n, nullptr, all);
   std::vector<uint32_t> goff;
   for (size_t k = 0; k < n; k++)
-    if (k == 0 || all.idx[k] != all.idx[k - 1] || k - goff.back() >= g_gmax) goff.push_back((uint32_t)k);
+    if (k == 0 || all.idx[k] != all.idx[k - 1] || k - goff.back() >= std::max<size_t>(1, g_gmax.load()))
+      goff.push_back((uint32_t)k);
   const size_t n_groups = goff.size();
   goff.push_back((uint32_t)n);
   Dev& d = *devs()[0];
@@ -2950,7 +2927,10 @@ int hbls_tune(const char* name, size_t value, size_t* previous) {
   static const std::pair<const char*, std::atomic<size_t>*> knobs[] = {
       {"HBLS_HASH_PAIR_MAX", &g_hash_pair_max}, {"HBLS_HASH_ONE_LANE", &g_hash_one_lane},
       {"HBLS_HASH_SPLIT", &g_hash_split},       {"HBLS_FE18_MAX", &g_fe18_max},
-      {"HBLS_TA_PAIR_MAX", &g_ta_pair_max},     {"HBLS_DEC_PAIR_MAX", &g_dec_pair_max}};
+      {"HBLS_TA_PAIR_MAX", &g_ta_pair_max},     {"HBLS_DEC_PAIR_MAX", &g_dec_pair_max},
+      // chunking of large verifications (tests run them at small sizes: several chunks per call)
+      {"HBLS_GROUP_CHUNK", &g_gcap},            {"HBLS_FALLBACK_CHUNK", &g_fbcap},
+      {"HBLS_GROUP_MAX", &g_gmax}};
   for (const auto& k : knobs)
     if (strcmp(k.first, name) == 0) {
       const size_t old = k.second->exchange(value);

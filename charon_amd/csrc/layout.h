@@ -8,34 +8,16 @@
 
 // Occupancy targets (waves per SIMD) of the heavy kernels: 1 lets the compiler use all 512
 // registers of a lane, 2 gives each wave 256, 3 gives 168 (spilling the rest to scratch).  Chosen
-// per kernel by measurement; tuning builds override them with -D.
-#ifndef HB_OCC_HASH
+// per kernel by measurement (DESIGN.md §4 "Occupancy"; the alternatives measured slower).
 #define HB_OCC_HASH 2
-#endif
-#ifndef HB_OCC_LINES
 #define HB_OCC_LINES 1
-#endif
-#ifndef HB_OCC_DECPK
 #define HB_OCC_DECPK 2
-#endif
-#ifndef HB_OCC_DECSIG
 #define HB_OCC_DECSIG 2
-#endif
-#ifndef HB_OCC_SUBG
 #define HB_OCC_SUBG 2  // k_g1_subgroup, k_g2_subgroup
-#endif
-#ifndef HB_OCC_RLC
 #define HB_OCC_RLC 2
-#endif
-#ifndef HB_OCC_PREP
 #define HB_OCC_PREP 2
-#endif
-#ifndef HB_OCC_PAIR3
 #define HB_OCC_PAIR3 1
-#endif
-#ifndef HB_OCC_STRAUS
 #define HB_OCC_STRAUS 2
-#endif
 #define KB_OCC(n) __launch_bounds__(64, n)
 
 namespace hb {
@@ -348,10 +330,7 @@ constexpr uint32_t MSM_C = 16, MSM_WINDOWS = 2, MSM_MASK = (1u << MSM_C) - 1;
 constexpr uint32_t MSM_KEYS = MSM_WINDOWS << MSM_C;  // buckets (window, digit); digit 0 unused
 // buckets per lane of the weighing pass: 4 (32 768 lanes) rather than 16 -- the pass is a latency
 // tail of every slot (one round of waves), so more, shorter lanes halve it for ~20 M more products
-#ifndef HB_MSM_CHUNK
-#define HB_MSM_CHUNK 4
-#endif
-constexpr uint32_t MSM_CHUNK = HB_MSM_CHUNK;
+constexpr uint32_t MSM_CHUNK = 4;
 constexpr uint32_t MSM_PARTS = MSM_KEYS / MSM_CHUNK;
 struct G2MsmArgs {
   const HmEntry* sig;      // items [0, n)

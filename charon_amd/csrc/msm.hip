@@ -24,12 +24,8 @@ constexpr int BLOCK = 64;
 
 // The reduction and the butterflies run 128 and at most 64 waves: far fewer than the SIMDs, so
 // they are latency-bound and take one wave per SIMD's full register file (no scratch spills).
-#ifndef HB_OCC_MSMBUCKET
 #define HB_OCC_MSMBUCKET HB_OCC_RLC
-#endif
-#ifndef HB_OCC_MSMTAIL
 #define HB_OCC_MSMTAIL 1
-#endif
 
 __device__ __forceinline__ bool msm_take(const G2MsmArgs& a, uint32_t i, uint2& ab) {
   ab = a.coef[i];
@@ -98,38 +94,23 @@ __global__ __launch_bounds__(1024) void k_msm_order(const uint32_t* __restrict__
 }
 
 // one lane per bucket (in the order of k_msm_order): the sum of its points (half 1: -psi^2 of the
-// signature); HB_MSM_LAZY=0: the stored-word ec.h addition (A/B runs)
-#ifndef HB_MSM_LAZY
-#define HB_MSM_LAZY 1
-#endif
+// signature), in lazily reduced 28-bit limbs (ec28.h g2l_madd)
 __global__ KB_OCC(HB_OCC_MSMBUCKET) void k_msm_bucket(G2MsmArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
   const uint32_t L = blockIdx.x * blockDim.x + threadIdx.x;
   if (L >= MSM_KEYS) return;
   const uint32_t k = a.order[L];
   const uint32_t b = a.off[k], e = a.off[k + 1];
-#if HB_MSM_LAZY
-  G2L acc = g2l_infinity();  // the sum in lazily reduced 28-bit limbs (ec28.h g2l_madd)
-#else
-  G2J acc = jac_infinity<Fp2>();
-#endif
+  G2L acc = g2l_infinity();
   HB_NOUNROLL for (uint32_t j = b; j < e; j++) {
     const uint32_t u = a.ent[j], i = u >> 1;
     const HmEntry se = i < a.n ? a.sig[i] : a.agg_sig[i - a.n];
     G2A P = {se.x, se.y, false};
     if (u & 1u) P = {f2_mul_fp(P.x, fp_from_const(PSI2_CX[0])), f2_neg(f2_mul_fp(P.y, fp_from_const(PSI2_CY[0]))), false};
-#if HB_MSM_LAZY
     acc = g2l_madd(acc, f2l_from(P.x), f2l_from(P.y));
-#else
-    acc = jac_add_aff(acc, P);
-#endif
   }
-#if HB_MSM_LAZY
   const G2J r = g2l_to_jac(acc);
   a.bucket[k] = {r.X, r.Y, r.Z};
-#else
-  a.bucket[k] = {acc.X, acc.Y, acc.Z};
-#endif
 #endif
 }
 

@@ -503,13 +503,10 @@ __device__ __forceinline__ Jac<F> msm_ladder_sparse(const Jac<F>* __restrict__ t
   return R;
 }
 
-// The pieces of the chunk kernels.  Split (HB_RLC_SPLIT, default): one kernel builds the
-// coefficients and ladder tables, then one kernel per side runs the ladder -- each kernel holds
-// only its own phase's state (the fused kernel spilled 1.6 KB per lane: the SHA schedule, the
-// inversion and both ladders in one register allocation).
-#ifndef HB_RLC_SPLIT
-#define HB_RLC_SPLIT 1
-#endif
+// The pieces of the chunk kernels, split: one kernel builds the coefficients and ladder tables,
+// then one kernel per side runs the ladder -- each kernel holds only its own phase's state (a fused
+// kernel spilled 1.6 KB per lane: the SHA schedule, the inversion and both ladders in one register
+// allocation; time-neutral, profiles/r04s_rlc_split_ab.txt).
 
 // a group of ONE item keeps r = 1 (unless `always`): its records written here; true if so
 template <int SIDES>
@@ -638,17 +635,11 @@ __device__ __forceinline__ void rlc_lad_g2(const RlcMsmArgs& a, uint32_t first, 
   for (uint32_t k = 1; k < cnt; k++) a.sout[first + k] = {zs.X, zs.Y, zs.Z};
 }
 
-// One lane per chunk.  PHASE 0: everything (fused); 1: coefficients and tables of SIDES; 2: the
-// ladder of side SIDES (1 or 2).  SIDES as RlcMsmArgs::sides, a template argument so that the
-// public-key-only launch of the slot-wide check does not allocate registers for the G2 side.
-#ifndef HB_OCC_RLC_LAD1
-#define HB_OCC_RLC_LAD1 HB_OCC_RLC
-#endif
-#ifndef HB_OCC_RLC_LAD2
-#define HB_OCC_RLC_LAD2 HB_OCC_RLC
-#endif
+// One lane per chunk.  PHASE 1: coefficients and tables of SIDES; 2: the ladder of side SIDES (1
+// or 2).  SIDES as RlcMsmArgs::sides, a template argument so that the public-key-only launch of
+// the slot-wide check does not allocate registers for the G2 side.
 template <int SIDES, int PHASE>
-__global__ KB_OCC(PHASE != 2 ? HB_OCC_RLC : SIDES == 1 ? HB_OCC_RLC_LAD1 : HB_OCC_RLC_LAD2) void k_rlc_msm(RlcMsmArgs a) {
+__global__ KB_OCC(HB_OCC_RLC) void k_rlc_msm(RlcMsmArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
   if (a.guard && *a.guard == 0) return;
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
@@ -660,14 +651,8 @@ __global__ KB_OCC(PHASE != 2 ? HB_OCC_RLC : SIDES == 1 ? HB_OCC_RLC_LAD1 : HB_OC
     else rlc_lad_g2(a, first, cnt);
     return;
   }
-  if (SIDES & 1) {
-    rlc_tab_g1(a, first, cnt);
-    if (PHASE == 0) rlc_lad_g1(a, first, cnt);
-  }
-  if (SIDES & 2) {
-    rlc_tab_g2(a, first, cnt);
-    if (PHASE == 0) rlc_lad_g2(a, first, cnt);
-  }
+  if (SIDES & 1) rlc_tab_g1(a, first, cnt);
+  if (SIDES & 2) rlc_tab_g2(a, first, cnt);
 #endif
 }
 
@@ -685,12 +670,6 @@ void launch_scan(const uint32_t* cnt, uint32_t n, uint32_t* off, hipStream_t s) 
 void launch_rlc_msm(const RlcMsmArgs& a, uint32_t max_chunks, hipStream_t s) {
   if (!max_chunks) return;
   const dim3 grid((max_chunks + BLOCK - 1) / BLOCK);
-  if (!HB_RLC_SPLIT) {
-    if (a.sides == 1) hipLaunchKernelGGL((k_rlc_msm<1, 0>), grid, dim3(BLOCK), 0, s, a);
-    else if (a.sides == 2) hipLaunchKernelGGL((k_rlc_msm<2, 0>), grid, dim3(BLOCK), 0, s, a);
-    else hipLaunchKernelGGL((k_rlc_msm<3, 0>), grid, dim3(BLOCK), 0, s, a);
-    return;
-  }
   if (a.sides == 1) hipLaunchKernelGGL((k_rlc_msm<1, 1>), grid, dim3(BLOCK), 0, s, a);
   else if (a.sides == 2) hipLaunchKernelGGL((k_rlc_msm<2, 1>), grid, dim3(BLOCK), 0, s, a);
   else hipLaunchKernelGGL((k_rlc_msm<3, 1>), grid, dim3(BLOCK), 0, s, a);

@@ -309,11 +309,13 @@ size_t hbls_single_max(size_t items);
  * item's ladder split over a lane pair (latency for calls that do not fill the chip; 0 = never, the
  * default, HBLS_DEC_PAIR_MAX).  Returns the previous value.  Verdicts do not depend on it. */
 size_t hbls_dec_pair_max(size_t items);
-/* Tuning by name, for the layouts of the latency-bound small calls (read from the environment at
- * init; verdicts and outputs never depend on them): "HBLS_HASH_PAIR_MAX", "HBLS_HASH_ONE_LANE",
+/* Tuning by name (read from the environment at init; verdicts and outputs never depend on them):
+ * the layouts of the latency-bound small calls "HBLS_HASH_PAIR_MAX", "HBLS_HASH_ONE_LANE",
  * "HBLS_HASH_SPLIT" (0: the unstaged hashing kernels), "HBLS_FE18_MAX", "HBLS_TA_PAIR_MAX",
- * "HBLS_DEC_PAIR_MAX".  *previous (if not NULL) receives the old value.  Returns 0, or -1 for an
- * unknown name. */
+ * "HBLS_DEC_PAIR_MAX"; the chunking of large verifications "HBLS_GROUP_CHUNK" (groups per pairing
+ * chunk), "HBLS_FALLBACK_CHUNK" (items per fallback pass), "HBLS_GROUP_MAX" (items per group of a
+ * host call).  *previous (if not NULL) receives the old value.  Returns 0, or -1 for an unknown
+ * name. */
 int hbls_tune(const char* name, size_t value, size_t* previous);
 /* Tuning: the random linear combination's public-key side groups a verification group's items
  * into shared-doubling chunks sized to keep about `lanes` lanes busy (at most 16 items per chunk;
