@@ -49,6 +49,12 @@ def main():
     tst = np.zeros(V, dtype=np.uint8)
     rc = L.hbls_threshold_aggregate_batch(_p(d["ta_sigs"]), _p(d["ta_idx"]), _p(d["grp_off"]), V, _p(out), _p(tst))
     res["aggregate_ok"] = rc == 0 and not tst.any() and bool(np.array_equal(out, d["root_sigs"]))
+    if not res["aggregate_ok"]:
+        res["aggregate_detail"] = {"rc": int(rc), "bad_status": int((tst != 0).sum()),
+                                   "statuses": sorted(set(int(x) for x in tst)),
+                                   "wrong": int((out.reshape(V, 96) != d["root_sigs"].reshape(V, 96)).any(axis=1).sum()),
+                                   "first_wrong": [int(x) for x in np.nonzero(
+                                       (out.reshape(V, 96) != d["root_sigs"].reshape(V, 96)).any(axis=1))[0][:8]]}
     errs = []
     off0 = np.zeros(1, dtype=np.uint64)
     len32 = np.full(1, 32, dtype=np.uint32)
