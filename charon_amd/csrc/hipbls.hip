@@ -365,6 +365,11 @@ struct Hc {
   // stream of its own beside the kernels the pageable copies took over a second)
   uint8_t* pin = nullptr;
   size_t pin_cap = 0;
+  // a signature-cache put (on the device's cache stream, after the call returned) still reading
+  // this context's staging buffers: the context's next call waits for it before it uploads into
+  // them (hc_acquire)
+  hipEvent_t put_ev = nullptr;
+  bool put_pending = false;
 };
 
 // host arrays packed into a context's pinned staging, then one asynchronous copy each
@@ -691,16 +696,29 @@ int upload_pinned(Dev& d, Hc& h, const PinnedUploads& u) {
   return 0;
 }
 
-Hc& hc_acquire(Dev& d) {
-  std::unique_lock<std::mutex> lk(d.hc_mu);
-  for (;;) {
-    for (int k = 0; k < g_ws_sets; k++)
-      if (!d.hc[k].busy) {
-        d.hc[k].busy = true;
-        return d.hc[k];
-      }
-    d.hc_cv.wait(lk);
+// a context's staging buffers are free once the signature-cache put of its previous call has read
+// them (a short kernel pair that started when that call's pipeline ended)
+void hc_ready(Hc& h) {
+  if (h.put_pending) {
+    (void)hipEventSynchronize(h.put_ev);
+    h.put_pending = false;
   }
+}
+Hc& hc_acquire(Dev& d) {
+  Hc* got = nullptr;
+  {
+    std::unique_lock<std::mutex> lk(d.hc_mu);
+    while (!got) {
+      for (int k = 0; k < g_ws_sets && !got; k++)
+        if (!d.hc[k].busy) {
+          d.hc[k].busy = true;
+          got = &d.hc[k];
+        }
+      if (!got) d.hc_cv.wait(lk);
+    }
+  }
+  hc_ready(*got);
+  return *got;
 }
 void hc_release(Dev& d, Hc& h) {
   {
@@ -711,13 +729,17 @@ void hc_release(Dev& d, Hc& h) {
 }
 // a free context or nullptr (never waits: a chunked call takes only what is idle)
 Hc* hc_try_acquire(Dev& d) {
-  std::lock_guard<std::mutex> lk(d.hc_mu);
-  for (int k = 0; k < g_ws_sets; k++)
-    if (!d.hc[k].busy) {
-      d.hc[k].busy = true;
-      return &d.hc[k];
-    }
-  return nullptr;
+  Hc* got = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(d.hc_mu);
+    for (int k = 0; k < g_ws_sets && !got; k++)
+      if (!d.hc[k].busy) {
+        d.hc[k].busy = true;
+        got = &d.hc[k];
+      }
+  }
+  if (got) hc_ready(*got);
+  return got;
 }
 
 // per-call random linear combination key (OS CSPRNG)
@@ -1714,10 +1736,12 @@ bool sc_ready(Dev& d, bool alloc) {
   d.sc_cursor = d.sc_filled = 0;
   return true;
 }
-// After a Verify batch's pipeline on s: its m signatures (bytes in group order, sig) and their
-// decompressed points and statuses (pts, st: the verification's workspace w) enter the ring on
-// sc_s, and the workspace is released behind the put -- or on s when nothing is put.
-int sc_put_release(Dev& d, Ws& w, const uint8_t* sig, const HmEntry* pts, const uint8_t* st, size_t m, hipStream_t s) {
+// After a Verify batch's pipeline on s: its m signatures (bytes in group order, sig: in the staging
+// buffers of the host-call context `owner`) and their decompressed points and statuses (pts, st:
+// the verification's workspace w) enter the ring on sc_s; the workspace is released behind the put
+// -- or on s when nothing is put -- and the owner's next call waits for it (hc_ready).
+int sc_put_release(Dev& d, Ws& w, const uint8_t* sig, const HmEntry* pts, const uint8_t* st, size_t m, hipStream_t s,
+                   Hc& owner) {
   if (!m || !sc_ready(d, true)) return ws_release(w, s);
   const size_t cap = d.sc_cap;
   if (m > cap) {  // only the last cap items fit
@@ -1736,6 +1760,10 @@ int sc_put_release(Dev& d, Ws& w, const uint8_t* sig, const HmEntry* pts, const 
         launch_sc_put(sig, pts, st, (uint32_t)m, (uint32_t)d.sc_cursor, (uint32_t)cap, d.sc_key.p, (HmEntry*)d.sc_ent.p,
                       (uint8_t*)d.sc_st.p, (uint32_t*)d.sc_tab.p, (uint32_t)(2 * cap), g_sc_k0, g_sc_k1, d.sc_s));
   HCHK(hipEventRecord(done, d.sc_s));
+  // sig lives in the owner context's staging buffers: its next call waits for this put
+  if (!owner.put_ev) HCHK(hipEventCreateWithFlags(&owner.put_ev, hipEventDisableTiming));
+  HCHK(hipEventRecord(owner.put_ev, d.sc_s));
+  owner.put_pending = true;
   d.sc_inflight.push_back({d.sc_cursor, m, pipe, done});
   d.sc_cursor = (d.sc_cursor + m) & (cap - 1);
   d.sc_filled = std::min(cap, d.sc_filled + m);
@@ -1913,7 +1941,7 @@ int verify_large(Dev& d, const uint8_t* pks, const uint8_t* sigs, const uint8_t*
       HmEntry* vsig;
       uint8_t* vsigst;
       if (wsbuf(w, W_VSIG, m, &vsig) || wsbuf(w, W_VSIGST, m, &vsigst) ||
-          sc_put_release(d, w, csig, vsig, vsigst, m, sc))
+          sc_put_release(d, w, csig, vsig, vsigst, m, sc, h0))
         return -1;
     }
     LAUNCH(k_scatter_status, m, sc, dst, dord + ib, (uint32_t)m, dst_out);
@@ -2044,7 +2072,7 @@ int verify_host(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msgs, co
       HmEntry* vsig;
       uint8_t* vsigst;
       if (wsbuf(w, W_VSIG, m, &vsig) || wsbuf(w, W_VSIGST, m, &vsigst) ||
-          sc_put_release(d, w, dsig, vsig, vsigst, m, h.s))
+          sc_put_release(d, w, dsig, vsig, vsigst, m, h.s, h))
         return -1;
     }
     if (whole) LAUNCH(k_scatter_status, m, h.s, dst, dord, (uint32_t)m, dst_out);
@@ -2122,7 +2150,7 @@ int verify_first_host(const uint8_t* pks, const uint8_t* sigs, const uint8_t* ms
   {  // the decoded signatures enter the signature cache as after hbls_verify_batch
     HmEntry* vsig;
     uint8_t* vsigst;
-    if (wsbuf(w, W_VSIG, n, &vsig) || wsbuf(w, W_VSIGST, n, &vsigst) || sc_put_release(d, w, dsig, vsig, vsigst, n, h.s))
+    if (wsbuf(w, W_VSIG, n, &vsig) || wsbuf(w, W_VSIGST, n, &vsigst) || sc_put_release(d, w, dsig, vsig, vsigst, n, h.s, h))
       return -1;
   }
   lk.unlock();

@@ -55,6 +55,17 @@ def main():
                                    "wrong": int((out.reshape(V, 96) != d["root_sigs"].reshape(V, 96)).any(axis=1).sum()),
                                    "first_wrong": [int(x) for x in np.nonzero(
                                        (out.reshape(V, 96) != d["root_sigs"].reshape(V, 96)).any(axis=1))[0][:8]]}
+    # back to back on the same host-call contexts: a Verify whose signature-cache put (after the
+    # call returned) still reads its staging buffers, then an aggregation that uploads into them
+    ok = True
+    for _ in range(10):
+        rc1 = L.hbls_verify_batch_first_error(_p(d["pks"]), _p(sigs), _p(d["item_msgs"]), _p(d["item_off"]),
+                                              _p(d["item_len"]), NP, ctypes.byref(first), ctypes.byref(fst), None)
+        rc2 = L.hbls_threshold_aggregate_batch(_p(d["ta_sigs"]), _p(d["ta_idx"]), _p(d["grp_off"]), V, _p(out),
+                                               _p(tst))
+        ok = ok and rc1 == 0 and rc2 == 0 and first.value == bad[0] and not tst.any() and \
+            bool(np.array_equal(out, d["root_sigs"]))
+    res["back_to_back_ok"] = ok
     errs = []
     off0 = np.zeros(1, dtype=np.uint64)
     len32 = np.full(1, 32, dtype=np.uint32)

@@ -98,10 +98,13 @@ ENV_SETS = [
      "HBLS_SIG_CACHE": "1024", "HBLS_FE_BATCH": "4", "HBLS_SLOT_MSM": "64", "HBLS_SINGLE_MAX": "1",
      "HBLS_RLC_LANES": "128", "HBLS_TA_JOINT": "3", "HBLS_TA_PAIR_MAX": "100000", "HBLS_HASH_PAIR_MAX": "100000",
      "HBLS_HASH_ONE_LANE": "100000", "HBLS_FE18_MAX": "100000", "HBLS_GROUP_MAX": "64"},
+    # one host-call context: every call reuses the staging buffers the previous call's
+    # signature-cache put reads (the race fixed by hc_ready)
+    {"HBLS_WS_SETS": "1", "HBLS_SIG_CACHE": "4096"},
 ]
 
 
-@pytest.mark.parametrize("env", ENV_SETS, ids=["set0", "set1"])
+@pytest.mark.parametrize("env", ENV_SETS, ids=["set0", "set1", "one_context"])
 def test_environment_settings(env):
     child_env = {k: v for k, v in os.environ.items() if not k.startswith("HBLS_")}
     child_env.update(env)
@@ -111,6 +114,7 @@ def test_environment_settings(env):
     assert p.returncode == 0 and lines, (p.returncode, p.stdout[-2000:], p.stderr[-2000:])
     res = json.loads(lines[-1])
     assert res["env"] == env
-    assert all(res[k] for k in ("verify_ok", "first_error_ok", "aggregate_ok", "single_callers_ok")), res
+    assert all(res[k] for k in ("verify_ok", "first_error_ok", "aggregate_ok", "back_to_back_ok",
+                                "single_callers_ok")), res
     if env.get("HBLS_HOST_TIMING") == "1":
         assert "hbls " in p.stderr  # the host-timing lines
