@@ -526,6 +526,25 @@ def _lib_timing(L):
     return _lib.timing_read(L)
 
 
+def valu_issue_of(kernel, ms_alone, n_cu):
+    """The dominant kernel against the VALU ISSUE ceiling: its wave-level VALU instructions per slot
+    (SQ_INSTS_VALU, committed PMC pass of this build, profiles/pmc_traffic.json) over its alone time,
+    against one wave instruction per SIMD per 4 clocks (n_cu x 4 SIMDs x clock / 4) at the peak's
+    measured clock.  v_mad_u64_u32 itself issues at 0.84 of that (profiles/r05b_peak_from_counters.json)."""
+    try:
+        k = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))["kernels"].get(kernel)
+    except (OSError, ValueError, KeyError):
+        return None
+    if not k or not k.get("valu_wave_insts") or not ms_alone:
+        return None
+    ceil = n_cu * opcounts.PEAK_CLOCK_MHZ * 1e6  # wave instructions / s
+    got = k["valu_wave_insts"] / (ms_alone * 1e-3)
+    return {"wave_insts_per_step": k["valu_wave_insts"], "achieved_G_per_s": round(got / 1e9, 1),
+            "ceiling_G_per_s": round(ceil / 1e9, 1), "frac": round(got / ceil, 4),
+            "mad_issue_frac_of_ceiling": round(opcounts.PEAK_MAD_TOPS / (n_cu * 64 * opcounts.PEAK_CLOCK_MHZ * 1e-6), 4),
+            "source": "profiles/pmc_traffic.json valu_wave_insts (SQ_INSTS_VALU of the PMC pass)"}
+
+
 def traffic_of(kernel):
     """HBM bytes per slot of `kernel` (all its launches, FETCH_SIZE x2 + WRITE_SIZE) from the
     committed PMC pass, or None (rocprofv3 counters cannot be read from inside the timed run)."""
@@ -994,6 +1013,8 @@ def main(argv=None):
                                             f"{opcounts.MAC_PER_FPMUL} MAC per step (executed {x['fpmul_per_unit_exec']} "
                                             f"Fp-mul per unit)",
                         "kernel_ms_alone": x["ms_per_step"],
+                        "valu_issue": valu_issue_of(dom, x["ms_per_step"],
+                                                    torch.cuda.get_device_properties(dev).multi_processor_count),
                         "timing": "HIP events around each launch on its stream, kernels serialised (one extra "
                                   "slot after the timed region, library timing mode 2)",
                         "slot": {"fpmul_alg_per_step": slot_fpmul, "achieved": round(slot_tops, 3),
