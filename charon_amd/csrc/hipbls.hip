@@ -370,6 +370,7 @@ struct Hc {
   // them (hc_acquire)
   hipEvent_t put_ev = nullptr;
   bool put_pending = false;
+  hipStream_t put_s = nullptr;  // its signature-cache puts (sc_put_release)
 };
 
 // host arrays packed into a context's pinned staging, then one asynchronous copy each
@@ -415,19 +416,22 @@ struct Dev {
   size_t kc_n = 0, kc_tcap = 0;
   // decompressed-signature cache (vbatch.hip k_sc_write / k_sc_index / k_sc_get): filled by host-buffer Verify
   // batches, read by host-buffer ThresholdAggregate batches; enqueued under `mu` like everything
-  // else.  Puts run on their own stream sc_s, off the Verify call's critical path: each waits for
-  // its call's pipeline (`pipe`) and for every get enqueued before it (a put rewrites ring entries
-  // a get may read), and records `done`.  A get waits only for puts whose pipeline has already
-  // completed (a short kernel pair); the ring entries of puts still behind their pipeline are
-  // passed to it as a range of misses (sc_inflight is in ring order: puts are serialised on sc_s).
+  // else.  A put runs on its host-call context's own put stream, off the Verify call's critical
+  // path and beside other contexts' puts: it waits for its call's pipeline (`pipe`), for every get
+  // enqueued before it (a put rewrites ring entries a get may read) and for any put still in flight
+  // whose ring range overlaps its own, and records `done`.  A get waits only for puts whose
+  // pipeline has already completed (a short kernel pair); the ring entries of puts still behind
+  // their pipeline are passed to it as a range of misses.  Ring positions are also counted without
+  // the wrap (`pos`), so the span of the in-flight puts is exact.
   DevBuf sc_key, sc_ent, sc_st, sc_tab;
   size_t sc_cap = 0, sc_cursor = 0, sc_filled = 0;
-  hipStream_t sc_s = nullptr;
+  uint64_t sc_pos = 0;
   struct ScPut {
     size_t start, m;
+    uint64_t pos;
     hipEvent_t pipe, done;
   };
-  std::deque<ScPut> sc_inflight;
+  std::deque<ScPut> sc_inflight;       // enqueue (= ring) order
   std::vector<hipEvent_t> sc_gets;     // gets not yet known complete
   std::vector<hipEvent_t> sc_ev_pool;  // spare events
   // adaptive slot-wide check (HBLS_ADAPTIVE): outcomes of recent checked calls, copied to pinned host
@@ -1704,14 +1708,17 @@ hipEvent_t sc_event(Dev& d) {
 }
 // drop the records of completed puts and gets (wait: block until every one has completed)
 void sc_prune(Dev& d, bool wait) {
-  while (!d.sc_inflight.empty()) {
-    Dev::ScPut& p = d.sc_inflight.front();
+  std::deque<Dev::ScPut> live_puts;
+  for (Dev::ScPut& p : d.sc_inflight) {
     if (wait) (void)hipEventSynchronize(p.done);
-    else if (hipEventQuery(p.done) != hipSuccess) break;
-    d.sc_ev_pool.push_back(p.pipe);
-    d.sc_ev_pool.push_back(p.done);
-    d.sc_inflight.pop_front();
+    if (wait || hipEventQuery(p.done) == hipSuccess) {
+      d.sc_ev_pool.push_back(p.pipe);
+      d.sc_ev_pool.push_back(p.done);
+    } else {
+      live_puts.push_back(p);
+    }
   }
+  d.sc_inflight.swap(live_puts);
   std::vector<hipEvent_t> live;
   for (hipEvent_t e : d.sc_gets) {
     if (wait) (void)hipEventSynchronize(e);
@@ -1731,15 +1738,15 @@ bool sc_ready(Dev& d, bool alloc) {
       ensure_buf(d.sc_st, cap, &p) || ensure_buf(d.sc_tab, 2 * cap * sizeof(uint32_t), &p))
     return false;
   if (hipMemset(d.sc_tab.p, 0, 2 * cap * sizeof(uint32_t)) != hipSuccess) return false;
-  if (!d.sc_s && hipStreamCreateWithFlags(&d.sc_s, hipStreamNonBlocking) != hipSuccess) return false;
   d.sc_cap = cap;
   d.sc_cursor = d.sc_filled = 0;
   return true;
 }
 // After a Verify batch's pipeline on s: its m signatures (bytes in group order, sig: in the staging
 // buffers of the host-call context `owner`) and their decompressed points and statuses (pts, st:
-// the verification's workspace w) enter the ring on sc_s; the workspace is released behind the put
-// -- or on s when nothing is put -- and the owner's next call waits for it (hc_ready).
+// the verification's workspace w) enter the ring on the owner's put stream; the workspace is
+// released behind the put -- or on s when nothing is put -- and the owner's next call waits for it
+// (hc_ready).
 int sc_put_release(Dev& d, Ws& w, const uint8_t* sig, const HmEntry* pts, const uint8_t* st, size_t m, hipStream_t s,
                    Hc& owner) {
   if (!m || !sc_ready(d, true)) return ws_release(w, s);
@@ -1751,23 +1758,31 @@ int sc_put_release(Dev& d, Ws& w, const uint8_t* sig, const HmEntry* pts, const 
     m = cap;
   }
   sc_prune(d, false);
+  if (!owner.put_s) HCHK(hipStreamCreateWithFlags(&owner.put_s, hipStreamNonBlocking));
+  if (!owner.put_ev) HCHK(hipEventCreateWithFlags(&owner.put_ev, hipEventDisableTiming));
+  hipStream_t ps = owner.put_s;
   hipEvent_t pipe = sc_event(d), done = sc_event(d);
   if (!pipe || !done) return set_err("signature cache: no event");
   HCHK(hipEventRecord(pipe, s));
-  HCHK(hipStreamWaitEvent(d.sc_s, pipe, 0));
-  for (hipEvent_t g : d.sc_gets) HCHK(hipStreamWaitEvent(d.sc_s, g, 0));
-  TIMED(d, "k_sc_put", d.sc_s,
+  HCHK(hipStreamWaitEvent(ps, pipe, 0));
+  for (hipEvent_t g : d.sc_gets) HCHK(hipStreamWaitEvent(ps, g, 0));
+  // an in-flight put [q, q + mq) (absolute positions, before this one's [P, P + m)) shares ring
+  // entries with this one only if some position of this one lies a whole ring after one of its:
+  // P + m - 1 - q >= cap (only when more than the ring is in flight)
+  for (const Dev::ScPut& p : d.sc_inflight)
+    if (p.pos + cap < d.sc_pos + m) HCHK(hipStreamWaitEvent(ps, p.done, 0));
+  TIMED(d, "k_sc_put", ps,
         launch_sc_put(sig, pts, st, (uint32_t)m, (uint32_t)d.sc_cursor, (uint32_t)cap, d.sc_key.p, (HmEntry*)d.sc_ent.p,
-                      (uint8_t*)d.sc_st.p, (uint32_t*)d.sc_tab.p, (uint32_t)(2 * cap), g_sc_k0, g_sc_k1, d.sc_s));
-  HCHK(hipEventRecord(done, d.sc_s));
+                      (uint8_t*)d.sc_st.p, (uint32_t*)d.sc_tab.p, (uint32_t)(2 * cap), g_sc_k0, g_sc_k1, ps));
+  HCHK(hipEventRecord(done, ps));
   // sig lives in the owner context's staging buffers: its next call waits for this put
-  if (!owner.put_ev) HCHK(hipEventCreateWithFlags(&owner.put_ev, hipEventDisableTiming));
-  HCHK(hipEventRecord(owner.put_ev, d.sc_s));
+  HCHK(hipEventRecord(owner.put_ev, ps));
   owner.put_pending = true;
-  d.sc_inflight.push_back({d.sc_cursor, m, pipe, done});
+  d.sc_inflight.push_back({d.sc_cursor, m, d.sc_pos, pipe, done});
   d.sc_cursor = (d.sc_cursor + m) & (cap - 1);
+  d.sc_pos += m;
   d.sc_filled = std::min(cap, d.sc_filled + m);
-  return ws_release(w, d.sc_s);
+  return ws_release(w, ps);
 }
 // before an aggregation's decompression: the cached points of its n members into pts / st, hit[i]
 // set for those (k_dec_sig_pt then skips them).  Returns whether the cache was consulted.  Never
@@ -1775,14 +1790,23 @@ int sc_put_release(Dev& d, Ws& w, const uint8_t* sig, const HmEntry* pts, const 
 bool sc_get(Dev& d, const uint8_t* sig, size_t n, HmEntry* pts, uint8_t* st, uint8_t* hit, hipStream_t s) {
   if (!n || !d.sc_filled || !sc_ready(d, false)) return false;
   sc_prune(d, false);
-  size_t k = 0;
-  while (k < d.sc_inflight.size() && hipEventQuery(d.sc_inflight[k].pipe) == hipSuccess) k++;
-  if (k && hipStreamWaitEvent(s, d.sc_inflight[k - 1].done, 0) != hipSuccess) return false;
+  // puts whose pipeline is done: wait for them; the others: their span is a range of misses
+  uint64_t busy_first = 0, busy_end = 0;
+  bool busy = false;
+  for (const Dev::ScPut& p : d.sc_inflight) {
+    if (hipEventQuery(p.pipe) == hipSuccess) {
+      if (hipStreamWaitEvent(s, p.done, 0) != hipSuccess) return false;
+      continue;
+    }
+    if (!busy) busy_first = p.pos;
+    busy = true;
+    busy_end = p.pos + p.m;
+  }
   size_t busy_lo = 0, busy_len = 0;
-  if (k < d.sc_inflight.size()) {
-    busy_lo = d.sc_inflight[k].start;
-    for (size_t j = k; j < d.sc_inflight.size(); j++) busy_len += d.sc_inflight[j].m;
-    if (busy_len >= d.sc_cap) return false;  // every entry is being rewritten
+  if (busy) {
+    if (busy_end - busy_first >= d.sc_cap) return false;  // every entry may be rewritten
+    busy_lo = (size_t)(busy_first & (d.sc_cap - 1));
+    busy_len = (size_t)(busy_end - busy_first);
   }
   hipEvent_t e = sc_event(d);
   if (!e) return false;
