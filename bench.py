@@ -545,6 +545,26 @@ def valu_issue_of(kernel, ms_alone, n_cu):
             "source": "profiles/pmc_traffic.json valu_wave_insts (SQ_INSTS_VALU of the PMC pass)"}
 
 
+def slot_valu_insts():
+    """Wave-level VALU instructions of one C3 slot, summed over the timed kernel labels of the
+    committed PMC pass (profiles/pmc_traffic.json), or None."""
+    try:
+        ks = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))["kernels"]
+    except (OSError, ValueError, KeyError):
+        return None
+    return sum(k.get("valu_wave_insts", 0) for k in ks.values()) or None
+
+
+def slot_issue(workload, step_s, n_cu):
+    """C3 only (the PMC pass is of a C3 slot): the slot's VALU instructions over the measured step
+    time against the issue ceiling (one wave instruction per SIMD per 4 clocks)."""
+    n = slot_valu_insts() if workload == "c3" else None
+    if not n:
+        return {}
+    return {"valu_wave_insts_per_step": n,
+            "valu_issue_frac": round(n / step_s / (n_cu * opcounts.PEAK_CLOCK_MHZ * 1e6), 4)}
+
+
 def traffic_of(kernel):
     """HBM bytes per slot of `kernel` (all its launches, FETCH_SIZE x2 + WRITE_SIZE) from the
     committed PMC pass, or None (rocprofv3 counters cannot be read from inside the timed run)."""
@@ -1019,7 +1039,9 @@ def main(argv=None):
                                   "slot after the timed region, library timing mode 2)",
                         "slot": {"fpmul_alg_per_step": slot_fpmul, "achieved": round(slot_tops, 3),
                                  "frac": round(slot_tops / opcounts.PEAK_MAD_TOPS, 4),
-                                 "note": "all kernels' algorithmic work over ms_per_step (slots in flight overlap)"},
+                                 "note": "all kernels' algorithmic work over ms_per_step (slots in flight overlap)",
+                                 **slot_issue(args.workload, elapsed / args.steps,
+                                              torch.cuda.get_device_properties(dev).multi_processor_count)},
                         "k_pair3": pair}
         return per, roofline
 
