@@ -697,6 +697,10 @@ def main(argv=None):
                     help="at one GPU: run the multi-GPU exchange (RCCL world of one) inside the timed region")
     ap.add_argument("--mode", default="slot", choices=["slot", "staged"],
                     help="slot: one hbls_slot_device call per step (stages overlap); staged: stage by stage")
+    ap.add_argument("--share-device", type=int, default=0,
+                    help="rehearsal of the N > 1 path on a one-GPU box: every rank on device 0, the slot "
+                         "exchange over gloo through host copies (RCCL refuses two ranks on one GPU); the line "
+                         "is marked rehearsal and is not a measurement")
     ap.add_argument("--dry-run", type=int, default=0,
                     help="1: no GPU -- every rank joins the gloo control plane, reports its rank environment "
                          "and prints the merged line (tests the launcher on a CPU host); 2: the same with "
@@ -724,6 +728,8 @@ def main(argv=None):
     from charon_amd.shard import (SlotExchange, init_library_comm, library_allgather, max_over_ranks,
                                    pack_layout, pack_views, unpack_gathered)
 
+    if args.share_device:
+        local = 0
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("gloo")  # control plane only: the slot exchange is the library's RCCL
@@ -778,8 +784,18 @@ def main(argv=None):
         # the library's RCCL communicator (rank 0's id over the gloo control plane), then ONE
         # exchange stream for the all-gathers of every in-flight slot (charon_amd/shard.py
         # SlotExchange: the same ordering code tests/test_shard.py runs over gloo)
-        init_library_comm(L, world, rank)
-        exch = SlotExchange(world, rank, {"pack": PB}, dev, library_allgather(L), stream=torch.cuda.Stream(device=dev))
+        if args.share_device:
+            def host_allgather(send, recv, nbytes, stream):  # the rehearsal's stand-in for RCCL
+                stream.synchronize()  # the producer's outputs (the exchange stream waited for them)
+                hr = torch.empty(world * nbytes, dtype=torch.uint8)
+                dist.all_gather_into_tensor(hr, send.cpu())
+                with torch.cuda.stream(stream):
+                    recv.copy_(hr.to(dev))
+            allgather = host_allgather
+        else:
+            init_library_comm(L, world, rank)
+            allgather = library_allgather(L)
+        exch = SlotExchange(world, rank, {"pack": PB}, dev, allgather, stream=torch.cuda.Stream(device=dev))
         for o in outs:
             o["xchg"] = exch.gather_buffers()
         xchg = outs[0]["xchg"]
@@ -1056,6 +1072,8 @@ def main(argv=None):
         # the ranks' own times (the line takes the slowest) and the RCCL world the library joined
         "per_rank_ms_per_step": [round(x / args.steps * 1e3, 3) for x in per_rank_s],
         "rccl_world": L.hbls_comm_size() if xw else 0,
+        **({"rehearsal": f"{world} ranks on ONE GPU, exchange over gloo through host copies: not a measurement"}
+           if args.share_device else {}),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "u32 (Fp/Fr Montgomery limbs, integer VALU)",
         "data": "synthetic: SHA-256-derived keys, Shamir shares and signing roots (charon_amd/synth.py); "
@@ -1174,7 +1192,7 @@ def main(argv=None):
         out["cpu_baseline"] = cpu_baseline(d, args.cpu_seconds)
 
     if xw:
-        if L.hbls_comm_size() != world:
+        if L.hbls_comm_size() != world and not args.share_device:
             parity["rccl_world_matches"] = False
         _chk(L, L.hbls_comm_destroy())
     if world > 1:

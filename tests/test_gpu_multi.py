@@ -16,6 +16,7 @@
   both (core/sigagg/sigagg.go:117 folded into the partial's group).
 """
 import ctypes
+import os
 import hashlib
 import random
 import threading
@@ -253,3 +254,30 @@ def test_singleton_group_folded_aggregate_cancelling_errors(L, hipbls):
         assert bytes(tout.cpu().numpy()[:96]) == dvsigs[0]
     finally:
         L.hbls_fe_batch(prev)
+
+
+@pytest.mark.parametrize("workload", ["c5", "c3"])
+def test_bench_two_ranks_rehearsal(workload):
+    """bench.py's N > 1 path end to end on the one-GPU box: `--gpus 2` starts two ranks itself
+    (launch_ranks), both on device 0 (`--share-device 1`; RCCL refuses two ranks on one GPU, so the
+    slot exchange runs over gloo through host copies -- the library's RCCL all-gather is covered as
+    a world of one above).  Every rank builds its own shard, runs its slots, exchanges the packed
+    verdicts and aggregates every slot, checks every rank's gathered blocks (C5: its own block
+    against its construction; C3: every rank's block all valid, its own aggregates equal to the
+    root signatures), and rank 0 prints one line with n_gpus 2 and both ranks' times."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT", "LOCAL_WORLD_SIZE")}
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--share-device", "1", "--workload", workload,
+           "--validators", "3000" if workload == "c5" else "2000", "--steps", "2", "--warmup", "1", "--cpu-seconds", "0",
+           "--callers", "0", "--aggregate-verify", "0", "--key-tables", "0", "--host-api", "0"]
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=280)
+    lines = [x for x in p.stdout.splitlines() if x.startswith("{")]
+    assert p.returncode == 0 and len(lines) == 1, (p.returncode, p.stdout[-1500:], p.stderr[-3000:])
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and "rehearsal" in line and len(line["per_rank_ms_per_step"]) == 2
+    assert line["parity"] and all(line["parity"].values()), line["parity"]
+    assert "allgather_ok" in line["parity"]
