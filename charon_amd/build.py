@@ -120,6 +120,25 @@ def build_hostcheck(force: bool = False, verbose: bool = True, defines=(), out: 
     return out
 
 
+def build_c_client(force: bool = False, verbose: bool = True) -> str:
+    """tests/native/cabi_client: a C program linked against libhipbls.so through include/hipbls.h
+    (what the Go shim's cgo does), compiled with -std=c99 -Wall -Wextra -Werror so the header is
+    checked as C; test-only."""
+    src = os.path.join(ROOT, "tests", "native", "cabi_client.c")
+    out = os.path.join(ROOT, "tests", "native", "cabi_client")
+    deps = [src, os.path.join(ROOT, "include", "hipbls.h")]
+    if not force and os.path.exists(out) and all(os.path.getmtime(d) <= os.path.getmtime(out) for d in deps):
+        return out
+    cmd = ["gcc", "-std=c99", "-O2", "-Wall", "-Wextra", "-Werror", "-o", out + ".tmp", src,
+           "-L" + os.path.dirname(LIB), "-lhipbls", "-Wl,-rpath," + os.path.dirname(LIB),
+           "-Wl,-rpath,/opt/rocm/lib"]
+    subprocess.run(cmd, check=True, timeout=300)
+    os.replace(out + ".tmp", out)
+    if verbose:
+        print(f"built {out}")
+    return out
+
+
 SANITIZED_FLAGS = ["-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
                    "-fno-sanitize-recover=undefined", "-std=c++17", "-pthread", "-shared", "-fPIC"]
 
@@ -145,6 +164,7 @@ def main(argv=None):
     force = "--force" in (argv or sys.argv[1:])
     build_library(force)
     build_hostcheck(force)
+    build_c_client(force)
 
 
 if __name__ == "__main__":

@@ -190,3 +190,30 @@ def test_lane_pair_subgroup_checks(hipbls, fixtures, kats):
     finally:
         L.hbls_dec_pair_max(prev)
     assert hipbls.verify_batch(P, M, S) == exp
+
+
+def test_c_client(kats):
+    """A C program through include/hipbls.h (tests/native/cabi_client.c, built by
+    charon_amd/build.py with -std=c99 -Werror; what the Go shim's cgo does, without Python): it
+    signs the reference's teku registration root with the teku key (byte-equal to the teku
+    signature), verifies it and a corrupted copy (the status the oracle gives), finds the first
+    failure of that pair, and threshold-aggregates a 3-of-4 split over shares {2, 3, 4} back to the
+    key's own signature."""
+    import json
+    import subprocess
+    from charon_amd.build import build_c_client
+    from oracle import bls12381 as B
+    r = kats["registration"]
+    exe = build_c_client(verbose=False)
+    p = subprocess.run([exe, r["sk"], r["msg"], r["sig"]], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    bad = bytearray(bytes.fromhex(r["sig"]))
+    bad[95] ^= 1
+    pk = B.secret_to_public_key(bytes.fromhex(r["sk"]))
+    want_bad = B.verify(pk, bytes.fromhex(r["msg"]), bytes(bad))
+    assert out["sign_equals_teku"] is True
+    assert out["verify"] == [0, want_bad] and want_bad != 0
+    assert out["first_error"] == [1, out["verify"][1]]
+    assert out["aggregate_status"] == 0 and out["aggregate_equals_signature"] is True
+    assert out["build"].startswith("hbls-build:")
