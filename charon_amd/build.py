@@ -104,7 +104,7 @@ def check_hostcheck(path: str, defines=(), root: str = "") -> str:
 
 
 def build_hostcheck(force: bool = False, verbose: bool = True, defines=(), out: str = "") -> str:
-    """defines / out: another build of the harness (e.g. ("HB_FP_ILP",): the two-accumulator
+    """defines / out: another build of the harness (e.g. ("HB_HOST_MUL28",): the 28-bit host
     products, tests/test_sanitizers.py).  A harness whose embedded id (hc_build_id) equals this
     tree's is reused; any other -- a header touched, other flags -- is rebuilt."""
     src = os.path.join(ROOT, "tests", "native", "hostcheck.cpp")

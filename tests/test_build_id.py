@@ -76,5 +76,5 @@ def test_stale_cpu_harness_is_refused(tmp_path):
     with pytest.raises(RuntimeError, match="stale CPU harness"):
         build.check_hostcheck(path, root=root)
     # other flags or defines are another harness
-    assert build.hostcheck_build_id(("HB_FP_ILP",)) != hid
+    assert build.hostcheck_build_id(("HB_HOST_MUL28",)) != hid
     assert build.hostcheck_build_id(flags=build.SANITIZED_FLAGS) != hid
