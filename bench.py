@@ -639,6 +639,17 @@ def launch_ranks(n: int, argv) -> int:
     return rc
 
 
+def keep_stdout_for_the_line() -> None:
+    """Stdout carries only rank 0's JSON line.  Native libraries write to file descriptor 1 of every
+    rank (gloo prints "[Gloo] Rank r is connected to ..." when a group forms, under
+    torch.distributed.run on the launcher's shared stdout): point descriptor 1 at stderr and give
+    Python's sys.stdout a stream on the original descriptor, which only the line is printed to."""
+    sys.stdout.flush()
+    fd = os.dup(1)
+    os.dup2(2, 1)
+    sys.stdout = os.fdopen(fd, "w", buffering=1)
+
+
 def dry_run(args, rank: int, world: int, local: int) -> int:
     """The launcher and the control plane without a GPU: every rank joins gloo, the ranks' own
     environments and a stand-in step time are gathered, rank 0 prints the merged line."""
@@ -720,6 +731,7 @@ def main(argv=None):
         # never measure a world other than the one asked for (a line labelled with the wrong N)
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}: refusing to run", file=sys.stderr)
         return 2
+    keep_stdout_for_the_line()
     if args.dry_run:
         return dry_run(args, rank, world, local)
 

@@ -32,6 +32,7 @@ def test_launcher_spawns_ranks_and_merges_one_line():
     assert p.returncode == 0, p.stderr
     lines = _json_lines(p.stdout)
     assert len(lines) == 1, p.stdout  # rank 0 only
+    assert len(p.stdout.strip().splitlines()) == 1, p.stdout  # nothing else: gloo's messages go to stderr
     line = lines[0]
     assert line["n_gpus"] == 2 and line["dry_run"] is True
     ranks = sorted(line["ranks"], key=lambda r: r["rank"])
@@ -70,3 +71,17 @@ def test_single_gpu_dry_run_is_world_of_one():
     assert p.returncode == 0, p.stderr
     (line,) = _json_lines(p.stdout)
     assert line["n_gpus"] == 1 and len(line["ranks"]) == 1
+
+
+def test_torchrun_launch_stdout_is_the_line():
+    # the driver's N > 1 command: torch.distributed.run merges every rank's stdout; the gloo
+    # control plane's "[Gloo] Rank r is connected ..." messages must not land there
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", "29561", BENCH, "--gpus", "2",
+                        "--dry-run", "1", "--steps", "3", "--warmup", "1"],
+                       env=_env(), capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr
+    out = p.stdout.strip().splitlines()
+    assert len(out) == 1, p.stdout
+    line = json.loads(out[0])
+    assert line["n_gpus"] == 2 and sorted(r["rank"] for r in line["ranks"]) == [0, 1]
